@@ -1,0 +1,397 @@
+// Implicit-GEMM 2-D convolution on MFMA (gfx950), NHWC activations.
+//
+// One engine serves every conv of the hot path (timm ResNet-50 OS8 at
+// foundation_model.py:260-267, the adapter necks model_module.py:440-447,
+// the ResNetLite blocks :259-280, heads :113-118/:150-187/:337-345 and the
+// fusion projections :857-862) in two roles:
+//   FWD  : Y[m = (n,ho,wo)][co] = sum_{(r,s,ci)} X[n, ho*st-pad+r*dil, wo*st-pad+s*dil, ci] * W[co][r][s][ci]
+//   DGRAD: dX[m = (n,h,w)][ci]  = sum_{(r,s,co)} dY[n, (h+pad-r*dil)/st, (w+pad-s*dil)/st, co] * Wt[ci][r][s][co]
+//          (terms whose division is inexact or out of range are zero)
+// GEMM view: M = output pixels, N = output channels, K = taps x input
+// channels; A gathered on the fly from the NHWC source (zero padding by
+// predicate), B = weights stored K-contiguous.
+//
+// Tiling (bf16): 128x128 block tile, BK = 64, 4 waves in 2x2, each wave a
+// 64x64 sub-tile of 4x4 v_mfma_f32_16x16x32_bf16 fragments, fp32
+// accumulation. f32 parity mode: same geometry with BK = 32 floats and
+// v_mfma_f32_16x16x4_f32 (exact f32 FMA chains).
+// LDS: double-buffered A/B stages of [128 rows][8 x 16-B chunks] with an XOR
+// swizzle chunk ^ (row & 7) (conflict-free ds_read_b128 fragment reads).
+// Epilogue: + bias, optional activation, optional per-channel batch-norm
+// partial statistics (sum, sum^2 over the tile's valid rows -> slab
+// partials[mtile][co][2], reduced deterministically by dmf_bn_finalize), then
+// an LDS-staged, 16-B coalesced store with an output channel stride (so
+// producers can write straight into a channel slice of a concat buffer).
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+struct ConvArgs {
+  const void* x;      // A source (FWD: input; DGRAD: dy)
+  const void* w;      // B source [Nout][Ktot]
+  const float* bias;  // [Nout] or null
+  void* y;            // output NHWC, channel stride ldy
+  float* partials;    // [mtiles][Nout][2] or null
+  int N, H, W, C, ldx;  // A-source geometry
+  int Ho, Wo, ldy;      // output geometry
+  int Nout;             // GEMM N
+  int KH, KW, stride, pad, dil;
+  int Ktot;             // KH*KW*C
+  int M;                // N*Ho*Wo
+  int act;
+  int mtiles, ntiles;
+};
+
+template <int ACT>
+__device__ __forceinline__ float apply_act(float v) {
+  if (ACT == DMF_ACT_RELU) return fmaxf(v, 0.f);
+  if (ACT == DMF_ACT_GELU) return gelu_f(v);
+  if (ACT == DMF_ACT_SIGMOID) return sigmoid_f(v);
+  return v;
+}
+__device__ __forceinline__ float apply_act_rt(int act, float v) {
+  switch (act) {
+    case DMF_ACT_RELU: return fmaxf(v, 0.f);
+    case DMF_ACT_GELU: return gelu_f(v);
+    case DMF_ACT_SIGMOID: return sigmoid_f(v);
+    default: return v;
+  }
+}
+
+constexpr int CBM = 128, CBN = 128, CTHREADS = 256;
+constexpr int STAGE_BYTES = (CBM + CBN) * 128;  // A + B, 128-byte rows
+
+// bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
+// an XCD; give each XCD a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, xcd = b % 8, loc = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+template <typename T, bool DGRAD>
+__global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
+  constexpr int BK = 8 * EPC;          // 8 chunks per LDS row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nblk = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, nblk);
+  const int mt = lin / a.ntiles, nt = lin % a.ntiles;
+  const int m0 = mt * CBM, n0 = nt * CBN;
+
+  const T* __restrict__ X = (const T*)a.x;
+  const T* __restrict__ Wt = (const T*)a.w;
+
+  // ---- per-thread load assignment: chunk q of rows (tid>>3) + 32*i
+  const int q = tid & 7;
+  const int rbase = tid >> 3;
+  // A rows: decode output pixel once
+  int a_n[4], a_h[4], a_w[4];
+  bool a_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rbase + 32 * i;
+    a_ok[i] = m < a.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    a_n[i] = mm / hw;
+    const int rem = mm - a_n[i] * hw;
+    a_h[i] = rem / a.Wo;
+    a_w[i] = rem - a_h[i] * a.Wo;
+  }
+  const int nk = (a.Ktot + BK - 1) / BK;
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int kt) {
+    const int k = kt * BK + q * EPC;
+    const bool kok = k < a.Ktot;
+    const int tap = kok ? k / a.C : 0;
+    const int c = k - tap * a.C;
+    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool ok = kok && a_ok[i];
+      int hi, wi;
+      if (!DGRAD) {
+        hi = a_h[i] * a.stride - a.pad + r * a.dil;
+        wi = a_w[i] * a.stride - a.pad + s * a.dil;
+      } else {
+        const int hn = a_h[i] + a.pad - r * a.dil, wn_ = a_w[i] + a.pad - s * a.dil;
+        ok = ok && hn >= 0 && wn_ >= 0 && (hn % a.stride) == 0 && (wn_ % a.stride) == 0;
+        hi = hn / a.stride;
+        wi = wn_ / a.stride;
+      }
+      ok = ok && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      if (ok) {
+        const size_t off = ((size_t)(a_n[i] * a.H + hi) * a.W + wi) * a.ldx + c;
+        ra[i] = *(const uint4*)(X + off);
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + rbase + 32 * i;
+      if (kok && n < a.Nout) {
+        rb[i] = *(const uint4*)(Wt + (size_t)n * a.Ktot + k);
+      } else {
+        rb[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lds_store = [&](int stage) {
+    char* base = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + 32 * i;
+      *(uint4*)(base + row * 128 + ((q ^ (row & 7)) << 4)) = ra[i];
+      *(uint4*)(base + CBM * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lds_store(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* As = smem + cur * STAGE_BYTES;
+    const char* Bs = As + CBM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fg;
+      uint4 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + fr;
+        bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
+      }
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                *(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float fa = __uint_as_float(((const uint32_t*)&av[i])[e]);
+              const float fb = __uint_as_float(((const uint32_t*)&bv[j])[e]);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, acc[i][j], 0, 0, 0);
+            }
+      }
+    }
+    if (kt + 1 < nk) lds_store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------ epilogue
+  const bool has_bias = a.bias != nullptr;
+  const bool stats = a.partials != nullptr;
+  float* red = (float*)smem;  // [2 wm][128 cols][2] floats = 2 KB
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + fr;
+    const float bsv = (has_bias && col < a.Nout) ? a.bias[col] : 0.f;
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
+        float v = acc[i][j][r] + bsv;
+        if (stats && row < a.M) { s += v; ss += v * v; }
+        if (!stats) v = apply_act_rt(a.act, v);
+        acc[i][j][r] = v;
+      }
+    }
+    if (stats) {
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
+      if (fg == 0) {
+        const int lc = wn * 64 + j * 16 + fr;
+        red[(wm * 128 + lc) * 2 + 0] = s;
+        red[(wm * 128 + lc) * 2 + 1] = ss;
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    if (tid < 128) {
+      const int col = n0 + tid;
+      if (col < a.Nout) {
+        float2 v;
+        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
+        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
+        *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+      }
+    }
+  }
+  __syncthreads();
+  // stage C tile through LDS: [128 rows][128 + pad] of T
+  constexpr int CPAD = 16 / sizeof(T);
+  constexpr int CST = CBN + CPAD;
+  T* Cs = (T*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + fg * 4 + r;
+        const int col = wn * 64 + j * 16 + fr;
+        Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
+      }
+  __syncthreads();
+  T* Y = (T*)a.y;
+  constexpr int CPR = CBN / EPC;  // chunks per row
+  for (int idx = tid; idx < CBM * CPR; idx += CTHREADS) {
+    const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
+    const int m = m0 + row, n = n0 + chn * EPC;
+    if (m < a.M && n < a.Nout) {
+      *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
+    }
+  }
+}
+
+static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
+  const int epc = dtype == DMF_BF16 ? 8 : 4;
+  DMF_CHECK_ARG(a.C % epc == 0 && a.ldx % epc == 0, "%s: input channels (%d) and stride (%d) must be multiples of %d",
+                what, a.C, a.ldx, epc);
+  DMF_CHECK_ARG(a.Nout % epc == 0 && a.ldy % epc == 0,
+                "%s: output channels (%d) and stride (%d) must be multiples of %d", what, a.Nout, a.ldy, epc);
+  DMF_CHECK_ARG(((uintptr_t)a.x % 16) == 0 && ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.w % 16) == 0,
+                "%s: pointers must be 16-byte aligned", what);
+  DMF_CHECK_ARG(a.M > 0 && a.Nout > 0 && a.Ktot > 0, "%s: empty problem (M=%d N=%d K=%d)", what, a.M, a.Nout,
+                a.Ktot);
+  a.mtiles = cdiv(a.M, CBM);
+  a.ntiles = cdiv(a.Nout, CBN);
+  const long long nblk = (long long)a.mtiles * a.ntiles;
+  DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
+  const size_t lds = 2 * STAGE_BYTES;  // 64 KB; C staging (<= 128*132*4) reuses it
+  const size_t lds_c = (size_t)CBM * (CBN + (dtype == DMF_BF16 ? 8 : 4)) * (dtype == DMF_BF16 ? 2 : 4);
+  const size_t lds_total = lds > lds_c ? lds : lds_c;
+  if (dtype == DMF_BF16) {
+    if (dgrad)
+      hipLaunchKernelGGL((k_conv_igemm<bf16_t, true>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+    else
+      hipLaunchKernelGGL((k_conv_igemm<bf16_t, false>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+  } else {
+    if (dgrad)
+      hipLaunchKernelGGL((k_conv_igemm<float, true>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+    else
+      hipLaunchKernelGGL((k_conv_igemm<float, false>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+  }
+  DMF_LAUNCH_CHECK(what);
+  return 0;
+}
+
+// ------------------------------------------------------- weight re-layout
+// torch Conv2d weight [Cout][Cin][KH][KW] (fp32 master) ->
+//   mode 0: [Cout][KH][KW][CinP]   (forward B operand, zero-padded channels)
+//   mode 1: [CinP][KH][KW][Cout]   (dgrad B operand)
+template <typename T>
+__global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, int Cout, int Cin, int CinP, int KH,
+                              int KW, int mode) {
+  const long long total = (long long)Cout * CinP * KH * KW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int co, ci, r, s;
+    if (mode == 0) {
+      ci = (int)(i % CinP);
+      long long t = i / CinP;
+      s = (int)(t % KW); t /= KW;
+      r = (int)(t % KH);
+      co = (int)(t / KH);
+    } else {
+      co = (int)(i % Cout);
+      long long t = i / Cout;
+      s = (int)(t % KW); t /= KW;
+      r = (int)(t % KH);
+      ci = (int)(t / KH);
+    }
+    const float v = ci < Cin ? w[(((long long)co * Cin + ci) * KH + r) * KW + s] : 0.f;
+    out[i] = Cvt<T>::store(v);
+  }
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_conv_m_tile(void) { return CBM; }
+
+extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                              int KH, int KW, int stride, int pad, int dil, const float* bias, void* y, int Ho, int Wo,
+                              int ldy, float* bn_partials, int act, void* stream) {
+  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_fwd: bad dtype %d", dtype);
+  DMF_CHECK_ARG(stride >= 1 && dil >= 1 && KH >= 1 && KW >= 1, "dmf_conv2d_fwd: bad geometry");
+  DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
+                "dmf_conv2d_fwd: output size %dx%d inconsistent with input %dx%d k%d s%d p%d d%d", Ho, Wo, H, W, KH,
+                stride, pad, dil);
+  ConvArgs a{};
+  a.x = x; a.w = w; a.bias = bias; a.y = y; a.partials = bn_partials;
+  a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = ldx;
+  a.Ho = Ho; a.Wo = Wo; a.ldy = ldy; a.Nout = Cout;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
+  a.Ktot = KH * KW * Cin;
+  a.M = N * Ho * Wo;
+  a.act = act;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd");
+}
+
+extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,
+                                int Cin, int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx,
+                                void* stream) {
+  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_dgrad: bad dtype %d", dtype);
+  DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
+                "dmf_conv2d_dgrad: geometry mismatch");
+  ConvArgs a{};
+  a.x = dy; a.w = wt; a.bias = nullptr; a.y = dx; a.partials = nullptr;
+  a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.ldx = lddy;
+  a.Ho = H; a.Wo = W; a.ldy = lddx; a.Nout = Cin;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
+  a.Ktot = KH * KW * Cout;
+  a.M = N * H * W;
+  a.act = DMF_ACT_NONE;
+  return launch_conv(dtype, true, a, (hipStream_t)stream, "dmf_conv2d_dgrad");
+}
+
+extern "C" int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW,
+                                    int mode, void* stream) {
+  DMF_CHECK_ARG(CinP >= Cin && (mode == 0 || mode == 1), "dmf_conv_weight_prep: bad args");
+  const long long total = (long long)Cout * CinP * KH * KW;
+  const int grid = (int)(total < 65536 * 256LL ? cdiv(total, 256) : 65536);
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_weight_prep<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)out, Cout,
+                       Cin, CinP, KH, KW, mode);
+  else
+    hipLaunchKernelGGL(k_weight_prep<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, (float*)out, Cout, Cin,
+                       CinP, KH, KW, mode);
+  DMF_LAUNCH_CHECK("dmf_conv_weight_prep");
+  return 0;
+}

@@ -1,0 +1,520 @@
+// Weight gradient of the implicit-GEMM convolution (NHWC), split over the
+// pixel (reduction) axis into fp32 slabs that dmf_conv2d_wgrad_reduce sums
+// deterministically into the torch-layout [Cout][Cin][KH][KW] gradient.
+//   dW[co][(r,s,ci)] = sum_{m=(n,ho,wo)} dY[m][co] * X[n, ho*st-pad+r*dil, wo*st-pad+s*dil, ci]
+// GEMM: M' = Cout, N' = KH*KW*Cin, K' = pixels. Both operands are
+// pixel-major in HBM, so tiles are loaded along channels (16-B vectors,
+// coalesced) and transposed into K'-contiguous LDS rows on the way in; the
+// MFMA core is the same 128x128 / 4-wave / 16x16 fragment layout as conv.hip.
+// Also: small-shape convolution kernels for the single-channel heads
+// (ReconHead's 3x3 conv to recon_ch=1, MaskHeadResize.out 1x1 to 1 channel,
+// model_module.py:117, :187) and the 1-input-channel 1x1 convs
+// (MaskGuidedSpatialAttention.mask_processor[0], Projector on r1/r2,
+// model_module.py:68, :639-640).
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_w;
+typedef __attribute__((ext_vector_type(4))) float f32x4_w;
+
+struct WgArgs {
+  const void* x;   // input NHWC [N][H][W][ldx]
+  const void* dy;  // grad out NHWC [N][Ho][Wo][lddy]
+  float* ws;       // slabs [splits][Cout][Ktot]
+  int N, H, W, Cin, ldx;
+  int Ho, Wo, Cout, lddy;
+  int KH, KW, stride, pad, dil;
+  int Ktot, M;  // Ktot = KH*KW*Cin, M = N*Ho*Wo
+  int mtiles, ntiles, splits, pix_per_split;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
+  constexpr int EPC = 16 / sizeof(T);
+  constexpr int BK = 8 * EPC;  // pixels per k-step
+  constexpr int ROWB = 128;    // bytes per LDS row (BK elements)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tile = blockIdx.x;
+  const int mt = tile / a.ntiles, nt = tile % a.ntiles;
+  const int split = blockIdx.y;
+  const int co0 = mt * 128, k0 = nt * 128;
+  const int p_begin = split * a.pix_per_split;
+  const int p_end = min(a.M, p_begin + a.pix_per_split);
+  const T* __restrict__ X = (const T*)a.x;
+  const T* __restrict__ DY = (const T*)a.dy;
+
+  // loader: 128 channels = 128/EPC chunks per pixel row; BK pixel rows
+  constexpr int CPR = 128 / EPC;            // chunks per pixel (16 bf16, 32 f32)
+  constexpr int LOADS = BK * CPR / 256;     // per thread per operand (4 both)
+  const int chunk = tid % CPR;
+  const int prow = tid / CPR;               // 0 .. 256/CPR-1
+  constexpr int PSTEP = 256 / CPR;
+
+  // B' column chunk -> tap, ci (fixed per thread)
+  const int kcol = k0 + chunk * EPC;
+  const bool kok = kcol < a.Ktot;
+  const int tap = kok ? kcol / a.Cin : 0;
+  const int ci = kcol - tap * a.Cin;
+  const int r = tap / a.KW, s = tap % a.KW;
+  const int cocol = co0 + chunk * EPC;
+  const bool cook = cocol < a.Cout;
+
+  T ra[LOADS][EPC], rb[LOADS][EPC];
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int p = p0 + prow + PSTEP * i;
+      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+      if (p < p_end) {
+        if (cook) va = *(const uint4*)(DY + (size_t)p * a.lddy + cocol);
+        if (kok) {
+          const int hw = a.Ho * a.Wo;
+          const int n = p / hw, rem = p - n * hw;
+          const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+          const int hi = ho * a.stride - a.pad + r * a.dil, wi = wo * a.stride - a.pad + s * a.dil;
+          if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
+            vb = *(const uint4*)(X + ((size_t)(n * a.H + hi) * a.W + wi) * a.ldx + ci);
+        }
+      }
+      *(uint4*)ra[i] = va;
+      *(uint4*)rb[i] = vb;
+    }
+  };
+  // transpose store: element (channel row cr, pixel col pc) at
+  // row*128 + ((pc/EPC) ^ (row&7))*16 + (pc%EPC)*sizeof(T)
+  auto lds_store = [&](int stage) {
+    char* As = smem + stage * 2 * 128 * ROWB;
+    char* Bs = As + 128 * ROWB;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int pc = prow + PSTEP * i;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        const int row = chunk * EPC + e;
+        const int off = row * ROWB + (((pc / EPC) ^ (row & 7)) << 4) + (pc % EPC) * (int)sizeof(T);
+        *(T*)(As + off) = ra[i][e];
+        *(T*)(Bs + off) = rb[i][e];
+      }
+    }
+  };
+
+  f32x4_w acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p_end - p_begin + BK - 1) / BK;
+  if (nk > 0) {
+    gload(p_begin);
+    lds_store(0);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(p_begin + (kt + 1) * BK);
+    const char* As = smem + cur * 2 * 128 * ROWB;
+    const char* Bs = As + 128 * ROWB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fg;
+      uint4 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        av[i] = *(const uint4*)(As + row * ROWB + ((ch ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + fr;
+        bv[j] = *(const uint4*)(Bs + col * ROWB + ((ch ^ (col & 7)) << 4));
+      }
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_w*)&av[i], *(bf16x8_w*)&bv[j], acc[i][j],
+                                                                0, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(((const uint32_t*)&av[i])[e]),
+                                                               __uint_as_float(((const uint32_t*)&bv[j])[e]),
+                                                               acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) lds_store(cur ^ 1);
+    __syncthreads();
+  }
+  // store slab: rows = co, cols = k
+  float* slab = a.ws + (size_t)split * a.Cout * a.Ktot;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = co0 + wm * 64 + i * 16 + fg * 4 + q;
+        const int k = k0 + wn * 64 + j * 16 + fr;
+        if (co < a.Cout && k < a.Ktot) slab[(size_t)co * a.Ktot + k] = acc[i][j][q];
+      }
+}
+
+// sum slabs, reorder [Cout][KH][KW][CinP] -> torch [Cout][Cin][KH][KW], accumulate
+__global__ void k_wgrad_reduce(const float* __restrict__ ws, int splits, int Cout, int Cin, int CinP, int KH, int KW,
+                               float* __restrict__ dw, int accumulate) {
+  const long long total = (long long)Cout * Cin * KH * KW;
+  const long long slab = (long long)Cout * KH * KW * CinP;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(i % KW);
+    long long t = i / KW;
+    const int r = (int)(t % KH); t /= KH;
+    const int ci = (int)(t % Cin);
+    const int co = (int)(t / Cin);
+    const long long src = (((long long)co * KH + r) * KW + s) * CinP + ci;
+    float v = 0.f;
+    for (int sp = 0; sp < splits; ++sp) v += ws[sp * slab + src];
+    dw[i] = accumulate ? dw[i] + v : v;
+  }
+}
+
+// --------------------------------------------------- single-output-channel
+// y[m] = sum_{r,s,ci} x[n, ho*st-pad+r*dil, wo*st-pad+s*dil, ci] * w[(r,s,ci)] + b
+// one 16-lane group per output pixel
+template <typename T>
+__global__ void k_conv_cout1(const T* __restrict__ x, int N, int H, int W, int Cin, int ldx,
+                             const float* __restrict__ w, const float* __restrict__ bias, int KH, int KW, int stride,
+                             int pad, int dil, T* __restrict__ y, int Ho, int Wo, int ldy, int act) {
+  const int g = threadIdx.x & 15;
+  const long long m = (long long)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4);
+  const long long M = (long long)N * Ho * Wo;
+  float acc = 0.f;
+  if (m < M) {
+    const int n = (int)(m / (Ho * Wo));
+    const int rem = (int)(m - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem % Wo;
+    for (int r = 0; r < KH; ++r) {
+      const int hi = ho * stride - pad + r * dil;
+      if (hi < 0 || hi >= H) continue;
+      for (int s = 0; s < KW; ++s) {
+        const int wi = wo * stride - pad + s * dil;
+        if (wi < 0 || wi >= W) continue;
+        const T* px = x + ((size_t)(n * H + hi) * W + wi) * ldx;
+        const float* pw = w + (size_t)(r * KW + s) * Cin;
+        for (int c = g; c < Cin; c += 16) acc += ld(px + c) * pw[c];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  if (m < M && g == 0) {
+    float v = acc + (bias ? bias[0] : 0.f);
+    if (act == DMF_ACT_GELU) v = gelu_f(v);
+    else if (act == DMF_ACT_SIGMOID) v = sigmoid_f(v);
+    else if (act == DMF_ACT_RELU) v = fmaxf(v, 0.f);
+    st(y + m * ldy, v);
+  }
+}
+
+// dx[n,h,w,ci] = sum_{r,s} dy[n,(h+pad-r*dil)/st,(w+pad-s*dil)/st] * w[(r,s,ci)]
+template <typename T>
+__global__ void k_conv_cout1_dgrad(const T* __restrict__ dy, int lddy, const float* __restrict__ w, int N, int H,
+                                   int W, int Cin, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo,
+                                   T* __restrict__ dx, int lddx) {
+  const long long total = (long long)N * H * W * Cin;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Cin);
+    const long long pix = i / Cin;
+    const int n = (int)(pix / (H * W));
+    const int rem = (int)(pix - (long long)n * H * W);
+    const int h = rem / W, wq = rem % W;
+    float acc = 0.f;
+    for (int r = 0; r < KH; ++r) {
+      const int hn = h + pad - r * dil;
+      if (hn < 0 || hn % stride) continue;
+      const int ho = hn / stride;
+      if (ho >= Ho) continue;
+      for (int s = 0; s < KW; ++s) {
+        const int wn = wq + pad - s * dil;
+        if (wn < 0 || wn % stride) continue;
+        const int wo = wn / stride;
+        if (wo >= Wo) continue;
+        acc += ld(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy) * w[(size_t)(r * KW + s) * Cin + ci];
+      }
+    }
+    st(dx + pix * lddx + ci, acc);
+  }
+}
+
+// dw[(r,s,ci)] partial over a pixel chunk: block = (tap-chunk of 256 columns, split)
+template <typename T>
+__global__ void k_conv_cout1_wgrad(const T* __restrict__ x, int N, int H, int W, int Cin, int ldx,
+                                   const T* __restrict__ dy, int lddy, int KH, int KW, int stride, int pad, int dil,
+                                   int Ho, int Wo, int ppsplit, float* __restrict__ ws, float* __restrict__ dbias_ws) {
+  const int K = KH * KW * Cin;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long M = (long long)N * Ho * Wo;
+  const long long p0 = (long long)blockIdx.y * ppsplit;
+  const long long p1 = min(M, p0 + ppsplit);
+  float acc = 0.f, accb = 0.f;
+  const bool kok = k < K;
+  const int tap = kok ? k / Cin : 0, ci = k - tap * Cin, r = tap / KW, s = tap % KW;
+  for (long long p = p0; p < p1; ++p) {
+    const int n = (int)(p / (Ho * Wo));
+    const int rem = (int)(p - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem % Wo;
+    const float g = ld(dy + p * lddy);
+    accb += g;
+    if (kok) {
+      const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + s * dil;
+      if (hi >= 0 && hi < H && wi >= 0 && wi < W) acc += g * ld(x + ((size_t)(n * H + hi) * W + wi) * ldx + ci);
+    }
+  }
+  if (kok) ws[(size_t)blockIdx.y * K + k] = acc;
+  if (dbias_ws && blockIdx.x == 0 && threadIdx.x == 0) dbias_ws[blockIdx.y] = accb;
+}
+
+__global__ void k_sum_splits(const float* __restrict__ ws, int splits, int K, float* __restrict__ out, int accumulate) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += ws[(size_t)s * K + k];
+  out[k] = accumulate ? out[k] + v : v;
+}
+
+// ----------------------------------------------------- single input channel
+// y[m][co] = x[m] * w[co] + b[co] (optionally with activation)
+template <typename T>
+__global__ void k_conv_cin1(const T* __restrict__ x, int ldx, const float* __restrict__ w, const float* __restrict__ b,
+                            T* __restrict__ y, int ldy, long long M, int Cout, int act) {
+  const long long total = M * Cout;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / Cout;
+    const int c = (int)(i - m * Cout);
+    float v = ld(x + m * ldx) * w[c] + (b ? b[c] : 0.f);
+    if (act == DMF_ACT_GELU) v = gelu_f(v);
+    else if (act == DMF_ACT_RELU) v = fmaxf(v, 0.f);
+    else if (act == DMF_ACT_SIGMOID) v = sigmoid_f(v);
+    st(y + m * ldy + c, v);
+  }
+}
+
+// dx[m] = sum_c dy[m][c] w[c]; one 64-lane wave per row
+template <typename T>
+__global__ void k_conv_cin1_dgrad(const T* __restrict__ dy, int lddy, const float* __restrict__ w, T* __restrict__ dx,
+                                  int lddx, long long M, int Cout) {
+  const int lane = threadIdx.x & 63;
+  const long long m = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float acc = 0.f;
+  for (int c = lane; c < Cout; c += 64) acc += ld(dy + m * lddy + c) * w[c];
+  acc = wave_sum(acc);
+  if (lane == 0) st(dx + m * lddx, acc);
+}
+
+// dw partial per row-tile: ws[tile][c] = sum_{m in tile} dy[m][c]*x[m]; db similarly
+template <typename T>
+__global__ void k_conv_cin1_wgrad(const T* __restrict__ x, int ldx, const T* __restrict__ dy, int lddy, long long M,
+                                  int Cout, float* __restrict__ ws, float* __restrict__ wsb) {
+  const int c = threadIdx.x;
+  const long long m0 = (long long)blockIdx.x * 256;
+  if (c >= Cout) return;
+  float a = 0.f, b = 0.f;
+  for (int r = 0; r < 256; ++r) {
+    const long long m = m0 + r;
+    if (m >= M) break;
+    const float g = ld(dy + m * lddy + c);
+    a += g * ld(x + m * ldx);
+    b += g;
+  }
+  ws[(size_t)blockIdx.x * Cout + c] = a;
+  if (wsb) wsb[(size_t)blockIdx.x * Cout + c] = b;
+}
+
+static inline int gsz(long long n) {
+  long long g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M) {
+  (void)dtype;
+  const long long tiles = (long long)cdiv(Cout, 128) * cdiv((long long)KH * KW * Cin, 128);
+  long long want = (1024 + tiles - 1) / tiles;      // aim for ~1024 blocks
+  long long maxs = (M + 1023) / 1024;              // >= 1024 pixels per split
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  if (want > 512) want = 512;
+  return (int)want;
+}
+
+extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy,
+                                int Ho, int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad, int dil,
+                                int splits, float* workspace, void* stream) {
+  const int epc = dtype == DMF_BF16 ? 8 : 4;
+  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_wgrad: bad dtype");
+  DMF_CHECK_ARG(Cin % epc == 0 && ldx % epc == 0 && Cout % epc == 0 && lddy % epc == 0,
+                "dmf_conv2d_wgrad: channel counts/strides must be multiples of %d (Cin=%d Cout=%d)", epc, Cin, Cout);
+  DMF_CHECK_ARG(splits >= 1 && workspace, "dmf_conv2d_wgrad: bad workspace");
+  DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
+                "dmf_conv2d_wgrad: geometry mismatch");
+  WgArgs a{};
+  a.x = x; a.dy = dy; a.ws = workspace;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ldx = ldx;
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.lddy = lddy;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
+  a.Ktot = KH * KW * Cin;
+  a.M = N * Ho * Wo;
+  a.mtiles = cdiv(Cout, 128);
+  a.ntiles = cdiv(a.Ktot, 128);
+  a.splits = splits;
+  const int bk = 8 * epc;
+  a.pix_per_split = cdiv(cdiv(a.M, splits), bk) * bk;
+  dim3 grid(a.mtiles * a.ntiles, splits);
+  const size_t lds = 2 * 2 * 128 * 128;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_wgrad<bf16_t>, grid, dim3(256), lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(k_conv_wgrad<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
+  DMF_LAUNCH_CHECK("dmf_conv2d_wgrad");
+  return 0;
+}
+
+extern "C" int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int Cout, int Cin, int CinP, int KH, int KW,
+                                       float* dw, int accumulate, void* stream) {
+  DMF_CHECK_ARG(workspace && dw && splits >= 1 && CinP >= Cin, "dmf_conv2d_wgrad_reduce: bad args");
+  const long long total = (long long)Cout * Cin * KH * KW;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, workspace, splits, Cout, Cin,
+                     CinP, KH, KW, dw, accumulate);
+  DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");
+  return 0;
+}
+
+extern "C" int dmf_conv_cout1_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const float* w,
+                                  const float* bias, int KH, int KW, int stride, int pad, int dil, void* y, int Ho,
+                                  int Wo, int ldy, int act, void* stream) {
+  DMF_CHECK_ARG(x && w && y, "dmf_conv_cout1_fwd: null pointer");
+  const long long M = (long long)N * Ho * Wo;
+  if (M == 0) return 0;
+  const int grid = (int)((M + 15) / 16);
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cout1<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
+                       Cin, ldx, w, bias, KH, KW, stride, pad, dil, (bf16_t*)y, Ho, Wo, ldy, act);
+  else
+    hipLaunchKernelGGL(k_conv_cout1<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
+                       Cin, ldx, w, bias, KH, KW, stride, pad, dil, (float*)y, Ho, Wo, ldy, act);
+  DMF_LAUNCH_CHECK("dmf_conv_cout1_fwd");
+  return 0;
+}
+
+extern "C" int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const float* w, int N, int H, int W, int Cin,
+                                    int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, void* dx, int lddx,
+                                    void* stream) {
+  DMF_CHECK_ARG(dy && w && dx, "dmf_conv_cout1_dgrad: null pointer");
+  const long long total = (long long)N * H * W * Cin;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cout1_dgrad<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (bf16_t*)dx, lddx);
+  else
+    hipLaunchKernelGGL(k_conv_cout1_dgrad<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (float*)dx, lddx);
+  DMF_LAUNCH_CHECK("dmf_conv_cout1_dgrad");
+  return 0;
+}
+
+extern "C" int dmf_conv_cout1_wgrad_splits(long long M) {
+  long long s = (M + 511) / 512;
+  if (s > 256) s = 256;
+  return (int)(s < 1 ? 1 : s);
+}
+
+// ws: [splits][KH*KW*Cin] + [splits] (bias partials); dw (layout [KH][KW][Cin]) and db accumulate
+extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy,
+                                    int lddy, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits,
+                                    float* workspace, float* dw, float* db, void* stream) {
+  DMF_CHECK_ARG(x && dy && workspace && splits >= 1, "dmf_conv_cout1_wgrad: bad args");
+  const long long M = (long long)N * Ho * Wo;
+  const int K = KH * KW * Cin;
+  const int pps = (int)((M + splits - 1) / splits);
+  dim3 grid(cdiv(K, 256), splits);
+  float* wsb = workspace + (size_t)splits * K;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cout1_wgrad<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
+                       Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+  else
+    hipLaunchKernelGGL(k_conv_cout1_wgrad<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
+                       Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+  DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad");
+  if (dw) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, workspace, splits, K, dw, 1);
+  if (db) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, (hipStream_t)stream, wsb, splits, 1, db, 1);
+  DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad(reduce)");
+  return 0;
+}
+
+extern "C" int dmf_conv_cin1_fwd(int dtype, const void* x, int ldx, const float* w, const float* bias, void* y, int ldy,
+                                 long long M, int Cout, int act, void* stream) {
+  DMF_CHECK_ARG(x && w && y, "dmf_conv_cin1_fwd: null pointer");
+  if (M == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cin1<bf16_t>, dim3(gsz(M * Cout)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, w, bias, (bf16_t*)y, ldy, M, Cout, act);
+  else
+    hipLaunchKernelGGL(k_conv_cin1<float>, dim3(gsz(M * Cout)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       ldx, w, bias, (float*)y, ldy, M, Cout, act);
+  DMF_LAUNCH_CHECK("dmf_conv_cin1_fwd");
+  return 0;
+}
+
+extern "C" int dmf_conv_cin1_dgrad(int dtype, const void* dy, int lddy, const float* w, void* dx, int lddx, long long M,
+                                   int Cout, void* stream) {
+  DMF_CHECK_ARG(dy && w && dx, "dmf_conv_cin1_dgrad: null pointer");
+  if (M == 0) return 0;
+  const int grid = (int)((M + 3) / 4);
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cin1_dgrad<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       lddy, w, (bf16_t*)dx, lddx, M, Cout);
+  else
+    hipLaunchKernelGGL(k_conv_cin1_dgrad<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
+                       w, (float*)dx, lddx, M, Cout);
+  DMF_LAUNCH_CHECK("dmf_conv_cin1_dgrad");
+  return 0;
+}
+
+extern "C" int dmf_conv_cin1_wgrad_tiles(long long M) { return (int)((M + 255) / 256); }
+
+// ws: [tiles][Cout] (+[tiles][Cout] for bias); dw/db accumulate
+extern "C" int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void* dy, int lddy, long long M, int Cout,
+                                   float* workspace, float* dw, float* db, void* stream) {
+  DMF_CHECK_ARG(x && dy && workspace && Cout <= 256, "dmf_conv_cin1_wgrad: bad args (Cout<=256)");
+  const int tiles = (int)((M + 255) / 256);
+  float* wsb = db ? workspace + (size_t)tiles * Cout : nullptr;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_conv_cin1_wgrad<bf16_t>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, (const bf16_t*)dy, lddy, M, Cout, workspace, wsb);
+  else
+    hipLaunchKernelGGL(k_conv_cin1_wgrad<float>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       (const float*)dy, lddy, M, Cout, workspace, wsb);
+  DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad");
+  // reduce tiles: treat [tiles][Cout] as splits x K
+  if (dw) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(Cout, 256)), dim3(256), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1);
+  if (db) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(Cout, 256)), dim3(256), 0, (hipStream_t)stream, wsb, tiles, Cout, db, 1);
+  DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad(reduce)");
+  return 0;
+}

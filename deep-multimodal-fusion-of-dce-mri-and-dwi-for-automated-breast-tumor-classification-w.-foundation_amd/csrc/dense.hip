@@ -1,0 +1,632 @@
+// Token-level pieces of the DCE x DWI cross-modal fusion op
+// (FusionModel.forward, model_module.py:919-1000) and the small dense layers
+// around it, fp32 throughout (B x 16 tokens x 128 channels -- latency-bound):
+//   - small GEMM with transposes + bias + activation (nn.Linear fwd/bwd,
+//     SE excitation MLPs on pooled vectors, MHA in/out projections)
+//   - LayerNorm fwd/bwd (CrossAttentionBlock.attn_ffn[0], :808)
+//   - multi-head attention core for short sequences (nn.MultiheadAttention,
+//     :806/:816; head-averaged weights as need_weights=True returns)
+//   - adaptive average pooling of a map into Hp x Wp tokens (_to_tokens,
+//     :903-917) and its transpose
+//   - the gated combine fused = g0*p_dwi + g1*p_dce + bilinear_up(attn tokens)
+//     (:952-973) with its backward
+//   - GatingAttention (:745-780): softmax(Linear(cat(pvec_dwi, pvec_dce,
+//     mean(mask_dwi), mean(mask_dce))))
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+static inline int gsz(long long n, int b = 256) {
+  long long g = (n + b - 1) / b;
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+__device__ __forceinline__ float actf(int act, float z) {
+  switch (act) {
+    case DMF_ACT_RELU: return fmaxf(z, 0.f);
+    case DMF_ACT_GELU: return gelu_f(z);
+    case DMF_ACT_SIGMOID: return sigmoid_f(z);
+    default: return z;
+  }
+}
+
+// C = alpha*op(A)op(B) + beta*C + bias ; then act
+__global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, float alpha,
+                                               const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                               int ldb, float beta, float* __restrict__ C, int ldc,
+                                               const float* __restrict__ bias, int act) {
+  __shared__ float As[16][65], Bs[16][65];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+      const int kk = i / 64, mm = i % 64;
+      const int m = m0 + mm, k = k0 + kk;
+      float va = 0.f;
+      if (m < M && k < K) va = tA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k];
+      As[kk][mm] = va;
+      const int n = n0 + mm;
+      float vb = 0.f;
+      if (n < N && k < K) vb = tB ? B[(size_t)n * ldb + k] : B[(size_t)k * ldb + n];
+      Bs[kk][mm] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
+      if (m < M && n < N) {
+        float v = alpha * acc[i][j];
+        if (beta != 0.f) v += beta * C[(size_t)m * ldc + n];
+        if (bias) v += bias[n];
+        C[(size_t)m * ldc + n] = actf(act, v);
+      }
+    }
+}
+
+// column sums: out[n] (+)= sum_m X[m][n]
+__global__ void k_colsum(const float* __restrict__ X, int ldx, int M, int N, float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (n < N)
+    for (int m = rl; m < M; m += 4) s += X[(size_t)m * ldx + n];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    out[n] = accumulate ? out[n] + v : v;
+  }
+}
+
+// elementwise activation backward on fp32: dx = dy * act'(z)  (z = pre-activation)
+__global__ void k_act_grad_f32(const float* __restrict__ dy, const float* __restrict__ z, float* __restrict__ dx,
+                               long long n, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = z[i];
+    float g;
+    switch (act) {
+      case DMF_ACT_RELU: g = v > 0.f ? 1.f : 0.f; break;
+      case DMF_ACT_GELU: g = gelu_grad_f(v); break;
+      case DMF_ACT_SIGMOID: { const float s = sigmoid_f(v); g = s * (1.f - s); break; }
+      default: g = 1.f;
+    }
+    dx[i] = dy[i] * g;
+  }
+}
+
+// --------------------------------------------------------------- LayerNorm
+__global__ void k_layernorm(const float* __restrict__ x, int R, int E, const float* __restrict__ g,
+                            const float* __restrict__ b, float eps, float* __restrict__ y, float* __restrict__ save) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* px = x + (size_t)r * E;
+  float s = 0.f;
+  for (int i = lane; i < E; i += 64) s += px[i];
+  const float mean = wave_sum(s) / E;
+  float q = 0.f;
+  for (int i = lane; i < E; i += 64) { const float d = px[i] - mean; q += d * d; }
+  const float rs = rsqrtf(wave_sum(q) / E + eps);
+  for (int i = lane; i < E; i += 64) y[(size_t)r * E + i] = (px[i] - mean) * rs * g[i] + b[i];
+  if (lane == 0 && save) { save[2 * r] = mean; save[2 * r + 1] = rs; }
+}
+
+__global__ void k_layernorm_bwd(const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ save,
+                                int R, int E, const float* __restrict__ g, float* __restrict__ dx, float* dg,
+                                float* db) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float mean = save[2 * r], rs = save[2 * r + 1];
+  const float* px = x + (size_t)r * E;
+  const float* pd = dy + (size_t)r * E;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = lane; i < E; i += 64) {
+    const float xh = (px[i] - mean) * rs;
+    const float gd = pd[i] * g[i];
+    s1 += gd;
+    s2 += gd * xh;
+    if (dg) atomicAdd(dg + i, pd[i] * xh);
+    if (db) atomicAdd(db + i, pd[i]);
+  }
+  s1 = wave_sum(s1) / E;
+  s2 = wave_sum(s2) / E;
+  for (int i = lane; i < E; i += 64) {
+    const float xh = (px[i] - mean) * rs;
+    dx[(size_t)r * E + i] = rs * (pd[i] * g[i] - s1 - xh * s2);
+  }
+}
+
+// ------------------------------------------------------ attention (short)
+// q,k,v: [B][N][ld] with head h at columns h*D..h*D+D-1. One block per (b,h);
+// requires Nq,Nk <= 64, D <= 128.
+__global__ void k_attn_fwd(const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
+                           const float* __restrict__ v, int ldv, int Nq, int Nk, int H, int D, float scale,
+                           float* __restrict__ o, int ldo, float* __restrict__ probs, float* __restrict__ avgw) {
+  __shared__ float Ks[64][129], Vs[64][129], Ps[64][65];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const float* qb = q + (size_t)b * Nq * ldq + h * D;
+  const float* kb = k + (size_t)b * Nk * ldk + h * D;
+  const float* vb = v + (size_t)b * Nk * ldv + h * D;
+  for (int i = threadIdx.x; i < Nk * D; i += blockDim.x) {
+    const int j = i / D, d = i % D;
+    Ks[j][d] = kb[(size_t)j * ldk + d];
+    Vs[j][d] = vb[(size_t)j * ldv + d];
+  }
+  __syncthreads();
+  // scores: one thread per (i, j)
+  for (int t = threadIdx.x; t < Nq * Nk; t += blockDim.x) {
+    const int i = t / Nk, j = t % Nk;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += qb[(size_t)i * ldq + d] * Ks[j][d];
+    Ps[i][j] = s * scale;
+  }
+  __syncthreads();
+  // softmax per row (one thread per row; Nk <= 64)
+  for (int i = threadIdx.x; i < Nq; i += blockDim.x) {
+    float mx = -INFINITY;
+    for (int j = 0; j < Nk; ++j) mx = fmaxf(mx, Ps[i][j]);
+    float sum = 0.f;
+    for (int j = 0; j < Nk; ++j) { const float e = __expf(Ps[i][j] - mx); Ps[i][j] = e; sum += e; }
+    const float inv = 1.f / sum;
+    for (int j = 0; j < Nk; ++j) Ps[i][j] *= inv;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < Nq * Nk; t += blockDim.x) {
+    const int i = t / Nk, j = t % Nk;
+    if (probs) probs[(((size_t)b * H + h) * Nq + i) * Nk + j] = Ps[i][j];
+    if (avgw) atomicAdd(avgw + ((size_t)b * Nq + i) * Nk + j, Ps[i][j] / H);
+  }
+  for (int t = threadIdx.x; t < Nq * D; t += blockDim.x) {
+    const int i = t / D, d = t % D;
+    float s = 0.f;
+    for (int j = 0; j < Nk; ++j) s += Ps[i][j] * Vs[j][d];
+    o[((size_t)b * Nq + i) * ldo + h * D + d] = s;
+  }
+}
+
+__global__ void k_attn_bwd(const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
+                           const float* __restrict__ v, int ldv, const float* __restrict__ probs,
+                           const float* __restrict__ dout, int lddo, int Nq, int Nk, int H, int D, float scale,
+                           float* __restrict__ dq, int lddq, float* __restrict__ dk, int lddk, float* __restrict__ dv,
+                           int lddv) {
+  __shared__ float Ps[64][65], dS[64][65];
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const float* P = probs + ((size_t)b * H + h) * Nq * Nk;
+  const float* qb = q + (size_t)b * Nq * ldq + h * D;
+  const float* kb = k + (size_t)b * Nk * ldk + h * D;
+  const float* vb = v + (size_t)b * Nk * ldv + h * D;
+  const float* gb = dout + (size_t)b * Nq * lddo + h * D;
+  for (int t = threadIdx.x; t < Nq * Nk; t += blockDim.x) Ps[t / Nk][t % Nk] = P[t];
+  __syncthreads();
+  // dP_ij = sum_d dO_id V_jd
+  for (int t = threadIdx.x; t < Nq * Nk; t += blockDim.x) {
+    const int i = t / Nk, j = t % Nk;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += gb[(size_t)i * lddo + d] * vb[(size_t)j * ldv + d];
+    dS[i][j] = s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < Nq; i += blockDim.x) {
+    float r = 0.f;
+    for (int j = 0; j < Nk; ++j) r += Ps[i][j] * dS[i][j];
+    for (int j = 0; j < Nk; ++j) dS[i][j] = Ps[i][j] * (dS[i][j] - r);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < Nq * D; t += blockDim.x) {
+    const int i = t / D, d = t % D;
+    float s = 0.f;
+    for (int j = 0; j < Nk; ++j) s += dS[i][j] * kb[(size_t)j * ldk + d];
+    dq[((size_t)b * Nq + i) * lddq + h * D + d] = s * scale;
+  }
+  for (int t = threadIdx.x; t < Nk * D; t += blockDim.x) {
+    const int j = t / D, d = t % D;
+    float sk = 0.f, sv = 0.f;
+    for (int i = 0; i < Nq; ++i) {
+      sk += dS[i][j] * qb[(size_t)i * ldq + d];
+      sv += Ps[i][j] * gb[(size_t)i * lddo + d];
+    }
+    dk[((size_t)b * Nk + j) * lddk + h * D + d] = sk * scale;
+    dv[((size_t)b * Nk + j) * lddv + h * D + d] = sv;
+  }
+}
+
+// --------------------------------------------------------------- tokens
+// tokens[b][(i*Wp+j)][c] = mean over the (H/Hp)x(W/Wp) cell; exact division required
+template <typename T>
+__global__ void k_tokens_fwd(const T* __restrict__ x, int ldx, int B, int H, int W, int C, int Hp, int Wp,
+                             float* __restrict__ tok) {
+  const long long total = (long long)B * Hp * Wp * C;
+  const int kh = H / Hp, kw = W / Wp;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    long long r = t / C;
+    const int j = (int)(r % Wp); r /= Wp;
+    const int i = (int)(r % Hp);
+    const int b = (int)(r / Hp);
+    float s = 0.f;
+    for (int a = 0; a < kh; ++a)
+      for (int e = 0; e < kw; ++e) s += ld(x + ((size_t)(b * H + i * kh + a) * W + j * kw + e) * ldx + c);
+    tok[t] = s / (float)(kh * kw);
+  }
+}
+
+template <typename T>
+__global__ void k_tokens_bwd(const float* __restrict__ dtok, int B, int H, int W, int C, int Hp, int Wp,
+                             T* __restrict__ dx, int lddx, int accumulate) {
+  const long long total = (long long)B * H * W * C;
+  const int kh = H / Hp, kw = W / Wp;
+  const float inv = 1.f / (float)(kh * kw);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    long long r = t / C;
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const int b = (int)(r / H);
+    float v = dtok[(((size_t)b * Hp + h / kh) * Wp + w / kw) * C + c] * inv;
+    T* p = dx + ((size_t)(b * H + h) * W + w) * lddx + c;
+    if (accumulate) v += ld(p);
+    st(p, v);
+  }
+}
+
+// ----------------------------------------------------------- combine
+__device__ __forceinline__ void lin_w(int o, int in, int out, int& i0, int& i1, float& l1) {
+  const float scale = (float)in / (float)out;
+  float src = (o + 0.5f) * scale - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+// y = g0*a + g1*b + bilinear(low) ; low: [B][Hp][Wp][C] fp32 (token layout), null -> no attention term
+template <typename T>
+__global__ void k_combine_fwd(const T* __restrict__ a, const T* __restrict__ bb, int ldm, const float* __restrict__ g,
+                              const float* __restrict__ low, int B, int H, int W, int C, int Hp, int Wp,
+                              T* __restrict__ y, int ldy) {
+  const long long total = (long long)B * H * W * C;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const long long pix = t / C;
+    const int n = (int)(pix / (H * W));
+    const int rem = (int)(pix - (long long)n * H * W);
+    const int h = rem / W, w = rem % W;
+    float v = g[2 * n] * ld(a + pix * ldm + c) + g[2 * n + 1] * ld(bb + pix * ldm + c);
+    if (low) {
+      int h0, h1, w0, w1;
+      float lh, lw;
+      lin_w(h, Hp, H, h0, h1, lh);
+      lin_w(w, Wp, W, w0, w1, lw);
+      const float* L = low + (size_t)n * Hp * Wp * C + c;
+      v += (1.f - lh) * ((1.f - lw) * L[(h0 * Wp + w0) * C] + lw * L[(h0 * Wp + w1) * C]) +
+           lh * ((1.f - lw) * L[(h1 * Wp + w0) * C] + lw * L[(h1 * Wp + w1) * C]);
+    }
+    st(y + pix * ldy + c, v);
+  }
+}
+
+// da = g0*dy, db = g1*dy (elementwise)
+template <typename T>
+__global__ void k_combine_bwd_maps(const T* __restrict__ dy, int lddy, const float* __restrict__ g, int HW, int C,
+                                   long long total, T* __restrict__ da, T* __restrict__ db, int ldd) {
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const long long pix = t / C;
+    const int n = (int)(pix / HW);
+    const float d = ld(dy + pix * lddy + c);
+    if (da) st(da + pix * ldd + c, g[2 * n] * d);
+    if (db) st(db + pix * ldd + c, g[2 * n + 1] * d);
+  }
+}
+
+// dg[n][0] = sum dy*a, dg[n][1] = sum dy*b ; block per sample
+template <typename T>
+__global__ void k_combine_bwd_gate(const T* __restrict__ dy, int lddy, const T* __restrict__ a,
+                                   const T* __restrict__ b, int ldm, int HW, int C, float* __restrict__ dg) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  float s0 = 0.f, s1 = 0.f;
+  const long long base = (long long)n * HW;
+  for (long long t = threadIdx.x; t < (long long)HW * C; t += blockDim.x) {
+    const long long pix = base + t / C;
+    const int c = (int)(t % C);
+    const float d = ld(dy + pix * lddy + c);
+    s0 += d * ld(a + pix * ldm + c);
+    s1 += d * ld(b + pix * ldm + c);
+  }
+  s0 = block_sum(s0, red);
+  s1 = block_sum(s1, red);
+  if (threadIdx.x == 0) { dg[2 * n] = s0; dg[2 * n + 1] = s1; }
+}
+
+// dlow[n][i][j][c] = sum over output pixels of bilinear weight * dy
+template <typename T>
+__global__ void k_combine_bwd_low(const T* __restrict__ dy, int lddy, int B, int H, int W, int C, int Hp, int Wp,
+                                  float* __restrict__ dlow) {
+  const long long total = (long long)B * Hp * Wp * C;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    long long r = t / C;
+    const int j = (int)(r % Wp); r /= Wp;
+    const int i = (int)(r % Hp);
+    const int n = (int)(r / Hp);
+    float acc = 0.f;
+    for (int h = 0; h < H; ++h) {
+      int h0, h1;
+      float lh;
+      lin_w(h, Hp, H, h0, h1, lh);
+      float wh = 0.f;
+      if (h0 == i) wh += 1.f - lh;
+      if (h1 == i) wh += lh;
+      if (wh == 0.f) continue;
+      for (int w = 0; w < W; ++w) {
+        int w0, w1;
+        float lw;
+        lin_w(w, Wp, W, w0, w1, lw);
+        float ww = 0.f;
+        if (w0 == j) ww += 1.f - lw;
+        if (w1 == j) ww += lw;
+        if (ww == 0.f) continue;
+        acc += wh * ww * ld(dy + ((size_t)(n * H + h) * W + w) * lddy + c);
+      }
+    }
+    dlow[t] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- gating
+// x = [pv_dwi (C), pv_dce (C), conf_dwi, conf_dce]; g = softmax(W x + b), 2 outputs
+__global__ void k_gate_fwd(const float* __restrict__ pa, const float* __restrict__ pb, const float* __restrict__ ca,
+                           const float* __restrict__ cb, int C, const float* __restrict__ Wt,
+                           const float* __restrict__ bias, float* __restrict__ g) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  const int In = 2 * C + (ca ? 2 : 0);
+  float z0 = 0.f, z1 = 0.f;
+  for (int i = threadIdx.x; i < In; i += blockDim.x) {
+    float x;
+    if (i < C) x = pa[n * C + i];
+    else if (i < 2 * C) x = pb[n * C + i - C];
+    else if (i == 2 * C) x = ca[n];
+    else x = cb[n];
+    z0 += Wt[i] * x;
+    z1 += Wt[In + i] * x;
+  }
+  z0 = block_sum(z0, red) + bias[0];
+  z1 = block_sum(z1, red) + bias[1];
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(z0, z1);
+    const float e0 = __expf(z0 - m), e1 = __expf(z1 - m);
+    g[2 * n] = e0 / (e0 + e1);
+    g[2 * n + 1] = e1 / (e0 + e1);
+  }
+}
+
+// dz = softmax backward; dW (+)=, db (+)=, dpa/dpb/dca/dcb written (nullable)
+__global__ void k_gate_bwd(const float* __restrict__ pa, const float* __restrict__ pb, const float* __restrict__ ca,
+                           const float* __restrict__ cb, int C, const float* __restrict__ Wt,
+                           const float* __restrict__ g, const float* __restrict__ dg, float* dW, float* db,
+                           float* __restrict__ dpa, float* __restrict__ dpb, float* __restrict__ dca,
+                           float* __restrict__ dcb) {
+  const int n = blockIdx.x;
+  const int In = 2 * C + (ca ? 2 : 0);
+  const float g0 = g[2 * n], g1 = g[2 * n + 1];
+  const float s = dg[2 * n] * g0 + dg[2 * n + 1] * g1;
+  const float dz0 = g0 * (dg[2 * n] - s), dz1 = g1 * (dg[2 * n + 1] - s);
+  for (int i = threadIdx.x; i < In; i += blockDim.x) {
+    float x;
+    if (i < C) x = pa[n * C + i];
+    else if (i < 2 * C) x = pb[n * C + i - C];
+    else if (i == 2 * C) x = ca[n];
+    else x = cb[n];
+    if (dW) {
+      atomicAdd(dW + i, dz0 * x);
+      atomicAdd(dW + In + i, dz1 * x);
+    }
+    const float dx = dz0 * Wt[i] + dz1 * Wt[In + i];
+    if (i < C) { if (dpa) dpa[n * C + i] = dx; }
+    else if (i < 2 * C) { if (dpb) dpb[n * C + i - C] = dx; }
+    else if (i == 2 * C) { if (dca) dca[n] = dx; }
+    else { if (dcb) dcb[n] = dx; }
+  }
+  if (threadIdx.x == 0 && db) {
+    atomicAdd(db, dz0);
+    atomicAdd(db + 1, dz1);
+  }
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda,
+                         const float* B, int ldb, float beta, float* C, int ldc, const float* bias, int act,
+                         void* stream) {
+  DMF_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "dmf_sgemm: bad args");
+  if (M == 0 || N == 0) return 0;
+  dim3 grid(cdiv(N, 64), cdiv(M, 64));
+  hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, (hipStream_t)stream, transA, transB, M, N, K, alpha, A, lda, B, ldb,
+                     beta, C, ldc, bias, act);
+  DMF_LAUNCH_CHECK("dmf_sgemm");
+  return 0;
+}
+
+extern "C" int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream) {
+  DMF_CHECK_ARG(X && out, "dmf_colsum_f32: bad args");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(k_colsum, dim3(cdiv(N, 64)), dim3(256), 0, (hipStream_t)stream, X, ldx, M, N, out, accumulate);
+  DMF_LAUNCH_CHECK("dmf_colsum_f32");
+  return 0;
+}
+
+extern "C" int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream) {
+  DMF_CHECK_ARG(dy && z && dx, "dmf_act_grad_f32: bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_act_grad_f32, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, dy, z, dx, n, act);
+  DMF_LAUNCH_CHECK("dmf_act_grad_f32");
+  return 0;
+}
+
+extern "C" int dmf_layernorm_fwd(const float* x, int R, int E, const float* gamma, const float* beta, float eps,
+                                 float* y, float* save, void* stream) {
+  DMF_CHECK_ARG(x && gamma && beta && y && R > 0 && E > 0, "dmf_layernorm_fwd: bad args");
+  hipLaunchKernelGGL(k_layernorm, dim3(cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, x, R, E, gamma, beta, eps, y,
+                     save);
+  DMF_LAUNCH_CHECK("dmf_layernorm_fwd");
+  return 0;
+}
+
+extern "C" int dmf_layernorm_bwd(const float* dy, const float* x, const float* save, int R, int E, const float* gamma,
+                                 float* dx, float* dgamma, float* dbeta, void* stream) {
+  DMF_CHECK_ARG(dy && x && save && gamma && dx, "dmf_layernorm_bwd: bad args");
+  hipLaunchKernelGGL(k_layernorm_bwd, dim3(cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, dy, x, save, R, E, gamma,
+                     dx, dgamma, dbeta);
+  DMF_LAUNCH_CHECK("dmf_layernorm_bwd");
+  return 0;
+}
+
+extern "C" int dmf_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, int B, int Nq,
+                            int Nk, int H, int D, float scale, float* out, int ldo, float* probs, float* avg_weights,
+                            void* stream) {
+  DMF_CHECK_ARG(q && k && v && out && Nq <= 64 && Nk <= 64 && D <= 128,
+                "dmf_attn_fwd: short-sequence kernel needs Nq,Nk<=64, D<=128 (got %d,%d,%d)", Nq, Nk, D);
+  hipLaunchKernelGGL(k_attn_fwd, dim3(B * H), dim3(256), 0, (hipStream_t)stream, q, ldq, k, ldk, v, ldv, Nq, Nk, H, D,
+                     scale, out, ldo, probs, avg_weights);
+  DMF_LAUNCH_CHECK("dmf_attn_fwd");
+  return 0;
+}
+
+extern "C" int dmf_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                            const float* probs, const float* dout, int lddo, int B, int Nq, int Nk, int H, int D,
+                            float scale, float* dq, int lddq, float* dk, int lddk, float* dv, int lddv, void* stream) {
+  DMF_CHECK_ARG(q && k && v && probs && dout && dq && dk && dv && Nq <= 64 && Nk <= 64,
+                "dmf_attn_bwd: bad args");
+  hipLaunchKernelGGL(k_attn_bwd, dim3(B * H), dim3(256), 0, (hipStream_t)stream, q, ldq, k, ldk, v, ldv, probs, dout,
+                     lddo, Nq, Nk, H, D, scale, dq, lddq, dk, lddk, dv, lddv);
+  DMF_LAUNCH_CHECK("dmf_attn_bwd");
+  return 0;
+}
+
+extern "C" int dmf_tokens_fwd(int dtype, const void* x, int ldx, int B, int H, int W, int C, int Hp, int Wp,
+                              float* tokens, void* stream) {
+  DMF_CHECK_ARG(x && tokens && Hp > 0 && Wp > 0 && H % Hp == 0 && W % Wp == 0,
+                "dmf_tokens_fwd: map %dx%d must divide into %dx%d tokens", H, W, Hp, Wp);
+  const long long total = (long long)B * Hp * Wp * C;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_tokens_fwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, B, H, W, C, Hp, Wp, tokens);
+  else
+    hipLaunchKernelGGL(k_tokens_fwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       B, H, W, C, Hp, Wp, tokens);
+  DMF_LAUNCH_CHECK("dmf_tokens_fwd");
+  return 0;
+}
+
+extern "C" int dmf_tokens_bwd(int dtype, const float* dtokens, int B, int H, int W, int C, int Hp, int Wp, void* dx,
+                              int lddx, int accumulate, void* stream) {
+  DMF_CHECK_ARG(dtokens && dx && H % Hp == 0 && W % Wp == 0, "dmf_tokens_bwd: bad args");
+  const long long total = (long long)B * H * W * C;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_tokens_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                       Hp, Wp, (bf16_t*)dx, lddx, accumulate);
+  else
+    hipLaunchKernelGGL(k_tokens_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                       Hp, Wp, (float*)dx, lddx, accumulate);
+  DMF_LAUNCH_CHECK("dmf_tokens_bwd");
+  return 0;
+}
+
+extern "C" int dmf_fusion_combine_fwd(int dtype, const void* p_dwi, const void* p_dce, int ld, const float* gates,
+                                      const float* lowres, int B, int H, int W, int C, int Hp, int Wp, void* y,
+                                      int ldy, void* stream) {
+  DMF_CHECK_ARG(p_dwi && p_dce && gates && y, "dmf_fusion_combine_fwd: bad args");
+  const long long total = (long long)B * H * W * C;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_combine_fwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, gates, lowres, B, H, W, C, Hp, Wp, (bf16_t*)y,
+                       ldy);
+  else
+    hipLaunchKernelGGL(k_combine_fwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)p_dwi,
+                       (const float*)p_dce, ld, gates, lowres, B, H, W, C, Hp, Wp, (float*)y, ldy);
+  DMF_LAUNCH_CHECK("dmf_fusion_combine_fwd");
+  return 0;
+}
+
+extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const void* p_dwi, const void* p_dce,
+                                      int ld, const float* gates, int B, int H, int W, int C, int Hp, int Wp,
+                                      void* dp_dwi, void* dp_dce, int ldd, float* dgates, float* dlowres,
+                                      void* stream) {
+  DMF_CHECK_ARG(dy && p_dwi && p_dce && gates, "dmf_fusion_combine_bwd: bad args");
+  const long long total = (long long)B * H * W * C;
+  hipStream_t st_ = (hipStream_t)stream;
+  if (dtype == DMF_BF16) {
+    if (dp_dwi || dp_dce)
+      hipLaunchKernelGGL(k_combine_bwd_maps<bf16_t>, dim3(gsz(total)), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
+                         gates, H * W, C, total, (bf16_t*)dp_dwi, (bf16_t*)dp_dce, ldd);
+    if (dgates)
+      hipLaunchKernelGGL(k_combine_bwd_gate<bf16_t>, dim3(B), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
+                         (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, H * W, C, dgates);
+    if (dlowres)
+      hipLaunchKernelGGL(k_combine_bwd_low<bf16_t>, dim3(gsz((long long)B * Hp * Wp * C)), dim3(256), 0, st_,
+                         (const bf16_t*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
+  } else {
+    if (dp_dwi || dp_dce)
+      hipLaunchKernelGGL(k_combine_bwd_maps<float>, dim3(gsz(total)), dim3(256), 0, st_, (const float*)dy, lddy, gates,
+                         H * W, C, total, (float*)dp_dwi, (float*)dp_dce, ldd);
+    if (dgates)
+      hipLaunchKernelGGL(k_combine_bwd_gate<float>, dim3(B), dim3(256), 0, st_, (const float*)dy, lddy,
+                         (const float*)p_dwi, (const float*)p_dce, ld, H * W, C, dgates);
+    if (dlowres)
+      hipLaunchKernelGGL(k_combine_bwd_low<float>, dim3(gsz((long long)B * Hp * Wp * C)), dim3(256), 0, st_,
+                         (const float*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
+  }
+  DMF_LAUNCH_CHECK("dmf_fusion_combine_bwd");
+  return 0;
+}
+
+extern "C" int dmf_gate_fwd(const float* pv_dwi, const float* pv_dce, const float* conf_dwi, const float* conf_dce,
+                            int B, int C, const float* W, const float* b, float* gates, void* stream) {
+  DMF_CHECK_ARG(pv_dwi && pv_dce && W && b && gates && ((conf_dwi == nullptr) == (conf_dce == nullptr)),
+                "dmf_gate_fwd: bad args");
+  hipLaunchKernelGGL(k_gate_fwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pv_dwi, pv_dce, conf_dwi, conf_dce, C, W,
+                     b, gates);
+  DMF_LAUNCH_CHECK("dmf_gate_fwd");
+  return 0;
+}
+
+extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const float* conf_dwi, const float* conf_dce,
+                            int B, int C, const float* W, const float* gates, const float* dgates, float* dW,
+                            float* db, float* dpv_dwi, float* dpv_dce, float* dconf_dwi, float* dconf_dce,
+                            void* stream) {
+  DMF_CHECK_ARG(pv_dwi && pv_dce && W && gates && dgates, "dmf_gate_bwd: bad args");
+  hipLaunchKernelGGL(k_gate_bwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pv_dwi, pv_dce, conf_dwi, conf_dce, C, W,
+                     gates, dgates, dW, db, dpv_dwi, dpv_dce, dconf_dwi, dconf_dce);
+  DMF_LAUNCH_CHECK("dmf_gate_bwd");
+  return 0;
+}

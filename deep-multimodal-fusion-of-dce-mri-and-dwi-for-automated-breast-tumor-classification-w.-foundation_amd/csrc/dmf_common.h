@@ -1,0 +1,114 @@
+// Shared device/host helpers for the gfx950 kernels behind include/dmf_hip.h.
+// Error model: every C-ABI entry point returns 0 on success or a negative
+// code; the message is kept in a thread-local buffer read by
+// dmf_last_error() (the Python boundary turns it into RuntimeError, never an
+// abort -- SURVEY.md 8(b) "Errors").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+namespace dmf {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+
+#define DMF_CHECK_ARG(cond, ...)                                   \
+  do {                                                             \
+    if (!(cond)) {                                                 \
+      ::dmf::set_error(__VA_ARGS__);                               \
+      return -1;                                                   \
+    }                                                              \
+  } while (0)
+
+#define DMF_LAUNCH_CHECK(what)                                     \
+  do {                                                             \
+    hipError_t e_ = hipGetLastError();                             \
+    if (e_ != hipSuccess) {                                        \
+      ::dmf::set_error("%s: launch failed: %s", what,              \
+                       hipGetErrorString(e_));                     \
+      return -2;                                                   \
+    }                                                              \
+  } while (0)
+
+// ------------------------------------------------------------ numerics
+typedef uint16_t bf16_t;  // raw storage of a bfloat16
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even, NaN preserving (hipcc lowers to v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+template <typename T> struct Cvt;
+template <> struct Cvt<float> {
+  __device__ __forceinline__ static float load(float v) { return v; }
+  __device__ __forceinline__ static float store(float v) { return v; }
+};
+template <> struct Cvt<bf16_t> {
+  __device__ __forceinline__ static float load(bf16_t v) { return bf2f(v); }
+  __device__ __forceinline__ static bf16_t store(float v) { return f2bf(v); }
+};
+template <typename T> __device__ __forceinline__ float ld(const T* p) { return Cvt<T>::load(*p); }
+template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = Cvt<T>::store(v); }
+
+// exact (erf) GELU, as torch nn.GELU() default
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// --------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// block-wide sum for blockDim.x multiple of 64 (<=1024); red needs 16 floats
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += red[i];
+  return r;
+}
+
+// ----------------------------------------------------- counter-based RNG
+// Philox-4x32-10; (seed, offset) live in device memory so captured graphs
+// draw fresh dropout masks on every replay.
+__device__ __forceinline__ void philox(uint32_t key0, uint32_t key1, uint32_t c0, uint32_t c1,
+                                       uint32_t c2, uint32_t c3, uint32_t out[4]) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ key0, n2 = hi0 ^ c3 ^ key1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    key0 += W0; key1 += W1;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace dmf

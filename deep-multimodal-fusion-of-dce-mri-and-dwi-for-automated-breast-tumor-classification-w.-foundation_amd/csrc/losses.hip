@@ -1,0 +1,351 @@
+// The fusion step's criteria (train_fusion.py:239-296) as fused
+// loss + gradient kernels. Each forward writes the scalar loss AND the
+// gradient w.r.t. its inputs for a unit upstream gradient; the autograd
+// backward rescales it by the incoming grad (dmf_scale_by).
+//   focal : LabelSmoothing (loss.py:190-213) -> SoftWeightedFocalLoss
+//           (loss.py:157-187), class weights from selector_helpers.py:25-41
+//   dice  : SoftDiceLoss (loss.py:45-62) via safe_mask_loss
+//           (train_fusion.py:747-760)
+//   recon : compute_recon_list_loss (train_fusion.py:709-744) with
+//           recon_image_loss/charbonnier (train.py:1041-1048): bilinear
+//           32->S upsample, sigmoid, clamp, sqrt((p-t)^2 + 1e-6) against the
+//           clamped channel mean of the input -- the SxS upsampled map is never
+//           materialised
+//   mimic : mimic_feat_loss (train.py:1033-1038) over batch items (Q5)
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+// one block; B rows, K <= 64 classes. labels int64.
+__global__ void k_focal(const float* __restrict__ logits, const long long* __restrict__ labels, int B, int K,
+                        float smoothing, int smooth, const float* __restrict__ cw, float gamma, float* __restrict__ loss,
+                        float* __restrict__ dlogits) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* z = logits + (size_t)b * K;
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, z[k]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += __expf(z[k] - mx);
+    const float lse = mx + __logf(se);
+    const long long y = labels[b];
+    // per-class term l_k = -t_k * w_k * (1-p_k)^g * logp_k ; d/dz via chain
+    // d l_k / d logp_j = -t_k w_k [ (1-p)^g * delta_kj  - g (1-p)^(g-1) p_k logp_k delta_kj ] (through p_k = exp(logp_k))
+    // dlogp_k/dz_j = delta_kj - p_j
+    float row = 0.f, gsum = 0.f;
+    float gk[64];
+    for (int k = 0; k < K; ++k) {
+      const float lp = z[k] - lse;
+      const float p = __expf(lp);
+      const float t = smooth ? (k == y ? 1.f - smoothing : smoothing / (float)(K - 1)) : (k == y ? 1.f : 0.f);
+      const float w = cw ? cw[k] : 1.f;
+      const float om = fmaxf(1.f - p, 0.f);
+      const float fw = powf(om, gamma);
+      row += -t * w * fw * lp;
+      // dl_k/dlogp_k
+      const float dfw = gamma > 0.f && om > 0.f ? gamma * powf(om, gamma - 1.f) : 0.f;
+      const float g = -t * w * (fw - dfw * p * lp);
+      gk[k] = g;
+      gsum += g;
+    }
+    acc += row;
+    if (dlogits) {
+      for (int j = 0; j < K; ++j) {
+        const float pj = __expf(z[j] - lse);
+        dlogits[(size_t)b * K + j] = (gk[j] - pj * gsum) / (float)B;
+      }
+    }
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) loss[0] = acc / (float)B;
+}
+
+// soft dice over [B][P] logits, target [B][P]; block per sample writes its dice,
+// then the last kernel forms the mean. grad: d/dx of 1 - mean_b dice_b
+template <typename T, typename TT>
+__global__ void k_dice_sums(const T* __restrict__ x, const TT* __restrict__ t, int P, float* __restrict__ sums) {
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  float si = 0.f, sp = 0.f, st_ = 0.f;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const float p = sigmoid_f(ld(x + (size_t)b * P + i));
+    const float tv = ld(t + (size_t)b * P + i);
+    si += p * tv;
+    sp += p;
+    st_ += tv;
+  }
+  si = block_sum(si, red);
+  sp = block_sum(sp, red);
+  st_ = block_sum(st_, red);
+  if (threadIdx.x == 0) {
+    sums[3 * b] = si;
+    sums[3 * b + 1] = sp;
+    sums[3 * b + 2] = st_;
+  }
+}
+
+template <typename T, typename TT>
+__global__ void k_dice_grad(const T* __restrict__ x, const TT* __restrict__ t, int B, int P, float eps,
+                            const float* __restrict__ sums, float* __restrict__ loss, float* __restrict__ dx) {
+  const long long total = (long long)B * P;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += (2.f * sums[3 * b] + eps) / (sums[3 * b + 1] + sums[3 * b + 2] + eps);
+    loss[0] = 1.f - s / (float)B;
+  }
+  if (!dx) return;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    const float I = sums[3 * b], U = sums[3 * b + 1] + sums[3 * b + 2];
+    const float p = sigmoid_f(ld(x + i));
+    const float tv = ld(t + i);
+    // dice = (2I+eps)/(U+eps); d dice/dp = (2t(U+eps) - (2I+eps))/(U+eps)^2
+    const float dd = (2.f * tv * (U + eps) - (2.f * I + eps)) / ((U + eps) * (U + eps));
+    dx[i] = -dd * p * (1.f - p) / (float)B;
+  }
+}
+
+// ------------------------------------------------------------ recon
+__device__ __forceinline__ void lin_r(int o, int in, int out, int& i0, int& i1, float& l1) {
+  const float scale = (float)in / (float)out;
+  float src = (o + 0.5f) * scale - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+struct ReconArgs {
+  const void* r[5];      // recon maps [B][h][w] (single channel, channel stride ldr)
+  int ldr[5];
+  int target[5];         // 0: target A, 1: target B, 2: (ca*A + cb*B)
+  int nterms;
+  const float* tA;       // [B][S][S] channel means
+  const float* tB;
+  float ca, cb;          // combination for target 2
+  int B, h, w, S;
+  float* sums;           // [5] loss sums (atomic)
+  float* grads[5];       // [B][h][w] fp32 (atomic accumulation, unit-upstream, scaled by 1/(B*S*S))
+};
+
+// block per (b, output row y); thread per output column x
+template <typename T>
+__global__ void k_recon(ReconArgs a) {
+  __shared__ float rowacc[5][2][64];  // contributions to input rows (i0, i1) for w <= 64 columns
+  __shared__ float red[16];
+  const int b = blockIdx.x / a.S, y = blockIdx.x % a.S;
+  int i0, i1;
+  float ly;
+  lin_r(y, a.h, a.S, i0, i1, ly);
+  for (int t = threadIdx.x; t < 5 * 2 * 64; t += blockDim.x) (&rowacc[0][0][0])[t] = 0.f;
+  __syncthreads();
+  const float inv_n = 1.f / ((float)a.B * a.S * a.S);
+  float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int x = threadIdx.x; x < a.S; x += blockDim.x) {
+    int j0, j1;
+    float lx;
+    lin_r(x, a.w, a.S, j0, j1, lx);
+    const size_t tp = ((size_t)b * a.S + y) * a.S + x;
+    const float tAv = a.tA ? a.tA[tp] : 0.f, tBv = a.tB ? a.tB[tp] : 0.f;
+    for (int k = 0; k < a.nterms; ++k) {
+      const T* R = (const T*)a.r[k] + (size_t)b * a.h * a.w * a.ldr[k];
+      const int ld_ = a.ldr[k];
+      const float v = (1.f - ly) * ((1.f - lx) * ld(R + (i0 * a.w + j0) * ld_) + lx * ld(R + (i0 * a.w + j1) * ld_)) +
+                      ly * ((1.f - lx) * ld(R + (i1 * a.w + j0) * ld_) + lx * ld(R + (i1 * a.w + j1) * ld_));
+      float tv = a.target[k] == 0 ? tAv : (a.target[k] == 1 ? tBv : a.ca * tAv + a.cb * tBv);
+      tv = fminf(fmaxf(tv, 0.f), 1.f);
+      const float s = sigmoid_f(v);
+      const float p = fminf(fmaxf(s, 0.f), 1.f);
+      const float d = p - tv;
+      const float q = sqrtf(d * d + 1e-6f);
+      part[k] += q;
+      // dL/dv = d/q * dsig (clamp is identity on (0,1))
+      const float g = d / q * s * (1.f - s) * inv_n;
+      atomicAdd(&rowacc[k][0][j0], (1.f - ly) * (1.f - lx) * g);
+      atomicAdd(&rowacc[k][0][j1], (1.f - ly) * lx * g);
+      atomicAdd(&rowacc[k][1][j0], ly * (1.f - lx) * g);
+      atomicAdd(&rowacc[k][1][j1], ly * lx * g);
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < a.nterms; ++k) {
+    const float s = block_sum(part[k], red);
+    if (threadIdx.x == 0) atomicAdd(a.sums + k, s);
+    if (a.grads[k])
+      for (int t = threadIdx.x; t < 2 * a.w; t += blockDim.x) {
+        const int which = t / a.w, j = t % a.w;
+        const float v = rowacc[k][which][j];
+        if (v != 0.f) atomicAdd(a.grads[k] + ((size_t)b * a.h + (which ? i1 : i0)) * a.w + j, v);
+      }
+  }
+}
+
+// ------------------------------------------------------------ mimic
+// pairs (s = items[2i], t = items[2i+1]) for i < npairs, feature map NHWC
+// [HW][C] per item; per channel cosine over HW; loss_i = mean_c(1 - clamp(cos)),
+// returns mean over pairs. Gradient only for the student item.
+template <typename T>
+__global__ void k_mimic(const T* __restrict__ f, int ldm, int HW, int C, int npairs, float eps_norm, float eps_clamp,
+                        float* __restrict__ loss, float* __restrict__ dstudent /* [npairs][HW][C] */) {
+  // block per (pair, channel)
+  __shared__ float red[16];
+  const int pr = blockIdx.x / C, c = blockIdx.x % C;
+  const T* S = f + (size_t)(2 * pr) * HW * ldm + c;
+  const T* Tt = f + (size_t)(2 * pr + 1) * HW * ldm + c;
+  float ss = 0.f, tt = 0.f, st_ = 0.f;
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    const float sv = ld(S + (size_t)p * ldm), tv = ld(Tt + (size_t)p * ldm);
+    ss += sv * sv;
+    tt += tv * tv;
+    st_ += sv * tv;
+  }
+  ss = block_sum(ss, red);
+  tt = block_sum(tt, red);
+  st_ = block_sum(st_, red);
+  const float ns = fmaxf(sqrtf(ss), eps_norm), nt = fmaxf(sqrtf(tt), eps_norm);
+  const float cos = st_ / (ns * nt);
+  const float lo = -1.f + eps_clamp, hi = 1.f - eps_clamp;
+  if (threadIdx.x == 0) atomicAdd(loss, (1.f - fminf(fmaxf(cos, lo), hi)) / (float)(C * npairs));
+  if (dstudent) {
+    const bool pass = cos > lo && cos < hi;
+    const float scale = -1.f / (float)(C * npairs);
+    const bool snorm_active = sqrtf(ss) > eps_norm;
+    for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+      float g = 0.f;
+      if (pass) {
+        const float sv = ld(S + (size_t)p * ldm), tv = ld(Tt + (size_t)p * ldm);
+        // d cos / d s_p = t_p/(ns*nt) - cos * s_p / ns^2   (if |s| > eps)
+        g = tv / (ns * nt) - (snorm_active ? cos * sv / (ns * ns) : 0.f);
+        g *= scale;
+      }
+      dstudent[((size_t)pr * HW + p) * C + c] = g;
+    }
+  }
+}
+
+__global__ void k_scale_by(const float* __restrict__ src, long long n, const float* __restrict__ s, float mul,
+                           float* __restrict__ dst) {
+  const float k = s[0] * mul;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i] * k;
+}
+
+template <typename T>
+__global__ void k_scale_by_cast(const float* __restrict__ src, long long n, const float* __restrict__ s, float mul,
+                                T* __restrict__ dst, int ldd, int C) {
+  const float k = s[0] * mul;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / C;
+    const int c = (int)(i - m * C);
+    st(dst + m * ldd + c, src[i] * k);
+  }
+}
+
+static inline int gsz(long long n) {
+  long long g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_focal_loss(const float* logits, const long long* labels, int B, int K, float smoothing,
+                              int use_smoothing, const float* class_weights, float gamma, float* loss, float* dlogits,
+                              void* stream) {
+  DMF_CHECK_ARG(logits && labels && loss && B > 0 && K > 1 && K <= 64, "dmf_focal_loss: bad args (K=%d)", K);
+  hipLaunchKernelGGL(k_focal, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, B, K, smoothing,
+                     use_smoothing, class_weights, gamma, loss, dlogits);
+  DMF_LAUNCH_CHECK("dmf_focal_loss");
+  return 0;
+}
+
+extern "C" int dmf_soft_dice(int dtype, const void* logits, const float* target, int B, int P, float eps,
+                             float* sums_ws, float* loss, float* dlogits, void* stream) {
+  DMF_CHECK_ARG(logits && target && sums_ws && loss && B > 0 && P > 0, "dmf_soft_dice: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DMF_BF16) {
+    hipLaunchKernelGGL((k_dice_sums<bf16_t, float>), dim3(B), dim3(256), 0, s, (const bf16_t*)logits, target, P,
+                       sums_ws);
+    hipLaunchKernelGGL((k_dice_grad<bf16_t, float>), dim3(gsz((long long)B * P)), dim3(256), 0, s,
+                       (const bf16_t*)logits, target, B, P, eps, sums_ws, loss, dlogits);
+  } else {
+    hipLaunchKernelGGL((k_dice_sums<float, float>), dim3(B), dim3(256), 0, s, (const float*)logits, target, P, sums_ws);
+    hipLaunchKernelGGL((k_dice_grad<float, float>), dim3(gsz((long long)B * P)), dim3(256), 0, s, (const float*)logits,
+                       target, B, P, eps, sums_ws, loss, dlogits);
+  }
+  DMF_LAUNCH_CHECK("dmf_soft_dice");
+  return 0;
+}
+
+// recon terms: up to 5 maps r_k ([B][h][w], channel stride ldr_k) against target sel_k in {0:A,1:B,2:ca*A+cb*B}.
+// sums[k] += sum of charbonnier terms (caller divides by B*S*S); grads[k] += unit-upstream grads (scaled 1/(B*S*S)).
+extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const void* r2, const void* r3,
+                              const void* r4, int ldr0, int ldr1, int ldr2, int ldr3, int ldr4, int sel0, int sel1,
+                              int sel2, int sel3, int sel4, const float* tA, const float* tB, float ca, float cb,
+                              int B, int h, int w, int S, float* sums, float* g0, float* g1, float* g2, float* g3,
+                              float* g4, void* stream) {
+  DMF_CHECK_ARG(nterms >= 1 && nterms <= 5 && sums && w <= 64 && B > 0 && S > 0, "dmf_recon_loss: bad args");
+  ReconArgs a{};
+  const void* rs[5] = {r0, r1, r2, r3, r4};
+  const int lds[5] = {ldr0, ldr1, ldr2, ldr3, ldr4};
+  const int sels[5] = {sel0, sel1, sel2, sel3, sel4};
+  float* gs[5] = {g0, g1, g2, g3, g4};
+  for (int k = 0; k < 5; ++k) {
+    a.r[k] = rs[k];
+    a.ldr[k] = lds[k];
+    a.target[k] = sels[k];
+    a.grads[k] = gs[k];
+    if (k < nterms) DMF_CHECK_ARG(rs[k] != nullptr, "dmf_recon_loss: missing map %d", k);
+  }
+  a.nterms = nterms;
+  a.tA = tA; a.tB = tB; a.ca = ca; a.cb = cb;
+  a.B = B; a.h = h; a.w = w; a.S = S;
+  a.sums = sums;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_recon<bf16_t>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(k_recon<float>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
+  DMF_LAUNCH_CHECK("dmf_recon_loss");
+  return 0;
+}
+
+extern "C" int dmf_mimic_loss(int dtype, const void* feats, int ld, int HW, int C, int npairs, float* loss,
+                              float* dstudent, void* stream) {
+  DMF_CHECK_ARG(feats && loss && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_mimic<bf16_t>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)feats, ld,
+                       HW, C, npairs, 1e-12f, 1e-6f, loss, dstudent);
+  else
+    hipLaunchKernelGGL(k_mimic<float>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const float*)feats, ld, HW,
+                       C, npairs, 1e-12f, 1e-6f, loss, dstudent);
+  DMF_LAUNCH_CHECK("dmf_mimic_loss");
+  return 0;
+}
+
+extern "C" int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream) {
+  DMF_CHECK_ARG(src && scalar && dst, "dmf_scale_by: bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_scale_by, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul, dst);
+  DMF_LAUNCH_CHECK("dmf_scale_by");
+  return 0;
+}
+
+extern "C" int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul,
+                                 void* dst, int ldd, void* stream) {
+  DMF_CHECK_ARG(src && scalar && dst, "dmf_scale_by_cast: bad args");
+  const long long n = M * C;
+  if (n == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_scale_by_cast<bf16_t>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
+                       (bf16_t*)dst, ldd, C);
+  else
+    hipLaunchKernelGGL(k_scale_by_cast<float>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
+                       (float*)dst, ldd, C);
+  DMF_LAUNCH_CHECK("dmf_scale_by_cast");
+  return 0;
+}

@@ -1,0 +1,674 @@
+// Memory-bound helpers of the encoder / fusion hot path (NHWC):
+//  - input staging: NCHW fp32 volume stack -> gated NHWC (SEBlock modality
+//    attention, model_module.py:25-43 used at :649-650) + per-pixel channel
+//    mean for the reconstruction target (train_fusion.py:735-737)
+//  - per-(n,c) spatial reductions (SE squeeze, GroupNorm(C,C) statistics,
+//    AdaptiveAvgPool2d(1), SE/gate gradients)
+//  - channel scaling (SE excite), GroupNorm(C,C) apply of the gated mix
+//    alpha*f_b + (1-alpha)*f (model_module.py:673-675, :688-690)
+//  - maxpool 3x3/s2/p1 (timm stem), nearest 2x upsample (AdaptiveAvgPool2d
+//    (64,64) of a 32x32 map, model_module.py:531-534, :707-710), bilinear
+//    resize (align_corners=False), column statistics for BN on non-conv inputs
+//  - MaskGuidedSpatialAttention (model_module.py:49-97) forward/backward
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+static inline int gsz(long long n, int b = 256) {
+  long long g = (n + b - 1) / b;
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
+// ---------------------------------------------------------- input staging
+template <typename T>
+__global__ void k_input_prep(const float* __restrict__ x, int N, int C, int H, int W, const float* __restrict__ gate,
+                             T* __restrict__ y, int Cp, float* __restrict__ cmean) {
+  const long long HW = (long long)H * W;
+  const long long total = (long long)N * HW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / HW, p = i - n * HW;
+    const float* src = x + n * C * HW + p;
+    T* dst = y + i * Cp;
+    float s = 0.f;
+    for (int c = 0; c < Cp; ++c) {
+      float v = 0.f;
+      if (c < C) {
+        v = src[c * HW];
+        s += v;
+        if (gate) v *= gate[n * C + c];
+      }
+      dst[c] = Cvt<T>::store(v);
+    }
+    if (cmean) cmean[i] = s / (float)C;
+  }
+}
+
+// per (n,c) mean of an NCHW fp32 tensor: block per (n,c)
+__global__ void k_nchw_mean(const float* __restrict__ x, long long HW, float* __restrict__ out) {
+  __shared__ float red[16];
+  const float* p = x + (long long)blockIdx.x * HW;
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < HW; i += blockDim.x) s += p[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = s / (float)HW;
+}
+
+// out[n][c] = scale * sum_hw a[n,hw,c] * (b ? b[n,hw,c] : 1); block = (n, 64-channel group), 4 row lanes
+template <typename T>
+__global__ void k_nhwc_reduce(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb, int HW, int C,
+                              float scale, float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x, c = blockIdx.y * 64 + cl;
+  float s = 0.f;
+  if (c < C) {
+    const T* pa = a + (long long)n * HW * lda + c;
+    const T* pb = b ? b + (long long)n * HW * ldb + c : nullptr;
+    for (int p = rl; p < HW; p += 4) {
+      const float v = ld(pa + (long long)p * lda);
+      s += pb ? v * ld(pb + (long long)p * ldb) : v;
+    }
+  }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const float r = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) * scale;
+    out[n * C + c] = accumulate ? out[n * C + c] + r : r;
+  }
+}
+
+// y = x * gate[n][c]
+template <typename T>
+__global__ void k_channel_scale(const T* __restrict__ x, int ldx, const float* __restrict__ gate,
+                                T* __restrict__ y, int ldy, long long N, int HW, int C) {
+  const long long total = N * HW * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / C;
+    const int c = (int)(i - row * C);
+    const long long n = row / HW;
+    st(y + row * ldy + c, ld(x + row * ldx + c) * gate[n * C + c]);
+  }
+}
+
+// z = sig(w)*a + (1-sig(w))*b
+template <typename T>
+__global__ void k_mix(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb, const float* __restrict__ wlogit,
+                      T* __restrict__ z, int ldz, long long M, int C) {
+  const float al = 1.f / (1.f + __expf(-wlogit[0]));
+  const long long total = M * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / C;
+    const int c = (int)(i - m * C);
+    st(z + m * ldz + c, al * ld(a + m * lda + c) + (1.f - al) * ld(b + m * ldb + c));
+  }
+}
+
+// GroupNorm(C, C): y = (z - mean[n][c]) * rsqrt(var + eps) * g[c] + b[c]; var = m2 - mean^2
+template <typename T>
+__global__ void k_gn_apply(const T* __restrict__ z, int ldz, const float* __restrict__ mean,
+                           const float* __restrict__ m2, const float* __restrict__ g, const float* __restrict__ b,
+                           float eps, T* __restrict__ y, int ldy, long long N, int HW, int C) {
+  const long long total = N * HW * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / C;
+    const int c = (int)(i - row * C);
+    const long long n = row / HW;
+    const float mu = mean[n * C + c];
+    const float var = fmaxf(m2[n * C + c] - mu * mu, 0.f);
+    const float v = (ld(z + row * ldz + c) - mu) * rsqrtf(var + eps) * g[c] + b[c];
+    st(y + row * ldy + c, v);
+  }
+}
+
+// GroupNorm(C,C) backward given per-(n,c) sums S1 = sum dy, S2 = sum dy*xhat:
+// dz = g*rstd/HW * (HW*dy - S1 - xhat*S2)
+template <typename T>
+__global__ void k_gn_bwd_apply(const T* __restrict__ dy, int lddy, const T* __restrict__ z, int ldz,
+                               const float* __restrict__ mean, const float* __restrict__ m2,
+                               const float* __restrict__ s1, const float* __restrict__ s2,
+                               const float* __restrict__ g, float eps, T* __restrict__ dz, int lddz, long long N,
+                               int HW, int C) {
+  const long long total = N * HW * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / C;
+    const int c = (int)(i - row * C);
+    const long long n = row / HW;
+    const float mu = mean[n * C + c];
+    const float rs = rsqrtf(fmaxf(m2[n * C + c] - mu * mu, 0.f) + eps);
+    const float xh = (ld(z + row * ldz + c) - mu) * rs;
+    const float v = g[c] * rs / (float)HW * ((float)HW * ld(dy + row * lddy + c) - s1[n * C + c] - xh * s2[n * C + c]);
+    st(dz + row * lddz + c, v);
+  }
+}
+
+// S2[n][c] = sum_hw dy * xhat  (xhat from z, mean, m2)
+template <typename T>
+__global__ void k_gn_bwd_reduce(const T* __restrict__ dy, int lddy, const T* __restrict__ z, int ldz,
+                                const float* __restrict__ mean, const float* __restrict__ m2, float eps, int HW, int C,
+                                float* __restrict__ s1, float* __restrict__ s2) {
+  __shared__ float red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x, c = blockIdx.y * 64 + cl;
+  float a = 0.f, q = 0.f;
+  if (c < C) {
+    const float mu = mean[n * C + c];
+    const float rs = rsqrtf(fmaxf(m2[n * C + c] - mu * mu, 0.f) + eps);
+    for (int p = rl; p < HW; p += 4) {
+      const long long row = (long long)n * HW + p;
+      const float g = ld(dy + row * lddy + c);
+      a += g;
+      q += g * (ld(z + row * ldz + c) - mu) * rs;
+    }
+  }
+  red[rl][cl][0] = a;
+  red[rl][cl][1] = q;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    s1[n * C + c] = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    s2[n * C + c] = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+  }
+}
+
+// ------------------------------------------------------------- max pool
+template <typename T>
+__global__ void k_maxpool(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y, int Ho,
+                          int Wo, int ldy, int k, int s, int p) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / (Ho * Wo));
+    const int rem = (int)(pix - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem % Wo;
+    float m = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * s - p + r;
+      if (hi < 0 || hi >= H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int wi = wo * s - p + q;
+        if (wi < 0 || wi >= W) continue;
+        const float v = ld(x + ((size_t)(n * H + hi) * W + wi) * ldx + c);
+        if (v > m || isnan(v)) m = v;
+      }
+    }
+    st(y + pix * ldy + c, m);
+  }
+}
+
+// backward: each input element receives dy of every window whose (first) argmax it is
+template <typename T>
+__global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int C, int ldx, const T* __restrict__ dy,
+                              int Ho, int Wo, int lddy, T* __restrict__ dx, int lddx, int k, int s, int p) {
+  const long long total = (long long)N * H * W * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / (H * W));
+    const int rem = (int)(pix - (long long)n * H * W);
+    const int h = rem / W, w = rem % W;
+    float g = 0.f;
+    const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
+    const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        // recompute the window argmax (first max in row-major window order)
+        float m = -INFINITY;
+        int am = -1;
+        for (int r = 0; r < k; ++r) {
+          const int hi = ho * s - p + r;
+          if (hi < 0 || hi >= H) continue;
+          for (int q = 0; q < k; ++q) {
+            const int wi = wo * s - p + q;
+            if (wi < 0 || wi >= W) continue;
+            const float v = ld(x + ((size_t)(n * H + hi) * W + wi) * ldx + c);
+            if (v > m || (isnan(v) && !isnan(m))) { m = v; am = hi * W + wi; }
+          }
+        }
+        if (am == h * W + w) g += ld(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy + c);
+      }
+    st(dx + pix * lddx + c, g);
+  }
+}
+
+// ----------------------------------------------------------- resampling
+template <typename T>
+__global__ void k_up2_nearest(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C) {
+  const long long total = (long long)N * 2 * H * 2 * W * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int wo = (int)(t % (2 * W)); t /= (2 * W);
+    const int ho = (int)(t % (2 * H));
+    const int n = (int)(t / (2 * H));
+    y[i] = x[((size_t)(n * H + ho / 2) * W + wo / 2) * ldx + c];
+  }
+}
+
+// sum of the 2x2 replicas (backward of nearest 2x upsample)
+template <typename T>
+__global__ void k_up2_nearest_bwd(const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C) {
+  const long long total = (long long)N * H * W * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float s = 0.f;
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b) s += ld(dy + ((size_t)(n * 2 * H + 2 * h + a) * 2 * W + 2 * w + b) * C + c);
+    st(dx + i, s);
+  }
+}
+
+__device__ __forceinline__ void lin_idx(int o, int in, int out, int& i0, int& i1, float& l1) {
+  const float scale = (float)in / (float)out;
+  float src = (o + 0.5f) * scale - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+// bilinear resize, align_corners=False (torch upsample_bilinear2d semantics)
+template <typename T>
+__global__ void k_bilinear(const T* __restrict__ x, int N, int Hi, int Wi, int C, int ldx, T* __restrict__ y, int Ho,
+                           int Wo, int ldy) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / (Ho * Wo));
+    const int rem = (int)(pix - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem % Wo;
+    int h0, h1, w0, w1;
+    float lh, lw;
+    lin_idx(ho, Hi, Ho, h0, h1, lh);
+    lin_idx(wo, Wi, Wo, w0, w1, lw);
+    const T* b = x + (size_t)n * Hi * Wi * ldx + c;
+    const float v = (1.f - lh) * ((1.f - lw) * ld(b + ((size_t)h0 * Wi + w0) * ldx) + lw * ld(b + ((size_t)h0 * Wi + w1) * ldx)) +
+                    lh * ((1.f - lw) * ld(b + ((size_t)h1 * Wi + w0) * ldx) + lw * ld(b + ((size_t)h1 * Wi + w1) * ldx));
+    st(y + pix * ldy + c, v);
+  }
+}
+
+// transpose of k_bilinear: dx[n,hi,wi,c] = sum over outputs of weight * dy (gather form)
+template <typename T>
+__global__ void k_bilinear_bwd(const T* __restrict__ dy, int N, int Ho, int Wo, int C, int lddy, T* __restrict__ dx,
+                               int Hi, int Wi, int lddx) {
+  const long long total = (long long)N * Hi * Wi * C;
+  const float sh = (float)Ho / (float)Hi, sw = (float)Wo / (float)Wi;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / (Hi * Wi));
+    const int rem = (int)(pix - (long long)n * Hi * Wi);
+    const int hi = rem / Wi, wi = rem % Wi;
+    // outputs whose source index lies within (hi-1, hi+1)
+    const int ho_lo = max(0, (int)floorf((hi - 1 + 0.5f) * sh - 0.5f) - 1);
+    const int ho_hi = min(Ho - 1, (int)ceilf((hi + 1 + 0.5f) * sh - 0.5f) + 1);
+    const int wo_lo = max(0, (int)floorf((wi - 1 + 0.5f) * sw - 0.5f) - 1);
+    const int wo_hi = min(Wo - 1, (int)ceilf((wi + 1 + 0.5f) * sw - 0.5f) + 1);
+    float acc = 0.f;
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      int h0, h1;
+      float lh;
+      lin_idx(ho, Hi, Ho, h0, h1, lh);
+      float wh = 0.f;
+      if (h0 == hi) wh += 1.f - lh;
+      if (h1 == hi) wh += lh;
+      if (wh == 0.f) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        int w0, w1;
+        float lw;
+        lin_idx(wo, Wi, Wo, w0, w1, lw);
+        float ww = 0.f;
+        if (w0 == wi) ww += 1.f - lw;
+        if (w1 == wi) ww += lw;
+        if (ww == 0.f) continue;
+        acc += wh * ww * ld(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy + c);
+      }
+    }
+    st(dx + pix * lddx + c, acc);
+  }
+}
+
+// column stats: partials[tile][c] = (sum, sum^2) over 256-row tiles
+template <typename T>
+__global__ void k_col_stats(const T* __restrict__ x, int ldx, long long M, int C, float* __restrict__ part) {
+  __shared__ float red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const long long r0 = (long long)blockIdx.x * 256;
+  float s = 0.f, q = 0.f;
+  if (c < C)
+    for (int r = rl; r < 256; r += 4) {
+      const long long m = r0 + r;
+      if (m >= M) break;
+      const float v = ld(x + m * ldx + c);
+      s += v;
+      q += v * v;
+    }
+  red[rl][cl][0] = s;
+  red[rl][cl][1] = q;
+  __syncthreads();
+  if (rl == 0 && c < C)
+    *(float2*)(part + ((size_t)blockIdx.x * C + c) * 2) =
+        make_float2(red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0],
+                    red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1]);
+}
+
+// ------------------------------------------ mask-guided spatial attention
+// mask m[n][p] (single channel, already at the feature resolution)
+// h[c] = w1[c]*m ; GroupNorm(1,16) over (c,p) per sample: mean = mean(w1)*mean(m),
+// E[h^2] = mean(w1^2)*mean(m^2) ; u_c = gelu((h-mu)*rs*g[c]+b[c]) ;
+// A = clamp(sig(sum_c w2[c] u_c + b2), 1e-4, 1-1e-4) ; out = f * (1 + gamma*A)
+// stats[n] = (sum m, sum m^2) computed by k_mask_stats.
+template <typename T>
+__global__ void k_mask_stats(const T* __restrict__ m, int HW, float* __restrict__ stats) {
+  __shared__ float red[16];
+  const T* p = m + (long long)blockIdx.x * HW;
+  float s = 0.f, q = 0.f;
+  for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+    const float v = ld(p + i);
+    s += v;
+    q += v * v;
+  }
+  s = block_sum(s, red);
+  q = block_sum(q, red);
+  if (threadIdx.x == 0) {
+    stats[blockIdx.x * 2] = s;
+    stats[blockIdx.x * 2 + 1] = q;
+  }
+}
+
+struct MaskAttnP {
+  const float* w1;  // [16]
+  const float* g;   // [16]
+  const float* b;   // [16]
+  const float* w2;  // [16]
+  const float* b2;  // [1]
+  const float* gamma;  // [1]
+  float eps;
+  int hid;
+};
+
+__device__ __forceinline__ void mask_attn_stats(const MaskAttnP& P, const float* stats, int n, int HW, float& mu,
+                                                float& rs) {
+  float mw = 0.f, mw2 = 0.f;
+  for (int c = 0; c < P.hid; ++c) { mw += P.w1[c]; mw2 += P.w1[c] * P.w1[c]; }
+  mw /= P.hid;
+  mw2 /= P.hid;
+  const float mm = stats[2 * n] / HW, mm2 = stats[2 * n + 1] / HW;
+  mu = mw * mm;
+  const float var = fmaxf(mw2 * mm2 - mu * mu, 0.f);
+  rs = rsqrtf(var + P.eps);
+}
+
+template <typename T>
+__global__ void k_mask_attn_fwd(const T* __restrict__ f, int ldf, const T* __restrict__ m, MaskAttnP P,
+                                const float* __restrict__ stats, T* __restrict__ out, int ldo, T* __restrict__ A_out,
+                                long long N, int HW, int C) {
+  const long long total = N * HW;
+  for (long long i = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < total;
+       i += (long long)gridDim.x * (blockDim.x / 64)) {
+    const int lane = threadIdx.x & 63;
+    const int n = (int)(i / HW);
+    float mu, rs;
+    mask_attn_stats(P, stats, n, HW, mu, rs);
+    const float mv = ld(m + i);
+    float z = P.b2[0];
+    for (int c = 0; c < P.hid; ++c) z += P.w2[c] * gelu_f((P.w1[c] * mv - mu) * rs * P.g[c] + P.b[c]);
+    float A = sigmoid_f(z);
+    A = fminf(fmaxf(A, 1e-4f), 1.f - 1e-4f);
+    const float sc = 1.f + P.gamma[0] * A;
+    for (int c = lane; c < C; c += 64) st(out + i * ldo + c, ld(f + i * ldf + c) * sc);
+    if (lane == 0 && A_out) st(A_out + i, A);
+  }
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, int W, const float* gate, void* y, int Cp,
+                              float* chan_mean, void* stream) {
+  DMF_CHECK_ARG(x && y && Cp >= C, "dmf_input_prep: bad args");
+  const long long total = (long long)N * H * W;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_input_prep<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
+                       (bf16_t*)y, Cp, chan_mean);
+  else
+    hipLaunchKernelGGL(k_input_prep<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
+                       (float*)y, Cp, chan_mean);
+  DMF_LAUNCH_CHECK("dmf_input_prep");
+  return 0;
+}
+
+extern "C" int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream) {
+  DMF_CHECK_ARG(x && out && NC > 0 && HW > 0, "dmf_nchw_mean: bad args");
+  hipLaunchKernelGGL(k_nchw_mean, dim3(NC), dim3(256), 0, (hipStream_t)stream, x, HW, out);
+  DMF_LAUNCH_CHECK("dmf_nchw_mean");
+  return 0;
+}
+
+extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C,
+                               float scale, float* out, int accumulate, void* stream) {
+  DMF_CHECK_ARG(a && out && N > 0 && HW > 0 && C > 0, "dmf_nhwc_reduce: bad args");
+  dim3 grid(N, cdiv(C, 64));
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_nhwc_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
+                       (const bf16_t*)b, ldb, HW, C, scale, out, accumulate);
+  else
+    hipLaunchKernelGGL(k_nhwc_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
+                       (const float*)b, ldb, HW, C, scale, out, accumulate);
+  DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
+  return 0;
+}
+
+extern "C" int dmf_channel_scale(int dtype, const void* x, int ldx, const float* gate, void* y, int ldy, int N, int HW,
+                                 int C, void* stream) {
+  DMF_CHECK_ARG(x && gate && y, "dmf_channel_scale: bad args");
+  const long long total = (long long)N * HW * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_channel_scale<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, gate, (bf16_t*)y, ldy, (long long)N, HW, C);
+  else
+    hipLaunchKernelGGL(k_channel_scale<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       ldx, gate, (float*)y, ldy, (long long)N, HW, C);
+  DMF_LAUNCH_CHECK("dmf_channel_scale");
+  return 0;
+}
+
+extern "C" int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb, const float* wlogit, void* z, int ldz,
+                       long long M, int C, void* stream) {
+  DMF_CHECK_ARG(a && b && wlogit && z, "dmf_mix: bad args");
+  if (M * C == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_mix<bf16_t>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
+                       (const bf16_t*)b, ldb, wlogit, (bf16_t*)z, ldz, M, C);
+  else
+    hipLaunchKernelGGL(k_mix<float>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
+                       (const float*)b, ldb, wlogit, (float*)z, ldz, M, C);
+  DMF_LAUNCH_CHECK("dmf_mix");
+  return 0;
+}
+
+extern "C" int dmf_gn_apply(int dtype, const void* z, int ldz, const float* mean, const float* m2, const float* gamma,
+                            const float* beta, float eps, void* y, int ldy, int N, int HW, int C, void* stream) {
+  DMF_CHECK_ARG(z && mean && m2 && gamma && beta && y, "dmf_gn_apply: bad args");
+  const long long total = (long long)N * HW * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_gn_apply<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)z, ldz,
+                       mean, m2, gamma, beta, eps, (bf16_t*)y, ldy, (long long)N, HW, C);
+  else
+    hipLaunchKernelGGL(k_gn_apply<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)z, ldz,
+                       mean, m2, gamma, beta, eps, (float*)y, ldy, (long long)N, HW, C);
+  DMF_LAUNCH_CHECK("dmf_gn_apply");
+  return 0;
+}
+
+extern "C" int dmf_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, const float* mean,
+                          const float* m2, const float* gamma, float eps, float* s1, float* s2, void* dz, int lddz,
+                          int N, int HW, int C, void* stream) {
+  DMF_CHECK_ARG(dy && z && mean && m2 && gamma && s1 && s2 && dz, "dmf_gn_bwd: bad args");
+  dim3 grid(N, cdiv(C, 64));
+  const long long total = (long long)N * HW * C;
+  if (dtype == DMF_BF16) {
+    hipLaunchKernelGGL(k_gn_bwd_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy, lddy,
+                       (const bf16_t*)z, ldz, mean, m2, eps, HW, C, s1, s2);
+    hipLaunchKernelGGL(k_gn_bwd_apply<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       lddy, (const bf16_t*)z, ldz, mean, m2, s1, s2, gamma, eps, (bf16_t*)dz, lddz, (long long)N, HW,
+                       C);
+  } else {
+    hipLaunchKernelGGL(k_gn_bwd_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
+                       (const float*)z, ldz, mean, m2, eps, HW, C, s1, s2);
+    hipLaunchKernelGGL(k_gn_bwd_apply<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
+                       lddy, (const float*)z, ldz, mean, m2, s1, s2, gamma, eps, (float*)dz, lddz, (long long)N, HW, C);
+  }
+  DMF_LAUNCH_CHECK("dmf_gn_bwd");
+  return 0;
+}
+
+extern "C" int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo,
+                             int ldy, int k, int s, int p, void* stream) {
+  DMF_CHECK_ARG(x && y && k > 0 && s > 0, "dmf_maxpool2d: bad args");
+  const long long total = (long long)N * Ho * Wo * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_maxpool<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
+                       W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, k, s, p);
+  else
+    hipLaunchKernelGGL(k_maxpool<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
+                       C, ldx, (float*)y, Ho, Wo, ldy, k, s, p);
+  DMF_LAUNCH_CHECK("dmf_maxpool2d");
+  return 0;
+}
+
+extern "C" int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* dy, int Ho,
+                                 int Wo, int lddy, void* dx, int lddx, int k, int s, int p, void* stream) {
+  DMF_CHECK_ARG(x && dy && dx, "dmf_maxpool2d_bwd: bad args");
+  const long long total = (long long)N * H * W * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_maxpool_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       N, H, W, C, ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, k, s, p);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N,
+                       H, W, C, ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, k, s, p);
+  DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd");
+  return 0;
+}
+
+extern "C" int dmf_upsample2x_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C,
+                                      void* stream) {
+  DMF_CHECK_ARG(x && y, "dmf_upsample2x_nearest: bad args");
+  const long long total = (long long)N * 4 * H * W * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_up2_nearest<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, (bf16_t*)y, N, H, W, C);
+  else
+    hipLaunchKernelGGL(k_up2_nearest<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       (float*)y, N, H, W, C);
+  DMF_LAUNCH_CHECK("dmf_upsample2x_nearest");
+  return 0;
+}
+
+extern "C" int dmf_upsample2x_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C,
+                                          void* stream) {
+  DMF_CHECK_ARG(dy && dx, "dmf_upsample2x_nearest_bwd: bad args");
+  const long long total = (long long)N * H * W * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_up2_nearest_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (bf16_t*)dx, N, H, W, C);
+  else
+    hipLaunchKernelGGL(k_up2_nearest_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
+                       (float*)dx, N, H, W, C);
+  DMF_LAUNCH_CHECK("dmf_upsample2x_nearest_bwd");
+  return 0;
+}
+
+extern "C" int dmf_bilinear(int dtype, const void* x, int N, int Hi, int Wi, int C, int ldx, void* y, int Ho, int Wo,
+                            int ldy, void* stream) {
+  DMF_CHECK_ARG(x && y, "dmf_bilinear: bad args");
+  const long long total = (long long)N * Ho * Wo * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_bilinear<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N,
+                       Hi, Wi, C, ldx, (bf16_t*)y, Ho, Wo, ldy);
+  else
+    hipLaunchKernelGGL(k_bilinear<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, Hi,
+                       Wi, C, ldx, (float*)y, Ho, Wo, ldy);
+  DMF_LAUNCH_CHECK("dmf_bilinear");
+  return 0;
+}
+
+extern "C" int dmf_bilinear_bwd(int dtype, const void* dy, int N, int Ho, int Wo, int C, int lddy, void* dx, int Hi,
+                                int Wi, int lddx, void* stream) {
+  DMF_CHECK_ARG(dy && dx, "dmf_bilinear_bwd: bad args");
+  const long long total = (long long)N * Hi * Wi * C;
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_bilinear_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
+                       N, Ho, Wo, C, lddy, (bf16_t*)dx, Hi, Wi, lddx);
+  else
+    hipLaunchKernelGGL(k_bilinear_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy, N,
+                       Ho, Wo, C, lddy, (float*)dx, Hi, Wi, lddx);
+  DMF_LAUNCH_CHECK("dmf_bilinear_bwd");
+  return 0;
+}
+
+extern "C" int dmf_col_stats_tiles(long long M) { return (int)((M + 255) / 256); }
+
+extern "C" int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream) {
+  DMF_CHECK_ARG(x && partials && M > 0 && C > 0, "dmf_col_stats: bad args");
+  dim3 grid((unsigned)((M + 255) / 256), (unsigned)cdiv(C, 64));
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_col_stats<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, C,
+                       partials);
+  else
+    hipLaunchKernelGGL(k_col_stats<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, M, C,
+                       partials);
+  DMF_LAUNCH_CHECK("dmf_col_stats");
+  return 0;
+}
+
+extern "C" int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* m, int N, int HW, int C,
+                                 const float* w1, const float* gn_w, const float* gn_b, const float* w2,
+                                 const float* b2, const float* gamma, int hidden, float eps, float* stats, void* out,
+                                 int ldo, void* A_out, void* stream) {
+  DMF_CHECK_ARG(f && m && w1 && gn_w && gn_b && w2 && b2 && gamma && stats && out && hidden > 0,
+                "dmf_mask_attn_fwd: bad args");
+  MaskAttnP P{w1, gn_w, gn_b, w2, b2, gamma, eps, hidden};
+  const long long total = (long long)N * HW;
+  const int grid = (int)((total + 3) / 4 > 16384 ? 16384 : (total + 3) / 4);
+  if (dtype == DMF_BF16) {
+    hipLaunchKernelGGL(k_mask_stats<bf16_t>, dim3(N), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)m, HW, stats);
+    hipLaunchKernelGGL(k_mask_attn_fwd<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)f, ldf,
+                       (const bf16_t*)m, P, stats, (bf16_t*)out, ldo, (bf16_t*)A_out, (long long)N, HW, C);
+  } else {
+    hipLaunchKernelGGL(k_mask_stats<float>, dim3(N), dim3(256), 0, (hipStream_t)stream, (const float*)m, HW, stats);
+    hipLaunchKernelGGL(k_mask_attn_fwd<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)f, ldf,
+                       (const float*)m, P, stats, (float*)out, ldo, (float*)A_out, (long long)N, HW, C);
+  }
+  DMF_LAUNCH_CHECK("dmf_mask_attn_fwd");
+  return 0;
+}

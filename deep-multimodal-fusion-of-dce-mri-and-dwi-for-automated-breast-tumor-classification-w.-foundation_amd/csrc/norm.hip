@@ -1,0 +1,360 @@
+// Batch-norm (train/eval), fused affine + residual + activation + dropout,
+// and their backward, on NHWC tensors. Semantics follow torch BatchNorm2d as
+// used everywhere on the hot path (timm Bottleneck bn1..bn3, adapter necks
+// model_module.py:440-447, ResNetLite :259-280, heads, projectors):
+//   train: mean/biased var over (N,H,W); running_mean/var updated with
+//          momentum and the unbiased (n/(n-1)) variance; eval: running stats.
+// Dropout (model_module.py:263, :273, nn.Dropout element-wise) uses a Philox
+// counter stream keyed by (seed, per-step offset from device memory, site id,
+// element index) so the backward regenerates the same mask.
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+__device__ __forceinline__ float act_fwd(int act, float z) {
+  switch (act) {
+    case DMF_ACT_RELU: return fmaxf(z, 0.f);
+    case DMF_ACT_GELU: return gelu_f(z);
+    case DMF_ACT_SIGMOID: return sigmoid_f(z);
+    default: return z;
+  }
+}
+__device__ __forceinline__ float act_grad(int act, float z) {
+  switch (act) {
+    case DMF_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case DMF_ACT_GELU: return gelu_grad_f(z);
+    case DMF_ACT_SIGMOID: { const float s = sigmoid_f(z); return s * (1.f - s); }
+    default: return 1.f;
+  }
+}
+
+// keep-mask for 4 consecutive elements starting at flat index e (multiple of 4)
+__device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int site, unsigned long long e,
+                                              float p, bool keep[4]) {
+  const unsigned long long seed = rng[0], off = rng[1];
+  uint32_t r[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)(e >> 2), (uint32_t)(e >> 34), (uint32_t)site,
+         (uint32_t)off, r);
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) keep[i] = r[i] >= thr;
+}
+
+// ---------------------------------------------------------- bn finalize
+// partials [T][C][2] -> mean/invstd, per-channel affine (scale, shift), and
+// running-stat update. Block: 64 channels x 4 tile lanes.
+__global__ void k_bn_finalize(const float* __restrict__ part, int T, int C, double count, double unbias_count,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
+                              int training, float* __restrict__ ss, float* __restrict__ save) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (training && c < C) {
+    for (int t = tl; t < T; t += 4) {
+      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
+  }
+  red[tl][cl][0] = s;
+  red[tl][cl][1] = q;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    float mean, var;
+    if (training) {
+      s = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+      q = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+      const double m = s / count;
+      double v = q / count - m * m;
+      if (v < 0.0) v = 0.0;
+      mean = (float)m;
+      var = (float)v;
+      if (running_mean) {
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+        const double n_ = unbias_count > 0.0 ? unbias_count : count;
+        const double unb = n_ > 1.0 ? v * n_ / (n_ - 1.0) : v;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+      }
+    } else {
+      mean = running_mean[c];
+      var = running_var[c];
+    }
+    const float inv = rsqrtf(var + eps);
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    ss[c] = g * inv;
+    ss[C + c] = b - mean * g * inv;
+    if (save) {
+      save[c] = mean;
+      save[C + c] = inv;
+    }
+  }
+  if (training && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+// ------------------------------------------------------ fused affine/act
+// y = drop(act(x*sa + ba + [res*sr + br | res]))
+template <typename T>
+__global__ void k_affine_act(const T* __restrict__ x, int ldx, const float* __restrict__ ssa,
+                             const T* __restrict__ res, int ldr, const float* __restrict__ ssr, int act,
+                             float p, const unsigned long long* rng, int site, T* __restrict__ y, int ldy,
+                             long long M, int C) {
+  constexpr int V = 4;
+  const int cv = C / V;
+  const long long total = M * cv;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / cv;
+    const int c0 = (int)(i - m * cv) * V;
+    float v[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float z = ld(x + m * ldx + c0 + k);
+      if (ssa) z = z * ssa[c0 + k] + ssa[C + c0 + k];
+      if (res) {
+        float r = ld(res + m * ldr + c0 + k);
+        if (ssr) r = r * ssr[c0 + k] + ssr[C + c0 + k];
+        z += r;
+      }
+      v[k] = act_fwd(act, z);
+    }
+    if (p > 0.f) {
+      bool keep[4];
+      dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[k] = keep[k] ? v[k] * sc : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) st(y + m * ldy + c0 + k, v[k]);
+  }
+}
+
+// dz = dy * drop' * act'(z), z recomputed exactly as in k_affine_act
+template <typename T>
+__global__ void k_act_bwd(const T* __restrict__ dy, int lddy, const T* __restrict__ x, int ldx,
+                          const float* __restrict__ ssa, const T* __restrict__ res, int ldr,
+                          const float* __restrict__ ssr, int act, float p, const unsigned long long* rng, int site,
+                          T* __restrict__ dz, int lddz, long long M, int C) {
+  constexpr int V = 4;
+  const int cv = C / V;
+  const long long total = M * cv;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / cv;
+    const int c0 = (int)(i - m * cv) * V;
+    bool keep[4] = {true, true, true, true};
+    if (p > 0.f) dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float g = ld(dy + m * lddy + c0 + k);
+      if (p > 0.f) g = keep[k] ? g * sc : 0.f;
+      if (act != DMF_ACT_NONE) {
+        float z = ld(x + m * ldx + c0 + k);
+        if (ssa) z = z * ssa[c0 + k] + ssa[C + c0 + k];
+        if (res) {
+          float r = ld(res + m * ldr + c0 + k);
+          if (ssr) r = r * ssr[c0 + k] + ssr[C + c0 + k];
+          z += r;
+        }
+        g *= act_grad(act, z);
+      }
+      st(dz + m * lddz + c0 + k, g);
+    }
+  }
+}
+
+// per-tile column sums of dz and dz*xhat: part[tile][c] = (sum dz, sum dz*(x-mean)*inv)
+// block = 256 threads = 64 channel lanes x 4 row lanes, tile = 256 rows
+template <typename T>
+__global__ void k_bn_bwd_reduce(const T* __restrict__ dz, int lddz, const T* __restrict__ x, int ldx,
+                                const float* __restrict__ save, long long M, int C, float* __restrict__ part) {
+  __shared__ float red[4][64][2];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const long long r0 = (long long)blockIdx.x * 256;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    const float mean = x ? save[c] : 0.f, inv = x ? save[C + c] : 0.f;
+    for (int r = rl; r < 256; r += 4) {
+      const long long m = r0 + r;
+      if (m >= M) break;
+      const float g = ld(dz + m * lddz + c);
+      s += g;
+      if (x) q += g * (ld(x + m * ldx + c) - mean) * inv;
+    }
+  }
+  red[rl][cl][0] = s;
+  red[rl][cl][1] = q;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    s = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    q = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    *(float2*)(part + ((size_t)blockIdx.x * C + c) * 2) = make_float2(s, q);
+  }
+}
+
+// sum tiles -> dbeta (=sum dz), dgamma (=sum dz*xhat) (accumulated into the
+// fp32 grads if given) and dx coefficients coef[3][C]: dx = A*dz + Cc*x + B
+__global__ void k_bn_bwd_finalize(const float* __restrict__ part, int T, int C, double count,
+                                  const float* __restrict__ gamma, const float* __restrict__ save,
+                                  float* dgamma, float* dbeta, float* __restrict__ coef) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int t = tl; t < T; t += 4) {
+      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
+  red[tl][cl][0] = s;
+  red[tl][cl][1] = q;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    s = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    q = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    if (dbeta) dbeta[c] += (float)s;
+    if (dgamma) dgamma[c] += (float)q;
+    if (coef) {
+      const double g = gamma ? gamma[c] : 1.0;
+      const double mean = save[c], inv = save[C + c];
+      const double A = g * inv;
+      const double Cc = -g * inv * inv * q / count;
+      const double B = -g * inv * s / count - Cc * mean;
+      coef[c] = (float)A;
+      coef[C + c] = (float)Cc;
+      coef[2 * C + c] = (float)B;
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_bn_bwd_apply(const T* __restrict__ dz, int lddz, const T* __restrict__ x, int ldx,
+                               const float* __restrict__ coef, T* __restrict__ dx, int lddx, long long M, int C) {
+  const long long total = M * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / C;
+    const int c = (int)(i - m * C);
+    const float v = coef[c] * ld(dz + m * lddz + c) + coef[C + c] * ld(x + m * ldx + c) + coef[2 * C + c];
+    st(dx + m * lddx + c, v);
+  }
+}
+
+static inline int grid_for(long long n, int block = 256) {
+  long long g = (n + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, double unbias_count,
+                               const float* gamma,
+                               const float* beta, float* running_mean, float* running_var,
+                               long long* num_batches_tracked, float momentum, float eps, int training,
+                               float* scale_shift, float* save_mean_invstd, void* stream) {
+  DMF_CHECK_ARG(C > 0 && scale_shift, "dmf_bn_finalize: bad args");
+  DMF_CHECK_ARG(!training || (partials && ntiles > 0 && count > 0), "dmf_bn_finalize: training needs partials");
+  DMF_CHECK_ARG(training || (running_mean && running_var), "dmf_bn_finalize: eval needs running stats");
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C, count,
+                     unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, training, scale_shift,
+                     save_mean_invstd);
+  DMF_LAUNCH_CHECK("dmf_bn_finalize");
+  return 0;
+}
+
+extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
+                              const float* res_scale_shift, int act, float dropout_p,
+                              const unsigned long long* rng, int site, void* y, int ldy, long long M, int C,
+                              void* stream) {
+  DMF_CHECK_ARG(C % 4 == 0, "dmf_affine_act: C=%d must be a multiple of 4", C);
+  DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_affine_act: dropout needs rng state");
+  DMF_CHECK_ARG(dropout_p < 1.f, "dmf_affine_act: dropout p must be < 1");
+  if (M == 0) return 0;
+  const int g = grid_for(M * (C / 4));
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_affine_act<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx,
+                       scale_shift, (const bf16_t*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (bf16_t*)y,
+                       ldy, M, C);
+  else
+    hipLaunchKernelGGL(k_affine_act<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       scale_shift, (const float*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (float*)y,
+                       ldy, M, C);
+  DMF_LAUNCH_CHECK("dmf_affine_act");
+  return 0;
+}
+
+extern "C" int dmf_act_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+                           const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
+                           const unsigned long long* rng, int site, void* dz, int lddz, long long M, int C,
+                           void* stream) {
+  DMF_CHECK_ARG(C % 4 == 0, "dmf_act_bwd: C=%d must be a multiple of 4", C);
+  DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_act_bwd: dropout needs rng state");
+  DMF_CHECK_ARG(act == DMF_ACT_NONE || x, "dmf_act_bwd: activation backward needs x");
+  if (M == 0) return 0;
+  const int g = grid_for(M * (C / 4));
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_act_bwd<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy, lddy,
+                       (const bf16_t*)x, ldx, scale_shift, (const bf16_t*)res, ldr, res_scale_shift, act, dropout_p,
+                       rng, site, (bf16_t*)dz, lddz, M, C);
+  else
+    hipLaunchKernelGGL(k_act_bwd<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
+                       (const float*)x, ldx, scale_shift, (const float*)res, ldr, res_scale_shift, act, dropout_p,
+                       rng, site, (float*)dz, lddz, M, C);
+  DMF_LAUNCH_CHECK("dmf_act_bwd");
+  return 0;
+}
+
+extern "C" int dmf_bn_bwd_tiles(long long M) { return (int)((M + 255) / 256); }
+
+extern "C" int dmf_bn_bwd_reduce(int dtype, const void* dz, int lddz, const void* x, int ldx,
+                                 const float* save_mean_invstd, long long M, int C, float* partials, void* stream) {
+  DMF_CHECK_ARG(M > 0 && C > 0 && partials, "dmf_bn_bwd_reduce: bad args");
+  DMF_CHECK_ARG(!x || save_mean_invstd, "dmf_bn_bwd_reduce: x given without saved stats");
+  const long long tiles = (M + 255) / 256;
+  DMF_CHECK_ARG(tiles < 65536LL * 32768LL, "dmf_bn_bwd_reduce: too many rows");
+  dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
+                       (const bf16_t*)x, ldx, save_mean_invstd, M, C, partials);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
+                       (const float*)x, ldx, save_mean_invstd, M, C, partials);
+  DMF_LAUNCH_CHECK("dmf_bn_bwd_reduce");
+  return 0;
+}
+
+extern "C" int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, const float* gamma,
+                                   const float* save_mean_invstd, float* dgamma, float* dbeta, float* coef,
+                                   void* stream) {
+  DMF_CHECK_ARG(partials && ntiles > 0 && C > 0, "dmf_bn_bwd_finalize: bad args");
+  DMF_CHECK_ARG(!coef || save_mean_invstd, "dmf_bn_bwd_finalize: coef needs saved stats");
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C,
+                     count, gamma, save_mean_invstd, dgamma, dbeta, coef);
+  DMF_LAUNCH_CHECK("dmf_bn_bwd_finalize");
+  return 0;
+}
+
+extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* coef,
+                                void* dx, int lddx, long long M, int C, void* stream) {
+  DMF_CHECK_ARG(dz && x && coef && dx, "dmf_bn_bwd_apply: bad args");
+  if (M == 0) return 0;
+  const int g = grid_for(M * C);
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_bn_bwd_apply<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
+                       (const bf16_t*)x, ldx, coef, (bf16_t*)dx, lddx, M, C);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
+                       (const float*)x, ldx, coef, (float*)dx, lddx, M, C);
+  DMF_LAUNCH_CHECK("dmf_bn_bwd_apply");
+  return 0;
+}

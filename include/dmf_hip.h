@@ -1,0 +1,210 @@
+/*
+ * dmf_hip.h -- C-ABI of the MI355X (gfx950) hot path for the DCE-MRI x DWI
+ * fusion classifier.
+ *
+ * The reference (simhelgithub/Deep-Multimodal-Fusion-..., pure Python on
+ * PyTorch) has no FFI: its "plugin interface" is the nn.Module API of
+ * code/model_module.py, code/foundation_model.py and code/loss.py. The
+ * Python package next to this header mirrors that API and binds the entry
+ * points below through ctypes (argtypes are parsed from THIS file; see
+ * INTEGRATION.md). Every function:
+ *   - takes plain device pointers, sizes and a hipStream_t passed as void*;
+ *   - never allocates, never synchronises (hipGraph-capture safe);
+ *   - returns 0 on success, <0 on error with dmf_last_error() describing it
+ *     (the Python layer raises RuntimeError -- SURVEY.md 8(b) "Errors").
+ *
+ * Layout conventions
+ *   activations : NHWC ("channels_last"); element type selected by `dtype`
+ *                 (DMF_F32 = float, DMF_BF16 = bfloat16 bits in uint16);
+ *                 `ld*` arguments are channel strides (elements per pixel)
+ *   conv weights: forward  [Cout][KH][KW][CinP]  (dmf_conv_weight_prep mode 0)
+ *                 dgrad    [CinP][KH][KW][Cout]  (mode 1)
+ *                 gradients are produced in torch layout [Cout][Cin][KH][KW]
+ *   BN partials : float [tiles][C][2] (sum, sum of squares)
+ *   scale_shift : float [2][C] (y = x*scale + shift)
+ *   dropout rng : unsigned long long [2] = (seed, per-step offset) in device memory
+ *
+ * Reference interfaces each group replaces are cited per entry point.
+ */
+#ifndef DMF_HIP_H
+#define DMF_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMF_ABI_VERSION 1
+
+enum { DMF_F32 = 0, DMF_BF16 = 1 };
+enum { DMF_ACT_NONE = 0, DMF_ACT_RELU = 1, DMF_ACT_GELU = 2, DMF_ACT_SIGMOID = 3 };
+
+/* ------------------------------------------------------------- runtime */
+const char* dmf_last_error(void);
+int dmf_abi_version(void);
+int dmf_iota_f32(float* y, long long n, float a, float b, void* stream);
+/* state[1] += inc (per-step dropout offset; graph-replay safe) */
+int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* stream);
+
+/* ---------------------------------------------------- convolution engine
+ * Replaces every nn.Conv2d forward/backward on the path: timm ResNet-50
+ * OS8 (foundation_model.py:260-267), BackboneAdapter necks
+ * (model_module.py:440-447), ResNetLiteBlock_withRecon (:259-280), ReconHead
+ * (:113-118), MaskHeadResize (:150-187), Projector (:337-345),
+ * FeatureDownAlign (:386-390), FusionModel.proj_in_* / reduce (:857-862,
+ * :788-792), PatchEmbed.proj (transformer_model.py:17-22). */
+int dmf_conv_m_tile(void);
+int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                   int KH, int KW, int stride, int pad, int dil, const float* bias, void* y, int Ho, int Wo,
+                   int ldy, float* bn_partials, int act, void* stream);
+int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
+                     int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
+int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
+                         void* stream);
+int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M);
+int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int Ho,
+                     int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad, int dil, int splits,
+                     float* workspace, void* stream);
+int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int Cout, int Cin, int CinP, int KH, int KW,
+                            float* dw, int accumulate, void* stream);
+/* single-output-channel convs: ReconHead.conv[3] (model_module.py:117),
+ * MaskHeadResize.out (:187); weights [KH][KW][Cin] fp32 */
+int dmf_conv_cout1_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const float* w,
+                       const float* bias, int KH, int KW, int stride, int pad, int dil, void* y, int Ho, int Wo,
+                       int ldy, int act, void* stream);
+int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const float* w, int N, int H, int W, int Cin, int KH,
+                         int KW, int stride, int pad, int dil, int Ho, int Wo, void* dx, int lddx, void* stream);
+int dmf_conv_cout1_wgrad_splits(long long M);
+int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int lddy,
+                         int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits, float* workspace,
+                         float* dw, float* db, void* stream);
+/* single-input-channel 1x1 convs: mask_processor[0] (model_module.py:68),
+ * proj_r1/proj_r2 first conv (:639-640) */
+int dmf_conv_cin1_fwd(int dtype, const void* x, int ldx, const float* w, const float* bias, void* y, int ldy,
+                      long long M, int Cout, int act, void* stream);
+int dmf_conv_cin1_dgrad(int dtype, const void* dy, int lddy, const float* w, void* dx, int lddx, long long M,
+                        int Cout, void* stream);
+int dmf_conv_cin1_wgrad_tiles(long long M);
+int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void* dy, int lddy, long long M, int Cout,
+                        float* workspace, float* dw, float* db, void* stream);
+
+/* ---------------------------------------------------- batch norm & acts
+ * nn.BatchNorm2d train/eval semantics + fused residual/activation/dropout
+ * (timm Bottleneck, ResNetLite :259-307, necks, heads, projectors). */
+int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, double unbias_count,
+                    const float* gamma, const float* beta, float* running_mean, float* running_var,
+                    long long* num_batches_tracked, float momentum, float eps, int training, float* scale_shift,
+                    float* save_mean_invstd, void* stream);
+int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
+                   const float* res_scale_shift, int act, float dropout_p, const unsigned long long* rng, int site,
+                   void* y, int ldy, long long M, int C, void* stream);
+int dmf_act_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+                const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
+                const unsigned long long* rng, int site, void* dz, int lddz, long long M, int C, void* stream);
+int dmf_bn_bwd_tiles(long long M);
+int dmf_bn_bwd_reduce(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* save_mean_invstd,
+                      long long M, int C, float* partials, void* stream);
+int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, const float* gamma,
+                        const float* save_mean_invstd, float* dgamma, float* dbeta, float* coef, void* stream);
+int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* coef, void* dx,
+                     int lddx, long long M, int C, void* stream);
+int dmf_col_stats_tiles(long long M);
+int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
+
+/* -------------------------------------------------- encoder elementwise
+ * SEBlock (model_module.py:25-43), GroupNorm(C,C) mix (:673-675, :688-690),
+ * maxpool (timm stem), proj_pool (:531-534), F.interpolate bilinear
+ * (:81-87, :206-211), MaskGuidedSpatialAttention (:49-97). */
+int dmf_input_prep(int dtype, const float* x, int N, int C, int H, int W, const float* gate, void* y, int Cp,
+                   float* chan_mean, void* stream);
+int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream);
+int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C, float scale,
+                    float* out, int accumulate, void* stream);
+int dmf_channel_scale(int dtype, const void* x, int ldx, const float* gate, void* y, int ldy, int N, int HW, int C,
+                      void* stream);
+int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb, const float* wlogit, void* z, int ldz,
+            long long M, int C, void* stream);
+int dmf_gn_apply(int dtype, const void* z, int ldz, const float* mean, const float* m2, const float* gamma,
+                 const float* beta, float eps, void* y, int ldy, int N, int HW, int C, void* stream);
+int dmf_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, const float* mean, const float* m2,
+               const float* gamma, float eps, float* s1, float* s2, void* dz, int lddz, int N, int HW, int C,
+               void* stream);
+int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo, int ldy,
+                  int k, int s, int p, void* stream);
+int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* dy, int Ho, int Wo,
+                      int lddy, void* dx, int lddx, int k, int s, int p, void* stream);
+int dmf_upsample2x_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, void* stream);
+int dmf_upsample2x_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C, void* stream);
+int dmf_bilinear(int dtype, const void* x, int N, int Hi, int Wi, int C, int ldx, void* y, int Ho, int Wo, int ldy,
+                 void* stream);
+int dmf_bilinear_bwd(int dtype, const void* dy, int N, int Ho, int Wo, int C, int lddy, void* dx, int Hi, int Wi,
+                     int lddx, void* stream);
+int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* m, int N, int HW, int C, const float* w1,
+                      const float* gn_w, const float* gn_b, const float* w2, const float* b2, const float* gamma,
+                      int hidden, float eps, float* stats, void* out, int ldo, void* A_out, void* stream);
+
+/* ------------------------------------------- cross-modal fusion op (fp32)
+ * FusionModel.forward (model_module.py:919-1000): GatingAttention
+ * (:745-780), _to_tokens (:903-917), CrossAttentionBlock (:799-818: MHA +
+ * LayerNorm/Linear FFN), gated combine + bilinear upsample-add (:952-973);
+ * nn.Linear layers (classifier, SE excitations) via dmf_sgemm. */
+int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
+              int ldb, float beta, float* C, int ldc, const float* bias, int act, void* stream);
+int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream);
+int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
+int dmf_layernorm_fwd(const float* x, int R, int E, const float* gamma, const float* beta, float eps, float* y,
+                      float* save, void* stream);
+int dmf_layernorm_bwd(const float* dy, const float* x, const float* save, int R, int E, const float* gamma,
+                      float* dx, float* dgamma, float* dbeta, void* stream);
+/* avg_weights must be zeroed by the caller (heads accumulate into it) */
+int dmf_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, int B, int Nq, int Nk,
+                 int H, int D, float scale, float* out, int ldo, float* probs, float* avg_weights, void* stream);
+int dmf_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* probs,
+                 const float* dout, int lddo, int B, int Nq, int Nk, int H, int D, float scale, float* dq, int lddq,
+                 float* dk, int lddk, float* dv, int lddv, void* stream);
+int dmf_tokens_fwd(int dtype, const void* x, int ldx, int B, int H, int W, int C, int Hp, int Wp, float* tokens,
+                   void* stream);
+int dmf_tokens_bwd(int dtype, const float* dtokens, int B, int H, int W, int C, int Hp, int Wp, void* dx, int lddx,
+                   int accumulate, void* stream);
+int dmf_fusion_combine_fwd(int dtype, const void* p_dwi, const void* p_dce, int ld, const float* gates,
+                           const float* lowres, int B, int H, int W, int C, int Hp, int Wp, void* y, int ldy,
+                           void* stream);
+int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const void* p_dwi, const void* p_dce, int ld,
+                           const float* gates, int B, int H, int W, int C, int Hp, int Wp, void* dp_dwi,
+                           void* dp_dce, int ldd, float* dgates, float* dlowres, void* stream);
+int dmf_gate_fwd(const float* pv_dwi, const float* pv_dce, const float* conf_dwi, const float* conf_dce, int B,
+                 int C, const float* W, const float* b, float* gates, void* stream);
+int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const float* conf_dwi, const float* conf_dce, int B,
+                 int C, const float* W, const float* gates, const float* dgates, float* dW, float* db,
+                 float* dpv_dwi, float* dpv_dce, float* dconf_dwi, float* dconf_dce, void* stream);
+
+/* ------------------------------------------------------------ criteria
+ * loss.py:45-62 (SoftDiceLoss), :157-187 (SoftWeightedFocalLoss), :190-213
+ * (LabelSmoothing); train_fusion.py:709-744 (compute_recon_list_loss);
+ * train.py:1033-1048 (mimic_feat_loss, recon_image_loss, charbonnier).
+ * Forward writes the loss and the unit-upstream gradient in one pass. */
+int dmf_focal_loss(const float* logits, const long long* labels, int B, int K, float smoothing, int use_smoothing,
+                   const float* class_weights, float gamma, float* loss, float* dlogits, void* stream);
+int dmf_soft_dice(int dtype, const void* logits, const float* target, int B, int P, float eps, float* sums_ws,
+                  float* loss, float* dlogits, void* stream);
+int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const void* r2, const void* r3,
+                   const void* r4, int ldr0, int ldr1, int ldr2, int ldr3, int ldr4, int sel0, int sel1, int sel2,
+                   int sel3, int sel4, const float* tA, const float* tB, float ca, float cb, int B, int h, int w,
+                   int S, float* sums, float* g0, float* g1, float* g2, float* g3, float* g4, void* stream);
+int dmf_mimic_loss(int dtype, const void* feats, int ld, int HW, int C, int npairs, float* loss, float* dstudent,
+                   void* stream);
+int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream);
+int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul, void* dst,
+                      int ldd, void* stream);
+
+/* ------------------------------------------------------------ optimizer
+ * torch.optim.AdamW as built by LightningFusionOptimizerFactory
+ * (selector_helpers.py:632-685, :617-629) -- multi-tensor, one launch. */
+int dmf_adamw_multi(int nchunks, const long long* chunks, const long long* tensors, const float* hyper,
+                    const int* steps, float grad_scale, void* stream);
+int dmf_steps_inc(int* steps, int n, void* stream);
+int dmf_multi_copy(int nchunks, const long long* chunks, const long long* pairs, float scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMF_HIP_H */
