@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the DCE+DWI fusion training step on MI355X.
+
+Metric (BASELINE.json): DCE+DWI volumes/sec/node (fwd+bwd). One volume = one
+patient sample = a DWI stack [14,256,256] + a DCE stack [6,256,256]
+(prepare_fusion_model.py:104-113). Workload = configuration 3 (fusion
+classifier, batch 32 per GPU, S=256) in the reference's default training
+state at epoch 0 ("mode A": both encoders frozen but in train mode -- dropout
+on, BN batch statistics -- backward + AdamW through FusionModel only,
+selector_helpers.py:437-443 / :632-685). ``--mode B`` unfreezes everything.
+
+  python bench.py --gpus N --steps K --warmup W      (N>1 under torchrun)
+
+Prints ONE JSON line (rank 0) including the roofline of the dominant kernel
+(the implicit-GEMM conv forward, timed per launch with HIP events on the
+stream it runs on) and the CPU baseline (the fp32 CPU oracle restatement on a
+bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "deep-multimodal-fusion-of-dce-mri-and-dwi-for-automated-breast-tumor-classification-w.-foundation_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (spec, no sparsity)
+F32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--mode", choices=["A", "B"], default="A")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def build(P, device, dtype, mode, seed=0):
+    import foundation_model as FM
+    import model_module as MM
+    import train_fusion as TF
+    from selector_helpers import get_classification_loss
+
+    torch.manual_seed(seed)
+    P["dwi_model_parameters"]["compute_dtype"] = dtype
+    P["backbone_freeze_on_start"] = mode == "A"
+    bb_dwi = FM.build_medical_backbone(P, "cpu", "dwi", P["dwi_channel_num"])
+    dwi = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, bb_dwi), True)
+    bb_dce = FM.build_medical_backbone(P, "cpu", "dce", P["dce_channel_num"])
+    dce = MM.initialize_model(MM.ModelMaskHeadBackbone("dce", P, bb_dce), True)
+    fm = MM.FusionModel(P)
+    dwi, dce, fm = dwi.to(device), dce.to(device), fm.to(device)
+    train_labels = torch.arange(1024) % P["class_num"]  # balanced synthetic "train" labels -> weights ~1
+    crit = get_classification_loss(P, train_labels, "fusion", device)
+    lm = TF.LightningFusionModel(dwi, dce, fm, P, crit)
+    lm.train()
+    return lm
+
+
+def synthetic_batch(B, S, device, seed, cd=14, cc=6):
+    """DWI clamp(0.5+randn/6,0,1), DCE U[0,1), disc masks, labels randint(0,4)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dwi = (0.5 + torch.randn(B, cd, S, S, generator=g) / 6).clamp(0, 1)
+    dce = torch.rand(B, cc, S, S, generator=g)
+    yy, xx = torch.meshgrid(torch.arange(32), torch.arange(32), indexing="ij")
+    masks = torch.zeros(B, 1, 32, 32)
+    cyx = torch.randint(8, 24, (B, 2), generator=g)
+    rad = torch.randint(4, 11, (B,), generator=g)
+    for b in range(B):
+        masks[b, 0] = (((yy - cyx[b, 0]) ** 2 + (xx - cyx[b, 1]) ** 2) <= rad[b] ** 2).float()
+    labels = torch.randint(0, 4, (B,), generator=g)
+    return tuple(t.to(device) for t in (dwi, dce, masks, labels))
+
+
+def roofline_probe(trainer, batch, dtype):
+    """Per-launch HIP-event timing of the dominant kernel (implicit-GEMM conv
+    forward) over one eager step, on the stream the kernels run on."""
+    import dmf_ops as O
+
+    recs = []
+    O.PROBE["conv_fwd"] = recs
+    torch.cuda.synchronize()
+    trainer.eager_step(batch)
+    torch.cuda.synchronize()
+    O.PROBE["conv_fwd"] = None
+    if not recs:
+        return None
+    flops = sum(r[2] for r in recs)
+    byt = sum(r[3] for r in recs)
+    ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+    n = len(recs)
+    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {
+        "kernel": "k_conv_igemm<%s, false>" % ("unsigned short" if dtype == torch.bfloat16 else "float"),
+        "bound": "mfma",
+        "achieved": round(achieved, 2),
+        "peak": peak,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": None,
+        "launches_per_step": n,
+        "avg_launch_us": round(ms * 1e3 / n, 2),
+        "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
+        "algorithmic_mb_per_launch": round(byt / n / 1e6, 2),
+        "hbm_gbs_per_launch_avg": round(byt / (ms * 1e-3) / 1e9, 1),
+    }
+
+
+def cpu_baseline(args, P_fn):
+    """fp32 CPU oracle (same eager op sequence as the reference) on a bounded
+    sample: cpu-batch volumes at SxS, mode A step, 1 warm-up + cpu-steps timed."""
+    from oracle import losses as OL
+    from oracle import model as OM
+
+    torch.set_num_threads(os.cpu_count() if os.cpu_count() <= 16 else 16)
+    P = P_fn()
+    P["dwi_model_parameters"]["backbone_index_lists"] = [[0], [1], [2, 3]]
+    torch.manual_seed(0)
+    dwi = OM.ModelMaskHeadBackbone("dwi", P, OM.ResNet50OS8(P["dwi_channel_num"]))
+    dce = OM.ModelMaskHeadBackbone("dce", P, OM.ResNet50OS8(P["dce_channel_num"]))
+    fm = OM.FusionModel(P)
+    for m in (dwi, dce):
+        for p in m.parameters():
+            p.requires_grad = (args.mode == "B")
+    params = [p for m in (dwi, dce, fm) for p in m.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4)
+    b = synthetic_batch(args.cpu_batch, args.size, "cpu", 1)
+    cw = OL.class_weights_from_labels(torch.arange(1024) % 4)
+
+    def step():
+        opt.zero_grad()
+        out = OL.fusion_shared_step(dwi, dce, fm, b, P, cw, epoch=0)
+        out["total"].backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(args.cpu_batch * args.cpu_steps / dt, 4), "unit": "volumes/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle fp32 CPU, mode {args.mode}, {args.cpu_steps} timed steps x {args.cpu_batch} volumes "
+                      f"at {args.size}x{args.size} (1 warm-up step)"}
+
+
+def main():
+    args = parse()
+    rank, local_rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), \
+        int(os.environ.get("WORLD_SIZE", 1))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    import parameters as PR
+    from dmf_dp import FusionTrainer
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    P = PR.default_parameters()
+    P["dwi_model_parameters"]["input_size"] = args.size
+    lm = build(P, device, dtype, args.mode, seed=0)
+    trainer = FusionTrainer(lm, world=world, use_graph=not args.no_graph)
+    batch = synthetic_batch(args.batch, args.size, device, seed=2 + rank)
+
+    roof = None
+    if not args.no_graph:
+        trainer.capture(batch)
+    for _ in range(args.warmup):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
+    if not args.no_roofline and rank == 0:
+        roof = roofline_probe(trainer, batch, dtype)
+
+    vols = args.batch * world * args.steps
+    out = {
+        "metric": "DCE+DWI volumes/sec/node (fwd+bwd)",
+        "value": round(vols / dt, 2),
+        "unit": "volumes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (config-3 recipe: DWI clamp(0.5+N/6), DCE U[0,1), disc masks); random-init weights",
+        "config": {"workload": f"fusion training step, config 3, mode {args.mode} "
+                               f"({'encoders frozen, train-mode' if args.mode == 'A' else 'all trainable'})",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch, "size": args.size,
+                   "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
+        "loss": loss_val,
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, PR.default_parameters)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

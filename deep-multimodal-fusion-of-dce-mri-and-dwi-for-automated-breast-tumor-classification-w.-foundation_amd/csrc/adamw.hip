@@ -54,7 +54,11 @@ __global__ void k_multi_copy(const long long* __restrict__ chunks, const long lo
   const long long* pr = pairs + 2 * ch[0];
   const float* src = (const float*)pr[0];
   float* dst = (float*)pr[1];
-  for (long long i = ch[1] + threadIdx.x; i < ch[2]; i += blockDim.x) dst[i] = src[i] * scale;
+  if (scale == 0.f) {  // zero fill (grad reset), NaN-safe
+    for (long long i = ch[1] + threadIdx.x; i < ch[2]; i += blockDim.x) dst[i] = 0.f;
+  } else {
+    for (long long i = ch[1] + threadIdx.x; i < ch[2]; i += blockDim.x) dst[i] = src[i] * scale;
+  }
 }
 
 }  // namespace dmf

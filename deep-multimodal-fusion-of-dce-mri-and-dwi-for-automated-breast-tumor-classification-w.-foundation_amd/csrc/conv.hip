@@ -36,7 +36,9 @@ struct ConvArgs {
   const float* bias;  // [Nout] or null
   void* y;            // output NHWC, channel stride ldy
   float* partials;    // [mtiles][Nout][2] or null
-  int N, H, W, C, ldx;  // A-source geometry
+  int N, H, W, C, ldx;  // A-source geometry (C = total channels over both sources)
+  const void* x2;       // optional second source concatenated along channels (FWD only)
+  int C1, ldx2;         // channels taken from x (the rest from x2), stride of x2
   int Ho, Wo, ldy;      // output geometry
   int Nout;             // GEMM N
   int KH, KW, stride, pad, dil;
@@ -112,8 +114,15 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
     const int k = kt * BK + q * EPC;
     const bool kok = k < a.Ktot;
     const int tap = kok ? k / a.C : 0;
-    const int c = k - tap * a.C;
+    int c = k - tap * a.C;
     const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
+    const T* src = X;
+    int ldsrc = a.ldx;
+    if (!DGRAD && c >= a.C1) {  // channel-concat second source (BackboneAdapter chain [2,3])
+      src = (const T*)a.x2;
+      c -= a.C1;
+      ldsrc = a.ldx2;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bool ok = kok && a_ok[i];
@@ -129,8 +138,8 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
       }
       ok = ok && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
       if (ok) {
-        const size_t off = ((size_t)(a_n[i] * a.H + hi) * a.W + wi) * a.ldx + c;
-        ra[i] = *(const uint4*)(X + off);
+        const size_t off = ((size_t)(a_n[i] * a.H + hi) * a.W + wi) * ldsrc + c;
+        ra[i] = *(const uint4*)(src + off);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
@@ -345,9 +354,10 @@ using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
-extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
-                              int KH, int KW, int stride, int pad, int dil, const float* bias, void* y, int Ho, int Wo,
-                              int ldy, float* bn_partials, int act, void* stream) {
+extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                              int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                              const float* bias, void* y, int Ho, int Wo, int ldy, float* bn_partials, int act,
+                              void* stream) {
   DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_fwd: bad dtype %d", dtype);
   DMF_CHECK_ARG(stride >= 1 && dil >= 1 && KH >= 1 && KW >= 1, "dmf_conv2d_fwd: bad geometry");
   DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
@@ -355,10 +365,14 @@ extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int
                 stride, pad, dil);
   ConvArgs a{};
   a.x = x; a.w = w; a.bias = bias; a.y = y; a.partials = bn_partials;
-  a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = ldx;
+  const int epc = dtype == DMF_BF16 ? 8 : 4;
+  DMF_CHECK_ARG(!x2 || (Cin2 > 0 && Cin2 % epc == 0 && ldx2 % epc == 0 && ((uintptr_t)x2 % 16) == 0),
+                "dmf_conv2d_fwd: bad second source (C2=%d ld2=%d)", Cin2, ldx2);
+  a.N = N; a.H = H; a.W = W; a.C = Cin + (x2 ? Cin2 : 0); a.ldx = ldx;
+  a.x2 = x2; a.C1 = Cin; a.ldx2 = ldx2;
   a.Ho = Ho; a.Wo = Wo; a.ldy = ldy; a.Nout = Cout;
   a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
-  a.Ktot = KH * KW * Cin;
+  a.Ktot = KH * KW * a.C;
   a.M = N * Ho * Wo;
   a.act = act;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd");
@@ -373,6 +387,7 @@ extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo
   ConvArgs a{};
   a.x = dy; a.w = wt; a.bias = nullptr; a.y = dx; a.partials = nullptr;
   a.N = N; a.H = Ho; a.W = Wo; a.C = Cout; a.ldx = lddy;
+  a.x2 = nullptr; a.C1 = Cout; a.ldx2 = 0;
   a.Ho = H; a.Wo = W; a.ldy = lddx; a.Nout = Cin;
   a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
   a.Ktot = KH * KW * Cout;

@@ -23,7 +23,9 @@ struct WgArgs {
   const void* x;   // input NHWC [N][H][W][ldx]
   const void* dy;  // grad out NHWC [N][Ho][Wo][lddy]
   float* ws;       // slabs [splits][Cout][Ktot]
-  int N, H, W, Cin, ldx;
+  int N, H, W, Cin, ldx;  // Cin = total channels over both sources
+  const void* x2;         // optional channel-concat second source
+  int C1, ldx2;
   int Ho, Wo, Cout, lddy;
   int KH, KW, stride, pad, dil;
   int Ktot, M;  // Ktot = KH*KW*Cin, M = N*Ho*Wo
@@ -58,7 +60,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
   const int kcol = k0 + chunk * EPC;
   const bool kok = kcol < a.Ktot;
   const int tap = kok ? kcol / a.Cin : 0;
-  const int ci = kcol - tap * a.Cin;
+  int ci = kcol - tap * a.Cin;
+  const T* xsrc = X;
+  int ldxs = a.ldx;
+  if (ci >= a.C1) {
+    xsrc = (const T*)a.x2;
+    ci -= a.C1;
+    ldxs = a.ldx2;
+  }
   const int r = tap / a.KW, s = tap % a.KW;
   const int cocol = co0 + chunk * EPC;
   const bool cook = cocol < a.Cout;
@@ -77,7 +86,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
           const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
           const int hi = ho * a.stride - a.pad + r * a.dil, wi = wo * a.stride - a.pad + s * a.dil;
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
-            vb = *(const uint4*)(X + ((size_t)(n * a.H + hi) * a.W + wi) * a.ldx + ci);
+            vb = *(const uint4*)(xsrc + ((size_t)(n * a.H + hi) * a.W + wi) * ldxs + ci);
         }
       }
       *(uint4*)ra[i] = va;
@@ -364,9 +373,9 @@ extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int
   return (int)want;
 }
 
-extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy,
-                                int Ho, int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad, int dil,
-                                int splits, float* workspace, void* stream) {
+extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                                int Cin2, int ldx2, const void* dy, int Ho, int Wo, int Cout, int lddy, int KH, int KW,
+                                int stride, int pad, int dil, int splits, float* workspace, void* stream) {
   const int epc = dtype == DMF_BF16 ? 8 : 4;
   DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_wgrad: bad dtype");
   DMF_CHECK_ARG(Cin % epc == 0 && ldx % epc == 0 && Cout % epc == 0 && lddy % epc == 0,
@@ -376,10 +385,12 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
                 "dmf_conv2d_wgrad: geometry mismatch");
   WgArgs a{};
   a.x = x; a.dy = dy; a.ws = workspace;
-  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ldx = ldx;
+  DMF_CHECK_ARG(!x2 || (Cin2 % epc == 0 && ldx2 % epc == 0), "dmf_conv2d_wgrad: bad second source");
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin + (x2 ? Cin2 : 0); a.ldx = ldx;
+  a.x2 = x2; a.C1 = x2 ? Cin : a.Cin; a.ldx2 = ldx2;
   a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.lddy = lddy;
   a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil;
-  a.Ktot = KH * KW * Cin;
+  a.Ktot = KH * KW * a.Cin;
   a.M = N * Ho * Wo;
   a.mtiles = cdiv(Cout, 128);
   a.ntiles = cdiv(a.Ktot, 128);

@@ -113,6 +113,50 @@ __global__ void k_act_grad_f32(const float* __restrict__ dy, const float* __rest
   }
 }
 
+__global__ void k_act_f32(const float* __restrict__ x, float* __restrict__ y, long long n, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = actf(act, x[i]);
+}
+
+// dz = dg * s * (1 - s) given the sigmoid OUTPUT s
+__global__ void k_sig_grad_f32(const float* __restrict__ dg, const float* __restrict__ s, float* __restrict__ dz,
+                               long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dz[i] = dg[i] * s[i] * (1.f - s[i]);
+}
+
+// F.normalize(x, dim=1) on rows (ClassificationHead, model_module.py:367-368):
+// y = x / max(||x||, eps); backward dx = (dy - y (y.dy)) / ||x|| (or dy/eps)
+__global__ void k_row_l2norm(const float* __restrict__ x, int R, int C, float eps, float* __restrict__ y,
+                             float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float s = 0.f;
+  for (int i = lane; i < C; i += 64) s += x[(size_t)r * C + i] * x[(size_t)r * C + i];
+  const float nrm = sqrtf(wave_sum(s));
+  const float d = fmaxf(nrm, eps);
+  for (int i = lane; i < C; i += 64) y[(size_t)r * C + i] = x[(size_t)r * C + i] / d;
+  if (lane == 0 && norms) norms[r] = nrm;
+}
+
+__global__ void k_row_l2norm_bwd(const float* __restrict__ dy, const float* __restrict__ y,
+                                 const float* __restrict__ norms, int R, int C, float eps, float* __restrict__ dx) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float nrm = norms[r];
+  float dot = 0.f;
+  for (int i = lane; i < C; i += 64) dot += y[(size_t)r * C + i] * dy[(size_t)r * C + i];
+  dot = wave_sum(dot);
+  const bool active = nrm > eps;
+  const float d = fmaxf(nrm, eps);
+  for (int i = lane; i < C; i += 64) {
+    const float g = dy[(size_t)r * C + i];
+    dx[(size_t)r * C + i] = active ? (g - y[(size_t)r * C + i] * dot) / d : g / d;
+  }
+}
+
 // --------------------------------------------------------------- LayerNorm
 __global__ void k_layernorm(const float* __restrict__ x, int R, int E, const float* __restrict__ g,
                             const float* __restrict__ b, float eps, float* __restrict__ y, float* __restrict__ save) {
@@ -490,6 +534,38 @@ extern "C" int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_act_grad_f32, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, dy, z, dx, n, act);
   DMF_LAUNCH_CHECK("dmf_act_grad_f32");
+  return 0;
+}
+
+extern "C" int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream) {
+  DMF_CHECK_ARG(x && y, "dmf_act_f32: bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_act_f32, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, act);
+  DMF_LAUNCH_CHECK("dmf_act_f32");
+  return 0;
+}
+
+extern "C" int dmf_sig_grad_f32(const float* dg, const float* s, float* dz, long long n, void* stream) {
+  DMF_CHECK_ARG(dg && s && dz, "dmf_sig_grad_f32: bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_sig_grad_f32, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, dg, s, dz, n);
+  DMF_LAUNCH_CHECK("dmf_sig_grad_f32");
+  return 0;
+}
+
+extern "C" int dmf_row_l2norm(const float* x, int R, int C, float eps, float* y, float* norms, void* stream) {
+  DMF_CHECK_ARG(x && y && R > 0 && C > 0, "dmf_row_l2norm: bad args");
+  hipLaunchKernelGGL(k_row_l2norm, dim3(cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, x, R, C, eps, y, norms);
+  DMF_LAUNCH_CHECK("dmf_row_l2norm");
+  return 0;
+}
+
+extern "C" int dmf_row_l2norm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float eps,
+                                  float* dx, void* stream) {
+  DMF_CHECK_ARG(dy && y && norms && dx, "dmf_row_l2norm_bwd: bad args");
+  hipLaunchKernelGGL(k_row_l2norm_bwd, dim3(cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, dy, y, norms, R, C, eps,
+                     dx);
+  DMF_LAUNCH_CHECK("dmf_row_l2norm_bwd");
   return 0;
 }
 

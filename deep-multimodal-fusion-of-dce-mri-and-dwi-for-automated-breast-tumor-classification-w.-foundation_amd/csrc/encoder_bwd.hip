@@ -1,0 +1,218 @@
+// Backward kernels that only the all-trainable (unfrozen encoder) step needs:
+//   - gated mix z = sig(w)*a + (1-sig(w))*b (model_module.py:674-675,
+//     :689-690): da, db, dw
+//   - MaskGuidedSpatialAttention (model_module.py:75-97): df, dmask and the
+//     parameter grads, recomputing the per-pixel 16-channel mask processor
+//     from the mask and the closed-form GroupNorm(1,16) statistics.
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+template <typename T>
+__global__ void k_mix_bwd(const T* __restrict__ dz, int lddz, const T* __restrict__ a, int lda,
+                          const T* __restrict__ b, int ldb, const float* __restrict__ wlogit, T* __restrict__ da,
+                          T* __restrict__ db, int ldd, float* __restrict__ dw, long long M, int C) {
+  __shared__ float red[16];
+  const float al = 1.f / (1.f + __expf(-wlogit[0]));
+  float acc = 0.f;
+  const long long total = M * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / C;
+    const int c = (int)(i - m * C);
+    const float g = ld(dz + m * lddz + c);
+    const float av = ld(a + m * lda + c), bv = ld(b + m * ldb + c);
+    st(da + m * ldd + c, al * g);
+    st(db + m * ldd + c, (1.f - al) * g);
+    acc += g * (av - bv);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) atomicAdd(dw, acc * al * (1.f - al));
+}
+
+struct MaskAttnB {
+  const float* w1;
+  const float* g;
+  const float* b;
+  const float* w2;
+  const float* b2;
+  const float* gamma;
+  float eps;
+  int hid;
+};
+
+__device__ __forceinline__ void ma_stats(const MaskAttnB& P, const float* stats, int n, int HW, float& mu, float& rs) {
+  float mw = 0.f, mw2 = 0.f;
+  for (int c = 0; c < P.hid; ++c) { mw += P.w1[c]; mw2 += P.w1[c] * P.w1[c]; }
+  mw /= P.hid;
+  mw2 /= P.hid;
+  const float mm = stats[2 * n] / HW, mm2 = stats[2 * n + 1] / HW;
+  mu = mw * mm;
+  rs = rsqrtf(fmaxf(mw2 * mm2 - mu * mu, 0.f) + P.eps);
+}
+
+// pass 1: block per sample, one wave per pixel at a time.
+// grads layout: [hid] dw1, [hid] dgn_w, [hid] dgn_b, [hid] dw2, [1] db2, [1] dgamma
+// ws: dhh [N][HW][hid], then S [N][2]
+template <typename T>
+__global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* __restrict__ f, int ldf,
+                                 const T* __restrict__ m, MaskAttnB P, const float* __restrict__ stats, int HW, int C,
+                                 T* __restrict__ df, int lddf, float* __restrict__ dhh, float* __restrict__ S,
+                                 float* __restrict__ grads) {
+  __shared__ float sacc[4][64];  // per-wave accumulators for lanes < hid: [gn_w, gn_b, w2] + [db2, dgamma, S1, S2]
+  __shared__ float sw[4][8];
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float mu, rs;
+  ma_stats(P, stats, n, HW, mu, rs);
+  float a_gw = 0.f, a_gb = 0.f, a_w2 = 0.f;  // lane c < hid
+  float a_db2 = 0.f, a_dgam = 0.f, a_s1 = 0.f, a_s2 = 0.f;
+  for (int p = wid; p < HW; p += 4) {
+    const long long pix = (long long)n * HW + p;
+    const float mv = ld(m + pix);
+    // recompute forward for this pixel (every lane computes the scalar z)
+    float z = P.b2[0];
+    for (int c = 0; c < P.hid; ++c) z += P.w2[c] * gelu_f((P.w1[c] * mv - mu) * rs * P.g[c] + P.b[c]);
+    const float s = sigmoid_f(z);
+    const float A = fminf(fmaxf(s, 1e-4f), 1.f - 1e-4f);
+    const float gam = P.gamma[0];
+    float gsum = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float d = ld(dout + pix * lddo + c);
+      const float fv = ld(f + pix * ldf + c);
+      gsum += d * fv;
+      st(df + pix * lddf + c, d * (1.f + gam * A));
+    }
+    gsum = wave_sum(gsum);
+    const float dA = gsum * gam;
+    if (lane == 0) a_dgam += gsum * A;
+    const float ds = (s >= 1e-4f && s <= 1.f - 1e-4f) ? dA : 0.f;
+    const float dzv = ds * s * (1.f - s);
+    if (lane == 0) a_db2 += dzv;
+    if (lane < P.hid) {
+      const int c = lane;
+      const float hh = (P.w1[c] * mv - mu) * rs;
+      const float v = hh * P.g[c] + P.b[c];
+      const float u = gelu_f(v);
+      a_w2 += dzv * u;
+      const float dv = dzv * P.w2[c] * gelu_grad_f(v);
+      a_gw += dv * hh;
+      a_gb += dv;
+      const float dh = dv * P.g[c];
+      dhh[pix * P.hid + c] = dh;
+      a_s1 += dh;
+      a_s2 += dh * hh;
+    }
+  }
+  // reduce over the 4 waves
+  a_s1 = wave_sum(a_s1);
+  a_s2 = wave_sum(a_s2);
+  sacc[wid][lane] = a_gw;
+  __syncthreads();
+  if (wid == 0 && lane < P.hid) atomicAdd(grads + P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  __syncthreads();
+  sacc[wid][lane] = a_gb;
+  __syncthreads();
+  if (wid == 0 && lane < P.hid) atomicAdd(grads + 2 * P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  __syncthreads();
+  sacc[wid][lane] = a_w2;
+  __syncthreads();
+  if (wid == 0 && lane < P.hid) atomicAdd(grads + 3 * P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  if (lane == 0) {
+    sw[wid][0] = a_db2;
+    sw[wid][1] = a_dgam;
+    sw[wid][2] = a_s1;
+    sw[wid][3] = a_s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < 4; ++w)
+      for (int k = 0; k < 4; ++k) t[k] += sw[w][k];
+    atomicAdd(grads + 4 * P.hid, t[0]);
+    atomicAdd(grads + 4 * P.hid + 1, t[1]);
+    S[2 * n] = t[2];
+    S[2 * n + 1] = t[3];
+  }
+}
+
+// pass 2: GroupNorm(1,hid) backward + 1x1 conv (1 -> hid) backward
+template <typename T>
+__global__ void k_mask_attn_bwd2(const T* __restrict__ m, MaskAttnB P, const float* __restrict__ stats, int HW,
+                                 const float* __restrict__ dhh, const float* __restrict__ S, T* __restrict__ dm,
+                                 float* __restrict__ grads) {
+  __shared__ float sacc[4][64];
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float mu, rs;
+  ma_stats(P, stats, n, HW, mu, rs);
+  const float G = (float)P.hid * HW;
+  const float m1 = S[2 * n] / G, m2 = S[2 * n + 1] / G;
+  float a_w1 = 0.f;
+  for (int p = wid; p < HW; p += 4) {
+    const long long pix = (long long)n * HW + p;
+    const float mv = ld(m + pix);
+    float contrib = 0.f;
+    if (lane < P.hid) {
+      const int c = lane;
+      const float hh = (P.w1[c] * mv - mu) * rs;
+      const float dh = rs * (dhh[pix * P.hid + c] - m1 - hh * m2);
+      a_w1 += dh * mv;
+      contrib = dh * P.w1[c];
+    }
+    contrib = wave_sum(contrib);
+    if (lane == 0) st(dm + pix, contrib);
+  }
+  sacc[wid][lane] = a_w1;
+  __syncthreads();
+  if (wid == 0 && lane < P.hid) atomicAdd(grads + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, const void* b, int ldb,
+                           const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C,
+                           void* stream) {
+  DMF_CHECK_ARG(dz && a && b && wlogit && da && db && dw, "dmf_mix_bwd: bad args");
+  long long g = (M * C + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_mix_bwd<bf16_t>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz,
+                       lddz, (const bf16_t*)a, lda, (const bf16_t*)b, ldb, wlogit, (bf16_t*)da, (bf16_t*)db, ldd, dw,
+                       M, C);
+  else
+    hipLaunchKernelGGL(k_mix_bwd<float>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
+                       (const float*)a, lda, (const float*)b, ldb, wlogit, (float*)da, (float*)db, ldd, dw, M, C);
+  DMF_LAUNCH_CHECK("dmf_mix_bwd");
+  return 0;
+}
+
+extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int ldf, const void* m, int N,
+                                 int HW, int C, const float* w1, const float* gn_w, const float* gn_b, const float* w2,
+                                 const float* b2, const float* gamma, int hidden, float eps, const float* stats,
+                                 void* df, int lddf, void* dm, float* workspace, float* grads, void* stream) {
+  DMF_CHECK_ARG(dout && f && m && w1 && gn_w && gn_b && w2 && b2 && gamma && stats && df && dm && workspace && grads &&
+                    hidden > 0 && hidden <= 64,
+                "dmf_mask_attn_bwd: bad args");
+  MaskAttnB P{w1, gn_w, gn_b, w2, b2, gamma, eps, hidden};
+  float* dhh = workspace;
+  float* S = workspace + (size_t)N * HW * hidden;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DMF_BF16) {
+    hipLaunchKernelGGL(k_mask_attn_bwd1<bf16_t>, dim3(N), dim3(256), 0, s, (const bf16_t*)dout, lddo, (const bf16_t*)f,
+                       ldf, (const bf16_t*)m, P, stats, HW, C, (bf16_t*)df, lddf, dhh, S, grads);
+    hipLaunchKernelGGL(k_mask_attn_bwd2<bf16_t>, dim3(N), dim3(256), 0, s, (const bf16_t*)m, P, stats, HW, dhh, S,
+                       (bf16_t*)dm, grads);
+  } else {
+    hipLaunchKernelGGL(k_mask_attn_bwd1<float>, dim3(N), dim3(256), 0, s, (const float*)dout, lddo, (const float*)f,
+                       ldf, (const float*)m, P, stats, HW, C, (float*)df, lddf, dhh, S, grads);
+    hipLaunchKernelGGL(k_mask_attn_bwd2<float>, dim3(N), dim3(256), 0, s, (const float*)m, P, stats, HW, dhh, S,
+                       (float*)dm, grads);
+  }
+  DMF_LAUNCH_CHECK("dmf_mask_attn_bwd");
+  return 0;
+}

@@ -17,49 +17,64 @@
 
 namespace dmf {
 
-// one block; B rows, K <= 64 classes. labels int64.
-__global__ void k_focal(const float* __restrict__ logits, const long long* __restrict__ labels, int B, int K,
-                        float smoothing, int smooth, const float* __restrict__ cw, float gamma, float* __restrict__ loss,
-                        float* __restrict__ dlogits) {
+// one block; B rows, K <= 64 classes. Targets: dense soft targets [B][K]
+// (LabelSmoothing output) if given, else int64 labels (one-hot, optionally
+// smoothed in-kernel). reduction: 0 mean, 1 sum, 2 none (per_row only).
+// dlogits: gradient of the reduced loss (per-row loss for 'none').
+__global__ void k_focal(const float* __restrict__ logits, const long long* __restrict__ labels,
+                        const float* __restrict__ soft, int B, int K, float smoothing, int smooth,
+                        const float* __restrict__ cw, float gamma, int reduction, float* __restrict__ loss,
+                        float* __restrict__ per_row, float* __restrict__ dlogits) {
   __shared__ float red[16];
   float acc = 0.f;
+  const float rscale = reduction == 0 ? 1.f / (float)B : 1.f;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const float* z = logits + (size_t)b * K;
     float mx = -INFINITY;
     for (int k = 0; k < K; ++k) mx = fmaxf(mx, z[k]);
     float se = 0.f;
-    for (int k = 0; k < K; ++k) se += __expf(z[k] - mx);
-    const float lse = mx + __logf(se);
-    const long long y = labels[b];
-    // per-class term l_k = -t_k * w_k * (1-p_k)^g * logp_k ; d/dz via chain
-    // d l_k / d logp_j = -t_k w_k [ (1-p)^g * delta_kj  - g (1-p)^(g-1) p_k logp_k delta_kj ] (through p_k = exp(logp_k))
+    for (int k = 0; k < K; ++k) se += expf(z[k] - mx);
+    const float lse = mx + logf(se);
+    const long long y = labels ? labels[b] : -1;
+    // l = -sum_k t_k w_k (1-p_k)^g logp_k ; dl/dlogp_k = -t_k w_k [(1-p)^g - g (1-p)^(g-1) p logp]
     // dlogp_k/dz_j = delta_kj - p_j
     float row = 0.f, gsum = 0.f;
     float gk[64];
     for (int k = 0; k < K; ++k) {
       const float lp = z[k] - lse;
-      const float p = __expf(lp);
-      const float t = smooth ? (k == y ? 1.f - smoothing : smoothing / (float)(K - 1)) : (k == y ? 1.f : 0.f);
+      const float p = expf(lp);
+      float t;
+      if (soft) t = soft[(size_t)b * K + k];
+      else t = smooth ? (k == y ? 1.f - smoothing : smoothing / (float)(K - 1)) : (k == y ? 1.f : 0.f);
       const float w = cw ? cw[k] : 1.f;
       const float om = fmaxf(1.f - p, 0.f);
       const float fw = powf(om, gamma);
       row += -t * w * fw * lp;
-      // dl_k/dlogp_k
       const float dfw = gamma > 0.f && om > 0.f ? gamma * powf(om, gamma - 1.f) : 0.f;
       const float g = -t * w * (fw - dfw * p * lp);
       gk[k] = g;
       gsum += g;
     }
     acc += row;
+    if (per_row) per_row[b] = row;
     if (dlogits) {
       for (int j = 0; j < K; ++j) {
-        const float pj = __expf(z[j] - lse);
-        dlogits[(size_t)b * K + j] = (gk[j] - pj * gsum) / (float)B;
+        const float pj = expf(z[j] - lse);
+        dlogits[(size_t)b * K + j] = (gk[j] - pj * gsum) * rscale;
       }
     }
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) loss[0] = acc / (float)B;
+  if (threadIdx.x == 0 && loss) loss[0] = acc * rscale;
+}
+
+// LabelSmoothing (loss.py:190-213): fill smoothing/(K-1), label -> 1-smoothing
+__global__ void k_label_smooth(const long long* __restrict__ labels, int B, int K, float smoothing,
+                               float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * K) return;
+  const int b = i / K, k = i % K;
+  out[i] = labels[b] == k ? 1.f - smoothing : smoothing / (float)(K - 1);
 }
 
 // soft dice over [B][P] logits, target [B][P]; block per sample writes its dice,
@@ -185,17 +200,19 @@ __global__ void k_recon(ReconArgs a) {
 }
 
 // ------------------------------------------------------------ mimic
-// pairs (s = items[2i], t = items[2i+1]) for i < npairs, feature map NHWC
-// [HW][C] per item; per channel cosine over HW; loss_i = mean_c(1 - clamp(cos)),
-// returns mean over pairs. Gradient only for the student item.
+// pair i: student S_i = s + i*sstride, teacher T_i = t + i*tstride, each an
+// [HW][C] NHWC map (channel stride ld). mimic_feat_loss flattens [C,H,W] to
+// [C, HW]: per-channel cosine over HW; loss = mean over channels and pairs.
+// Gradient only for the student (teacher detached).
 template <typename T>
-__global__ void k_mimic(const T* __restrict__ f, int ldm, int HW, int C, int npairs, float eps_norm, float eps_clamp,
-                        float* __restrict__ loss, float* __restrict__ dstudent /* [npairs][HW][C] */) {
+__global__ void k_mimic(const T* __restrict__ sbase, const T* __restrict__ tbase, long long sstride,
+                        long long tstride, int ldm, int HW, int C, int npairs, float eps_norm, float eps_clamp,
+                        float* __restrict__ loss, T* __restrict__ dstudent, long long dstride) {
   // block per (pair, channel)
   __shared__ float red[16];
   const int pr = blockIdx.x / C, c = blockIdx.x % C;
-  const T* S = f + (size_t)(2 * pr) * HW * ldm + c;
-  const T* Tt = f + (size_t)(2 * pr + 1) * HW * ldm + c;
+  const T* S = sbase + (size_t)pr * sstride + c;
+  const T* Tt = tbase + (size_t)pr * tstride + c;
   float ss = 0.f, tt = 0.f, st_ = 0.f;
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     const float sv = ld(S + (size_t)p * ldm), tv = ld(Tt + (size_t)p * ldm);
@@ -211,18 +228,18 @@ __global__ void k_mimic(const T* __restrict__ f, int ldm, int HW, int C, int npa
   const float lo = -1.f + eps_clamp, hi = 1.f - eps_clamp;
   if (threadIdx.x == 0) atomicAdd(loss, (1.f - fminf(fmaxf(cos, lo), hi)) / (float)(C * npairs));
   if (dstudent) {
-    const bool pass = cos > lo && cos < hi;
+    const bool pass = cos >= lo && cos <= hi;
     const float scale = -1.f / (float)(C * npairs);
     const bool snorm_active = sqrtf(ss) > eps_norm;
+    T* D = dstudent + (size_t)pr * dstride + c;
     for (int p = threadIdx.x; p < HW; p += blockDim.x) {
       float g = 0.f;
       if (pass) {
         const float sv = ld(S + (size_t)p * ldm), tv = ld(Tt + (size_t)p * ldm);
-        // d cos / d s_p = t_p/(ns*nt) - cos * s_p / ns^2   (if |s| > eps)
         g = tv / (ns * nt) - (snorm_active ? cos * sv / (ns * ns) : 0.f);
         g *= scale;
       }
-      dstudent[((size_t)pr * HW + p) * C + c] = g;
+      st(D + (size_t)p * ldm, g);
     }
   }
 }
@@ -254,13 +271,22 @@ static inline int gsz(long long n) {
 
 using namespace dmf;
 
-extern "C" int dmf_focal_loss(const float* logits, const long long* labels, int B, int K, float smoothing,
-                              int use_smoothing, const float* class_weights, float gamma, float* loss, float* dlogits,
-                              void* stream) {
-  DMF_CHECK_ARG(logits && labels && loss && B > 0 && K > 1 && K <= 64, "dmf_focal_loss: bad args (K=%d)", K);
-  hipLaunchKernelGGL(k_focal, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, B, K, smoothing,
-                     use_smoothing, class_weights, gamma, loss, dlogits);
+extern "C" int dmf_focal_loss(const float* logits, const long long* labels, const float* soft_targets, int B, int K,
+                              float smoothing, int use_smoothing, const float* class_weights, float gamma,
+                              int reduction, float* loss, float* per_row, float* dlogits, void* stream) {
+  DMF_CHECK_ARG(logits && (labels || soft_targets) && B > 0 && K > 1 && K <= 64 && reduction >= 0 && reduction <= 2,
+                "dmf_focal_loss: bad args (K=%d, reduction=%d)", K, reduction);
+  hipLaunchKernelGGL(k_focal, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, soft_targets, B, K,
+                     smoothing, use_smoothing, class_weights, gamma, reduction, loss, per_row, dlogits);
   DMF_LAUNCH_CHECK("dmf_focal_loss");
+  return 0;
+}
+
+extern "C" int dmf_label_smooth(const long long* labels, int B, int K, float smoothing, float* out, void* stream) {
+  DMF_CHECK_ARG(labels && out && B > 0 && K > 1, "dmf_label_smooth: bad args");
+  hipLaunchKernelGGL(k_label_smooth, dim3(cdiv(B * K, 256)), dim3(256), 0, (hipStream_t)stream, labels, B, K,
+                     smoothing, out);
+  DMF_LAUNCH_CHECK("dmf_label_smooth");
   return 0;
 }
 
@@ -314,15 +340,18 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
   return 0;
 }
 
-extern "C" int dmf_mimic_loss(int dtype, const void* feats, int ld, int HW, int C, int npairs, float* loss,
-                              float* dstudent, void* stream) {
-  DMF_CHECK_ARG(feats && loss && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
+extern "C" int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long long sstride,
+                              long long tstride, int ld, int HW, int C, int npairs, float* loss, void* dstudent,
+                              long long dstride, void* stream) {
+  DMF_CHECK_ARG(student && teacher && loss && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
   if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_mimic<bf16_t>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)feats, ld,
-                       HW, C, npairs, 1e-12f, 1e-6f, loss, dstudent);
+    hipLaunchKernelGGL(k_mimic<bf16_t>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)student,
+                       (const bf16_t*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
+                       (bf16_t*)dstudent, dstride);
   else
-    hipLaunchKernelGGL(k_mimic<float>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const float*)feats, ld, HW,
-                       C, npairs, 1e-12f, 1e-6f, loss, dstudent);
+    hipLaunchKernelGGL(k_mimic<float>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const float*)student,
+                       (const float*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
+                       (float*)dstudent, dstride);
   DMF_LAUNCH_CHECK("dmf_mimic_loss");
   return 0;
 }

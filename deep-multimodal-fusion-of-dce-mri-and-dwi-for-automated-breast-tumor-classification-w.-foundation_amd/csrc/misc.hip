@@ -30,16 +30,20 @@ __global__ void k_input_prep(const float* __restrict__ x, int N, int C, int H, i
        i += (long long)gridDim.x * blockDim.x) {
     const long long n = i / HW, p = i - n * HW;
     const float* src = x + n * C * HW + p;
-    T* dst = y + i * Cp;
     float s = 0.f;
-    for (int c = 0; c < Cp; ++c) {
-      float v = 0.f;
-      if (c < C) {
-        v = src[c * HW];
-        s += v;
-        if (gate) v *= gate[n * C + c];
+    if (y) {
+      T* dst = y + i * Cp;
+      for (int c = 0; c < Cp; ++c) {
+        float v = 0.f;
+        if (c < C) {
+          v = src[c * HW];
+          s += v;
+          if (gate) v *= gate[n * C + c];
+        }
+        dst[c] = Cvt<T>::store(v);
       }
-      dst[c] = Cvt<T>::store(v);
+    } else {
+      for (int c = 0; c < C; ++c) s += src[c * HW];
     }
     if (cmean) cmean[i] = s / (float)C;
   }
@@ -240,22 +244,22 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int 
 
 // ----------------------------------------------------------- resampling
 template <typename T>
-__global__ void k_up2_nearest(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C) {
-  const long long total = (long long)N * 2 * H * 2 * W * C;
+__global__ void k_up_nearest(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C, int r) {
+  const long long total = (long long)N * r * H * r * W * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     long long t = i / C;
-    const int wo = (int)(t % (2 * W)); t /= (2 * W);
-    const int ho = (int)(t % (2 * H));
-    const int n = (int)(t / (2 * H));
-    y[i] = x[((size_t)(n * H + ho / 2) * W + wo / 2) * ldx + c];
+    const int wo = (int)(t % (r * W)); t /= (r * W);
+    const int ho = (int)(t % (r * H));
+    const int n = (int)(t / (r * H));
+    y[i] = x[((size_t)(n * H + ho / r) * W + wo / r) * ldx + c];
   }
 }
 
-// sum of the 2x2 replicas (backward of nearest 2x upsample)
+// sum of the r x r replicas (backward of nearest r-x upsample)
 template <typename T>
-__global__ void k_up2_nearest_bwd(const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C) {
+__global__ void k_up_nearest_bwd(const T* __restrict__ dy, T* __restrict__ dx, int N, int H, int W, int C, int r) {
   const long long total = (long long)N * H * W * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -265,8 +269,8 @@ __global__ void k_up2_nearest_bwd(const T* __restrict__ dy, T* __restrict__ dx, 
     const int h = (int)(t % H);
     const int n = (int)(t / H);
     float s = 0.f;
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b) s += ld(dy + ((size_t)(n * 2 * H + 2 * h + a) * 2 * W + 2 * w + b) * C + c);
+    for (int a = 0; a < r; ++a)
+      for (int b = 0; b < r; ++b) s += ld(dy + ((size_t)(n * r * H + r * h + a) * r * W + r * w + b) * C + c);
     st(dx + i, s);
   }
 }
@@ -446,7 +450,7 @@ using namespace dmf;
 
 extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, int W, const float* gate, void* y, int Cp,
                               float* chan_mean, void* stream) {
-  DMF_CHECK_ARG(x && y && Cp >= C, "dmf_input_prep: bad args");
+  DMF_CHECK_ARG(x && (y || chan_mean) && Cp >= C, "dmf_input_prep: bad args");
   const long long total = (long long)N * H * W;
   if (total == 0) return 0;
   if (dtype == DMF_BF16)
@@ -576,33 +580,33 @@ extern "C" int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, 
   return 0;
 }
 
-extern "C" int dmf_upsample2x_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C,
-                                      void* stream) {
-  DMF_CHECK_ARG(x && y, "dmf_upsample2x_nearest: bad args");
-  const long long total = (long long)N * 4 * H * W * C;
+extern "C" int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, int r,
+                                    void* stream) {
+  DMF_CHECK_ARG(x && y && r >= 1, "dmf_upsample_nearest: bad args");
+  const long long total = (long long)N * r * r * H * W * C;
   if (total == 0) return 0;
   if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_up2_nearest<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, (bf16_t*)y, N, H, W, C);
+    hipLaunchKernelGGL(k_up_nearest<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       ldx, (bf16_t*)y, N, H, W, C, r);
   else
-    hipLaunchKernelGGL(k_up2_nearest<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
-                       (float*)y, N, H, W, C);
-  DMF_LAUNCH_CHECK("dmf_upsample2x_nearest");
+    hipLaunchKernelGGL(k_up_nearest<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
+                       (float*)y, N, H, W, C, r);
+  DMF_LAUNCH_CHECK("dmf_upsample_nearest");
   return 0;
 }
 
-extern "C" int dmf_upsample2x_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C,
-                                          void* stream) {
-  DMF_CHECK_ARG(dy && dx, "dmf_upsample2x_nearest_bwd: bad args");
+extern "C" int dmf_upsample_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C, int r,
+                                        void* stream) {
+  DMF_CHECK_ARG(dy && dx && r >= 1, "dmf_upsample_nearest_bwd: bad args");
   const long long total = (long long)N * H * W * C;
   if (total == 0) return 0;
   if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_up2_nearest_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, (bf16_t*)dx, N, H, W, C);
+    hipLaunchKernelGGL(k_up_nearest_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, (bf16_t*)dx, N, H, W, C, r);
   else
-    hipLaunchKernelGGL(k_up2_nearest_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
-                       (float*)dx, N, H, W, C);
-  DMF_LAUNCH_CHECK("dmf_upsample2x_nearest_bwd");
+    hipLaunchKernelGGL(k_up_nearest_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
+                       (float*)dx, N, H, W, C, r);
+  DMF_LAUNCH_CHECK("dmf_upsample_nearest_bwd");
   return 0;
 }
 

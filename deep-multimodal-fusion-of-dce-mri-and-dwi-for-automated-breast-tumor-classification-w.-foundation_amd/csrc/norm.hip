@@ -199,7 +199,7 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dz, int lddz, const T* __r
 
 // sum tiles -> dbeta (=sum dz), dgamma (=sum dz*xhat) (accumulated into the
 // fp32 grads if given) and dx coefficients coef[3][C]: dx = A*dz + Cc*x + B
-__global__ void k_bn_bwd_finalize(const float* __restrict__ part, int T, int C, double count,
+__global__ void k_bn_bwd_finalize(const float* __restrict__ part, int T, int C, double count, int training,
                                   const float* __restrict__ gamma, const float* __restrict__ save,
                                   float* dgamma, float* dbeta, float* __restrict__ coef) {
   __shared__ double red[4][64][2];
@@ -224,8 +224,9 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ part, int T, int C, 
       const double g = gamma ? gamma[c] : 1.0;
       const double mean = save[c], inv = save[C + c];
       const double A = g * inv;
-      const double Cc = -g * inv * inv * q / count;
-      const double B = -g * inv * s / count - Cc * mean;
+      // eval-mode BN (running stats) is a per-channel affine: dx = A*dz
+      const double Cc = training ? -g * inv * inv * q / count : 0.0;
+      const double B = training ? -g * inv * s / count - Cc * mean : 0.0;
       coef[c] = (float)A;
       coef[C + c] = (float)Cc;
       coef[2 * C + c] = (float)B;
@@ -333,13 +334,13 @@ extern "C" int dmf_bn_bwd_reduce(int dtype, const void* dz, int lddz, const void
   return 0;
 }
 
-extern "C" int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, const float* gamma,
-                                   const float* save_mean_invstd, float* dgamma, float* dbeta, float* coef,
-                                   void* stream) {
+extern "C" int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, int training,
+                                   const float* gamma, const float* save_mean_invstd, float* dgamma, float* dbeta,
+                                   float* coef, void* stream) {
   DMF_CHECK_ARG(partials && ntiles > 0 && C > 0, "dmf_bn_bwd_finalize: bad args");
   DMF_CHECK_ARG(!coef || save_mean_invstd, "dmf_bn_bwd_finalize: coef needs saved stats");
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C,
-                     count, gamma, save_mean_invstd, dgamma, dbeta, coef);
+                     count, training, gamma, save_mean_invstd, dgamma, dbeta, coef);
   DMF_LAUNCH_CHECK("dmf_bn_bwd_finalize");
   return 0;
 }

@@ -1,0 +1,1381 @@
+"""Autograd-aware wrappers around the HIP kernels of ``libdmf_hip.so``.
+
+Activations travel as torch tensors with NCHW *logical* shape and NHWC
+(``channels_last``) *physical* layout, so callers of the reference API see the
+shapes ``model_module.py`` documents while every kernel reads contiguous
+channel vectors. Channel slices of a wider buffer (concat without copies,
+``BackboneAdapter`` chains at model_module.py:453-472) are plain strided views:
+``ld`` (the channel stride) is read off the tensor's strides.
+
+Every op here runs on the device through the C-ABI; there is no CPU path.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+
+import torch
+
+import dmf_native as N
+
+F32, BF16 = N.F32, N.BF16
+ACT = {"none": N.ACT_NONE, "relu": N.ACT_RELU, "gelu": N.ACT_GELU, "sigmoid": N.ACT_SIGMOID}
+
+
+def _stream():
+    return N.stream_ptr()
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------ layout
+def nhwc(t):
+    """(N, C, H, W, ld) of an NCHW-logical, NHWC-physical tensor (or slice)."""
+    if t.dim() != 4:
+        raise RuntimeError(f"expected a 4-D activation, got shape {tuple(t.shape)}")
+    n, c, h, w = t.shape
+    s0, s1, s2, s3 = t.stride()
+    ld = s3 if w > 1 else (s2 // max(w, 1) if h > 1 else (s0 // max(h * w, 1) if n > 1 else c))
+    ok = (c == 1 or s1 == 1) and (w == 1 or s3 == ld) and (h == 1 or s2 == w * ld) and (n == 1 or s0 == h * w * ld)
+    if not ok:
+        raise RuntimeError(f"tensor is not NHWC-addressable: shape {tuple(t.shape)} strides {t.stride()}")
+    return n, c, h, w, ld
+
+
+def as_nhwc(t):
+    """Make t NHWC-addressable (a copy only if it is not already)."""
+    try:
+        nhwc(t)
+        return t
+    except RuntimeError:
+        return t.contiguous(memory_format=torch.channels_last)
+
+
+def empty_nhwc(n, c, h, w, dtype, device):
+    return torch.empty((n, c, h, w), dtype=dtype, device=device, memory_format=torch.channels_last)
+
+
+def dt(t):
+    return N.dtype_code(t.dtype)
+
+
+# ------------------------------------------------------------- dropout rng
+class _Rng:
+    """Per-device Philox state (seed, offset) kept in device memory."""
+
+    def __init__(self):
+        self.states = {}
+        self.site_ids = itertools.count(1)
+
+    def state(self, device):
+        key = torch.device(device).index or 0
+        st = self.states.get(key)
+        if st is None:
+            seed = torch.initial_seed() & ((1 << 63) - 1)
+            st = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+            self.states[key] = st
+        return st
+
+    def snapshot(self, device):
+        """Copy of the current (seed, offset) for one model forward; the
+        global offset advances so the next forward draws new masks."""
+        st = self.state(device)
+        snap = st.clone()
+        N.call("dmf_rng_advance", st.data_ptr(), 1, _stream())
+        return snap
+
+    def manual_seed(self, seed, device):
+        st = self.state(device)
+        st.copy_(torch.tensor([seed, 0], dtype=torch.int64))
+
+    def new_site(self):
+        return next(self.site_ids)
+
+
+RNG = _Rng()
+
+
+# ------------------------------------------------------------ weight cache
+class WeightCache:
+    """Device re-layout of a conv weight ([Cout][KH][KW][CinP] / transposed)
+    in the compute dtype. Frozen weights are prepared once per version;
+    trainable ones every call (so a captured graph re-reads updated params)."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, weight, dtype, cinp, mode):
+        co, ci, kh, kw = weight.shape
+        key = (weight.data_ptr(), weight._version, dtype, cinp, mode)
+        if not weight.requires_grad and self.key == key:
+            return self.val
+        shape = (co, kh, kw, cinp) if mode == 0 else (cinp, kh, kw, co)
+        out = torch.empty(shape, dtype=dtype, device=weight.device)
+        w = weight.detach()
+        if not w.is_contiguous():
+            w = w.contiguous()
+        N.call("dmf_conv_weight_prep", N.dtype_code(dtype), w.data_ptr(), out.data_ptr(), co, ci, cinp, kh, kw, mode,
+               _stream())
+        if not weight.requires_grad:
+            self.key, self.val = key, out
+        return out
+
+
+# =================================================================== conv
+class ConvGeom:
+    __slots__ = ("stride", "pad", "dil", "kh", "kw")
+
+    def __init__(self, conv):
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.dil = conv.dilation[0]
+        self.kh, self.kw = conv.kernel_size
+
+    def out_hw(self, h, w):
+        ho = (h + 2 * self.pad - self.dil * (self.kh - 1) - 1) // self.stride + 1
+        wo = (w + 2 * self.pad - self.dil * (self.kw - 1) - 1) // self.stride + 1
+        return ho, wo
+
+
+def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=None):
+    """Returns (y, partials|None). partials: [tiles][Cout][2] fp32.
+    x2: optional second input concatenated along channels (no copy)."""
+    n, cx, h, w, ldx = nhwc(x)
+    cx2, ldx2 = 0, 0
+    if x2 is not None:
+        _, cx2, _, _, ldx2 = nhwc(x2)
+    co, ci, kh, kw = weight.shape
+    ho, wo = g.out_hw(h, w)
+    dtc = dt(x)
+    dev = x.device
+    if out is None:
+        y = empty_nhwc(n, co, ho, wo, x.dtype, dev)
+    else:
+        y = out
+    _, _, _, _, ldy = nhwc(y)
+    partials = None
+    act_c = ACT[act]
+    if x2 is not None and (co == 1 or ci == 1):
+        raise RuntimeError("channel-concat input only supported on the MFMA conv path")
+    if co == 1:
+        wf = caches[0].get(weight, torch.float32, cx, 0)
+        N.call("dmf_conv_cout1_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, wf.data_ptr(), _p(bias), kh, kw, g.stride,
+               g.pad, g.dil, y.data_ptr(), ho, wo, ldy, act_c if not want_stats else N.ACT_NONE, _stream())
+        if want_stats:
+            partials = _col_stats(y)
+    elif ci == 1 and kh == 1 and kw == 1 and g.stride == 1:
+        wf = weight.detach().reshape(co).contiguous()
+        N.call("dmf_conv_cin1_fwd", dtc, x.data_ptr(), ldx, wf.data_ptr(), _p(bias), y.data_ptr(), ldy, n * h * w, co,
+               act_c if not want_stats else N.ACT_NONE, _stream())
+        if want_stats:
+            partials = _col_stats(y)
+    else:
+        wk = caches[0].get(weight, x.dtype, cx + cx2, 0)
+        if want_stats:
+            tiles = (n * ho * wo + 127) // 128
+            partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
+        N.call("dmf_conv2d_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
+               g.stride, g.pad,
+               g.dil, _p(bias), y.data_ptr(), ho, wo, ldy, _p(partials), act_c if not want_stats else N.ACT_NONE,
+               _stream())
+    return y, partials
+
+
+def _col_stats(y):
+    n, c, h, w, ld = nhwc(y)
+    m = n * h * w
+    tiles = (m + 255) // 256
+    part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
+    N.call("dmf_col_stats", dt(y), y.data_ptr(), ld, m, c, part.data_ptr(), _stream())
+    return part
+
+
+def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None):
+    """Returns (dx, dw, db) -- with x2 given, dx is (dx, dx2) (views into one
+    concat-gradient buffer)."""
+    n, cx, h, w, ldx = nhwc(x)
+    cx2, ldx2 = 0, 0
+    if x2 is not None:
+        _, cx2, _, _, ldx2 = nhwc(x2)
+    co, ci, kh, kw = weight.shape
+    dy = as_nhwc(dy)
+    _, _, ho, wo, lddy = nhwc(dy)
+    dtc = dt(x)
+    dev = x.device
+    dx = dw = db = None
+    m = n * ho * wo
+    if need_dx:
+        dx = empty_nhwc(n, cx + cx2, h, w, x.dtype, dev)
+        _, _, _, _, lddx = nhwc(dx)
+        if co == 1:
+            wf = caches[0].get(weight, torch.float32, cx, 0)
+            N.call("dmf_conv_cout1_dgrad", dtc, dy.data_ptr(), lddy, wf.data_ptr(), n, h, w, cx, kh, kw, g.stride,
+                   g.pad, g.dil, ho, wo, dx.data_ptr(), lddx, _stream())
+        elif ci == 1 and kh == 1 and kw == 1 and g.stride == 1:
+            wf = weight.detach().reshape(co).contiguous()
+            N.call("dmf_conv_cin1_dgrad", dtc, dy.data_ptr(), lddy, wf.data_ptr(), dx.data_ptr(), lddx, n * h * w, co,
+                   _stream())
+        else:
+            wt = caches[1].get(weight, x.dtype, cx + cx2, 1)
+            N.call("dmf_conv2d_dgrad", dtc, dy.data_ptr(), n, ho, wo, co, lddy, wt.data_ptr(), cx + cx2, kh, kw,
+                   g.stride, g.pad, g.dil, dx.data_ptr(), h, w, lddx, _stream())
+        if x2 is not None:
+            dx = (dx[:, :cx], dx[:, cx:])
+    if need_dw or need_db:
+        if co == 1:
+            splits = N.load().dmf_conv_cout1_wgrad_splits(m)
+            k = kh * kw * cx
+            ws = torch.empty(splits * k + splits, dtype=torch.float32, device=dev)
+            dwl = torch.zeros(k, dtype=torch.float32, device=dev) if need_dw else None
+            db = torch.zeros(1, dtype=torch.float32, device=dev) if need_db else None
+            N.call("dmf_conv_cout1_wgrad", dtc, x.data_ptr(), n, h, w, cx, ldx, dy.data_ptr(), lddy, kh, kw, g.stride,
+                   g.pad, g.dil, ho, wo, splits, ws.data_ptr(), _p(dwl), _p(db), _stream())
+            if need_dw:
+                # [KH][KW][CinP] -> torch [1][Cin][KH][KW]
+                dw = dwl.view(kh, kw, cx)[:, :, :ci].permute(2, 0, 1).unsqueeze(0).contiguous()
+        elif ci == 1 and kh == 1 and kw == 1 and g.stride == 1:
+            tiles = (n * h * w + 255) // 256
+            ws = torch.empty(2 * tiles * co, dtype=torch.float32, device=dev)
+            dwl = torch.zeros(co, dtype=torch.float32, device=dev)
+            db = torch.zeros(co, dtype=torch.float32, device=dev) if need_db else None
+            N.call("dmf_conv_cin1_wgrad", dtc, x.data_ptr(), ldx, dy.data_ptr(), lddy, n * h * w, co, ws.data_ptr(),
+                   dwl.data_ptr(), _p(db), _stream())
+            dw = dwl.view(co, 1, 1, 1) if need_dw else None
+        else:
+            if need_dw:
+                ct = cx + cx2
+                splits = N.load().dmf_conv2d_wgrad_splits(dtc, co, ct, kh, kw, m)
+                ws = torch.empty(splits * co * kh * kw * ct, dtype=torch.float32, device=dev)
+                N.call("dmf_conv2d_wgrad", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, dy.data_ptr(), ho,
+                       wo, co, lddy, kh, kw, g.stride, g.pad, g.dil, splits, ws.data_ptr(), _stream())
+                dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dev)
+                N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), splits, co, ci, ct, kh, kw, dw.data_ptr(), 0,
+                       _stream())
+            if need_db:
+                db = _colsum_nhwc(dy)
+    return dx, dw, db
+
+
+def _colsum_nhwc(t):
+    """sum over (N,H,W) per channel -> fp32 [C]"""
+    n, c, h, w, ld = nhwc(t)
+    m = n * h * w
+    tiles = (m + 255) // 256
+    part = torch.empty((tiles, c, 2), dtype=torch.float32, device=t.device)
+    N.call("dmf_bn_bwd_reduce", dt(t), t.data_ptr(), ld, None, 0, None, m, c, part.data_ptr(), _stream())
+    out = torch.zeros(c, dtype=torch.float32, device=t.device)
+    N.call("dmf_bn_bwd_finalize", part.data_ptr(), tiles, c, float(m), 1, None, None, None, out.data_ptr(), None,
+           _stream())
+    return out
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, g, caches, act):
+        y, _ = _conv_forward_raw(x, weight, bias, g, caches, False, act)
+        if act != "none" and torch.is_grad_enabled():
+            raise RuntimeError("fused conv activation is forward-only")
+        ctx.save_for_backward(x, weight, bias)
+        ctx.g, ctx.caches = g, caches
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias = ctx.saved_tensors
+        dx, dw, db = _conv_backward(x, weight, bias, ctx.g, ctx.caches, dy, ctx.needs_input_grad[0],
+                                    ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
+        return dx, dw, db, None, None, None
+
+
+def conv2d(x, conv, caches, act="none"):
+    """nn.Conv2d forward on NHWC data (no BN). ``act`` only when no grad."""
+    g = ConvGeom(conv)
+    if act != "none":
+        with torch.no_grad():
+            y, _ = _conv_forward_raw(x, conv.weight, conv.bias, g, caches, False, act)
+        return y
+    return _ConvFn.apply(x, conv.weight, conv.bias, g, caches, "none")
+
+
+# ================================================= conv + batch norm + act
+class BNState:
+    """Handles of one nn.BatchNorm2d for the fused kernels."""
+
+    __slots__ = ("bn",)
+
+    def __init__(self, bn):
+        self.bn = bn
+
+
+def _bn_finalize(partials, count, bn, unbias_count=0.0):
+    c = bn.num_features
+    dev = partials.device if partials is not None else bn.weight.device
+    ss = torch.empty(2 * c, dtype=torch.float32, device=dev)
+    save = torch.empty(2 * c, dtype=torch.float32, device=dev)
+    training = bn.training or bn.running_mean is None
+    track = bn.training and bn.track_running_stats and bn.running_mean is not None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    N.call("dmf_bn_finalize", _p(partials), 0 if partials is None else partials.shape[0], c, float(count),
+           float(unbias_count), _p(bn.weight), _p(bn.bias), _p(bn.running_mean) if (track or not training) else None,
+           _p(bn.running_var) if (track or not training) else None,
+           _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), 1 if training else 0,
+           ss.data_ptr(), save.data_ptr(), _stream())
+    return ss, save
+
+
+class _ConvBNActFn(torch.autograd.Function):
+    """act( BN(conv(x)) [+ residual] ) [-> dropout]; the residual is either a
+    raw tensor (identity skip) or BN(conv_skip(x_skip)) (projection skip).
+
+    Inputs needing grads: x, w, b, gamma, beta, (x_r, w_r, gamma_r, beta_r | res).
+    """
+
+    @staticmethod
+    def forward(ctx, x, x2, w, b, gamma, beta, res, xr, wr, gamma_r, beta_r, spec):
+        (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult) = spec
+        y, part = _conv_forward_raw(x, w, b, g, caches, True, "none", x2=x2)
+        n, c, ho, wo, ldy = nhwc(y)
+        m = n * ho * wo
+        ss, save = _bn_finalize(part, m, bn, unbias_count=m * unbias_mult if unbias_mult != 1 else 0.0)
+        yr = ss_r = save_r = None
+        if xr is not None:
+            yr, part_r = _conv_forward_raw(xr, wr, None, gr, caches_r, True, "none")
+            ss_r, save_r = _bn_finalize(part_r, m, bn_r)
+            res_t, ldr = yr, nhwc(yr)[4]
+        elif res is not None:
+            res_t, ldr = res, nhwc(res)[4]
+        else:
+            res_t, ldr = None, 0
+        out = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        N.call("dmf_affine_act", dt(y), y.data_ptr(), ldy, ss.data_ptr(), _p(res_t), ldr, _p(ss_r), ACT[act],
+               float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
+        ctx.save_for_backward(x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng)
+        ctx.spec = spec
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng) = ctx.saved_tensors
+        (g, caches, bn, act, p, _rng, site, gr, caches_r, bn_r, unbias_mult) = ctx.spec
+        dout = as_nhwc(dout)
+        n, c, ho, wo, ldy = nhwc(y)
+        m = n * ho * wo
+        dtc = dt(y)
+        res_t = yr if yr is not None else res
+        ldr = nhwc(res_t)[4] if res_t is not None else 0
+        dz = empty_nhwc(n, c, ho, wo, y.dtype, y.device)
+        N.call("dmf_act_bwd", dtc, dout.data_ptr(), nhwc(dout)[4], y.data_ptr(), ldy, ss.data_ptr(), _p(res_t), ldr,
+               _p(ss_r), ACT[act], float(p), _p(rng), site, dz.data_ptr(), nhwc(dz)[4], m, c, _stream())
+        need = ctx.needs_input_grad
+        dgamma = torch.zeros_like(bn.weight) if need[4] else None
+        dbeta = torch.zeros_like(bn.bias) if need[5] else None
+        dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training)
+        need_dx = need[0] or (x2 is not None and need[1])
+        dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2)
+        dx2 = None
+        if x2 is not None and dx is not None:
+            dx, dx2 = dx
+        dres = dxr = dwr = dgr = dbr = None
+        if xr is not None:
+            dgr = torch.zeros_like(bn_r.weight) if need[9] else None
+            dbr = torch.zeros_like(bn_r.bias) if need[10] else None
+            dyr = _bn_backward(dz, yr, save_r, bn_r, dgr, dbr, training=bn_r.training)
+            dxr, dwr, _ = _conv_backward(xr, wr, None, gr, caches_r, dyr, need[7], need[8], False)
+        elif res is not None and need[6]:
+            dres = dz
+        return dx, dx2, dw, db, dgamma, dbeta, dres, dxr, dwr, dgr, dbr, None
+
+
+def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True):
+    n, c, h, w, ldy = nhwc(y)
+    m = n * h * w
+    tiles = (m + 255) // 256
+    part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
+    N.call("dmf_bn_bwd_reduce", dt(y), dz.data_ptr(), nhwc(dz)[4], y.data_ptr(), ldy, save.data_ptr(), m, c,
+           part.data_ptr(), _stream())
+    coef = torch.empty(3 * c, dtype=torch.float32, device=y.device)
+    N.call("dmf_bn_bwd_finalize", part.data_ptr(), tiles, c, float(m), 1 if training else 0, _p(bn.weight),
+           save.data_ptr(), _p(dgamma), _p(dbeta), coef.data_ptr(), _stream())
+    dy = empty_nhwc(n, c, h, w, y.dtype, y.device)
+    N.call("dmf_bn_bwd_apply", dt(y), dz.data_ptr(), nhwc(dz)[4], y.data_ptr(), ldy, coef.data_ptr(), dy.data_ptr(),
+           nhwc(dy)[4], m, c, _stream())
+    return dy
+
+
+def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0, res=None, skip=None,
+                unbias_mult=1, x2=None):
+    """act(bn(conv(x)) + residual) with optional dropout.
+
+    ``skip`` = (x_skip, conv_skip, caches_skip, bn_skip) for a projection
+    shortcut; ``res`` = an identity-shortcut tensor. ``unbias_mult`` scales the
+    element count used for the running-variance correction (a map that the
+    reference evaluates after a nearest 2x upsample has 4x the elements)."""
+    g = ConvGeom(conv)
+    p = float(dropout_p) if bn.training else 0.0
+    if p > 0 and rng is None:
+        raise RuntimeError("dropout requested without an rng snapshot")
+    if skip is not None:
+        xr, conv_r, caches_r, bn_r = skip
+        gr = ConvGeom(conv_r)
+        wr, gamma_r, beta_r = conv_r.weight, bn_r.weight, bn_r.bias
+    else:
+        xr = wr = gamma_r = beta_r = None
+        gr = caches_r = bn_r = None
+    spec = (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult)
+    return _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r, beta_r, spec)
+
+
+# ============================================================ elementwise
+class _AffineActFn(torch.autograd.Function):
+    """y = drop(act(x [+ res])) on NHWC data (no BN)."""
+
+    @staticmethod
+    def forward(ctx, x, res, act, p, rng, site):
+        n, c, h, w, ldx = nhwc(x)
+        out = empty_nhwc(n, c, h, w, x.dtype, x.device)
+        ldr = nhwc(res)[4] if res is not None else 0
+        N.call("dmf_affine_act", dt(x), x.data_ptr(), ldx, None, _p(res), ldr, None, ACT[act], float(p), _p(rng),
+               site, out.data_ptr(), nhwc(out)[4], n * h * w, c, _stream())
+        ctx.save_for_backward(x, res, rng)
+        ctx.cfg = (act, p, site)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, res, rng = ctx.saved_tensors
+        act, p, site = ctx.cfg
+        dout = as_nhwc(dout)
+        n, c, h, w, ldx = nhwc(x)
+        dz = empty_nhwc(n, c, h, w, x.dtype, x.device)
+        ldr = nhwc(res)[4] if res is not None else 0
+        N.call("dmf_act_bwd", dt(x), dout.data_ptr(), nhwc(dout)[4], x.data_ptr(), ldx, None, _p(res), ldr, None,
+               ACT[act], float(p), _p(rng), site, dz.data_ptr(), nhwc(dz)[4], n * h * w, c, _stream())
+        return dz, (dz if res is not None and ctx.needs_input_grad[1] else None), None, None, None, None
+
+
+def act_nhwc(x, act, res=None, dropout_p=0.0, rng=None, site=0):
+    return _AffineActFn.apply(x, res, act, float(dropout_p), rng, site)
+
+
+def spatial_mean(x):
+    """AdaptiveAvgPool2d(1) -> fp32 [N][C] (forward only helper)."""
+    n, c, h, w, ld = nhwc(x)
+    out = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    N.call("dmf_nhwc_reduce", dt(x), x.data_ptr(), ld, None, 0, n, h * w, c, 1.0 / (h * w), out.data_ptr(), 0,
+           _stream())
+    return out
+
+
+class _GapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        ctx.dtype = x.dtype
+        return spatial_mean(x)
+
+    @staticmethod
+    def backward(ctx, dv):
+        n, c, h, w = ctx.shape
+        dv = dv.contiguous().float()
+        dx = empty_nhwc(n, c, h, w, ctx.dtype, dv.device)
+        N.call("dmf_broadcast_hw", N.dtype_code(ctx.dtype), dv.data_ptr(), 1.0 / (h * w), dx.data_ptr(),
+               nhwc(dx)[4], n, h * w, c, 0, _stream())
+        return dx
+
+
+def gap(x):
+    return _GapFn.apply(x)
+
+
+# ----------------------------------------------------------------- linear
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x = x.contiguous()
+        r, k = x.shape
+        nout = w.shape[0]
+        y = torch.empty((r, nout), dtype=torch.float32, device=x.device)
+        wc = w.detach().contiguous()
+        N.call("dmf_sgemm", 0, 1, r, nout, k, 1.0, x.data_ptr(), k, wc.data_ptr(), k, 0.0, y.data_ptr(), nout, _p(b),
+               N.ACT_NONE, _stream())
+        pre = y
+        if act != "none":
+            out = torch.empty_like(y)
+            _act_f32(y, out, act)
+            y = out
+        ctx.save_for_backward(x, w, b, pre if act != "none" else None)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, pre = ctx.saved_tensors
+        dy = dy.contiguous().float()
+        r, k = x.shape
+        nout = w.shape[0]
+        if ctx.act != "none":
+            dpre = torch.empty_like(dy)
+            N.call("dmf_act_grad_f32", dy.data_ptr(), pre.data_ptr(), dpre.data_ptr(), dy.numel(), ACT[ctx.act],
+                   _stream())
+        else:
+            dpre = dy
+        dx = dw = db = None
+        wc = w.detach().contiguous()
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((r, k), dtype=torch.float32, device=x.device)
+            N.call("dmf_sgemm", 0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
+                   None, N.ACT_NONE, _stream())
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((nout, k), dtype=torch.float32, device=x.device)
+            N.call("dmf_sgemm", 1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 0.0, dw.data_ptr(), k,
+                   None, N.ACT_NONE, _stream())
+            dw = dw.view_as(w)
+        if b is not None and ctx.needs_input_grad[2]:
+            db = torch.empty(nout, dtype=torch.float32, device=x.device)
+            N.call("dmf_colsum_f32", dpre.data_ptr(), nout, r, nout, db.data_ptr(), 0, _stream())
+        return dx, dw, db, None
+
+
+def _act_f32(x, out, act):
+    """fp32 elementwise activation (contiguous tensors)."""
+    N.call("dmf_act_f32", x.data_ptr(), out.data_ptr(), x.numel(), ACT[act], _stream())
+
+
+def linear(x, w, b=None, act="none"):
+    return _LinearFn.apply(x, w, b, act)
+
+
+# --------------------------------------------------------------------- SE
+class _SEFn(torch.autograd.Function):
+    """SEBlock (model_module.py:25-43) on an NHWC map: returns (x*w, w)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        n, c, h, w, ld = nhwc(x)
+        pooled = spatial_mean(x)
+        mid = w1.shape[0]
+        hpre = torch.empty((n, mid), dtype=torch.float32, device=x.device)
+        N.call("dmf_sgemm", 0, 1, n, mid, c, 1.0, pooled.data_ptr(), c, w1.detach().reshape(mid, c).contiguous()
+               .data_ptr(), c, 0.0, hpre.data_ptr(), mid, _p(b1), N.ACT_NONE, _stream())
+        hact = torch.empty_like(hpre)
+        _act_f32(hpre, hact, "gelu")
+        z2 = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        N.call("dmf_sgemm", 0, 1, n, c, mid, 1.0, hact.data_ptr(), mid, w2.detach().reshape(c, mid).contiguous()
+               .data_ptr(), mid, 0.0, z2.data_ptr(), c, _p(b2), N.ACT_NONE, _stream())
+        gate = torch.empty_like(z2)
+        _act_f32(z2, gate, "sigmoid")
+        y = empty_nhwc(n, c, h, w, x.dtype, x.device)
+        N.call("dmf_channel_scale", dt(x), x.data_ptr(), ld, gate.data_ptr(), y.data_ptr(), nhwc(y)[4], n, h * w, c,
+               _stream())
+        ctx.save_for_backward(x, w1, w2, pooled, hpre, hact, gate)
+        ctx.mark_non_differentiable(gate)
+        return y, gate.view(n, c, 1, 1)
+
+    @staticmethod
+    def backward(ctx, dy, _dgate):
+        x, w1, w2, pooled, hpre, hact, gate = ctx.saved_tensors
+        dy = as_nhwc(dy)
+        n, c, h, w, ld = nhwc(x)
+        mid = w1.shape[0]
+        dev = x.device
+        dg = torch.empty((n, c), dtype=torch.float32, device=dev)
+        N.call("dmf_nhwc_reduce", dt(x), dy.data_ptr(), nhwc(dy)[4], x.data_ptr(), ld, n, h * w, c, 1.0,
+               dg.data_ptr(), 0, _stream())
+        # through sigmoid: dz2 = dg * g * (1 - g)
+        dz2 = torch.empty_like(dg)
+        N.call("dmf_sig_grad_f32", dg.data_ptr(), gate.data_ptr(), dz2.data_ptr(), dg.numel(), _stream())
+        w2m = w2.detach().reshape(c, mid).contiguous()
+        w1m = w1.detach().reshape(mid, c).contiguous()
+        dw2 = torch.empty((c, mid), dtype=torch.float32, device=dev)
+        N.call("dmf_sgemm", 1, 0, c, mid, n, 1.0, dz2.data_ptr(), c, hact.data_ptr(), mid, 0.0, dw2.data_ptr(), mid,
+               None, N.ACT_NONE, _stream())
+        db2 = torch.empty(c, dtype=torch.float32, device=dev)
+        N.call("dmf_colsum_f32", dz2.data_ptr(), c, n, c, db2.data_ptr(), 0, _stream())
+        dh = torch.empty((n, mid), dtype=torch.float32, device=dev)
+        N.call("dmf_sgemm", 0, 0, n, mid, c, 1.0, dz2.data_ptr(), c, w2m.data_ptr(), mid, 0.0, dh.data_ptr(), mid,
+               None, N.ACT_NONE, _stream())
+        dh1 = torch.empty_like(dh)
+        N.call("dmf_act_grad_f32", dh.data_ptr(), hpre.data_ptr(), dh1.data_ptr(), dh.numel(), N.ACT_GELU, _stream())
+        dw1 = torch.empty((mid, c), dtype=torch.float32, device=dev)
+        N.call("dmf_sgemm", 1, 0, mid, c, n, 1.0, dh1.data_ptr(), mid, pooled.data_ptr(), c, 0.0, dw1.data_ptr(), c,
+               None, N.ACT_NONE, _stream())
+        db1 = torch.empty(mid, dtype=torch.float32, device=dev)
+        N.call("dmf_colsum_f32", dh1.data_ptr(), mid, n, mid, db1.data_ptr(), 0, _stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dpooled = torch.empty((n, c), dtype=torch.float32, device=dev)
+            N.call("dmf_sgemm", 0, 0, n, c, mid, 1.0, dh1.data_ptr(), mid, w1m.data_ptr(), c, 0.0, dpooled.data_ptr(),
+                   c, None, N.ACT_NONE, _stream())
+            dx = empty_nhwc(n, c, h, w, x.dtype, dev)
+            N.call("dmf_channel_affine", dt(x), dy.data_ptr(), nhwc(dy)[4], gate.data_ptr(), dpooled.data_ptr(),
+                   1.0 / (h * w), dx.data_ptr(), nhwc(dx)[4], n, h * w, c, _stream())
+        return dx, dw1.view_as(w1), db1, dw2.view_as(w2), db2
+
+
+def se_block(x, se_module):
+    fc = se_module.fc
+    return _SEFn.apply(x, fc[1].weight, fc[1].bias, fc[3].weight, fc[3].bias)
+
+
+# ---------------------------------------------------------- input staging
+def channel_pad(c, dtype):
+    """Channels padded so the conv engine's 16-byte K chunks align."""
+    m = 8 if dtype == torch.bfloat16 else 4
+    return ((c + m - 1) // m) * m
+
+
+class _InputFn(torch.autograd.Function):
+    """x (NCHW fp32) -> NHWC compute-dtype x*gate (gate [N][C] or None)
+    with zero padded channels; also returns the per-pixel channel mean of x
+    (recon target, train_fusion.py:735-737)."""
+
+    @staticmethod
+    def forward(ctx, x, gate, dtype):
+        x = x.contiguous().float()
+        n, c, h, w = x.shape
+        cp = channel_pad(c, dtype)
+        y = empty_nhwc(n, cp, h, w, dtype, x.device)
+        cmean = torch.empty((n, h, w), dtype=torch.float32, device=x.device)
+        g = gate.contiguous() if gate is not None else None
+        N.call("dmf_input_prep", N.dtype_code(dtype), x.data_ptr(), n, c, h, w, _p(g), y.data_ptr(), cp,
+               cmean.data_ptr(), _stream())
+        ctx.save_for_backward(x)
+        ctx.mark_non_differentiable(cmean)
+        return y, cmean
+
+    @staticmethod
+    def backward(ctx, dy, _dc):
+        (x,) = ctx.saved_tensors
+        dgate = None
+        if ctx.needs_input_grad[1]:
+            n, c, h, w = x.shape
+            dy = as_nhwc(dy)
+            dgate = torch.empty((n, c), dtype=torch.float32, device=x.device)
+            N.call("dmf_gate_grad_nchw", dt(dy), dy.data_ptr(), nhwc(dy)[4], x.data_ptr(), n, c, h * w,
+                   dgate.data_ptr(), _stream())
+        return None, dgate, None
+
+
+def input_stage(x, dtype, gate=None):
+    return _InputFn.apply(x, gate, dtype)
+
+
+def nchw_mean(x):
+    x = x.contiguous().float()
+    n, c, h, w = x.shape
+    out = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    N.call("dmf_nchw_mean", x.data_ptr(), n * c, h * w, out.data_ptr(), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- maxpool
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        n, c, h, w, ld = nhwc(x)
+        ho = (h + 2 * p - k) // s + 1
+        wo = (w + 2 * p - k) // s + 1
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        N.call("dmf_maxpool2d", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4], k, s, p,
+               _stream())
+        ctx.save_for_backward(x)
+        ctx.cfg = (k, s, p, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        k, s, p, ho, wo = ctx.cfg
+        dy = as_nhwc(dy)
+        n, c, h, w, ld = nhwc(x)
+        dx = empty_nhwc(n, c, h, w, x.dtype, x.device)
+        N.call("dmf_maxpool2d_bwd", dt(x), x.data_ptr(), n, h, w, c, ld, dy.data_ptr(), ho, wo, nhwc(dy)[4],
+               dx.data_ptr(), nhwc(dx)[4], k, s, p, _stream())
+        return dx, None, None, None
+
+
+def maxpool2d(x, k=3, s=2, p=1):
+    return _MaxPoolFn.apply(x, k, s, p)
+
+
+# -------------------------------------------------- GroupNorm(C,C) of a mix
+class _GNMixFn(torch.autograd.Function):
+    """GroupNorm(C,C)(sig(w)*a + (1-sig(w))*b), model_module.py:673-675."""
+
+    @staticmethod
+    def forward(ctx, a, b, wlogit, gamma, beta, eps):
+        n, c, h, w, lda = nhwc(a)
+        ldb = nhwc(b)[4]
+        z = empty_nhwc(n, c, h, w, a.dtype, a.device)
+        ldz = nhwc(z)[4]
+        N.call("dmf_mix", dt(a), a.data_ptr(), lda, b.data_ptr(), ldb, wlogit.data_ptr(), z.data_ptr(), ldz,
+               n * h * w, c, _stream())
+        mean = torch.empty((n, c), dtype=torch.float32, device=a.device)
+        m2 = torch.empty((n, c), dtype=torch.float32, device=a.device)
+        N.call("dmf_nhwc_reduce", dt(z), z.data_ptr(), ldz, None, 0, n, h * w, c, 1.0 / (h * w), mean.data_ptr(), 0,
+               _stream())
+        N.call("dmf_nhwc_reduce", dt(z), z.data_ptr(), ldz, z.data_ptr(), ldz, n, h * w, c, 1.0 / (h * w),
+               m2.data_ptr(), 0, _stream())
+        y = empty_nhwc(n, c, h, w, a.dtype, a.device)
+        N.call("dmf_gn_apply", dt(z), z.data_ptr(), ldz, mean.data_ptr(), m2.data_ptr(), gamma.data_ptr(),
+               beta.data_ptr(), float(eps), y.data_ptr(), nhwc(y)[4], n, h * w, c, _stream())
+        ctx.save_for_backward(a, b, wlogit, gamma, z, mean, m2)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, b, wlogit, gamma, z, mean, m2 = ctx.saved_tensors
+        dy = as_nhwc(dy)
+        n, c, h, w, ldz = nhwc(z)
+        dev = z.device
+        s1 = torch.empty((n, c), dtype=torch.float32, device=dev)
+        s2 = torch.empty((n, c), dtype=torch.float32, device=dev)
+        dz = empty_nhwc(n, c, h, w, z.dtype, dev)
+        N.call("dmf_gn_bwd", dt(z), dy.data_ptr(), nhwc(dy)[4], z.data_ptr(), ldz, mean.data_ptr(), m2.data_ptr(),
+               gamma.data_ptr(), float(ctx.eps), s1.data_ptr(), s2.data_ptr(), dz.data_ptr(), nhwc(dz)[4], n, h * w,
+               c, _stream())
+        # dgamma = sum_n s2 ; dbeta = sum_n s1
+        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+        dbeta = torch.empty(c, dtype=torch.float32, device=dev)
+        N.call("dmf_colsum_f32", s2.data_ptr(), c, n, c, dgamma.data_ptr(), 0, _stream())
+        N.call("dmf_colsum_f32", s1.data_ptr(), c, n, c, dbeta.data_ptr(), 0, _stream())
+        da = db_ = dw = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            da = empty_nhwc(n, c, h, w, z.dtype, dev)
+            db_ = empty_nhwc(n, c, h, w, z.dtype, dev)
+            dw = torch.zeros(1, dtype=torch.float32, device=dev)
+            N.call("dmf_mix_bwd", dt(z), dz.data_ptr(), nhwc(dz)[4], a.data_ptr(), nhwc(a)[4], b.data_ptr(),
+                   nhwc(b)[4], wlogit.data_ptr(), da.data_ptr(), db_.data_ptr(), nhwc(da)[4], dw.data_ptr(),
+                   n * h * w, c, _stream())
+            dw = dw.view_as(wlogit)
+        return da, db_, dw, dgamma, dbeta, None
+
+
+def gn_mix(a, b, wlogit, gn):
+    return _GNMixFn.apply(a, b, wlogit, gn.weight, gn.bias, gn.eps)
+
+
+# ------------------------------------------------------- resampling
+class _UpNearestFn(torch.autograd.Function):
+    """Nearest r-x upsample == AdaptiveAvgPool2d to an r-x larger size."""
+
+    @staticmethod
+    def forward(ctx, x, r):
+        n, c, h, w, ld = nhwc(x)
+        y = torch.empty((n, r * h, r * w, c), dtype=x.dtype, device=x.device)
+        N.call("dmf_upsample_nearest", dt(x), x.data_ptr(), ld, y.data_ptr(), n, h, w, c, r, _stream())
+        ctx.shape = (n, c, h, w, r)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w, r = ctx.shape
+        dy = dy.permute(0, 2, 3, 1).contiguous()
+        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        N.call("dmf_upsample_nearest_bwd", dt(dy), dy.data_ptr(), dx.data_ptr(), n, h, w, c, r, _stream())
+        return dx, None
+
+
+def upsample_nearest(x, r):
+    return x if r == 1 else _UpNearestFn.apply(x, r)
+
+
+def upsample2x_nearest(x):
+    return _UpNearestFn.apply(x, 2)
+
+
+class _BilinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        n, c, h, w, ld = nhwc(x)
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        N.call("dmf_bilinear", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4], _stream())
+        ctx.shape = (n, c, h, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.shape
+        dy = as_nhwc(dy)
+        _, _, ho, wo, lddy = nhwc(dy)
+        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        N.call("dmf_bilinear_bwd", dt(dy), dy.data_ptr(), n, ho, wo, c, lddy, dx.data_ptr(), h, w, nhwc(dx)[4],
+               _stream())
+        return dx, None, None
+
+
+def bilinear(x, ho, wo):
+    if tuple(x.shape[-2:]) == (ho, wo):
+        return x
+    return _BilinearFn.apply(x, ho, wo)
+
+
+# ------------------------------------------- mask-guided spatial attention
+class _MaskAttnFn(torch.autograd.Function):
+    """model_module.py:75-97 with the GroupNorm(1,16) statistics in closed
+    form (the 1x1 conv from one channel makes them separable)."""
+
+    @staticmethod
+    def forward(ctx, f, m, w1, gn_w, gn_b, w2, b2, gamma, eps):
+        n, c, h, w, ldf = nhwc(f)
+        hid = w1.shape[0]
+        stats = torch.empty(2 * n, dtype=torch.float32, device=f.device)
+        out = empty_nhwc(n, c, h, w, f.dtype, f.device)
+        A = empty_nhwc(n, 1, h, w, f.dtype, f.device)
+        mc = as_nhwc(m)
+        if nhwc(mc)[4] != 1:
+            mc = mc.contiguous(memory_format=torch.channels_last)
+        N.call("dmf_mask_attn_fwd", dt(f), f.data_ptr(), ldf, mc.data_ptr(), n, h * w, c,
+               w1.detach().reshape(hid).contiguous().data_ptr(), gn_w.data_ptr(), gn_b.data_ptr(),
+               w2.detach().reshape(hid).contiguous().data_ptr(), b2.data_ptr(), gamma.data_ptr(), hid, float(eps),
+               stats.data_ptr(), out.data_ptr(), nhwc(out)[4], A.data_ptr(), _stream())
+        ctx.save_for_backward(f, mc, w1, gn_w, gn_b, w2, b2, gamma, stats, A)
+        ctx.eps = eps
+        return out, A
+
+    @staticmethod
+    def backward(ctx, dout, dA):
+        f, m, w1, gn_w, gn_b, w2, b2, gamma, stats, A = ctx.saved_tensors
+        dout = as_nhwc(dout)
+        n, c, h, w, ldf = nhwc(f)
+        hid = w1.shape[0]
+        dev = f.device
+        df = empty_nhwc(n, c, h, w, f.dtype, dev)
+        dm = empty_nhwc(n, 1, h, w, f.dtype, dev)
+        grads = torch.zeros(4 * hid + 2, dtype=torch.float32, device=dev)  # dw1, dgn_w, dgn_b, dw2, db2, dgamma
+        ws = torch.empty(n * h * w * hid + 2 * n, dtype=torch.float32, device=dev)
+        N.call("dmf_mask_attn_bwd", dt(f), dout.data_ptr(), nhwc(dout)[4], f.data_ptr(), ldf, m.data_ptr(), n, h * w,
+               c, w1.detach().reshape(hid).contiguous().data_ptr(), gn_w.data_ptr(), gn_b.data_ptr(),
+               w2.detach().reshape(hid).contiguous().data_ptr(), b2.data_ptr(), gamma.data_ptr(), hid,
+               float(ctx.eps), stats.data_ptr(), df.data_ptr(), nhwc(df)[4], dm.data_ptr(), ws.data_ptr(),
+               grads.data_ptr(), _stream())
+        dw1 = grads[0:hid].view_as(w1)
+        dgw = grads[hid:2 * hid]
+        dgb = grads[2 * hid:3 * hid]
+        dw2 = grads[3 * hid:4 * hid].view_as(w2)
+        db2 = grads[4 * hid:4 * hid + 1]
+        dgam = grads[4 * hid + 1:4 * hid + 2].view_as(gamma)
+        return df, dm, dw1, dgw, dgb, dw2, db2, dgam, None
+
+
+def mask_attention(f, m, msa):
+    mp = msa.mask_processor
+    if tuple(m.shape[-2:]) != tuple(f.shape[-2:]):
+        m = bilinear(m, f.shape[-2], f.shape[-1])
+    return _MaskAttnFn.apply(f, m, mp[0].weight, mp[1].weight, mp[1].bias, mp[3].weight, mp[3].bias, msa.gamma,
+                             mp[1].eps)
+
+
+# ======================================================= fusion op pieces
+class _TokensFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, hp, wp):
+        n, c, h, w, ld = nhwc(x)
+        tok = torch.empty((n, hp * wp, c), dtype=torch.float32, device=x.device)
+        N.call("dmf_tokens_fwd", dt(x), x.data_ptr(), ld, n, h, w, c, hp, wp, tok.data_ptr(), _stream())
+        ctx.cfg = (n, c, h, w, hp, wp, x.dtype)
+        return tok
+
+    @staticmethod
+    def backward(ctx, dtok):
+        n, c, h, w, hp, wp, dtype = ctx.cfg
+        dtok = dtok.contiguous().float()
+        dx = empty_nhwc(n, c, h, w, dtype, dtok.device)
+        N.call("dmf_tokens_bwd", N.dtype_code(dtype), dtok.data_ptr(), n, h, w, c, hp, wp, dx.data_ptr(),
+               nhwc(dx)[4], 0, _stream())
+        return dx, None, None
+
+
+def to_tokens(x, hp, wp):
+    return _TokensFn.apply(x, hp, wp)
+
+
+class _GateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pa, pb, ca, cb, W, b):
+        n, c = pa.shape
+        g = torch.empty((n, 2), dtype=torch.float32, device=pa.device)
+        N.call("dmf_gate_fwd", pa.data_ptr(), pb.data_ptr(), _p(ca), _p(cb), n, c, W.data_ptr(), b.data_ptr(),
+               g.data_ptr(), _stream())
+        ctx.save_for_backward(pa, pb, ca, cb, W, g)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        pa, pb, ca, cb, W, g = ctx.saved_tensors
+        dg = dg.contiguous()
+        n, c = pa.shape
+        dev = pa.device
+        dW = torch.zeros_like(W)
+        db = torch.zeros(2, dtype=torch.float32, device=dev)
+        dpa = torch.empty_like(pa)
+        dpb = torch.empty_like(pb)
+        dca = torch.empty_like(ca) if ca is not None else None
+        dcb = torch.empty_like(cb) if cb is not None else None
+        N.call("dmf_gate_bwd", pa.data_ptr(), pb.data_ptr(), _p(ca), _p(cb), n, c, W.data_ptr(), g.data_ptr(),
+               dg.data_ptr(), dW.data_ptr(), db.data_ptr(), dpa.data_ptr(), dpb.data_ptr(), _p(dca), _p(dcb),
+               _stream())
+        return dpa, dpb, dca, dcb, dW, db
+
+
+def gating(pa, pb, ca, cb, fc):
+    return _GateFn.apply(pa, pb, ca, cb, fc.weight, fc.bias)
+
+
+class _CombineFn(torch.autograd.Function):
+    """fused = g0*p_dwi + g1*p_dce + bilinear(lowres) (model_module.py:958-973)."""
+
+    @staticmethod
+    def forward(ctx, pa, pb, g, low, hp, wp):
+        n, c, h, w, ld = nhwc(pa)
+        if nhwc(pb)[4] != ld:
+            raise RuntimeError("p_dwi/p_dce must share a layout")
+        y = empty_nhwc(n, c, h, w, pa.dtype, pa.device)
+        lowc = low.contiguous() if low is not None else None
+        N.call("dmf_fusion_combine_fwd", dt(pa), pa.data_ptr(), pb.data_ptr(), ld, g.data_ptr(), _p(lowc), n, h, w, c,
+               hp, wp, y.data_ptr(), nhwc(y)[4], _stream())
+        ctx.save_for_backward(pa, pb, g)
+        ctx.cfg = (hp, wp, low is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        pa, pb, g = ctx.saved_tensors
+        hp, wp, has_low = ctx.cfg
+        dy = as_nhwc(dy)
+        n, c, h, w, ld = nhwc(pa)
+        dev = pa.device
+        dpa = empty_nhwc(n, c, h, w, pa.dtype, dev)
+        dpb = empty_nhwc(n, c, h, w, pa.dtype, dev)
+        dg = torch.empty((n, 2), dtype=torch.float32, device=dev)
+        dlow = torch.empty((n, hp * wp, c), dtype=torch.float32, device=dev) if has_low else None
+        N.call("dmf_fusion_combine_bwd", dt(pa), dy.data_ptr(), nhwc(dy)[4], pa.data_ptr(), pb.data_ptr(), ld,
+               g.data_ptr(), n, h, w, c, hp, wp, dpa.data_ptr(), dpb.data_ptr(), nhwc(dpa)[4], dg.data_ptr(),
+               _p(dlow), _stream())
+        return dpa, dpb, dg, dlow, None, None
+
+
+def fusion_combine(pa, pb, g, low, hp, wp):
+    return _CombineFn.apply(pa, pb, g, low, hp, wp)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        shp = x.shape
+        e = shp[-1]
+        x2 = x.reshape(-1, e).contiguous()
+        r = x2.shape[0]
+        y = torch.empty_like(x2)
+        save = torch.empty(2 * r, dtype=torch.float32, device=x.device)
+        N.call("dmf_layernorm_fwd", x2.data_ptr(), r, e, gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(),
+               save.data_ptr(), _stream())
+        ctx.save_for_backward(x2, gamma, save)
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gamma, save = ctx.saved_tensors
+        shp = dy.shape
+        r, e = x2.shape
+        dy2 = dy.reshape(r, e).contiguous()
+        dx = torch.empty_like(x2)
+        dg = torch.zeros_like(gamma)
+        db = torch.zeros_like(gamma)
+        N.call("dmf_layernorm_bwd", dy2.data_ptr(), x2.data_ptr(), save.data_ptr(), r, e, gamma.data_ptr(),
+               dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _stream())
+        return dx.view(shp), dg, db, None
+
+
+def layer_norm(x, ln):
+    return _LayerNormFn.apply(x, ln.weight, ln.bias, ln.eps)
+
+
+class _AttnCoreFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads):
+        b, nq, e = q.shape
+        nk = k.shape[1]
+        d = e // heads
+        scale = d ** -0.5
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o = torch.empty((b, nq, e), dtype=torch.float32, device=q.device)
+        probs = torch.empty((b, heads, nq, nk), dtype=torch.float32, device=q.device)
+        avgw = torch.zeros((b, nq, nk), dtype=torch.float32, device=q.device)
+        N.call("dmf_attn_fwd", q.data_ptr(), e, k.data_ptr(), e, v.data_ptr(), e, b, nq, nk, heads, d, scale,
+               o.data_ptr(), e, probs.data_ptr(), avgw.data_ptr(), _stream())
+        ctx.save_for_backward(q, k, v, probs)
+        ctx.cfg = (heads, d, scale)
+        ctx.mark_non_differentiable(avgw)
+        return o, avgw
+
+    @staticmethod
+    def backward(ctx, do, _davg):
+        q, k, v, probs = ctx.saved_tensors
+        heads, d, scale = ctx.cfg
+        b, nq, e = q.shape
+        nk = k.shape[1]
+        do = do.contiguous()
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k)
+        dv = torch.empty_like(v)
+        N.call("dmf_attn_bwd", q.data_ptr(), e, k.data_ptr(), e, v.data_ptr(), e, probs.data_ptr(), do.data_ptr(), e,
+               b, nq, nk, heads, d, scale, dq.data_ptr(), e, dk.data_ptr(), e, dv.data_ptr(), e, _stream())
+        return dq, dk, dv, None
+
+
+def attention_core(q, k, v, heads):
+    return _AttnCoreFn.apply(q, k, v, heads)
+
+
+def residual_add_f32(a, b):
+    """a + b for fp32 token tensors (any shape) via the affine kernel."""
+    return _AddF32Fn.apply(a, b)
+
+
+class _AddF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a2, b2 = a.contiguous(), b.contiguous()
+        n = a2.numel()
+        out = torch.empty_like(a2)
+        if n % 4:
+            raise RuntimeError("residual_add_f32 needs numel % 4 == 0")
+        N.call("dmf_affine_act", F32, a2.data_ptr(), 4, None, b2.data_ptr(), 4, None, N.ACT_NONE, 0.0, None, 0,
+               out.data_ptr(), 4, n // 4, 4, _stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+class _L2NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        x = x.contiguous().float()
+        r, c = x.shape
+        y = torch.empty_like(x)
+        norms = torch.empty(r, dtype=torch.float32, device=x.device)
+        N.call("dmf_row_l2norm", x.data_ptr(), r, c, float(eps), y.data_ptr(), norms.data_ptr(), _stream())
+        ctx.save_for_backward(y, norms)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, norms = ctx.saved_tensors
+        dy = dy.contiguous()
+        r, c = y.shape
+        dx = torch.empty_like(y)
+        N.call("dmf_row_l2norm_bwd", dy.data_ptr(), y.data_ptr(), norms.data_ptr(), r, c, float(ctx.eps),
+               dx.data_ptr(), _stream())
+        return dx, None
+
+
+def l2_normalize_rows(x, eps=1e-12):
+    return _L2NormFn.apply(x, eps)
+
+
+class _CrossAttnFn(torch.autograd.Function):
+    """Attention with q = qf[..., 0:E], k = kvf[..., E:2E], v = kvf[..., 2E:3E]
+    (nn.MultiheadAttention packed in_proj, computed as two full-width GEMMs so
+    no parameter slicing is needed)."""
+
+    @staticmethod
+    def forward(ctx, qf, kvf, heads, e):
+        qf, kvf = qf.contiguous(), kvf.contiguous()
+        b, nq, w3 = qf.shape
+        nk = kvf.shape[1]
+        d = e // heads
+        scale = d ** -0.5
+        o = torch.empty((b, nq, e), dtype=torch.float32, device=qf.device)
+        probs = torch.empty((b, heads, nq, nk), dtype=torch.float32, device=qf.device)
+        avgw = torch.zeros((b, nq, nk), dtype=torch.float32, device=qf.device)
+        N.call("dmf_attn_fwd", qf.data_ptr(), w3, kvf.data_ptr() + 4 * e, w3, kvf.data_ptr() + 8 * e, w3, b, nq, nk,
+               heads, d, scale, o.data_ptr(), e, probs.data_ptr(), avgw.data_ptr(), _stream())
+        ctx.save_for_backward(qf, kvf, probs)
+        ctx.cfg = (heads, d, scale, e)
+        ctx.mark_non_differentiable(avgw)
+        return o, avgw
+
+    @staticmethod
+    def backward(ctx, do, _davg):
+        qf, kvf, probs = ctx.saved_tensors
+        heads, d, scale, e = ctx.cfg
+        b, nq, w3 = qf.shape
+        nk = kvf.shape[1]
+        do = do.contiguous()
+        dqf = torch.zeros_like(qf)
+        dkvf = torch.zeros_like(kvf)
+        N.call("dmf_attn_bwd", qf.data_ptr(), w3, kvf.data_ptr() + 4 * e, w3, kvf.data_ptr() + 8 * e, w3,
+               probs.data_ptr(), do.data_ptr(), e, b, nq, nk, heads, d, scale, dqf.data_ptr(), w3,
+               dkvf.data_ptr() + 4 * e, w3, dkvf.data_ptr() + 8 * e, w3, _stream())
+        return dqf, dkvf, None, None
+
+
+def cross_attention(qf, kvf, heads, e):
+    return _CrossAttnFn.apply(qf, kvf, heads, e)
+
+
+def channel_mean_map(x):
+    """mean over channels of an NCHW fp32 tensor -> [N, H, W] fp32 (recon target)."""
+    x = x.contiguous().float()
+    n, c, h, w = x.shape
+    out = torch.empty((n, h, w), dtype=torch.float32, device=x.device)
+    N.call("dmf_input_prep", F32, x.data_ptr(), n, c, h, w, None, None, c, out.data_ptr(), _stream())
+    return out
+
+
+# ================================================================ criteria
+class _FocalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, soft, cw, gamma, smoothing, use_smoothing, reduction):
+        z = logits.contiguous().float()
+        b, k = z.shape
+        red = {"mean": 0, "sum": 1, "none": 2}[reduction]
+        loss = torch.empty((), dtype=torch.float32, device=z.device)
+        per_row = torch.empty(b, dtype=torch.float32, device=z.device) if red == 2 else None
+        dl = torch.empty_like(z) if z.requires_grad or logits.requires_grad else None
+        lab = labels.contiguous().long() if labels is not None else None
+        st_ = soft.contiguous().float() if soft is not None else None
+        N.call("dmf_focal_loss", z.data_ptr(), _p(lab), _p(st_), b, k, float(smoothing), int(use_smoothing), _p(cw),
+               float(gamma), red, loss.data_ptr() if red != 2 else None, _p(per_row), _p(dl), _stream())
+        ctx.save_for_backward(dl)
+        ctx.red = red
+        return per_row if red == 2 else loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        if dl is None:
+            return (None,) * 8
+        g = g.contiguous().float()
+        out = torch.empty_like(dl)
+        if ctx.red == 2:
+            b, k = dl.shape
+            # per-row upstream: dl[b,:] * g[b]
+            N.call("dmf_channel_affine", F32, dl.data_ptr(), k, g.data_ptr(), None, 0.0, out.data_ptr(), k, b, 1, k,
+                   _stream()) if False else out.copy_(dl * g.view(-1, 1))
+        else:
+            N.call("dmf_scale_by", dl.data_ptr(), dl.numel(), g.data_ptr(), 1.0, out.data_ptr(), _stream())
+        return out, None, None, None, None, None, None, None
+
+
+def focal_loss(logits, targets, gamma, class_weights=None, reduction="mean", smoothing=0.0, use_smoothing=False):
+    """SoftWeightedFocalLoss semantics (loss.py:157-187): ``targets`` are
+    class indices [B] or soft targets [B,K]."""
+    if targets.dim() == 1:
+        return _FocalFn.apply(logits, targets, None, class_weights, gamma, smoothing, use_smoothing, reduction)
+    return _FocalFn.apply(logits, None, targets, class_weights, gamma, 0.0, False, reduction)
+
+
+def label_smooth(labels, classes, smoothing):
+    lab = labels.contiguous().long()
+    b = lab.shape[0]
+    out = torch.empty((b, classes), dtype=torch.float32, device=lab.device)
+    N.call("dmf_label_smooth", lab.data_ptr(), b, classes, float(smoothing), out.data_ptr(), _stream())
+    return out
+
+
+class _DiceFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, eps):
+        x = as_nhwc(logits) if logits.dim() == 4 else logits
+        b = x.shape[0]
+        p = x[0].numel()
+        if x.dim() == 4:
+            n, c, h, w, ld = nhwc(x)
+            if c != 1 or ld != 1:
+                x = x.contiguous()
+        else:
+            x = x.contiguous()
+        t = target.contiguous().float()
+        if t.numel() != b * p:
+            raise RuntimeError(f"soft dice: target shape {tuple(target.shape)} != logits {tuple(logits.shape)}")
+        sums = torch.empty(3 * b, dtype=torch.float32, device=x.device)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        dx = torch.empty((b, p), dtype=torch.float32, device=x.device) if logits.requires_grad else None
+        N.call("dmf_soft_dice", dt(x), x.data_ptr(), t.data_ptr(), b, p, float(eps), sums.data_ptr(), loss.data_ptr(),
+               _p(dx), _stream())
+        ctx.save_for_backward(dx)
+        ctx.shape = logits.shape
+        ctx.dtype = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dx,) = ctx.saved_tensors
+        if dx is None:
+            return None, None, None
+        b = dx.shape[0]
+        p = dx.shape[1]
+        if len(ctx.shape) == 4 and ctx.shape[1] == 1:
+            out = empty_nhwc(ctx.shape[0], 1, ctx.shape[2], ctx.shape[3], ctx.dtype, dx.device)
+        else:
+            out = torch.empty(ctx.shape, dtype=ctx.dtype, device=dx.device)
+        N.call("dmf_scale_by_cast", N.dtype_code(ctx.dtype), dx.data_ptr(), b * p, 1, g.contiguous().data_ptr(), 1.0,
+               out.data_ptr(), 1, _stream())
+        return out, None, None
+
+
+def soft_dice(logits, target, eps=1e-6):
+    return _DiceFn.apply(logits, target, eps)
+
+
+class _ReconFn(torch.autograd.Function):
+    """Sum of recon_image_loss(bilinear(r_k -> SxS), target_k) over k (each
+    term already averaged over B*S*S). Returns a [nterms] vector."""
+
+    @staticmethod
+    def forward(ctx, tA, tB, ca, cb, sels, *maps):
+        k = len(maps)
+        r0 = maps[0]
+        b, _, h, w = r0.shape
+        s = tA.shape[-1] if tA is not None else tB.shape[-1]
+        dev = r0.device
+        prepared = []
+        lds = []
+        for m in maps:
+            mm = as_nhwc(m)
+            prepared.append(mm)
+            lds.append(nhwc(mm)[4])
+        dtc = dt(prepared[0])
+        for m in prepared:
+            if dt(m) != dtc:
+                raise RuntimeError("recon maps must share a dtype")
+        sums = torch.zeros(5, dtype=torch.float32, device=dev)
+        need = any(m.requires_grad for m in maps)
+        grads = [torch.zeros((b, h, w), dtype=torch.float32, device=dev) if (need and maps[i].requires_grad) else None
+                 for i in range(k)]
+        ptrs = [m.data_ptr() for m in prepared] + [None] * (5 - k)
+        ldl = lds + [0] * (5 - k)
+        sel = list(sels) + [0] * (5 - k)
+        gp = [_p(g) for g in grads] + [None] * (5 - k)
+        N.call("dmf_recon_loss", dtc, k, *ptrs, *ldl, *sel, _p(tA), _p(tB), float(ca), float(cb), b, h, w, s,
+               sums.data_ptr(), *gp, _stream())
+        out = sums[:k] / float(b * s * s)
+        ctx.save_for_backward(*[g if g is not None else torch.empty(0, device=dev) for g in grads])
+        ctx.meta = [(m.shape, m.dtype, g is not None) for m, g in zip(maps, grads)]
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        gs = ctx.saved_tensors
+        gout = gout.contiguous().float()
+        res = [None, None, None, None, None]
+        for i, (shape, dtype, has) in enumerate(ctx.meta):
+            if not has:
+                res.append(None)
+                continue
+            g = gs[i]
+            b, _, h, w = shape
+            out = empty_nhwc(b, 1, h, w, dtype, g.device)
+            # grads were accumulated with a 1/(B*S*S) factor already
+            N.call("dmf_scale_by_cast", N.dtype_code(dtype), g.data_ptr(), b * h * w, 1, gout.data_ptr() + 4 * i, 1.0,
+                   out.data_ptr(), 1, _stream())
+            res.append(out)
+        return tuple(res)
+
+
+def recon_terms(maps, sels, tA, tB=None, ca=0.0, cb=0.0):
+    """Charbonnier recon terms for up to 5 single-channel maps; sel 0 -> tA,
+    1 -> tB, 2 -> ca*tA + cb*tB."""
+    return _ReconFn.apply(tA, tB, ca, cb, tuple(sels), *maps)
+
+
+class _MimicFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t, npairs, sstride, tstride, hw, c, ld):
+        loss = torch.zeros((), dtype=torch.float32, device=s.device)
+        ds = None
+        if s.requires_grad:
+            ds = torch.zeros_like(s)
+        N.call("dmf_mimic_loss", dt(s), s.data_ptr(), t.data_ptr(), sstride, tstride, ld, hw, c, npairs,
+               loss.data_ptr(), _p(ds), sstride, _stream())
+        ctx.save_for_backward(ds)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (ds,) = ctx.saved_tensors
+        if ds is None:
+            return (None,) * 8
+        out = torch.empty_like(ds)
+        if ds.dtype == torch.float32:
+            N.call("dmf_scale_by", ds.data_ptr(), ds.numel(), g.contiguous().data_ptr(), 1.0, out.data_ptr(),
+                   _stream())
+        else:
+            f = ds.float()
+            N.call("dmf_scale_by_cast", dt(ds), f.data_ptr(), f.numel(), 1, g.contiguous().data_ptr(), 1.0,
+                   out.data_ptr(), 1, _stream())
+        return out, None, None, None, None, None, None, None
+
+
+# the Philox snapshot shared by the dropout sites of one top-level forward
+RNG_CURRENT = [None]
+
+
+def self_attention(qkv, heads, e):
+    """softmax(q k^T / sqrt(d)) v with q|k|v packed along the last dim of qkv."""
+    if qkv.shape[1] > 64:
+        raise NotImplementedError("long-sequence attention kernel (config 5, >64 tokens) is not built yet")
+    o, _ = _CrossAttnFn.apply(qkv, qkv, heads, e)
+    return o
+
+
+def layerscale_residual(x, y, gamma):
+    """x + y * gamma (LayerScale, transformer_model.py:79-80)."""
+    return x + y * gamma
+
+
+def focal_ce(logits, labels, gamma, alpha_scalar=1.0, alpha_vec=None, reduction="mean"):
+    """Hard-label focal CE (loss.py:66-130): alpha_y (1-p_y)^gamma (-log p_y)
+    == the soft focal kernel with one-hot targets and class weights alpha."""
+    k = logits.shape[1]
+    if alpha_vec is None:
+        alpha_vec = torch.full((k,), float(alpha_scalar), dtype=torch.float32, device=logits.device)
+    return _FocalFn.apply(logits, labels, None, alpha_vec, gamma, 0.0, False, reduction)
+
+
+def dice_bce(logits, target, bce_weight=1.0, dice_weight=1.0, eps=1e-6):
+    """DiceBCELoss (loss.py:11-43). Not on the default path (mask_loss_type
+    'dice'); expressed with device tensor ops."""
+    x = logits.float()
+    t = target.float()
+    bce = (x.clamp_min(0) - x * t + torch.log1p(torch.exp(-x.abs()))).mean()
+    p = torch.sigmoid(x).reshape(x.shape[0], -1)
+    tt = t.reshape(t.shape[0], -1)
+    dice = 2.0 * (p * tt).sum(1) / (p.sum(1) + tt.sum(1) + eps)
+    return bce_weight * bce + dice_weight * (1.0 - dice.mean())
+
+
+def _channel_last_item(x):
+    """[C,H,W] view with channel stride 1 (copy only if needed)."""
+    if x.dim() != 3:
+        raise RuntimeError(f"mimic expects [C,H,W] items, got {tuple(x.shape)}")
+    c, h, w = x.shape
+    if x.stride(0) == 1 and x.stride(2) == c and x.stride(1) == w * c:
+        return x
+    return x.permute(1, 2, 0).contiguous().permute(2, 0, 1)
+
+
+def mimic(s_feat, t_feat):
+    """mimic_feat_loss for one (student, teacher) pair of [C,H,W] items."""
+    s = _channel_last_item(s_feat)
+    t = _channel_last_item(t_feat.to(s.dtype))
+    c, h, w = s.shape
+    return _MimicFn.apply(s, t, 1, 0, 0, h * w, c, c)
+
+
+def mimic_pairs(feats, npairs=2):
+    """train_fusion.py:291-294: mean over pairs (items 2i, 2i+1) of
+    mimic_feat_loss(feats[2i], feats[2i+1]) -- one launch."""
+    f = as_nhwc(feats)
+    n, c, h, w, ld = nhwc(f)
+    stride = 2 * h * w * ld
+    return _MimicFn.apply(f, f.detach()[1:], npairs, stride, stride, h * w, c, ld)

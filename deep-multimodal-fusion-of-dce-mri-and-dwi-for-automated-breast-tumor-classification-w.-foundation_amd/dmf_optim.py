@@ -1,0 +1,196 @@
+"""Multi-tensor AdamW on the device -- drop-in for the ``torch.optim.AdamW``
+that ``LightningFusionOptimizerFactory._get_base_optimizer`` builds
+(selector_helpers.py:617-629, amsgrad=False).
+
+One launch updates every parameter that has a gradient (parameters whose
+grad is None are skipped, exactly like torch). Step counts and the per-group
+hyper-parameters live in device memory, so a captured hipGraph replays the
+update with the current values. ``pack_grads``/``grads_from`` let the
+data-parallel driver all-reduce ONE flat gradient bucket and feed the
+reduced bucket straight into the update (no unpack pass).
+"""
+from __future__ import annotations
+
+import torch
+
+import dmf_native as N
+
+CHUNK = 8192
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("amsgrad is not used on the reference path")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False)
+        super().__init__(params, defaults)
+        self._table_key = None
+        self._hyper = None
+        self._hyper_host = None
+        self._steps = None
+        self._index = {}
+        self.grad_source = None  # optional flat bucket (see pack_grads)
+        self.grad_scale = 1.0
+
+    # -------------------------------------------------------------- tables
+    def _live(self):
+        out = []
+        for gi, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                if p.grad is not None or (self.grad_source is not None and p in self._bucket_offsets):
+                    out.append((gi, p))
+        return out
+
+    def _hyper_values(self):
+        vals = []
+        for g in self.param_groups:
+            b1, b2 = g["betas"]
+            vals += [float(g["lr"]), float(g["weight_decay"]), float(b1), float(b2), float(g["eps"])]
+        return vals
+
+    def sync_hyper(self):
+        vals = self._hyper_values()
+        dev = self.param_groups[0]["params"][0].device
+        if self._hyper is None or self._hyper.numel() != len(vals):
+            self._hyper = torch.tensor(vals, dtype=torch.float32, device=dev)
+            self._hyper_host = vals
+        elif vals != self._hyper_host:
+            self._hyper.copy_(torch.tensor(vals, dtype=torch.float32))
+            self._hyper_host = vals
+
+    def _build(self, live):
+        dev = live[0][1].device
+        # every param ever stepped keeps its slot (and step count) in _index
+        for gi, p in live:
+            if id(p) not in self._index:
+                st = self.state[p]
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                self._index[id(p)] = len(self._index)
+        nslots = len(self._index)
+        if self._steps is None or self._steps.numel() < nslots:
+            old = self._steps
+            self._steps = torch.zeros(max(nslots, 1), dtype=torch.int32, device=dev)
+            if old is not None:
+                self._steps[: old.numel()].copy_(old)
+        rows, chunks = [], []
+        slot_ids = []
+        for t, (gi, p) in enumerate(live):
+            if not p.is_contiguous():
+                raise RuntimeError("FusedAdamW needs contiguous parameters")
+            st = self.state[p]
+            g = self._grad_ptr(p)
+            rows.append([p.data_ptr(), g, st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), gi, p.numel()])
+            slot_ids.append(self._index[id(p)])
+            for b in range(0, p.numel(), CHUNK):
+                chunks.append([t, b, min(p.numel(), b + CHUNK)])
+        self._tensors = torch.tensor(rows, dtype=torch.int64, device=dev)
+        self._chunks = torch.tensor(chunks, dtype=torch.int64, device=dev)
+        self._nchunks = len(chunks)
+        # per-live-tensor step counters: gather/scatter via a slot map kept on device
+        self._slot = torch.tensor(slot_ids, dtype=torch.int64, device=dev)
+        self._live_steps = self._steps[self._slot].clone()
+
+    def _grad_ptr(self, p):
+        if self.grad_source is not None:
+            off = self._bucket_offsets[p]
+            return self.grad_source.data_ptr() + 4 * off
+        if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
+            raise RuntimeError("FusedAdamW needs contiguous fp32 gradients")
+        return p.grad.data_ptr()
+
+    def _key(self, live):
+        return tuple((id(p), self._grad_ptr(p), p.data_ptr()) for _, p in live)
+
+    # ---------------------------------------------------------------- step
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        live = self._live()
+        if not live:
+            return loss
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing:
+            self.sync_hyper()
+            key = self._key(live)
+            if key != self._table_key:
+                if self._table_key is not None:
+                    self._steps[self._slot] = self._live_steps
+                self._build(live)
+                self._table_key = key
+        elif self._table_key is None:
+            raise RuntimeError("run one eager optimizer step before capturing it in a graph")
+        s = N.stream_ptr()
+        N.call("dmf_steps_inc", self._live_steps.data_ptr(), self._live_steps.numel(), s)
+        N.call("dmf_adamw_multi", self._nchunks, self._chunks.data_ptr(), self._tensors.data_ptr(),
+               self._hyper.data_ptr(), self._live_steps.data_ptr(), float(self.grad_scale), s)
+        return loss
+
+    @torch.no_grad()
+    def zero_grad(self, set_to_none=False):
+        if set_to_none:
+            return super().zero_grad(set_to_none=True)
+        pairs, chunks = [], []
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    t = len(pairs)
+                    pairs.append([p.grad.data_ptr(), p.grad.data_ptr()])
+                    for b in range(0, p.grad.numel(), CHUNK):
+                        chunks.append([t, b, min(p.grad.numel(), b + CHUNK)])
+        if not pairs:
+            return
+        key = tuple(x[0] for x in pairs)
+        if getattr(self, "_zero_key", None) != key:
+            dev = self.param_groups[0]["params"][0].device
+            self._zero_pairs = torch.tensor(pairs, dtype=torch.int64, device=dev)
+            self._zero_chunks = torch.tensor(chunks, dtype=torch.int64, device=dev)
+            self._zero_key = key
+        N.call("dmf_multi_copy", self._zero_chunks.shape[0], self._zero_chunks.data_ptr(), self._zero_pairs.data_ptr(),
+               0.0, N.stream_ptr())
+
+    def step_counts(self):
+        """Per-parameter step counts (host copy; for tests)."""
+        if self._table_key is None:
+            return {}
+        self._steps[self._slot] = self._live_steps
+        return {i: int(v) for i, v in enumerate(self._steps.tolist())}
+
+    # ----------------------------------------------------- flat grad bucket
+    def make_bucket(self, params):
+        """Allocate ONE fp32 bucket laid out over ``params`` (the ones that
+        receive gradients); returns it. Use ``pack_grads`` after backward."""
+        self._bucket_params = list(params)
+        self._bucket_offsets = {}
+        off = 0
+        for p in self._bucket_params:
+            self._bucket_offsets[p] = off
+            off += p.numel()
+        dev = self._bucket_params[0].device
+        self.bucket = torch.zeros(off, dtype=torch.float32, device=dev)
+        self._pack_key = None
+        return self.bucket
+
+    @torch.no_grad()
+    def pack_grads(self):
+        """bucket <- concat(p.grad) in one launch."""
+        pairs, chunks = [], []
+        for t, p in enumerate(self._bucket_params):
+            if p.grad is None:
+                raise RuntimeError("pack_grads: a bucket parameter has no gradient")
+            pairs.append([p.grad.data_ptr(), self.bucket.data_ptr() + 4 * self._bucket_offsets[p]])
+            for b in range(0, p.numel(), CHUNK):
+                chunks.append([t, b, min(p.numel(), b + CHUNK)])
+        key = tuple(x[0] for x in pairs)
+        if key != self._pack_key:
+            dev = self.bucket.device
+            self._pk_pairs = torch.tensor(pairs, dtype=torch.int64, device=dev)
+            self._pk_chunks = torch.tensor(chunks, dtype=torch.int64, device=dev)
+            self._pack_key = key
+        N.call("dmf_multi_copy", self._pk_chunks.shape[0], self._pk_chunks.data_ptr(), self._pk_pairs.data_ptr(), 1.0,
+               N.stream_ptr())
+
+    def use_bucket_grads(self, enabled=True, scale=1.0):
+        self.grad_source = self.bucket if enabled else None
+        self.grad_scale = scale
+        self._table_key = None if not enabled else self._table_key

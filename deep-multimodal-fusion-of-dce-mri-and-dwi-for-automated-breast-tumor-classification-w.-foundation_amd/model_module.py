@@ -1,0 +1,644 @@
+"""Encoder and fusion model -- MI355X build of the reference's
+``code/model_module.py``.
+
+Same class names, constructor signatures, parameter/buffer names (so
+state_dicts interchange, including the ``backbone._orig_mod.*`` duplicate of
+model_module.py:539/:545) and forward return structures. The arithmetic runs
+in the gfx950 kernels of ``libdmf_hip.so`` through ``dmf_ops``; activations
+are NCHW-shaped tensors with NHWC storage in the model's compute dtype
+(``set_compute_dtype``; bf16 by default, f32 for the parity mode).
+"""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+from torch.nn import init
+
+import dmf_ops as O
+from foundation_model import _DisabledWrapper, _caches
+from transformer_model import TransformerStage
+
+
+@dataclass
+class FeatureSpec:
+    channels: int
+    stride: int
+
+
+def _dt(module):
+    return getattr(module, "compute_dtype", torch.bfloat16)
+
+
+def _to_compute(x, dtype):
+    """Bring an activation into NHWC compute dtype (no copy when it already is)."""
+    if x.dtype != dtype:
+        x = x.to(dtype)
+    return O.as_nhwc(x)
+
+
+@contextlib.contextmanager
+def _rng_scope(module, device):
+    """One Philox snapshot per top-level forward, shared by every dropout
+    site below it (sites are distinguished by their ids)."""
+    if O.RNG_CURRENT[0] is not None or not module.training:
+        yield
+        return
+    O.RNG_CURRENT[0] = O.RNG.snapshot(device)
+    try:
+        yield
+    finally:
+        O.RNG_CURRENT[0] = None
+
+
+def _rng(device):
+    cur = O.RNG_CURRENT[0]
+    return cur if cur is not None else O.RNG.snapshot(device)
+
+
+# ------------------------------------------------------------------ SE
+class SEBlock(nn.Module):
+    """model_module.py:25-43: returns (x * w, w), w = sigmoid(fc(avgpool(x)))."""
+
+    def __init__(self, channels, reduction=2, dim=2):
+        super().__init__()
+        hidden = max(channels // reduction, 1)
+        self.fc = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(channels, hidden, 1, bias=True), nn.GELU(),
+                                nn.Conv2d(hidden, channels, 1, bias=True), nn.Sigmoid())
+
+    def forward(self, x):
+        return O.se_block(_to_compute(x, _dt(self)), self)
+
+
+class TemporalAttention(SEBlock):
+    pass
+
+
+class ChannelAttention(SEBlock):
+    pass
+
+
+class MaskGuidedSpatialAttention(nn.Module):
+    """model_module.py:49-97."""
+
+    def __init__(self, in_channels_img, in_channels_mask, hidden_channels=16, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        if in_channels_mask != 1:
+            raise NotImplementedError("mask guidance expects a single-channel mask (as on the reference path)")
+        self.dim = dim
+        self.interp_mode = "bilinear"
+        self.gamma = nn.Parameter(torch.tensor(0.1))
+        self.mask_processor = nn.Sequential(nn.Conv2d(in_channels_mask, hidden_channels, 1, bias=False),
+                                            nn.GroupNorm(1, hidden_channels), nn.GELU(),
+                                            nn.Conv2d(hidden_channels, 1, 1), nn.Sigmoid())
+
+    def forward(self, img_features, mask_features):
+        dt = _dt(self)
+        return O.mask_attention(_to_compute(img_features, dt), _to_compute(mask_features, dt), self)
+
+
+class ReconHead(nn.Module):
+    """model_module.py:100-125: conv3x3 -> BN -> GELU -> conv3x3 (+bias) to recon_ch."""
+
+    def __init__(self, in_ch, recon_ch=1, upsample=False, dim=2):
+        super().__init__()
+        self.upsample = upsample
+        self.dim = dim
+        self.conv = nn.Sequential(nn.Conv2d(in_ch, in_ch, 3, padding=1, bias=False), nn.BatchNorm2d(in_ch), nn.GELU(),
+                                  nn.Conv2d(in_ch, recon_ch, 3, padding=1))
+
+    def forward(self, x):
+        x = _to_compute(x, _dt(self))
+        c0, bn, c3 = self.conv[0], self.conv[1], self.conv[3]
+        h = O.conv_bn_act(x, c0, _caches(c0), bn, "gelu")
+        out = O.conv2d(h, c3, _caches(c3))
+        if self.upsample:
+            out = O.bilinear(out, out.shape[-2] * 2, out.shape[-1] * 2)
+        return out
+
+
+class MaskHeadResize(nn.Module):
+    """model_module.py:131-215: 1x1 pre -> size dispatch (identity at 32,
+    stride-2 3x3+GELU chains from 64..512, bilinear otherwise) -> 1x1 out."""
+
+    def __init__(self, in_ch, mid_ch=64, out_ch=1, out_size=32, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        self.dim = dim
+        self.out_size = out_size
+        self.interp_mode = "bilinear"
+        self.pre = nn.Conv2d(in_ch, mid_ch, 1)
+
+        def chain(n):
+            layers = []
+            for _ in range(n):
+                layers += [nn.Conv2d(mid_ch, mid_ch, 3, stride=2, padding=1), nn.GELU()]
+            return nn.Sequential(*layers)
+
+        self.down_64_to_32 = chain(1)
+        self.down_128_to_32 = chain(2)
+        self.down_256_to_32 = chain(3)
+        self.down_512_to_32 = chain(4)
+        self.out = nn.Conv2d(mid_ch, out_ch, 1)
+        self.dispatch = {32: None, 64: self.down_64_to_32, 128: self.down_128_to_32, 256: self.down_256_to_32,
+                         512: self.down_512_to_32}
+
+    def forward(self, x):
+        x = _to_compute(x, _dt(self))
+        h = O.conv2d(x, self.pre, _caches(self.pre))
+        op = self.dispatch.get(h.shape[-1], "interp")
+        if op is None:
+            pass
+        elif op == "interp":
+            h = O.bilinear(h, self.out_size, self.out_size)
+        else:
+            for i in range(0, len(op), 2):
+                h = O.act_nhwc(O.conv2d(h, op[i], _caches(op[i])), "gelu")
+        return O.conv2d(h, self.out, _caches(self.out))
+
+
+class ResNetLiteBlock_withRecon(nn.Module):
+    """model_module.py:220-316: bottleneck stack + projection/identity skip,
+    act -> dropout -> SE -> optional ReconHead."""
+
+    def __init__(self, in_ch, out_ch, downsample=False, recon_ch=1, use_se=False, se_reduction=2, dropout=0.4, dim=2,
+                 num_repeats=1, downsample_each_repeat=False, mid_squeeze=2):
+        super().__init__()
+        self.dim = dim
+        self.num_repeats = num_repeats
+        stride = 2 if downsample else 1
+        mid = max(out_ch // mid_squeeze, 1)
+        self.p = float(dropout)
+        self.bottlenecks = nn.ModuleList()
+        for i in range(num_repeats):
+            s = stride if (downsample_each_repeat or i == 0) else 1
+            cin = in_ch if i == 0 else out_ch
+            self.bottlenecks.append(nn.Sequential(
+                nn.Conv2d(cin, mid, 1, stride=s, bias=False), nn.BatchNorm2d(mid), nn.GELU(), nn.Dropout(p=dropout),
+                nn.Conv2d(mid, mid, 3, padding=1, bias=False), nn.BatchNorm2d(mid), nn.GELU(),
+                nn.Conv2d(mid, out_ch, 1, bias=False), nn.BatchNorm2d(out_ch)))
+        self.act = nn.GELU()
+        self.dropout = nn.Dropout(p=dropout)
+        self.skip = (nn.Sequential(nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False), nn.BatchNorm2d(out_ch))
+                     if (stride > 1 or in_ch != out_ch) else None)
+        self.use_se = use_se
+        self.se = SEBlock(out_ch, reduction=se_reduction, dim=dim) if use_se else None
+        self.recon_ch = int(recon_ch)
+        self.reconstruct = ReconHead(out_ch, recon_ch, upsample=False, dim=dim) if self.recon_ch > 0 else None
+        self._sites = [(O.RNG.new_site(), O.RNG.new_site()) for _ in range(num_repeats)]
+
+    def forward(self, x):
+        x = _to_compute(x, _dt(self))
+        p = self.p if self.training else 0.0
+        rng = _rng(x.device) if p > 0 else None
+        h = x
+        last = len(self.bottlenecks) - 1
+        for i, b in enumerate(self.bottlenecks):
+            site_a, site_b = self._sites[i]
+            h = O.conv_bn_act(h, b[0], _caches(b[0]), b[1], "gelu", dropout_p=p, rng=rng, site=site_a)
+            h = O.conv_bn_act(h, b[4], _caches(b[4]), b[5], "gelu")
+            if i < last:
+                h = O.conv_bn_act(h, b[7], _caches(b[7]), b[8], "none")
+            else:
+                # act(bn(conv(h)) + identity) -> dropout, fused in one pass
+                kw = dict(dropout_p=p, rng=rng, site=site_b)
+                if self.skip is not None:
+                    kw["skip"] = (x, self.skip[0], _caches(self.skip[0]), self.skip[1])
+                else:
+                    kw["res"] = x
+                h = O.conv_bn_act(h, b[7], _caches(b[7]), b[8], "gelu", **kw)
+        out = h
+        if self.use_se:
+            out, _ = O.se_block(out, self.se)
+        rec = self.reconstruct(out) if self.reconstruct is not None else None
+        return out, rec
+
+
+class Projector(nn.Module):
+    """model_module.py:323-348: [1x1 conv -> BN -> GELU] x 2."""
+
+    def __init__(self, in_ch, proj_dim=64, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        self.dim = dim
+        self.proj = nn.Sequential(nn.Conv2d(in_ch, proj_dim, 1, bias=False), nn.BatchNorm2d(proj_dim), nn.GELU(),
+                                  nn.Conv2d(proj_dim, proj_dim, 1, bias=False), nn.BatchNorm2d(proj_dim), nn.GELU())
+
+    def forward(self, x, replicate=1):
+        """``replicate``: the reference evaluates this on AdaptiveAvgPool2d
+        output that is an exact nearest 2x upsample of x; per-pixel ops and
+        batch statistics commute with that replication, so the projector runs
+        at x's resolution and only the result is replicated (running-var
+        unbiasing still uses the replicated element count)."""
+        x = _to_compute(x, _dt(self))
+        pr = self.proj
+        h = O.conv_bn_act(x, pr[0], _caches(pr[0]), pr[1], "gelu", unbias_mult=replicate * replicate)
+        h = O.conv_bn_act(h, pr[3], _caches(pr[3]), pr[4], "gelu", unbias_mult=replicate * replicate)
+        return O.upsample_nearest(h, replicate)
+
+
+class ClassificationHead(nn.Module):
+    """model_module.py:355-369: GAP -> flatten -> (L2 normalize) -> Linear."""
+
+    def __init__(self, in_ch, num_classes, dim=2, normalize=True):
+        super().__init__()
+        self.pool = nn.AdaptiveAvgPool2d((1, 1))
+        self.flatten = nn.Flatten()
+        self.fc = nn.Linear(in_ch, num_classes)
+        self.normalize = normalize
+
+    def forward(self, x):
+        v = O.gap(_to_compute(x, _dt(self)))
+        if self.normalize:
+            v = O.l2_normalize_rows(v)
+        return O.linear(v, self.fc.weight, self.fc.bias)
+
+
+class FeatureDownAlign(nn.Module):
+    """model_module.py:371-396."""
+
+    def __init__(self, in_ch, out_ch, dim=2, downsample=True):
+        super().__init__()
+        assert dim in (2, 3)
+        if in_ch != out_ch or downsample:
+            k, s, p = (3, 2, 1) if downsample else (1, 1, 0)
+            self.proj = nn.Sequential(nn.Conv2d(in_ch, out_ch, k, stride=s, padding=p, bias=False),
+                                      nn.BatchNorm2d(out_ch), nn.GELU())
+        else:
+            self.proj = nn.Identity()
+
+    def forward(self, x):
+        if isinstance(self.proj, nn.Identity):
+            return x
+        x = _to_compute(x, _dt(self))
+        return O.conv_bn_act(x, self.proj[0], _caches(self.proj[0]), self.proj[1], "gelu")
+
+
+class BackboneAdapter(nn.Module):
+    """model_module.py:401-476: backbone -> per-chain channel concat -> neck
+    [conv3x3 -> BN -> GELU] x 2. A two-map chain (C4+C5) is consumed by the
+    conv engine's dual-source path, so the 3072-channel concat is never
+    materialised."""
+
+    def __init__(self, backbone, selected_indices_chains, out_channels=(64, 128, 256), dim=2, is_transformer=False):
+        super().__init__()
+        assert len(selected_indices_chains) == 3, "Must provide 3 chains for f1/f2/f3"
+        assert len(out_channels) == 3, "Must provide 3 output channels for f1/f2/f3"
+        self.backbone = backbone
+        self.selected_indices_chains = selected_indices_chains
+        self.dim = dim
+        self.is_transformer = is_transformer
+        info = backbone.feature_info
+        self.features = [FeatureSpec(c, s) for c, s in zip(info.channels(), info.reduction())]
+        self.necks = nn.ModuleDict()
+        for i, chain in enumerate(selected_indices_chains):
+            cin = sum(self.features[j].channels for j in chain)
+            co = out_channels[i]
+            self.necks[f"f{i + 1}"] = nn.Sequential(nn.Conv2d(cin, co, 3, padding=1), nn.BatchNorm2d(co), nn.GELU(),
+                                                   nn.Conv2d(co, co, 3, padding=1), nn.BatchNorm2d(co), nn.GELU())
+
+    def forward(self, x):
+        feats = self.backbone(x)
+        outs = []
+        for i, chain in enumerate(self.selected_indices_chains):
+            parts = [feats[j] for j in chain]
+            if self.is_transformer:
+                parts = [_tokens_to_map(f) for f in parts]
+            nk = self.necks[f"f{i + 1}"]
+            if len(parts) == 1:
+                h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu")
+            elif len(parts) == 2:
+                h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu", x2=parts[1])
+            else:
+                raise NotImplementedError("neck chains of more than two feature maps are not built yet")
+            outs.append(O.conv_bn_act(h, nk[3], _caches(nk[3]), nk[4], "gelu"))
+        return outs[0], outs[1], outs[2]
+
+
+def _tokens_to_map(f):
+    if f.ndim == 4:
+        return f
+    if f.ndim != 3:
+        raise ValueError(f"Unexpected transformer feature shape: {f.shape}")
+    b, n, c = f.shape
+    s = int(n ** 0.5)
+    return O.as_nhwc(f.view(b, s, s, c).permute(0, 3, 1, 2))
+
+
+# -------------------------------------------------------------- encoder
+class ModelMaskHeadBackbone(nn.Module):
+    """model_module.py:481-733. forward(x [B,C,H,W] fp32, masks=None) ->
+    (logits [B,K], aux, mask_pred [B,1,32,32])."""
+
+    def __init__(self, method, parameters_dict, backbone=None):
+        super().__init__()
+        P = parameters_dict
+        mp = P[f"{method}_model_parameters"]
+        self.channel_num = P[f"{method}_channel_num"]
+        self.num_classes = P["class_num"]
+        self.dim = P["dim"]
+        if self.dim != 2:
+            raise NotImplementedError("the MI355X build covers the 2-D path (parameters['dim'] == 2)")
+        self.enable_modality_attention = mp["enable_modality_attention"]
+        self.use_se = mp["use_se"]
+        self.use_hybrid_transformer = mp["use_hybrid_transformer"]
+        self.use_backbone = mp["use_backbone"]
+        self.channels = mp["channels"]
+        self.proj_dim = mp["proj_dim"]
+        self.dropout = mp["dropout"]
+        self.num_repeats = mp["repeat_blocks"]
+        self.mid_squeeze = mp["mid_squeeze"]
+        self.downsample = mp["downsample"]
+        self.downsample_each_repeat = mp["downsample_each_repeat"]
+        self.selected_indices_chains = mp["backbone_index_lists"]
+        self.backbone_out_channels = mp["backbone_out_channels"]
+        self.transformer_backbone = mp["transformer_backbone"]
+        mk = mp["mask_parameters"]
+        self.mask_enabled = mk["mask"]
+        self.mask_stage = mk["mask_stage"].lower()
+        self.mask_size = mk["mask_target_size"][0]
+        c1, c2, c3 = self.channels
+
+        self.proj_pool = nn.AdaptiveAvgPool2d((self.proj_dim, self.proj_dim))
+        self.backbone = _DisabledWrapper(backbone) if backbone is not None else None
+        if self.use_backbone:
+            if self.backbone is None:
+                raise ValueError("use_backbone=True needs a backbone (build_medical_backbone)")
+            self.backbone_adapter = BackboneAdapter(self.backbone, self.selected_indices_chains, (c1, c1, c2),
+                                                    is_transformer=self.transformer_backbone)
+            b1_in = c1
+        else:
+            b1_in = self.channel_num
+
+        blk = dict(use_se=self.use_se, dim=self.dim, dropout=self.dropout,
+                   downsample_each_repeat=self.downsample_each_repeat, mid_squeeze=self.mid_squeeze)
+        self.block1 = ResNetLiteBlock_withRecon(b1_in, c1, downsample=self.downsample[0], recon_ch=1,
+                                                num_repeats=self.num_repeats[0], **blk)
+        self.block2 = ResNetLiteBlock_withRecon(c1, c2, downsample=self.downsample[1], recon_ch=1,
+                                                num_repeats=self.num_repeats[1], **blk)
+        if not self.use_hybrid_transformer:
+            self.block3 = ResNetLiteBlock_withRecon(c2, c3, downsample=self.downsample[2], recon_ch=0,
+                                                    num_repeats=self.num_repeats[2], **blk)
+        else:
+            self.transformer = TransformerStage(in_ch=c2, embed_dim=mp["transformer_embed_dim"],
+                                                depth=mp["transformer_depth"], heads=mp["transformer_heads"],
+                                                patch_size=mp["transformer_patch_size"], dim=self.dim)
+            self.trans_out_proj = nn.Conv2d(mp["transformer_embed_dim"], c3, kernel_size=1)
+
+        self.modality_attention = None
+        if self.enable_modality_attention:
+            if method == "dce":
+                self.modality_attention = TemporalAttention(self.channel_num, reduction=2)
+            elif method == "dwi":
+                self.modality_attention = ChannelAttention(self.channel_num, reduction=2)
+            else:
+                raise ValueError("Unknown method for modality attention.")
+        self.f2_weight = nn.Parameter(torch.tensor(0.5))
+        self.f3_weight = nn.Parameter(torch.tensor(0.5))
+        self.norm_f2 = nn.GroupNorm(c1, c1)
+        self.norm_f3 = nn.GroupNorm(c2, c2)
+        if self.mask_enabled:
+            self.f1_to_f2 = FeatureDownAlign(c1, c2, dim=self.dim, downsample=False)
+            self.f2_to_f3 = FeatureDownAlign(c2, c3, dim=self.dim, downsample=False)
+            mask_in = {"f1": c1, "f2": c2, "f3": c3}.get(self.mask_stage)
+            if mask_in is None:
+                raise ValueError(f"mask_stage must be f1/f2/f3, got {self.mask_stage!r}")
+            self.mask_head = MaskHeadResize(in_ch=mask_in, out_size=self.mask_size, dim=self.dim)
+            self.mask_spatial_attention = MaskGuidedSpatialAttention(in_channels_img=c3, in_channels_mask=1,
+                                                                     dim=self.dim)
+            if self.use_hybrid_transformer and self.mask_stage == "f3":
+                raise ValueError("mask_stage='f3' not supported with hybrid transformer")
+        self.classification_head = ClassificationHead(in_ch=c3, num_classes=self.num_classes, dim=self.dim)
+        self.proj_f1 = Projector(c1, self.proj_dim, dim=self.dim)
+        self.proj_f2 = Projector(c2, self.proj_dim, dim=self.dim)
+        self.proj_r1 = Projector(1, self.proj_dim, dim=self.dim)
+        self.proj_r2 = Projector(1, self.proj_dim, dim=self.dim)
+        set_compute_dtype(self, mp.get("compute_dtype", torch.bfloat16))
+
+    # ------------------------------------------------------------- helpers
+    def _projector(self, proj, f):
+        """proj_pool (AdaptiveAvgPool2d((proj_dim, proj_dim))) then Projector."""
+        h, w = f.shape[-2], f.shape[-1]
+        if h == w and self.proj_dim % h == 0:
+            return proj(f, replicate=self.proj_dim // h)
+        raise NotImplementedError(f"proj_pool from {tuple(f.shape[-2:])} to {self.proj_dim} is not built")
+
+    def _stage_input(self, x):
+        dt = _dt(self)
+        if self.modality_attention is not None:
+            fc = self.modality_attention.fc
+            pooled = O.nchw_mean(x)
+            hmid = O.linear(pooled, fc[1].weight, fc[1].bias, act="gelu")
+            gate = O.linear(hmid, fc[3].weight, fc[3].bias, act="sigmoid")
+            x_in, _ = O.input_stage(x, dt, gate)
+            return x_in, gate.view(gate.shape[0], gate.shape[1], 1, 1)
+        x_in, _ = O.input_stage(x, dt, None)
+        return x_in, None
+
+    def forward(self, x, masks=None):
+        mask_pred = None
+        mask_attn_map = None
+        with _rng_scope(self, x.device):
+            x_in, mod_attn_map = self._stage_input(x)
+            if self.use_backbone:
+                f1_b, f2_b, f3_b = self.backbone_adapter(x_in)
+                f1, r1 = self.block1(f1_b)
+            else:
+                f1, r1 = self.block1(x_in)
+            if self.mask_enabled and self.mask_stage == "f1":
+                mask_pred = self.mask_head(f1)
+                f1, mask_attn_map = self.mask_spatial_attention(f1, mask_pred)
+            f2_in = O.gn_mix(f2_b, f1, self.f2_weight, self.norm_f2) if self.use_backbone else f1
+            f2, r2 = self.block2(f2_in)
+            if self.mask_enabled and self.mask_stage == "f2":
+                f1_aligned = self.f1_to_f2(f1)
+                mask_pred = self.mask_head(O.act_nhwc(f2, "none", res=f1_aligned))
+                f2, mask_attn_map = self.mask_spatial_attention(f2, mask_pred)
+            if not self.use_hybrid_transformer:
+                f3_in = O.gn_mix(f3_b, f2, self.f3_weight, self.norm_f3) if self.use_backbone else f2
+                f3, _ = self.block3(f3_in)
+                if self.mask_enabled and self.mask_stage == "f3":
+                    f2_aligned = self.f2_to_f3(f2)
+                    mask_pred = self.mask_head(O.act_nhwc(f3, "none", res=f2_aligned))
+                    f3, mask_attn_map = self.mask_spatial_attention(f3, mask_pred)
+            else:
+                f3 = O.conv2d(self.transformer(f2), self.trans_out_proj, _caches(self.trans_out_proj))
+            p1 = self._projector(self.proj_f1, f1)
+            p2 = self._projector(self.proj_f2, f2)
+            p1_r = self._projector(self.proj_r1, r1)
+            p2_r = self._projector(self.proj_r2, r2)
+            logits = self.classification_head(f3)
+        aux = {"raw_feats": [f1, f2, f3], "recon_feats": [r1, r2], "proj_pairs": [p1, p1_r, p2, p2_r],
+               "mask_attn_map": mask_attn_map, "mod_attn_map": mod_attn_map}
+        return logits, aux, mask_pred
+
+
+# ----------------------------------------------------------------- fusion
+class GatingAttention(nn.Module):
+    """model_module.py:745-780."""
+
+    def __init__(self, feat_dim, use_mask_attention=True, dim=2):
+        super().__init__()
+        self.use_mask_attention = use_mask_attention
+        self.fc = nn.Linear(feat_dim * 2 + (2 if use_mask_attention else 0), 2)
+        self.dim = dim
+
+    def forward(self, pvec_dwi, pvec_dce, dwi_mask=None, dce_mask=None):
+        ca = cb = None
+        if self.use_mask_attention and dwi_mask is not None and dce_mask is not None:
+            dt = getattr(self, "compute_dtype", torch.bfloat16)
+            ca = O.gap(_to_compute(dwi_mask, dt)).reshape(-1)
+            cb = O.gap(_to_compute(dce_mask, dt)).reshape(-1)
+        elif self.use_mask_attention:
+            # the reference then feeds 2C inputs into a 2C+2 Linear (a shape error); keep that contract
+            raise RuntimeError("GatingAttention with use_mask_attention=True needs both mask predictions")
+        return O.gating(pvec_dwi.contiguous().float(), pvec_dce.contiguous().float(), ca, cb, self.fc)
+
+
+class FusionReduce(nn.Module):
+    """model_module.py:782-794."""
+
+    def __init__(self, in_ch, out_ch, dim=2):
+        super().__init__()
+        self.reduce = nn.Sequential(nn.Conv2d(in_ch, out_ch, 1, bias=False), nn.BatchNorm2d(out_ch), nn.GELU())
+
+    def forward(self, x, x2=None):
+        return O.conv_bn_act(x, self.reduce[0], _caches(self.reduce[0]), self.reduce[1], "gelu", x2=x2)
+
+
+class CrossAttentionBlock(nn.Module):
+    """model_module.py:799-818: MHA(q, kv, kv) + (LN -> Linear -> GELU -> Linear) residual."""
+
+    def __init__(self, channels, num_heads=4):
+        super().__init__()
+        self.cross_attn = nn.MultiheadAttention(embed_dim=channels, num_heads=num_heads, batch_first=True)
+        self.attn_ffn = nn.Sequential(nn.LayerNorm(channels), nn.Linear(channels, channels), nn.GELU(),
+                                      nn.Linear(channels, channels))
+
+    def forward(self, query_tokens, key_value_tokens):
+        mha = self.cross_attn
+        b, nq, e = query_tokens.shape
+        nk = key_value_tokens.shape[1]
+        qf = O.linear(query_tokens.reshape(b * nq, e).float(), mha.in_proj_weight, mha.in_proj_bias).view(b, nq, 3 * e)
+        kvf = O.linear(key_value_tokens.reshape(b * nk, e).float(), mha.in_proj_weight, mha.in_proj_bias).view(
+            b, nk, 3 * e)
+        o, attn_w = O.cross_attention(qf, kvf, mha.num_heads, e)
+        out = O.linear(o.reshape(b * nq, e), mha.out_proj.weight, mha.out_proj.bias)
+        f = self.attn_ffn
+        h = O.layer_norm(out, f[0])
+        h = O.linear(h, f[1].weight, f[1].bias, act="gelu")
+        h = O.linear(h, f[3].weight, f[3].bias)
+        return O.residual_add_f32(out, h).view(b, nq, e), attn_w
+
+
+class FusionModel(nn.Module):
+    """model_module.py:821-1000 -- the DCE x DWI cross-modal fusion op."""
+
+    def __init__(self, parameters_dict):
+        super().__init__()
+        fc = parameters_dict["fusion_model_parameters"]
+        fs = fc["fusion_specific_parameters"]
+        self.dim = parameters_dict["dim"]
+        self.num_classes = parameters_dict["class_num"]
+        self.fusion_channels = fs["fusion_channels"]
+        self.token_pool = fs["token_pool"]
+        self.mha_heads = fs["mha_heads"]
+        self.dwi_ch = fs["dwi_out_channels"]
+        self.dce_ch = fs["dce_out_channels"]
+        self.use_cross_attention = fs["use_cross_attention"]
+        self.use_mask_attention = fs["use_mask_attention"]
+        self.fusion_recon_ch = fs["fusion_recon_ch"]
+        self.proj_dim = fc["proj_dim"]
+        self.mask_size = fc["mask_parameters"]["mask_target_size"][0]
+        self.dropout = fc["dropout"]
+        self.use_se_in_fusion = fc["use_se"]
+        C = self.fusion_channels
+        self.proj_in_dwi = nn.Conv2d(self.dwi_ch, C, 1, bias=False) if self.dwi_ch != C else nn.Identity()
+        self.proj_in_dce = nn.Conv2d(self.dce_ch, C, 1, bias=False) if self.dce_ch != C else nn.Identity()
+        self.fusion_conv_reduce = FusionReduce(2 * C, C, dim=self.dim)
+        self.refine_act = nn.GELU()
+        self.fusion_se = SEBlock(C, reduction=2, dim=self.dim) if self.use_se_in_fusion else None
+        self.gating = GatingAttention(feat_dim=C, use_mask_attention=self.use_mask_attention, dim=self.dim)
+        self.refine = ResNetLiteBlock_withRecon(in_ch=C, out_ch=C, dim=self.dim, dropout=self.dropout, mid_squeeze=2)
+        if self.use_cross_attention:
+            self.cross_attn_block = CrossAttentionBlock(C, num_heads=self.mha_heads)
+        self.mask_head = MaskHeadResize(in_ch=C, out_size=self.mask_size, dim=self.dim)
+        self.fusion_reconstruct = ReconHead(in_ch=C, recon_ch=self.fusion_recon_ch, upsample=False, dim=self.dim)
+        self.classifier = nn.Sequential(nn.AdaptiveAvgPool2d((1, 1)), nn.Flatten(), nn.Linear(C, self.num_classes))
+        self.projF = Projector(in_ch=C, proj_dim=self.proj_dim, dim=self.dim)
+        set_compute_dtype(self, fc.get("compute_dtype", torch.bfloat16))
+
+    def _proj(self, mod, f):
+        f = _to_compute(f, _dt(self))
+        return f if isinstance(mod, nn.Identity) else O.conv2d(f, mod, _caches(mod))
+
+    def _to_tokens(self, feat):
+        hp, wp = self.token_pool
+        return O.to_tokens(_to_compute(feat, _dt(self)), hp, wp)
+
+    def forward(self, raw_feats_dwi, raw_feats_dce, dwi_mask_pred=None, dce_mask_pred=None):
+        with _rng_scope(self, raw_feats_dwi[-1].device):
+            p_dwi = self._proj(self.proj_in_dwi, raw_feats_dwi[-1])
+            p_dce = self._proj(self.proj_in_dce, raw_feats_dce[-1])
+            # Q4: reduce + refine are computed (BN running stats move in train
+            # mode) but never reach an output -- as in the reference (:935-940)
+            reduced = self.fusion_conv_reduce(p_dwi, x2=p_dce)
+            residual, _ = self.refine(reduced)
+            _refined = O.act_nhwc(reduced, "gelu", res=residual)
+            pvec_dwi = O.gap(p_dwi)
+            pvec_dce = O.gap(p_dce)
+            gating_weights = self.gating(pvec_dwi, pvec_dce, dwi_mask=dwi_mask_pred, dce_mask=dce_mask_pred)
+            attn_weights = None
+            low = None
+            hp, wp = self.token_pool
+            if self.use_cross_attention:
+                t_dwi = self._to_tokens(p_dwi)
+                t_dce = self._to_tokens(p_dce)
+                low, attn_weights = self.cross_attn_block(t_dwi, t_dce)
+            fused = O.fusion_combine(p_dwi, p_dce, gating_weights, low, hp, wp)
+            fused_refined = O.se_block(fused, self.fusion_se)[0] if self.fusion_se is not None else fused
+            fused_mask_logits = self.mask_head(fused_refined)
+            cl = self.classifier[2]
+            logits = O.linear(O.gap(fused_refined), cl.weight, cl.bias)
+            recon_fused = self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None
+            proj_fused = self.projF(fused_refined)
+        aux = {"proj_fused": proj_fused, "recon_fused": recon_fused, "gating_weights": gating_weights,
+               "attn_weights": attn_weights, "p_dwi": p_dwi, "p_dce": p_dce}
+        return logits, fused_mask_logits, aux
+
+
+# ------------------------------------------------------------------ init
+def init_parameter(model):
+    """model_module.py:1002-1015: Linear kaiming_uniform_/zero bias; every
+    BatchNorm gamma ~ N(1, 0.02), beta 0 (also the backbone's: quirk Q3)."""
+    if isinstance(model, nn.Linear):
+        if model.weight is not None:
+            init.kaiming_uniform_(model.weight.data)
+        if model.bias is not None:
+            init.constant_(model.bias.data, 0)
+    elif isinstance(model, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d)):
+        if model.weight is not None:
+            init.normal_(model.weight.data, mean=1, std=0.02)
+        if model.bias is not None:
+            init.constant_(model.bias.data, 0)
+
+
+def initialize_model(model, requires_grad):
+    """model_module.py:1018-1023."""
+    for param in model.parameters():
+        param.requires_grad = requires_grad
+    model.apply(init_parameter)
+    return model
+
+
+def set_compute_dtype(model, dtype):
+    """Select the arithmetic type of every kernel under ``model``:
+    torch.bfloat16 (throughput, fp32 accumulation) or torch.float32 (parity)."""
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"compute dtype must be float32 or bfloat16, got {dtype}")
+    for m in model.modules():
+        m.compute_dtype = dtype
+    return model

@@ -1,0 +1,218 @@
+"""Fusion training step -- MI355X build of the reference's
+``code/train_fusion.py`` (LightningFusionModel, :13-702; helpers :709-760).
+
+``LightningFusionModel`` keeps the reference's constructor, hooks and
+``_shared_step(batch, phase, return_preds)`` contract, without the Lightning
+runtime: a driver (``bench.py``, ``dmf_dp.FusionDPTrainer``) calls
+``training_step`` -> backward -> optimizer step, on one process per GPU.
+The loss terms run in the fused criterion kernels (csrc/losses.hip); the five
+reconstruction terms of one step share a single launch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+import dmf_ops as O
+from loss import LabelSmoothing
+from selector_helpers import LightningFusionOptimizerFactory, mask_criterion_selector
+from train import (compute_attn_energy_loss, compute_feat_norm_loss, compute_feature_consistency_loss, tta_flip_lr,
+                   tta_flip_lrud, tta_flip_ud, tta_id)
+
+
+class LightningFusionModel(nn.Module):
+    def __init__(self, dwi_model, dce_model, fusion_model, parameters_dict, criterion_clf, optimizer_fn=None,
+                 scheduler_fn=None, paths=None):
+        super().__init__()
+        self.method = "fusion"
+        self.dwi_model = dwi_model
+        self.dce_model = dce_model
+        self.fusion_model = fusion_model
+        self.parameters_dict = parameters_dict
+        self.criterion_clf = criterion_clf
+        self.paths = paths
+        fp = parameters_dict["fusion_model_parameters"]
+        self.recon_enabled = fp["recon_enabled"]
+        self.lambda_recon = fp["lambda_recon"]
+        self.mask_enabled = fp["mask_parameters"]["mask"]
+        self.lambda_mask = fp["mask_parameters"]["lambda_mask"]
+        self.class_num = parameters_dict["class_num"]
+        self.mimic_enabled = fp["mimic_enabled"]
+        self.lambda_mimic = fp["lambda_mimic"]
+        self.label_smoother = LabelSmoothing(self.class_num, fp["label_smoothing_alpha"]) \
+            if fp["label_smoothing_enabled"] else None
+        self.mask_criterion = mask_criterion_selector(parameters_dict, self.method)
+        self.enable_modality_attention = fp["enable_modality_attention"]
+        self.use_aux_loss_sched = parameters_dict["use_simple_aux_loss_scheduling"]
+        self.aux_loss_limit = parameters_dict["aux_loss_weight_epoch_limit"]
+        self.attn_reg_enabled = fp["attn_reg_enabled"]
+        self.lambda_attn_energy = fp["lambda_attn_energy"]
+        self.lambda_feature_consistency = fp["lambda_feature_consistency"]
+        self.feat_norm_reg_enabled = fp["feat_norm_reg_enabled"]
+        self.lambda_feat_norm = fp["lambda_feat_norm"]
+        self.unfreeze_timer = int(parameters_dict["unfreeze_timer"])
+        self.backbone_freeze_on_start = parameters_dict["backbone_freeze_on_start"]
+        self.backbone_num_groups = parameters_dict["backbone_num_groups"]
+        self.current_epoch = 0
+        self.global_step = 0
+        self.transforms_list = [tta_id, tta_flip_lr, tta_flip_ud, tta_flip_lrud]
+        self.opt_factory = LightningFusionOptimizerFactory(dwi_model=dwi_model, dce_model=dce_model,
+                                                           fusion_model=fusion_model, parameters=parameters_dict)
+        self.optimizer_fn = self.opt_factory.optimizer_fn
+        self.scheduler_fn = self.opt_factory.scheduler_fn
+        self.optimizer = None
+        self.last_metrics = {}
+
+    @property
+    def device(self):
+        return next(self.fusion_model.parameters()).device
+
+    # ---------------------------------------------------------------- hooks
+    def configure_optimizers(self):
+        self.optimizer = self.optimizer_fn(None)
+        if self.scheduler_fn is None:
+            return self.optimizer
+        sched = self.scheduler_fn(self.optimizer)
+        return {"optimizer": self.optimizer, "lr_scheduler": sched}
+
+    def on_train_epoch_start(self):
+        """train_fusion.py:155-169: gradual unfreeze."""
+        if self.backbone_freeze_on_start and self.current_epoch <= (self.unfreeze_timer * self.backbone_num_groups
+                                                                    + 1):
+            new = self.opt_factory.gradual_unfreeze(epoch=self.current_epoch,
+                                                    unfreeze_every_n_epochs=self.unfreeze_timer)
+            if new and self.optimizer is not None:
+                self.opt_factory.sync_unfrozen_params_to_optimizer(self.optimizer, new)
+
+    def forward(self, dwi_feats, dce_feats, dwi_mask=None, dce_mask=None):
+        return self.fusion_model(dwi_feats, dce_feats, dwi_mask, dce_mask)
+
+    # ---------------------------------------------------------------- step
+    def _shared_step(self, batch, phase="train", return_preds=False):
+        """train_fusion.py:204-321."""
+        is_train = phase == "train"
+        if self.mask_enabled:
+            dwi_inputs, dce_inputs, masks_batch, labels = batch
+        else:
+            dwi_inputs, dce_inputs, labels = batch
+            masks_batch = None
+        dev = self.device
+        dwi_inputs = dwi_inputs.to(dev, non_blocking=True)
+        dce_inputs = dce_inputs.to(dev, non_blocking=True)
+        labels = labels.long().to(dev, non_blocking=True)
+        if masks_batch is not None:
+            masks_batch = masks_batch.to(dev, non_blocking=True)
+        aux_w = max(0.0, 1 - self.current_epoch / self.aux_loss_limit) if self.use_aux_loss_sched else 1.0
+
+        _, dwi_aux, dwi_mask_pred = self.dwi_model(dwi_inputs)
+        _, dce_aux, dce_mask_pred = self.dce_model(dce_inputs)
+        logits, fused_mask_logits, aux = self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask_pred,
+                                                      dce_mask_pred)
+
+        if self.label_smoother is not None:
+            smoothed = self.label_smoother(logits, labels)
+        if is_train:
+            cls_loss = self.criterion_clf(logits, smoothed)  # Q7: undefined without smoothing, as in the reference
+        else:
+            cls_loss = self.criterion_clf(logits, labels)
+        total = cls_loss
+
+        mask_loss_val = torch.zeros((), device=dev)
+        if self.mask_enabled:
+            mask_loss_val = (safe_mask_loss(dwi_mask_pred, masks_batch, self.mask_criterion)
+                             + safe_mask_loss(dce_mask_pred, masks_batch, self.mask_criterion)
+                             + safe_mask_loss(fused_mask_logits, masks_batch, self.mask_criterion)) / 3
+            if is_train:
+                total = total + self.lambda_mask * mask_loss_val
+
+        if self.attn_reg_enabled and is_train:
+            total = total + compute_attn_energy_loss(aux, dev) * self.lambda_attn_energy \
+                + compute_feature_consistency_loss(aux, dev) * self.lambda_feature_consistency
+        if self.feat_norm_reg_enabled and is_train:
+            total = total + compute_feat_norm_loss(aux, dev) * self.lambda_feat_norm
+
+        recon_loss_val = torch.zeros((), device=dev)
+        mimic_loss_val = torch.zeros((), device=dev)
+        if aux_w > 0.0 and self.recon_enabled and is_train:
+            recon_loss_val = fused_recon_losses(dwi_aux["recon_feats"], dce_aux["recon_feats"], aux["recon_fused"],
+                                                dwi_inputs.detach(), dce_inputs.detach())
+            total = total + self.lambda_recon * recon_loss_val * aux_w
+            pf = aux.get("proj_fused", None)
+            if self.mimic_enabled and pf is not None and len(pf) >= 4:
+                mimic_loss_val = O.mimic_pairs(pf, npairs=2)
+                total = total + self.lambda_mimic * mimic_loss_val * aux_w
+
+        preds = torch.argmax(logits, dim=1)
+        acc = (preds == labels).float().mean()
+        self.last_metrics = {"loss": total.detach(), "acc": acc.detach(), "cls": cls_loss.detach(),
+                             "mask": mask_loss_val.detach(), "recon": recon_loss_val.detach(),
+                             "mimic": mimic_loss_val.detach()}
+        if return_preds:
+            return total.detach(), logits.detach(), aux, fused_mask_logits
+        return total
+
+    def training_step(self, batch, batch_idx=0):
+        return self._shared_step(batch, "train")
+
+    def validation_step(self, batch, batch_idx=0):
+        loss, _, _, _ = self._shared_step(batch, phase="val", return_preds=True)
+        return loss
+
+    # ------------------------------------------------------------- predict
+    def forward_from_inputs(self, dwi_inputs, dce_inputs, masks=None):
+        _, dwi_aux, dwi_mask = self.dwi_model(dwi_inputs)
+        _, dce_aux, dce_mask = self.dce_model(dce_inputs)
+        return self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask, dce_mask)
+
+    @torch.no_grad()
+    def predict_custom(self, batch, mode="normal", mc_passes=10):
+        dwi = batch[0].to(self.device)
+        dce = batch[1].to(self.device)
+        if mode == "normal":
+            return self.forward_from_inputs(dwi, dce)
+        raise NotImplementedError(f"predict mode {mode!r} (TTA / MC-dropout) is a 'next' row (SURVEY 8(f) rank 2)")
+
+
+# ------------------------------------------------------------------ helpers
+def compute_recon_list_loss(recon_list, input_img):
+    """train_fusion.py:709-744 (2-D): mean over the valid maps of
+    recon_image_loss(bilinear(r -> input size), channel-mean(input))."""
+    if recon_list is None:
+        return torch.zeros((), device=input_img.device)
+    if isinstance(recon_list, torch.Tensor):
+        recon_list = [recon_list]
+    maps = [r for r in recon_list if r is not None]
+    if not maps:
+        return torch.zeros((), device=input_img.device)
+    for r in maps:
+        if r.shape[1] != 1:
+            raise NotImplementedError("multi-channel reconstructions are not on the reference path")
+    tgt = O.channel_mean_map(input_img)
+    terms = O.recon_terms(maps, [0] * len(maps), tgt)
+    return terms.sum() / len(maps)
+
+
+def fused_recon_losses(dwi_recons, dce_recons, fused_recon, dwi_img, dce_img):
+    """The three compute_recon_list_loss calls of train_fusion.py:281-285
+    (dwi [r1,r2], dce [r1,r2], fused vs cat(dwi, dce)) / 3, in ONE launch."""
+    dw = [r for r in dwi_recons if r is not None]
+    dc = [r for r in dce_recons if r is not None]
+    if fused_recon is None or len(dw) != 2 or len(dc) != 2:
+        return (compute_recon_list_loss(dwi_recons, dwi_img) + compute_recon_list_loss(dce_recons, dce_img)
+                + compute_recon_list_loss(fused_recon, torch.cat([dwi_img, dce_img], 1))) / 3
+    ta = O.channel_mean_map(dwi_img)
+    tb = O.channel_mean_map(dce_img)
+    ca, cb = dwi_img.shape[1], dce_img.shape[1]
+    t = O.recon_terms([dw[0], dw[1], dc[0], dc[1], fused_recon], [0, 0, 1, 1, 2], ta, tb, ca / (ca + cb),
+                      cb / (ca + cb))
+    return ((t[0] + t[1]) / 2 + (t[2] + t[3]) / 2 + t[4]) / 3
+
+
+def safe_mask_loss(pred_logits, gt_mask, mask_criterion):
+    """train_fusion.py:747-760 (quirk Q6: the resized mask is computed but the
+    original one is passed to the criterion)."""
+    if pred_logits is None:
+        raise ValueError("pred_logits is None in safe_mask_loss")
+    if gt_mask is None:
+        raise ValueError("gt_mask is None in safe_mask_loss")
+    return mask_criterion(pred_logits, gt_mask)

@@ -1,0 +1,134 @@
+"""Hybrid CNN -> Transformer stage -- MI355X build of the reference's
+``code/transformer_model.py`` (used when ``use_hybrid_transformer`` replaces
+block3, model_module.py:564-579, :701-703; configuration 5).
+
+Module and parameter names match the reference (PatchEmbed :7-32,
+TokensToFeatureMap :34-52, TransformerEncoder :54-66, TransformerBlock
+:68-81, MultiHeadSelfAttention :83-116, MLP :118-134, TransformerStage
+:137-175). Patch embedding runs on the conv engine; LayerNorm, the linear
+layers and attention on the fp32 token kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+import dmf_ops as O
+
+
+def _caches(conv):
+    c = getattr(conv, "_dmf_caches", None)
+    if c is None:
+        c = (O.WeightCache(), O.WeightCache())
+        conv._dmf_caches = c
+    return c
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, in_ch, embed_dim, patch_size=2, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        self.dim = dim
+        self.norm = nn.LayerNorm(embed_dim)
+        self.proj = nn.Conv2d(in_ch, embed_dim, kernel_size=patch_size, stride=patch_size)
+
+    def forward(self, x):
+        dt = getattr(self, "compute_dtype", torch.bfloat16)
+        x = O.as_nhwc(x.to(dt))
+        y = O.conv2d(x, self.proj, _caches(self.proj))           # [B, E, h, w] NHWC
+        b, e, h, w = y.shape
+        tokens = y.permute(0, 2, 3, 1).reshape(b, h * w, e).float()  # NHWC storage == token order
+        return O.layer_norm(tokens, self.norm), (h, w)
+
+
+class TokensToFeatureMap(nn.Module):
+    def __init__(self, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        self.dim = dim
+
+    def forward(self, tokens, spatial_shape):
+        b, n, c = tokens.shape
+        h, w = spatial_shape
+        return tokens.reshape(b, h, w, c).permute(0, 3, 1, 2)   # NCHW logical, NHWC storage
+
+
+class MultiHeadSelfAttention(nn.Module):
+    def __init__(self, embed_dim, num_heads, qkv_bias=True, attn_drop=0.1, proj_drop=0.1):
+        super().__init__()
+        assert embed_dim % num_heads == 0, "embed_dim must be divisible by num_heads"
+        self.embed_dim = embed_dim
+        self.num_heads = num_heads
+        self.head_dim = embed_dim // num_heads
+        self.scale = self.head_dim ** -0.5
+        self.qkv = nn.Linear(embed_dim, embed_dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(embed_dim, embed_dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+
+    def forward(self, x):
+        if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
+            raise NotImplementedError("attention/projection dropout in train mode is not built yet (config 5)")
+        b, n, c = x.shape
+        qkv = O.linear(x.reshape(b * n, c), self.qkv.weight, self.qkv.bias).view(b, n, 3 * c)
+        o = O.self_attention(qkv, self.num_heads, c)
+        return O.linear(o.reshape(b * n, c), self.proj.weight, self.proj.bias).view(b, n, c)
+
+
+class MLP(nn.Module):
+    def __init__(self, embed_dim, mlp_ratio=4.0, drop=0.1):
+        super().__init__()
+        hidden_dim = int(embed_dim * mlp_ratio)
+        self.fc1 = nn.Linear(embed_dim, hidden_dim)
+        self.act = nn.GELU()
+        self.fc2 = nn.Linear(hidden_dim, embed_dim)
+        self.drop = nn.Dropout(drop)
+
+    def forward(self, x):
+        if self.training and self.drop.p > 0:
+            raise NotImplementedError("MLP dropout in train mode is not built yet (config 5)")
+        b, n, c = x.shape
+        h = O.linear(x.reshape(b * n, c), self.fc1.weight, self.fc1.bias, act="gelu")
+        return O.linear(h, self.fc2.weight, self.fc2.bias).view(b, n, c)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, embed_dim, heads, init_scale=0.1):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(embed_dim)
+        self.attn = MultiHeadSelfAttention(embed_dim, heads)
+        self.norm2 = nn.LayerNorm(embed_dim)
+        self.mlp = MLP(embed_dim)
+        self.gamma1 = nn.Parameter(init_scale * torch.ones(embed_dim))
+        self.gamma2 = nn.Parameter(init_scale * torch.ones(embed_dim))
+
+    def forward(self, x):
+        x = O.layerscale_residual(x, self.attn(O.layer_norm(x, self.norm1)), self.gamma1)
+        return O.layerscale_residual(x, self.mlp(O.layer_norm(x, self.norm2)), self.gamma2)
+
+
+class TransformerEncoder(nn.Module):
+    def __init__(self, embed_dim, depth=4, heads=8):
+        super().__init__()
+        self.layers = nn.ModuleList([TransformerBlock(embed_dim, heads=heads) for _ in range(depth)])
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x
+
+
+class TransformerStage(nn.Module):
+    def __init__(self, in_ch, embed_dim, depth=2, heads=8, patch_size=2, dim=2):
+        super().__init__()
+        assert dim in (2, 3)
+        self.dim = dim
+        self.patch_embed = PatchEmbed(in_ch=in_ch, embed_dim=embed_dim, patch_size=patch_size, dim=dim)
+        self.transformer = TransformerEncoder(embed_dim=embed_dim, depth=depth, heads=heads)
+        self.tokens_to_map = TokensToFeatureMap(dim=dim)
+
+    def forward(self, x):
+        tokens, hw = self.patch_embed(x)
+        tokens = self.transformer(tokens)
+        dt = getattr(self, "compute_dtype", torch.bfloat16)
+        return self.tokens_to_map(tokens, hw).to(dt)

@@ -53,17 +53,19 @@ int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* str
  * FeatureDownAlign (:386-390), FusionModel.proj_in_* / reduce (:857-862,
  * :788-792), PatchEmbed.proj (transformer_model.py:17-22). */
 int dmf_conv_m_tile(void);
-int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
-                   int KH, int KW, int stride, int pad, int dil, const float* bias, void* y, int Ho, int Wo,
-                   int ldy, float* bn_partials, int act, void* stream);
+/* x2 (nullable): second input concatenated along channels after the Cin
+ * channels of x (BackboneAdapter chain [C4, C5], model_module.py:471) */
+int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
+                   int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil, const float* bias,
+                   void* y, int Ho, int Wo, int ldy, float* bn_partials, int act, void* stream);
 int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
                          void* stream);
 int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M);
-int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int Ho,
-                     int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad, int dil, int splits,
-                     float* workspace, void* stream);
+int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
+                     int ldx2, const void* dy, int Ho, int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad,
+                     int dil, int splits, float* workspace, void* stream);
 int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int Cout, int Cin, int CinP, int KH, int KW,
                             float* dw, int accumulate, void* stream);
 /* single-output-channel convs: ReconHead.conv[3] (model_module.py:117),
@@ -103,7 +105,7 @@ int dmf_act_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, con
 int dmf_bn_bwd_tiles(long long M);
 int dmf_bn_bwd_reduce(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* save_mean_invstd,
                       long long M, int C, float* partials, void* stream);
-int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, const float* gamma,
+int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, int training, const float* gamma,
                         const float* save_mean_invstd, float* dgamma, float* dbeta, float* coef, void* stream);
 int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* coef, void* dx,
                      int lddx, long long M, int C, void* stream);
@@ -132,15 +134,30 @@ int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx,
                   int k, int s, int p, void* stream);
 int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* dy, int Ho, int Wo,
                       int lddy, void* dx, int lddx, int k, int s, int p, void* stream);
-int dmf_upsample2x_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, void* stream);
-int dmf_upsample2x_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C, void* stream);
+int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, int r,
+                         void* stream);
+int dmf_upsample_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C, int r, void* stream);
 int dmf_bilinear(int dtype, const void* x, int N, int Hi, int Wi, int C, int ldx, void* y, int Ho, int Wo, int ldy,
                  void* stream);
 int dmf_bilinear_bwd(int dtype, const void* dy, int N, int Ho, int Wo, int C, int lddy, void* dx, int Hi, int Wi,
                      int lddx, void* stream);
+int dmf_channel_affine(int dtype, const void* x, int ldx, const float* gate, const float* add, float add_scale,
+                       void* y, int ldy, int N, int HW, int C, void* stream);
+int dmf_broadcast_hw(int dtype, const float* vec, float scale, void* y, int ldy, int N, int HW, int C,
+                     int accumulate, void* stream);
+int dmf_gate_grad_nchw(int dtype, const void* dy, int lddy, const float* x, int N, int C, int HW, float* out,
+                       void* stream);
 int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* m, int N, int HW, int C, const float* w1,
                       const float* gn_w, const float* gn_b, const float* w2, const float* b2, const float* gamma,
                       int hidden, float eps, float* stats, void* out, int ldo, void* A_out, void* stream);
+/* workspace: N*HW*hidden + 2*N floats; grads (accumulated):
+ * [hidden] dw1, [hidden] dgn_w, [hidden] dgn_b, [hidden] dw2, [1] db2, [1] dgamma */
+int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int ldf, const void* m, int N, int HW,
+                      int C, const float* w1, const float* gn_w, const float* gn_b, const float* w2, const float* b2,
+                      const float* gamma, int hidden, float eps, const float* stats, void* df, int lddf, void* dm,
+                      float* workspace, float* grads, void* stream);
+int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, const void* b, int ldb,
+                const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C, void* stream);
 
 /* ------------------------------------------- cross-modal fusion op (fp32)
  * FusionModel.forward (model_module.py:919-1000): GatingAttention
@@ -151,6 +168,11 @@ int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const fl
               int ldb, float beta, float* C, int ldc, const float* bias, int act, void* stream);
 int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream);
 int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
+int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream);
+int dmf_sig_grad_f32(const float* dg, const float* s, float* dz, long long n, void* stream);
+int dmf_row_l2norm(const float* x, int R, int C, float eps, float* y, float* norms, void* stream);
+int dmf_row_l2norm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float eps, float* dx,
+                       void* stream);
 int dmf_layernorm_fwd(const float* x, int R, int E, const float* gamma, const float* beta, float eps, float* y,
                       float* save, void* stream);
 int dmf_layernorm_bwd(const float* dy, const float* x, const float* save, int R, int E, const float* gamma,
@@ -182,16 +204,20 @@ int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const float* conf_dwi
  * (LabelSmoothing); train_fusion.py:709-744 (compute_recon_list_loss);
  * train.py:1033-1048 (mimic_feat_loss, recon_image_loss, charbonnier).
  * Forward writes the loss and the unit-upstream gradient in one pass. */
-int dmf_focal_loss(const float* logits, const long long* labels, int B, int K, float smoothing, int use_smoothing,
-                   const float* class_weights, float gamma, float* loss, float* dlogits, void* stream);
+/* targets: soft_targets [B][K] (nullable) else labels; reduction 0 mean, 1 sum, 2 none */
+int dmf_focal_loss(const float* logits, const long long* labels, const float* soft_targets, int B, int K,
+                   float smoothing, int use_smoothing, const float* class_weights, float gamma, int reduction,
+                   float* loss, float* per_row, float* dlogits, void* stream);
+int dmf_label_smooth(const long long* labels, int B, int K, float smoothing, float* out, void* stream);
 int dmf_soft_dice(int dtype, const void* logits, const float* target, int B, int P, float eps, float* sums_ws,
                   float* loss, float* dlogits, void* stream);
 int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const void* r2, const void* r3,
                    const void* r4, int ldr0, int ldr1, int ldr2, int ldr3, int ldr4, int sel0, int sel1, int sel2,
                    int sel3, int sel4, const float* tA, const float* tB, float ca, float cb, int B, int h, int w,
                    int S, float* sums, float* g0, float* g1, float* g2, float* g3, float* g4, void* stream);
-int dmf_mimic_loss(int dtype, const void* feats, int ld, int HW, int C, int npairs, float* loss, float* dstudent,
-                   void* stream);
+/* loss must be zeroed by the caller (pairs/channels accumulate) */
+int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long long sstride, long long tstride, int ld,
+                   int HW, int C, int npairs, float* loss, void* dstudent, long long dstride, void* stream);
 int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream);
 int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul, void* dst,
                       int ldd, void* stream);

@@ -18,7 +18,10 @@ import torch.nn.functional as F
 
 
 def _bn(x, bn: nn.BatchNorm2d):
-    # torch BatchNorm2d semantics (train: batch stats + running-stat update)
+    # torch BatchNorm2d semantics (train: batch stats + running-stat update,
+    # num_batches_tracked += 1 as nn.BatchNorm2d.forward does)
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
     return F.batch_norm(
         x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
         bn.training, bn.momentum, bn.eps,

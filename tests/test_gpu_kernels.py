@@ -1,0 +1,317 @@
+"""Kernel-level numerics: each HIP op against a plain PyTorch fp32 reference of
+the same op (computed on the CPU), in the f32 parity mode (tight tolerance)
+and the bf16 throughput mode (bf16 tolerance)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import dmf_ops as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _to_dev(x, dtype):
+    return x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+
+
+def _tol(dtype):
+    return (2e-4, 2e-4) if dtype == torch.float32 else (3e-2, 3e-2)
+
+
+CONV_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, dil)
+    (2, 64, 16, 16, 64, 1, 1, 0, 1),
+    (2, 64, 16, 16, 128, 3, 1, 1, 1),
+    (2, 128, 17, 13, 64, 3, 2, 1, 1),
+    (1, 64, 20, 20, 256, 3, 1, 2, 2),
+    (1, 256, 12, 12, 128, 3, 1, 4, 4),
+    (2, 16, 32, 32, 64, 7, 2, 3, 1),
+    (2, 256, 8, 8, 512, 1, 2, 0, 1),
+    (3, 8, 9, 9, 8, 3, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case, dtype):
+    n, ci, h, w, co, k, s, p, d = case
+    torch.manual_seed(0)
+    conv = nn.Conv2d(ci, co, k, stride=s, padding=p, dilation=d, bias=True)
+    x = torch.randn(n, ci, h, w)
+    xr = x.clone().requires_grad_(True)
+    yr = F.conv2d(xr, conv.weight, conv.bias, s, p, d)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    cd = copy.deepcopy(conv).to(DEV)
+    cd.zero_grad(set_to_none=True)
+    xd = _to_dev(x, dtype).requires_grad_(True)
+    caches = (O.WeightCache(), O.WeightCache())
+    y = O.conv2d(xd, cd, caches)
+    rtol, atol = _tol(dtype)
+    scale = yr.abs().max().item()
+    assert torch.allclose(y.float().cpu(), yr.detach(), rtol=rtol, atol=atol * scale), \
+        (y.float().cpu() - yr.detach()).abs().max()
+    y.backward(_to_dev(gy, dtype))
+    gscale = xr.grad.abs().max().item()
+    assert torch.allclose(xd.grad.float().cpu(), xr.grad, rtol=rtol, atol=atol * gscale), \
+        (xd.grad.float().cpu() - xr.grad).abs().max()
+    wscale = conv.weight.grad.abs().max().item() if conv.weight.grad is not None else 1
+    ref_w = torch.nn.grad.conv2d_weight(x, conv.weight.shape, gy, s, p, d)
+    assert torch.allclose(cd.weight.grad.cpu(), ref_w, rtol=rtol, atol=atol * ref_w.abs().max().item()), \
+        (cd.weight.grad.cpu() - ref_w).abs().max()
+    assert torch.allclose(cd.bias.grad.cpu(), gy.sum((0, 2, 3)), rtol=rtol, atol=atol * gy.abs().sum((0, 2, 3)).max())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_dual_source(dtype):
+    torch.manual_seed(1)
+    a = torch.randn(2, 64, 8, 8)
+    b = torch.randn(2, 128, 8, 8)
+    conv = nn.Conv2d(192, 64, 3, padding=1)
+    bn = nn.BatchNorm2d(64)
+    ref = F.gelu(bn(F.conv2d(torch.cat([a, b], 1), conv.weight, conv.bias, 1, 1)))
+    cd, bd = conv.to(DEV), nn.BatchNorm2d(64).to(DEV)
+    y = O.conv_bn_act(_to_dev(a, dtype), cd, (O.WeightCache(), O.WeightCache()), bd, "gelu", x2=_to_dev(b, dtype))
+    rtol, atol = _tol(dtype)
+    assert torch.allclose(y.float().cpu(), ref.detach(), rtol=rtol, atol=atol * 4)
+    assert torch.allclose(bd.running_mean.cpu(), bn.running_mean, rtol=1e-3, atol=1e-4 if dtype == torch.float32 else 1e-2)
+    assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=1e-3, atol=1e-3 if dtype == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+def test_conv_bn_act_residual_grads(act):
+    torch.manual_seed(2)
+    x = torch.randn(2, 32, 10, 10)
+    xs = torch.randn(2, 16, 20, 20)
+    conv = nn.Conv2d(32, 64, 1)
+    bn = nn.BatchNorm2d(64)
+    cs = nn.Conv2d(16, 64, 1, stride=2, bias=False)
+    bns = nn.BatchNorm2d(64)
+    for m in (bn, bns):
+        m.weight.data.uniform_(0.5, 1.5)
+        m.bias.data.uniform_(-0.5, 0.5)
+    xr, xsr = x.clone().requires_grad_(True), xs.clone().requires_grad_(True)
+    f = F.relu if act == "relu" else F.gelu
+    ref = f(bn(F.conv2d(xr, conv.weight, conv.bias)) + bns(F.conv2d(xsr, cs.weight, None, 2)))
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    mods = [copy.deepcopy(m).to(DEV) for m in (conv, bn, cs, bns)]
+    for m in mods:
+        m.zero_grad(set_to_none=True)
+    xd = _to_dev(x, torch.float32).requires_grad_(True)
+    xsd = _to_dev(xs, torch.float32).requires_grad_(True)
+    y = O.conv_bn_act(xd, mods[0], (O.WeightCache(), O.WeightCache()), mods[1], act,
+                      skip=(xsd, mods[2], (O.WeightCache(), O.WeightCache()), mods[3]))
+    y.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(y.cpu(), ref.detach(), atol=2e-4, rtol=2e-4)
+    assert torch.allclose(xd.grad.cpu(), xr.grad, atol=2e-4, rtol=2e-3)
+    assert torch.allclose(xsd.grad.cpu(), xsr.grad, atol=2e-4, rtol=2e-3)
+    assert torch.allclose(mods[1].weight.grad.cpu(), bn.weight.grad, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(mods[3].bias.grad.cpu(), bns.bias.grad, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(mods[0].weight.grad.cpu(), conv.weight.grad, atol=1e-3, rtol=1e-3)
+
+
+def test_dropout_statistics_and_backward():
+    torch.manual_seed(3)
+    x = torch.randn(4, 64, 16, 16, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    rng = O.RNG.snapshot(DEV)
+    site = O.RNG.new_site()
+    y = O.act_nhwc(x, "none", dropout_p=0.2, rng=rng, site=site)
+    kept = (y != 0).float().mean().item()
+    assert abs(kept - 0.8) < 0.01
+    nz = y != 0
+    assert torch.allclose(y[nz], x.detach()[nz] / 0.8, rtol=1e-6)
+    y.sum().backward()
+    assert torch.equal(x.grad != 0, nz)
+    # same snapshot + site -> same mask
+    y2 = O.act_nhwc(x.detach(), "none", dropout_p=0.2, rng=rng, site=site)
+    assert torch.equal(y2 != 0, nz)
+
+
+def test_gn_mix_and_grads():
+    torch.manual_seed(4)
+    a = torch.randn(2, 32, 8, 8)
+    b = torch.randn(2, 32, 8, 8)
+    w = torch.tensor(0.3)
+    gn = nn.GroupNorm(32, 32)
+    gn.weight.data.uniform_(0.5, 1.5)
+    gn.bias.data.uniform_(-1, 1)
+    ar, br, wr = a.clone().requires_grad_(True), b.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    al = torch.sigmoid(wr)
+    ref = gn(al * ar + (1 - al) * br)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    gnd = copy.deepcopy(gn).to(DEV)
+    gnd.zero_grad(set_to_none=True)
+    ad = _to_dev(a, torch.float32).requires_grad_(True)
+    bd = _to_dev(b, torch.float32).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = O.gn_mix(ad, bd, wd, gnd)
+    y.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(y.cpu(), ref.detach(), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(ad.grad.cpu(), ar.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(bd.grad.cpu(), br.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(wd.grad.cpu(), wr.grad, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(gnd.weight.grad.cpu(), gn.weight.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(gnd.bias.grad.cpu(), gn.bias.grad, atol=1e-4, rtol=1e-3)
+
+
+def test_maxpool_and_bilinear_and_tokens():
+    torch.manual_seed(5)
+    x = torch.randn(2, 16, 17, 15)
+    xr = x.clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    xd = _to_dev(x, torch.float32).requires_grad_(True)
+    y = O.maxpool2d(xd, 3, 2, 1)
+    y.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(y.cpu(), ref.detach())
+    assert torch.allclose(xd.grad.cpu(), xr.grad, atol=1e-6)
+    # bilinear 4 -> 32 and 32 -> 64
+    for (h, H) in [(4, 32), (32, 64), (7, 20)]:
+        z = torch.randn(2, 8, h, h)
+        zr = z.clone().requires_grad_(True)
+        r = F.interpolate(zr, size=(H, H), mode="bilinear", align_corners=False)
+        gg = torch.randn_like(r)
+        r.backward(gg)
+        zd = _to_dev(z, torch.float32).requires_grad_(True)
+        o = O.bilinear(zd, H, H)
+        o.backward(_to_dev(gg, torch.float32))
+        assert torch.allclose(o.cpu(), r.detach(), atol=1e-5)
+        assert torch.allclose(zd.grad.cpu(), zr.grad, atol=1e-4, rtol=1e-4)
+    # tokens (adaptive avg pool 32 -> 4)
+    t = torch.randn(2, 16, 32, 32)
+    tr = t.clone().requires_grad_(True)
+    ref_t = F.adaptive_avg_pool2d(tr, (4, 4)).flatten(2).transpose(1, 2)
+    gt = torch.randn_like(ref_t)
+    ref_t.backward(gt)
+    td = _to_dev(t, torch.float32).requires_grad_(True)
+    tok = O.to_tokens(td, 4, 4)
+    tok.backward(gt.to(DEV))
+    assert torch.allclose(tok.cpu(), ref_t.detach(), atol=1e-5)
+    assert torch.allclose(td.grad.cpu(), tr.grad, atol=1e-6)
+
+
+def test_se_block_grads():
+    torch.manual_seed(6)
+    import model_module as MM
+
+    se = MM.SEBlock(32, 2)
+    MM.set_compute_dtype(se, torch.float32)
+    x = torch.randn(2, 32, 8, 8)
+    xr = x.clone().requires_grad_(True)
+    fc = se.fc
+    w = torch.sigmoid(F.conv2d(F.gelu(F.conv2d(xr.mean((2, 3), keepdim=True), fc[1].weight, fc[1].bias)),
+                               fc[3].weight, fc[3].bias))
+    ref = xr * w
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    ref_g1 = torch.autograd.grad(
+        (xr.detach() * torch.sigmoid(F.conv2d(F.gelu(F.conv2d(xr.detach().mean((2, 3), keepdim=True), fc[1].weight,
+                                                              fc[1].bias)), fc[3].weight, fc[3].bias)) * g).sum(),
+        fc[1].weight)[0]
+    sed = copy.deepcopy(se).to(DEV)
+    sed.zero_grad(set_to_none=True)
+    xd = _to_dev(x, torch.float32).requires_grad_(True)
+    y, wgt = sed(xd)
+    y.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(y.cpu(), ref.detach(), atol=1e-5)
+    assert torch.allclose(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(sed.fc[1].weight.grad.cpu(), ref_g1, atol=1e-5, rtol=1e-3)
+
+
+def test_mask_attention_fwd_bwd():
+    torch.manual_seed(7)
+    import model_module as MM
+    from oracle.model import MaskGuidedSpatialAttention as RefMSA
+
+    ref = RefMSA(32, 1)
+    ref.mask_processor[1].weight.data.uniform_(0.5, 1.5)
+    ref.mask_processor[1].bias.data.uniform_(-0.5, 0.5)
+    mine = MM.MaskGuidedSpatialAttention(32, 1)
+    mine.load_state_dict(ref.state_dict())
+    MM.set_compute_dtype(mine, torch.float32)
+    mine = mine.to(DEV)
+    f = torch.randn(2, 32, 8, 8)
+    m = torch.randn(2, 1, 8, 8)
+    fr, mr = f.clone().requires_grad_(True), m.clone().requires_grad_(True)
+    out_r, a_r = ref(fr, mr)
+    g = torch.randn_like(out_r)
+    out_r.backward(g)
+    fd = _to_dev(f, torch.float32).requires_grad_(True)
+    md = _to_dev(m, torch.float32).requires_grad_(True)
+    out, a = mine(fd, md)
+    out.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(out.cpu(), out_r.detach(), atol=1e-5)
+    assert torch.allclose(a.cpu(), a_r.detach(), atol=1e-5)
+    assert torch.allclose(fd.grad.cpu(), fr.grad, atol=1e-5)
+    assert torch.allclose(md.grad.cpu(), mr.grad, atol=1e-4, rtol=1e-3)
+    for (n1, p1), (n2, p2) in zip(ref.named_parameters(), mine.named_parameters()):
+        assert torch.allclose(p2.grad.cpu().reshape(p1.grad.shape), p1.grad, atol=1e-4, rtol=1e-3), n1
+
+
+def test_losses_match_oracle():
+    torch.manual_seed(8)
+    from oracle import losses as L
+    import loss as LM
+
+    logits = torch.randn(8, 4)
+    labels = torch.randint(0, 4, (8,))
+    cw = torch.tensor([0.5, 1.0, 1.5, 2.0])
+    lr_ = logits.clone().requires_grad_(True)
+    t = L.label_smoothing(lr_, labels, 4, 0.1)
+    ref = L.soft_weighted_focal(lr_, t, 1.5, cw)
+    ref.backward()
+    ld = logits.to(DEV).requires_grad_(True)
+    crit = LM.SoftWeightedFocalLoss(1.5, cw.to(DEV))
+    sm = LM.LabelSmoothing(4, 0.1)(ld, labels.to(DEV))
+    out = crit(ld, sm)
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-5
+    assert torch.allclose(ld.grad.cpu(), lr_.grad, atol=1e-6)
+    # dice
+    x = torch.randn(4, 1, 32, 32)
+    m = (torch.rand(4, 1, 32, 32) > 0.5).float()
+    xr = x.clone().requires_grad_(True)
+    rd = L.soft_dice(xr, m)
+    rd.backward()
+    xd = _to_dev(x, torch.float32).requires_grad_(True)
+    od = LM.SoftDiceLoss()(xd, m.to(DEV))
+    od.backward()
+    assert abs(od.item() - rd.item()) < 1e-5
+    assert torch.allclose(xd.grad.cpu(), xr.grad, atol=1e-7)
+
+
+def test_recon_and_mimic_match_oracle():
+    torch.manual_seed(9)
+    from oracle import losses as L
+    import train_fusion as TF
+    import dmf_ops
+
+    img = torch.rand(2, 6, 64, 64)
+    r1 = torch.randn(2, 1, 8, 8)
+    r2 = torch.randn(2, 1, 8, 8)
+    a, b = r1.clone().requires_grad_(True), r2.clone().requires_grad_(True)
+    ref = L.recon_list_loss([a, b], img)
+    ref.backward()
+    ad = _to_dev(r1, torch.float32).requires_grad_(True)
+    bd = _to_dev(r2, torch.float32).requires_grad_(True)
+    out = TF.compute_recon_list_loss([ad, bd], img.to(DEV))
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-5
+    assert torch.allclose(ad.grad.cpu(), a.grad, atol=1e-6, rtol=1e-4)
+    # mimic over batch-item pairs (Q5)
+    pf = torch.randn(4, 16, 8, 8)
+    pr = pf.clone().requires_grad_(True)
+    refm = (L.mimic_feat_loss(pr[0], pr[1]) + L.mimic_feat_loss(pr[2], pr[3])) / 2
+    refm.backward()
+    pd = _to_dev(pf, torch.float32).requires_grad_(True)
+    om = dmf_ops.mimic_pairs(pd, 2)
+    om.backward()
+    assert abs(om.item() - refm.item()) < 1e-5
+    assert torch.allclose(pd.grad.cpu(), pr.grad, atol=1e-6)

@@ -1,0 +1,161 @@
+"""Module / step parity: the HIP path (f32 parity mode) against the CPU
+oracle restatement (oracle/), sharing one state_dict and one seeded batch.
+
+Tolerance (north star): logits within 1e-3 absolute in the f32 mode; loss
+terms within 1e-4 relative; the bf16 throughput mode is checked against a
+looser 5e-2 bound on logits (expected ~1e-2)."""
+import copy
+
+import pytest
+import torch
+
+import foundation_model as FM
+import model_module as MM
+import parameters as PR
+import train_fusion as TF
+from oracle import losses as OL
+from oracle import model as OM
+from selector_helpers import get_classification_loss
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _randomize_bn(model, seed):
+    g = torch.Generator().manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.GroupNorm, torch.nn.LayerNorm)):
+            m.weight.data = 1 + 0.2 * torch.randn(m.weight.shape, generator=g)
+            m.bias.data = 0.1 * torch.randn(m.bias.shape, generator=g)
+
+
+def build_pair(P, method, in_ch, seed, dtype=torch.float32):
+    torch.manual_seed(seed)
+    P = copy.deepcopy(P)
+    bb = FM.build_medical_backbone(P, "cpu", method, in_ch)
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone(method, P, bb), True)
+    _randomize_bn(enc, seed)
+    bb_o = OM.ResNet50OS8(in_ch)
+    ref = OM.ModelMaskHeadBackbone(method, P, bb_o)
+    ref.load_state_dict(enc.state_dict())
+    MM.set_compute_dtype(enc, dtype)
+    return enc.to(DEV), ref, P
+
+
+def batch(B, S, seed, cd=14, cc=6):
+    g = torch.Generator().manual_seed(seed)
+    dwi = (0.5 + torch.randn(B, cd, S, S, generator=g) / 6).clamp(0, 1)
+    dce = torch.rand(B, cc, S, S, generator=g)
+    yy, xx = torch.meshgrid(torch.arange(32), torch.arange(32), indexing="ij")
+    masks = torch.zeros(B, 1, 32, 32)
+    for b in range(B):
+        cy, cx = torch.randint(8, 24, (2,), generator=g).tolist()
+        r = torch.randint(4, 11, (1,), generator=g).item()
+        masks[b, 0] = (((yy - cy) ** 2 + (xx - cx) ** 2) <= r * r).float()
+    labels = torch.randint(0, 4, (B,), generator=g)
+    return dwi, dce, masks, labels
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_encoder_forward_parity(train):
+    P = PR.small_parameters(dropout=0.0)
+    enc, ref, _ = build_pair(P, "dwi", 14, 11)
+    enc.train(train)
+    ref.train(train)
+    dwi, _, _, _ = batch(2, 64, 5)
+    with torch.no_grad():
+        lo, aux, mp = enc(dwi.to(DEV))
+        lr_, auxr, mpr = ref(dwi)
+    assert (lo.float().cpu() - lr_).abs().max() < 1e-3
+    assert (mp.float().cpu() - mpr).abs().max() < 1e-3
+    for a, b in zip(aux["raw_feats"], auxr["raw_feats"]):
+        assert (a.float().cpu() - b).abs().max() < 2e-3 * max(1.0, b.abs().max().item())
+    for a, b in zip(aux["proj_pairs"], auxr["proj_pairs"]):
+        assert a.shape == b.shape
+        assert (a.float().cpu() - b).abs().max() < 2e-3 * max(1.0, b.abs().max().item())
+    if train:
+        for (n, b1), (_, b2) in zip(enc.named_buffers(), ref.named_buffers()):
+            if b1.dtype.is_floating_point:
+                assert (b1.cpu() - b2).abs().max() < 1e-3 * max(1.0, b2.abs().max().item()), n
+            else:
+                assert torch.equal(b1.cpu(), b2), n
+
+
+def _fusion_pair(P, seed):
+    torch.manual_seed(seed)
+    fm = MM.FusionModel(P)
+    _randomize_bn(fm, seed)
+    fr = OM.FusionModel(P)
+    fr.load_state_dict(fm.state_dict())
+    MM.set_compute_dtype(fm, torch.float32)
+    return fm.to(DEV), fr
+
+
+def test_fusion_step_parity_mode_a():
+    """Reference default at epoch 0: encoders frozen (train mode), backward
+    through FusionModel only; compare every loss term and every fusion grad."""
+    P = PR.small_parameters(dropout=0.0)
+    dwi_m, dwi_r, P1 = build_pair(P, "dwi", 14, 21)
+    dce_m, dce_r, _ = build_pair(P, "dce", 6, 22)
+    P = P1
+    fm, fr = _fusion_pair(P, 23)
+    train_labels = torch.arange(64) % 4
+    crit = get_classification_loss(P, train_labels, "fusion", DEV)
+    lm = TF.LightningFusionModel(dwi_m, dce_m, fm, P, crit)
+    lm.train()
+    for m in (dwi_r, dce_r, fr):
+        m.train()
+    for p in list(dwi_r.parameters()) + list(dce_r.parameters()):
+        p.requires_grad = False
+    bt = batch(4, 64, 7)
+    loss = lm.training_step(tuple(t.to(DEV) for t in bt))
+    loss.backward()
+    cw = OL.class_weights_from_labels(train_labels)
+    ref = OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, cw, epoch=0)
+    ref["total"].backward()
+    assert abs(loss.item() - ref["total"].item()) < 1e-4 * max(1, abs(ref["total"].item()))
+    for k in ("cls", "mask", "recon", "mimic"):
+        assert abs(lm.last_metrics[k].item() - ref[k].item()) < 1e-4 * max(1, abs(ref[k].item())), k
+    for (n, p1), (_, p2) in zip(fm.named_parameters(), fr.named_parameters()):
+        if p2.grad is None:
+            assert p1.grad is None or p1.grad.abs().max().item() == 0, n
+            continue
+        assert p1.grad is not None, n
+        tol = 2e-3 * max(1e-3, p2.grad.abs().max().item())
+        assert (p1.grad.cpu().reshape(p2.grad.shape) - p2.grad).abs().max() < tol, n
+
+
+def test_adamw_step_matches_torch():
+    import dmf_optim
+
+    torch.manual_seed(3)
+    ps = [torch.randn(37, 5), torch.randn(129), torch.randn(4, 3, 3, 3)]
+    gs = [torch.randn_like(p) for p in ps]
+    ref = [torch.nn.Parameter(p.clone()) for p in ps]
+    mine = [torch.nn.Parameter(p.clone().to(DEV)) for p in ps]
+    o_ref = torch.optim.AdamW([{"params": ref[:2], "lr": 1e-3, "weight_decay": 1e-4},
+                               {"params": ref[2:], "lr": 5e-4, "weight_decay": 0.0}], eps=1e-8)
+    o_mine = dmf_optim.FusedAdamW([{"params": mine[:2], "lr": 1e-3, "weight_decay": 1e-4},
+                                   {"params": mine[2:], "lr": 5e-4, "weight_decay": 0.0}], eps=1e-8)
+    for it in range(3):
+        for p, g in zip(ref, gs):
+            p.grad = g * (it + 1)
+        for p, g in zip(mine, gs):
+            p.grad = (g * (it + 1)).to(DEV)
+        o_ref.step()
+        o_mine.step()
+    for a, b in zip(mine, ref):
+        assert torch.allclose(a.detach().cpu(), b.detach(), atol=1e-6, rtol=1e-5)
+
+
+def test_bf16_logits_close():
+    P = PR.small_parameters(dropout=0.0)
+    enc, ref, _ = build_pair(P, "dce", 6, 31, dtype=torch.bfloat16)
+    enc.eval()
+    ref.eval()
+    _, dce, _, _ = batch(2, 64, 9)
+    with torch.no_grad():
+        lo, _, _ = enc(dce.to(DEV))
+        lr_, _, _ = ref(dce)
+    err = (lo.float().cpu() - lr_).abs().max().item()
+    assert err < 5e-2, err
