@@ -106,8 +106,15 @@ def roofline_probe(trainer, batch, dtype):
         return None
     flops = sum(r[2] for r in recs)
     byt = sum(r[3] for r in recs)
-    ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+    times = [r[0].elapsed_time(r[1]) for r in recs]
+    ms = sum(times)
     n = len(recs)
+    dump = os.environ.get("DMF_CONV_DUMP")
+    if dump:
+        with open(dump, "w") as f:
+            for r, t in zip(recs, times):
+                f.write(json.dumps({"shape": r[4], "ms": round(t, 4), "gflop": round(r[2] / 1e9, 3),
+                                    "tflops": round(r[2] / (t * 1e-3) / 1e12, 1)}) + "\n")
     peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
     achieved = flops / (ms * 1e-3) / 1e12
     return {

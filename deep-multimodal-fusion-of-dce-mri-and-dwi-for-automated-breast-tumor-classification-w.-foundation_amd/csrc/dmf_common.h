@@ -57,6 +57,32 @@ template <> struct Cvt<bf16_t> {
 template <typename T> __device__ __forceinline__ float ld(const T* p) { return Cvt<T>::load(*p); }
 template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = Cvt<T>::store(v); }
 
+// 8-element vector access (16 B for bf16, 32 B for f32); p must be aligned
+__device__ __forceinline__ void ld8(const bf16_t* p, float v[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float v[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float v[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void st8(float* p, const float v[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // exact (erf) GELU, as torch nn.GELU() default
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));

@@ -44,7 +44,30 @@ __device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int
 // ---------------------------------------------------------- bn finalize
 // partials [T][C][2] -> mean/invstd, per-channel affine (scale, shift), and
 // running-stat update. Block: 64 channels x 4 tile lanes.
-__global__ void k_bn_finalize(const float* __restrict__ part, int T, int C, double count, double unbias_count,
+// stage 1 (large T): block (channel group, tile chunk) -> double partials [S][C][2]
+__global__ void k_bn_stage1(const float* __restrict__ part, int T, int C, int chunk, double* __restrict__ out) {
+  __shared__ double red[4][64][2];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int t0 = blockIdx.y * chunk, t1 = min(T, t0 + chunk);
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int t = t0 + tl; t < t1; t += 4) {
+      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
+  red[tl][cl][0] = s;
+  red[tl][cl][1] = q;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    out[((size_t)blockIdx.y * C + c) * 2] = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    out[((size_t)blockIdx.y * C + c) * 2 + 1] = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+  }
+}
+
+template <typename PT>
+__global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, double count, double unbias_count,
                               const float* __restrict__ gamma, const float* __restrict__ beta,
                               float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
                               int training, float* __restrict__ ss, float* __restrict__ save) {
@@ -54,9 +77,8 @@ __global__ void k_bn_finalize(const float* __restrict__ part, int T, int C, doub
   double s = 0.0, q = 0.0;
   if (training && c < C) {
     for (int t = tl; t < T; t += 4) {
-      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
-      s += v.x;
-      q += v.y;
+      s += (double)part[((size_t)t * C + c) * 2];
+      q += (double)part[((size_t)t * C + c) * 2 + 1];
     }
   }
   red[tl][cl][0] = s;
@@ -129,6 +151,55 @@ __global__ void k_affine_act(const T* __restrict__ x, int ldx, const float* __re
     }
 #pragma unroll
     for (int k = 0; k < V; ++k) st(y + m * ldy + c0 + k, v[k]);
+  }
+}
+
+// 8-channel vectorised variant (C, strides multiple of 8; 16-B bf16 accesses)
+template <typename T, int ACT>
+__global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __restrict__ ssa,
+                              const T* __restrict__ res, int ldr, const float* __restrict__ ssr, float p,
+                              const unsigned long long* rng, int site, T* __restrict__ y, int ldy, long long M,
+                              int C) {
+  const int cv = C >> 3;
+  const long long total = M * cv;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / cv;
+    const int c0 = (int)(i - m * cv) << 3;
+    float v[8], r[8];
+    ld8(x + m * ldx + c0, v);
+    if (ssa) {
+      const float4 s0 = *(const float4*)(ssa + c0), s1 = *(const float4*)(ssa + c0 + 4);
+      const float4 b0 = *(const float4*)(ssa + C + c0), b1 = *(const float4*)(ssa + C + c0 + 4);
+      v[0] = v[0] * s0.x + b0.x; v[1] = v[1] * s0.y + b0.y; v[2] = v[2] * s0.z + b0.z; v[3] = v[3] * s0.w + b0.w;
+      v[4] = v[4] * s1.x + b1.x; v[5] = v[5] * s1.y + b1.y; v[6] = v[6] * s1.z + b1.z; v[7] = v[7] * s1.w + b1.w;
+    }
+    if (res) {
+      ld8(res + m * ldr + c0, r);
+      if (ssr) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = r[k] * ssr[c0 + k] + ssr[C + c0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
+      else if (ACT == DMF_ACT_GELU) v[k] = gelu_f(v[k]);
+      else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+    }
+    if (p > 0.f) {
+      bool keep[4];
+      dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * sc : 0.f;
+      dropout_keep4(rng, site, (unsigned long long)(m * C + c0 + 4), p, keep);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * sc : 0.f;
+    }
+    st8(y + m * ldy + c0, v);
   }
 }
 
@@ -258,17 +329,30 @@ static inline int grid_for(long long n, int block = 256) {
 
 using namespace dmf;
 
+extern "C" int dmf_bn_finalize_ws_size(int ntiles, int C) {
+  return ntiles <= 64 ? 0 : ((ntiles + 31) / 32) * C * 2;
+}
+
 extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, double unbias_count,
-                               const float* gamma,
-                               const float* beta, float* running_mean, float* running_var,
+                               const float* gamma, const float* beta, float* running_mean, float* running_var,
                                long long* num_batches_tracked, float momentum, float eps, int training,
-                               float* scale_shift, float* save_mean_invstd, void* stream) {
+                               float* scale_shift, float* save_mean_invstd, double* workspace, void* stream) {
   DMF_CHECK_ARG(C > 0 && scale_shift, "dmf_bn_finalize: bad args");
   DMF_CHECK_ARG(!training || (partials && ntiles > 0 && count > 0), "dmf_bn_finalize: training needs partials");
   DMF_CHECK_ARG(training || (running_mean && running_var), "dmf_bn_finalize: eval needs running stats");
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C, count,
-                     unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, training, scale_shift,
-                     save_mean_invstd);
+  hipStream_t st_ = (hipStream_t)stream;
+  if (training && ntiles > 64) {
+    DMF_CHECK_ARG(workspace, "dmf_bn_finalize: %d tiles need a workspace (dmf_bn_finalize_ws_size)", ntiles);
+    const int S = (ntiles + 31) / 32;
+    hipLaunchKernelGGL(k_bn_stage1, dim3(cdiv(C, 64), S), dim3(256), 0, st_, partials, ntiles, C, 32, workspace);
+    hipLaunchKernelGGL(k_bn_finalize<double>, dim3(cdiv(C, 64)), dim3(256), 0, st_, (const double*)workspace, S, C,
+                       count, unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+                       training, scale_shift, save_mean_invstd);
+  } else {
+    hipLaunchKernelGGL(k_bn_finalize<float>, dim3(cdiv(C, 64)), dim3(256), 0, st_, partials, ntiles, C, count,
+                       unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+                       training, scale_shift, save_mean_invstd);
+  }
   DMF_LAUNCH_CHECK("dmf_bn_finalize");
   return 0;
 }
@@ -281,6 +365,34 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_affine_act: dropout needs rng state");
   DMF_CHECK_ARG(dropout_p < 1.f, "dmf_affine_act: dropout p must be < 1");
   if (M == 0) return 0;
+  const bool vec8 = C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!res || ldr % 8 == 0) &&
+                    ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0) &&
+                    (!scale_shift || ((uintptr_t)scale_shift % 16) == 0);
+  if (vec8) {
+    const int g8 = grid_for(M * (C / 8));
+    hipStream_t s = (hipStream_t)stream;
+#define DMF_AA8(TT, A)                                                                                          \
+  hipLaunchKernelGGL((k_affine_act8<TT, A>), dim3(g8), dim3(256), 0, s, (const TT*)x, ldx, scale_shift,          \
+                     (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, (TT*)y, ldy, M, C)
+    if (dtype == DMF_BF16) {
+      switch (act) {
+        case DMF_ACT_RELU: DMF_AA8(bf16_t, DMF_ACT_RELU); break;
+        case DMF_ACT_GELU: DMF_AA8(bf16_t, DMF_ACT_GELU); break;
+        case DMF_ACT_SIGMOID: DMF_AA8(bf16_t, DMF_ACT_SIGMOID); break;
+        default: DMF_AA8(bf16_t, DMF_ACT_NONE);
+      }
+    } else {
+      switch (act) {
+        case DMF_ACT_RELU: DMF_AA8(float, DMF_ACT_RELU); break;
+        case DMF_ACT_GELU: DMF_AA8(float, DMF_ACT_GELU); break;
+        case DMF_ACT_SIGMOID: DMF_AA8(float, DMF_ACT_SIGMOID); break;
+        default: DMF_AA8(float, DMF_ACT_NONE);
+      }
+    }
+#undef DMF_AA8
+    DMF_LAUNCH_CHECK("dmf_affine_act");
+    return 0;
+  }
   const int g = grid_for(M * (C / 4));
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_affine_act<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx,

@@ -177,10 +177,21 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
         if want_stats:
             tiles = (n * ho * wo + 127) // 128
             partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
+        probe = PROBE["conv_fwd"]
+        if probe is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         N.call("dmf_conv2d_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
                g.stride, g.pad,
                g.dil, _p(bias), y.data_ptr(), ho, wo, ldy, _p(partials), act_c if not want_stats else N.ACT_NONE,
                _stream())
+        if probe is not None:
+            e1.record()
+            es = x.element_size()
+            k_tot = kh * kw * (cx + cx2)
+            flops = 2.0 * n * ho * wo * co * k_tot
+            byts = es * (n * h * w * (cx + cx2) + co * k_tot + n * ho * wo * co)
+            probe.append((e0, e1, flops, byts, (n, h, w, cx + cx2, co, kh, g.stride, g.dil)))
     return y, partials
 
 
@@ -318,11 +329,14 @@ def _bn_finalize(partials, count, bn, unbias_count=0.0):
     training = bn.training or bn.running_mean is None
     track = bn.training and bn.track_running_stats and bn.running_mean is not None
     mom = bn.momentum if bn.momentum is not None else 0.1
-    N.call("dmf_bn_finalize", _p(partials), 0 if partials is None else partials.shape[0], c, float(count),
+    ntiles = 0 if partials is None else partials.shape[0]
+    wsn = N.load().dmf_bn_finalize_ws_size(ntiles, c) if training else 0
+    ws = torch.empty(wsn, dtype=torch.float64, device=dev) if wsn > 0 else None
+    N.call("dmf_bn_finalize", _p(partials), ntiles, c, float(count),
            float(unbias_count), _p(bn.weight), _p(bn.bias), _p(bn.running_mean) if (track or not training) else None,
            _p(bn.running_var) if (track or not training) else None,
            _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), 1 if training else 0,
-           ss.data_ptr(), save.data_ptr(), _stream())
+           ss.data_ptr(), save.data_ptr(), _p(ws), _stream())
     return ss, save
 
 
@@ -1379,3 +1393,9 @@ def mimic_pairs(feats, npairs=2):
     n, c, h, w, ld = nhwc(f)
     stride = 2 * h * w * ld
     return _MimicFn.apply(f, f.detach()[1:], npairs, stride, stride, h * w, c, ld)
+
+
+# bench.py's roofline probe: when PROBE["conv_fwd"] is a list, every MFMA conv
+# forward launch appends (start_event, end_event, flops, bytes, shape) -- events
+# are recorded on the stream the kernel is launched on.
+PROBE = {"conv_fwd": None}

@@ -92,10 +92,12 @@ int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void* dy, int l
 /* ---------------------------------------------------- batch norm & acts
  * nn.BatchNorm2d train/eval semantics + fused residual/activation/dropout
  * (timm Bottleneck, ResNetLite :259-307, necks, heads, projectors). */
+/* workspace: dmf_bn_finalize_ws_size(ntiles, C) doubles (two-stage reduction when ntiles > 64) */
+int dmf_bn_finalize_ws_size(int ntiles, int C);
 int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, double unbias_count,
                     const float* gamma, const float* beta, float* running_mean, float* running_var,
                     long long* num_batches_tracked, float momentum, float eps, int training, float* scale_shift,
-                    float* save_mean_invstd, void* stream);
+                    float* save_mean_invstd, double* workspace, void* stream);
 int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
                    const float* res_scale_shift, int act, float dropout_p, const unsigned long long* rng, int site,
                    void* y, int ldy, long long M, int C, void* stream);
