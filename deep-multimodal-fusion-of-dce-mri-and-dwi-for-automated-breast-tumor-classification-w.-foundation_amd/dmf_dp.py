@@ -36,7 +36,9 @@ def rank_strided_indices(n_items, rank, world, epoch=0, shuffle=False, seed=0):
         idx = torch.randperm(n_items, generator=g).tolist()
     per = (n_items + world - 1) // world
     total = per * world
-    idx = idx + idx[: total - n_items]
+    pad = total - n_items
+    if pad > 0 and idx:
+        idx = idx + (idx * (pad // len(idx) + 1))[:pad]
     return idx[rank:total:world]
 
 

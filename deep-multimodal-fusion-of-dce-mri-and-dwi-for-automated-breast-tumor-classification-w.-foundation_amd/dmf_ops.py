@@ -27,7 +27,11 @@ def _stream():
 
 
 def _p(t):
-    return None if t is None else t.data_ptr()
+    if t is None:
+        return None
+    if not t.is_cuda:
+        N.require_cuda(t)
+    return t.data_ptr()
 
 
 # ------------------------------------------------------------------ layout
@@ -35,6 +39,8 @@ def nhwc(t):
     """(N, C, H, W, ld) of an NCHW-logical, NHWC-physical tensor (or slice)."""
     if t.dim() != 4:
         raise RuntimeError(f"expected a 4-D activation, got shape {tuple(t.shape)}")
+    if not t.is_cuda:
+        N.require_cuda(t)
     n, c, h, w = t.shape
     s0, s1, s2, s3 = t.stride()
     ld = s3 if w > 1 else (s2 // max(w, 1) if h > 1 else (s0 // max(h * w, 1) if n > 1 else c))
@@ -46,6 +52,7 @@ def nhwc(t):
 
 def as_nhwc(t):
     """Make t NHWC-addressable (a copy only if it is not already)."""
+    N.require_cuda(t)
     try:
         nhwc(t)
         return t

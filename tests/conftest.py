@@ -8,7 +8,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "deep-multimodal-fusion-of-dce-mri-and-dwi-for-automated-breast-tumor-classification-w.-foundation_amd")
-for p in (ROOT, PKG):
+TOOLS = os.path.join(ROOT, "tools")  # make_golden's seeded recipes
+for p in (ROOT, PKG, TOOLS):
     if p not in sys.path:
         sys.path.insert(0, p)
 

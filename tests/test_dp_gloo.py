@@ -1,0 +1,120 @@
+"""CPU, world_size 2 over gloo: the data-parallel protocol of dmf_dp.
+
+The GPU path (FusionTrainer) does exactly this per step: each rank takes its
+rank-strided volumes, computes local-BN gradients, packs them into one flat
+fp32 bucket, sums the bucket with ONE all_reduce, and AdamW reads it scaled by
+1/world. Here the per-rank compute is the CPU oracle's fusion step (the HIP
+kernels need a device); what is under test is the sharding, the single
+bucket exchange and the 1/world scaling, against a single-process reference
+of the same DDP semantics (mean of per-rank gradients), plus the epoch-end
+all-gather + AUROC."""
+import copy
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import parameters as PR
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _models(seed=0):
+    from oracle import model as OM
+    import foundation_model as FM
+    import model_module as MM
+
+    P = copy.deepcopy(PR.small_parameters(channels=(8, 16, 32), input_size=64))
+    torch.manual_seed(seed)
+    FM.build_medical_backbone(P, "cpu", "dwi", 14)  # sets backbone_index_lists
+    dwi = OM.ModelMaskHeadBackbone("dwi", P, OM.ResNet50OS8(14))
+    dce = OM.ModelMaskHeadBackbone("dce", P, OM.ResNet50OS8(6))
+    fm = OM.FusionModel(P)
+    for m in (dwi, dce):
+        for p in m.parameters():
+            p.requires_grad = False
+    return P, dwi, dce, fm
+
+
+def _batch(n):
+    import make_golden as MG
+
+    return MG.volume_batch(n, 64, 3)
+
+
+def _local_grads(P, dwi, dce, fm, batch):
+    from oracle import losses as OL
+
+    fm.zero_grad(set_to_none=True)
+    for m in (dwi, dce, fm):
+        m.train()
+    out = OL.fusion_shared_step(dwi, dce, fm, batch, P, OL.class_weights_from_labels(torch.arange(8) % 4))
+    out["total"].backward()
+    return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                      for p in fm.parameters()]), out["logits"].detach()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        from dmf_dp import allgather_rows, allreduce_mean_, rank_strided_indices
+        import metrics as MT
+
+        P, dwi, dce, fm = _models()
+        full = _batch(4)
+        idx = rank_strided_indices(4, rank, world)
+        local = tuple(t[idx] for t in full)
+        bucket, logits = _local_grads(P, dwi, dce, fm, local)
+        allreduce_mean_(bucket, world)
+        bucket /= world  # the consumer's grad_scale
+        probs = torch.softmax(logits, 1)
+        allp = allgather_rows(probs, world)
+        alll = allgather_rows(local[3], world)
+        auc = MT.multiclass_auroc(allp, alll)
+        if rank == 0:
+            q.put((bucket, allp, alll, auc))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_bucket_allreduce_matches_ddp_mean():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    bucket, allp, alll, auc = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    # single-process reference of the same semantics: mean of per-shard grads
+    from dmf_dp import rank_strided_indices
+    import metrics as MT
+
+    P, dwi, dce, fm = _models()
+    full = _batch(4)
+    grads, labels = [], []
+    for r in range(world):
+        idx = rank_strided_indices(4, r, world)
+        g, _ = _local_grads(P, dwi, dce, fm, tuple(t[idx] for t in full))
+        grads.append(g)
+        labels.append(full[3][idx])
+    want = sum(grads) / world
+    torch.testing.assert_close(bucket, want, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(alll, torch.cat(labels))
+    assert auc == pytest.approx(MT.multiclass_auroc(allp, alll))

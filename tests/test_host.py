@@ -1,0 +1,218 @@
+"""CPU: host-side logic of the boundary -- configuration schema, module
+structure / state-dict names (drop-in checkpoints), optimizer grouping and
+gradual unfreeze, class weights, first-conv adaptation, checkpoint key
+mapping, epoch metrics, rank sampling. No kernel is launched."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import foundation_model as FM
+import metrics as MT
+import model_module as MM
+import parameters as PR
+import selector_helpers as SH
+import train_fusion as TF
+from dmf_dp import rank_strided_indices
+from dmf_optim import FusedAdamW
+from oracle import model as OM
+
+
+def _enc(P, method, cin, seed=0):
+    torch.manual_seed(seed)
+    bb = FM.build_medical_backbone(P, "cpu", method, cin)
+    return MM.initialize_model(MM.ModelMaskHeadBackbone(method, P, bb), True)
+
+
+@pytest.fixture(scope="module")
+def small():
+    P = copy.deepcopy(PR.small_parameters())
+    dwi = _enc(P, "dwi", 14, 1)
+    dce = _enc(P, "dce", 6, 2)
+    fm = MM.FusionModel(P)
+    return P, dwi, dce, fm
+
+
+def test_parameters_alias_like_reference():
+    P = PR.default_parameters()
+    assert P["dce_model_parameters"] is P["dwi_model_parameters"]
+    assert P["fusion_model_parameters"] is P["dwi_model_parameters"]
+    mp = P["dwi_model_parameters"]
+    assert mp["channels"] == (128, 256, 512) and mp["proj_dim"] == 64 and mp["input_size"] == 256
+    assert mp["fusion_specific_parameters"]["fusion_channels"] == 128
+    assert P["dwi_channel_num"] == 14 and P["dce_channel_num"] == 6 and P["class_num"] == 4
+    assert P["aux_loss_weight_epoch_limit"] == 200
+
+
+def test_build_medical_backbone_side_effects():
+    P = copy.deepcopy(PR.default_parameters())
+    bb = FM.build_medical_backbone(P, "cpu", "dwi", 14)
+    mp = P["dwi_model_parameters"]
+    assert mp["backbone_index_lists"] == [[0], [1], [2, 3]]
+    assert mp["backbone_out_channels"] == ()  # "not implemented" in the reference (model_module.py:516)
+    m = bb._orig_mod if hasattr(bb, "_orig_mod") else bb
+    assert m.conv1.weight.shape == (64, 14, 7, 7)
+    # output stride 8 (timm): layer3/4 dilated instead of strided; each stage's first
+    # block keeps the previous stage's dilation
+    assert m.layer3[0].conv2.dilation == (1, 1) and m.layer3[0].conv2.stride == (1, 1)
+    assert m.layer3[1].conv2.dilation == (2, 2)
+    assert m.layer4[0].conv2.dilation == (2, 2) and m.layer4[0].conv2.stride == (1, 1)
+    assert m.layer4[2].conv2.dilation == (4, 4)
+    assert m.layer2[0].conv2.stride == (2, 2)
+
+
+def test_state_dict_names_match_oracle(small):
+    P, dwi, dce, fm = small
+    ref = OM.ModelMaskHeadBackbone("dwi", P, OM.ResNet50OS8(14))
+    a, b = dwi.state_dict(), ref.state_dict()
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+    fr = OM.FusionModel(P)
+    assert list(fm.state_dict().keys()) == list(fr.state_dict().keys())
+    ref.load_state_dict(a)  # strict
+
+
+def test_default_model_sizes():
+    P = copy.deepcopy(PR.default_parameters())
+    enc = _enc(P, "dwi", 14)
+    n = sum(p.numel() for p in enc.parameters())
+    assert 30e6 < n < 40e6, n
+    fm = MM.FusionModel(P)
+    nf = sum(p.numel() for p in fm.parameters())
+    assert 0.5e6 < nf < 2e6, nf
+
+
+def test_wfl_class_weights():
+    P = PR.default_parameters()
+    labels = torch.tensor([0] * 10 + [1] * 3 + [2] * 6 + [3])
+    crit = SH.get_classification_loss(P, labels, "fusion", "cpu")
+    w = crit.class_weights.cpu().numpy().reshape(-1)
+    np.testing.assert_allclose(w, 20 / (4 * (np.array([10, 3, 6, 1]) + 1e-6)), rtol=1e-6)
+    P2 = copy.deepcopy(P)
+    P2["fusion_model_parameters"]["classification_loss_parameters"]["classification_loss_code"] = "bad"
+    with pytest.raises(ValueError):
+        SH.get_classification_loss(P2, labels, "fusion", "cpu")
+
+
+def _lfm(small, freeze):
+    P, dwi, dce, fm = small
+    P = copy.deepcopy(P)
+    P["backbone_freeze_on_start"] = freeze
+    dwi, dce, fm = copy.deepcopy(dwi), copy.deepcopy(dce), copy.deepcopy(fm)
+    for p in list(dwi.parameters()) + list(dce.parameters()):
+        p.requires_grad = True
+    crit = SH.get_classification_loss(P, torch.arange(8) % 4, "fusion", "cpu")
+    return TF.LightningFusionModel(dwi, dce, fm, P, crit)
+
+
+def test_optimizer_groups_mode_a(small):
+    lm = _lfm(small, True)
+    cfg = lm.configure_optimizers()
+    opt = cfg["optimizer"] if isinstance(cfg, dict) else cfg
+    assert isinstance(opt, FusedAdamW)
+    assert len(opt.param_groups) == 1
+    g = opt.param_groups[0]
+    assert g["lr"] == pytest.approx(1e-4) and g["weight_decay"] == pytest.approx(1e-4)
+    assert {id(p) for p in g["params"]} == {id(p) for p in lm.fusion_model.parameters()}
+    assert not any(p.requires_grad for p in lm.dwi_model.parameters())
+    assert "scheduler" in cfg["lr_scheduler"]
+
+
+def test_optimizer_groups_mode_b(small):
+    lm = _lfm(small, False)
+    cfg = lm.configure_optimizers()
+    opt = cfg["optimizer"] if isinstance(cfg, dict) else cfg
+    assert len(opt.param_groups) == 4
+    for i, g in enumerate(opt.param_groups):
+        assert g["lr"] == pytest.approx(1e-4 / 1.2 ** (3 - i))
+        assert g["weight_decay"] == pytest.approx(1e-4 * 0.8 ** (3 - i))
+    n_all = sum(1 for m in (lm.dwi_model, lm.dce_model) for n, _ in m.named_parameters()
+                if "classification_head" not in n) + sum(1 for _ in lm.fusion_model.parameters())
+    assert sum(len(g["params"]) for g in opt.param_groups) == n_all
+    # group 0 = both backbones
+    names = {id(p): n for m in (lm.dwi_model, lm.dce_model) for n, p in m.named_parameters()}
+    assert all("backbone" in names[id(p)] for p in opt.param_groups[0]["params"])
+
+
+def test_gradual_unfreeze_schedule(small):
+    lm = _lfm(small, True)
+    opt = lm.configure_optimizers()["optimizer"]
+    f = lm.opt_factory
+    assert f.gradual_unfreeze(0, 40) == [] and f.gradual_unfreeze(39, 40) == []
+    new = f.gradual_unfreeze(40, 40)
+    assert new and f.layers_unfrozen == 1
+    deep = {id(p) for _, p in f.dwi_named_groups[2] + f.dce_named_groups[2]}
+    assert all(id(p) in deep for p in new)
+    f.sync_unfrozen_params_to_optimizer(opt, new)
+    assert len(opt.param_groups) == 2
+    assert opt.param_groups[1]["lr"] == pytest.approx(1e-5)  # backbone_unfreeze_lr * 0.25**0
+    assert opt.param_groups[1]["weight_decay"] == pytest.approx(1e-4)
+    new2 = f.gradual_unfreeze(80, 40)
+    f.sync_unfrozen_params_to_optimizer(opt, new2)
+    assert opt.param_groups[2]["lr"] == pytest.approx(1e-5 * 0.25)
+    f.gradual_unfreeze(120, 40)
+    assert f.layers_unfrozen == 3
+    assert f.gradual_unfreeze(160, 40) == []
+    # every grouped parameter is trainable again; encoder classification heads are
+    # never grouped (selector_helpers.py:396-430) and stay frozen, as in the reference
+    for n, p in lm.dwi_model.named_parameters():
+        assert p.requires_grad == ("classification_head" not in n), n
+
+
+def test_adapt_first_conv():
+    w = torch.randn(64, 3, 7, 7)
+    sd = FM.adapt_first_conv({"conv1.weight": w.clone()}, 14)
+    assert sd["conv1.weight"].shape == (64, 14, 7, 7)
+    torch.testing.assert_close(sd["conv1.weight"][:, 5], w.mean(1))
+    sd = FM.advanced_adapt_first_conv({"conv1.weight": w.clone()}, 6, eps=0.05)
+    lum = 0.2989 * w[:, 0] + 0.5870 * w[:, 1] + 0.1140 * w[:, 2]
+    torch.testing.assert_close(sd["conv1.weight"][:, 0], lum * 0.95)
+    torch.testing.assert_close(sd["conv1.weight"][:, 5], lum * 1.05)
+
+
+def test_map_rasool_keys():
+    sd = {"backbone.0.weight": 1, "backbone.1.running_mean": 2, "backbone.4.0.conv1.weight": 3,
+          "backbone.7.2.bn3.bias": 4, "fc.weight": 5, "5.1.downsample.0.weight": 6}
+    out = FM.map_rasool_to_timm_keys(sd)
+    assert out == {"conv1.weight": 1, "bn1.running_mean": 2, "layer1.0.conv1.weight": 3,
+                   "layer4.2.bn3.bias": 4, "layer2.1.downsample.0.weight": 6}
+
+
+def test_local_checkpoint_loads_weights_only(tmp_path):
+    P = copy.deepcopy(PR.default_parameters())
+    torch.manual_seed(0)
+    src = FM.ResNet50OS8(3)
+    sd = {"state_dict": {k: v for k, v in src.state_dict().items()}}
+    path = tmp_path / "radimagenet.pt"
+    torch.save(sd, path)
+    P["dwi_model_parameters"]["pretrained_path"] = str(path)
+    bb = FM.build_medical_backbone(P, "cpu", "dwi", 14)
+    m = bb._orig_mod if hasattr(bb, "_orig_mod") else bb
+    torch.testing.assert_close(m.conv1.weight[:, 3], src.conv1.weight.mean(1))
+    torch.testing.assert_close(m.layer4[2].conv3.weight, src.layer4[2].conv3.weight)
+
+
+def test_multiclass_auroc_matches_rank_formula():
+    sk = pytest.importorskip("sklearn.metrics")
+    g = torch.Generator().manual_seed(0)
+    probs = torch.softmax(torch.randn(200, 4, generator=g), 1)
+    probs[::7] = probs[3]  # ties
+    labels = torch.randint(0, 4, (200,), generator=g)
+    want = sk.roc_auc_score(labels.numpy(), probs.numpy(), multi_class="ovr", average="macro")
+    assert MT.multiclass_auroc(probs, labels) == pytest.approx(want, abs=1e-12)
+    cm = MT.confusion_matrix(probs.argmax(1), labels, 4)
+    np.testing.assert_array_equal(cm.numpy(), sk.confusion_matrix(labels.numpy(), probs.argmax(1).numpy(),
+                                                                   labels=[0, 1, 2, 3]))
+
+
+@pytest.mark.parametrize("n,world", [(10, 1), (10, 2), (11, 4), (3, 8), (64, 8)])
+def test_rank_strided_indices(n, world):
+    parts = [rank_strided_indices(n, r, world) for r in range(world)]
+    assert len({len(p) for p in parts}) == 1
+    flat = sorted(i for p in parts for i in p)
+    assert set(flat) == set(range(n))
+    assert len(flat) == -(-n // world) * world
+    sh = [rank_strided_indices(n, r, world, epoch=3, shuffle=True, seed=1) for r in range(world)]
+    assert set(i for p in sh for i in p) == set(range(n))

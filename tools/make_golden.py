@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/*.npz from the CPU oracle restatement.
+
+The reference itself could not be imported here (refused by
+the environment), so these vectors are produced by ``oracle/`` -- they pin
+the oracle (and, through the GPU tests, the HIP path) against silent drift;
+they do NOT pin the reference ("parity unpinned").
+
+Weights are not stored: each fixture records the seed recipe the tests
+re-run (product-side seeded construction, state_dict loaded into the oracle).
+
+    python tools/make_golden.py
+"""
+import copy
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "deep-multimodal-fusion-of-dce-mri-and-dwi-for-automated-breast-tumor-classification-w.-foundation_amd")
+sys.path[:0] = [ROOT, PKG]
+
+import foundation_model as FM  # noqa: E402
+import model_module as MM  # noqa: E402
+import parameters as PR  # noqa: E402
+from oracle import losses as OL  # noqa: E402
+from oracle import model as OM  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def seeded_encoder(P, method, cin, seed):
+    """Product-side seeded construction (same recipe the tests use)."""
+    torch.manual_seed(seed)
+    bb = FM.build_medical_backbone(P, "cpu", method, cin)  # sets P's backbone_index_lists (reference side effect)
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone(method, P, bb), True)
+    ref = OM.ModelMaskHeadBackbone(method, P, OM.ResNet50OS8(cin))
+    ref.load_state_dict(enc.state_dict())
+    return enc, ref
+
+
+def seeded_fusion(P, seed):
+    torch.manual_seed(seed)
+    fm = MM.FusionModel(P)
+    fr = OM.FusionModel(P)
+    fr.load_state_dict(fm.state_dict())
+    return fm, fr
+
+
+def volume_batch(B, S, seed, cd=14, cc=6):
+    g = torch.Generator().manual_seed(seed)
+    dwi = (0.5 + torch.randn(B, cd, S, S, generator=g) / 6).clamp(0, 1)
+    dce = torch.rand(B, cc, S, S, generator=g)
+    yy, xx = torch.meshgrid(torch.arange(32), torch.arange(32), indexing="ij")
+    masks = torch.zeros(B, 1, 32, 32)
+    for b in range(B):
+        cy, cx = torch.randint(8, 24, (2,), generator=g).tolist()
+        r = torch.randint(4, 11, (1,), generator=g).item()
+        masks[b, 0] = (((yy - cy) ** 2 + (xx - cx) ** 2) <= r * r).float()
+    labels = torch.randint(0, 4, (B,), generator=g)
+    return dwi, dce, masks, labels
+
+
+def losses_fixture():
+    g = torch.Generator().manual_seed(100)
+    B, K = 16, 4
+    logits = torch.randn(B, K, generator=g) * 2
+    labels = torch.randint(0, K, (B,), generator=g)
+    train_labels = torch.cat([torch.zeros(10), torch.ones(3), torch.full((6,), 2), torch.full((1,), 3)]).long()
+    cw = OL.class_weights_from_labels(train_labels)
+    tgt = OL.label_smoothing(logits, labels, K, 0.1)
+    mlog = torch.randn(4, 1, 32, 32, generator=g) * 3
+    mtgt = (torch.rand(4, 1, 32, 32, generator=g) > 0.7).float()
+    rec = torch.randn(2, 6, 16, 16, generator=g)
+    img = torch.rand(2, 6, 64, 64, generator=g)
+    s = torch.randn(4, 64, 8, 8, generator=g)
+    t = torch.randn(4, 64, 8, 8, generator=g)
+    return dict(
+        logits=logits.numpy(), labels=labels.numpy(), train_labels=train_labels.numpy(),
+        class_weights=cw.numpy(), smooth_targets=tgt.numpy(),
+        focal_w=OL.soft_weighted_focal(logits, tgt, 2.0, cw).numpy(),
+        focal_w_hard=OL.soft_weighted_focal(logits, labels, 2.0, cw).numpy(),
+        focal_rows=OL.soft_weighted_focal(logits, tgt, 2.0, cw, reduction="none").numpy(),
+        mask_logits=mlog.numpy(), mask_target=mtgt.numpy(),
+        dice=OL.soft_dice(mlog, mtgt).numpy(), dice_bce=OL.dice_bce(mlog, mtgt).numpy(),
+        recon=rec.numpy(), image=img.numpy(),
+        recon_same=OL.recon_list_loss([rec], img).numpy(),
+        recon_mean=OL.recon_list_loss([rec[:, :1]], img).numpy(),
+        mimic_s=s.numpy(), mimic_t=t.numpy(), mimic=OL.mimic_feat_loss(s, t).numpy(),
+    )
+
+
+def encoder_fixture():
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0))
+    _, ref = seeded_encoder(P, "dwi", 14, 11)
+    ref.eval()
+    dwi, _, _, _ = volume_batch(2, 64, 5)
+    with torch.no_grad():
+        lo, aux, mp = ref(dwi)
+    return dict(recipe=np.array("small_parameters(dropout=0); dwi encoder seed 11; eval"), dwi=dwi.numpy(),
+                logits=lo.numpy(), mask_logits=mp.numpy(),
+                raw_feat_sums=np.array([f.double().sum().item() for f in aux["raw_feats"]]))
+
+
+def step_fixture():
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0))
+    _, dwi_r = seeded_encoder(P, "dwi", 14, 21)
+    _, dce_r = seeded_encoder(P, "dce", 6, 22)
+    _, fr = seeded_fusion(P, 23)
+    for m in (dwi_r, dce_r, fr):
+        m.train()
+    for p in list(dwi_r.parameters()) + list(dce_r.parameters()):
+        p.requires_grad = False
+    bt = volume_batch(4, 64, 7)
+    train_labels = torch.arange(64) % 4
+    out = OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, OL.class_weights_from_labels(train_labels), epoch=0)
+    out["total"].backward()
+    gn = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0 for p in fr.parameters()])
+    return dict(recipe=np.array("small_parameters(dropout=0); dwi seed 21, dce seed 22, fusion seed 23; train; "
+                                "mode A; batch volume_batch(4,64,7); train_labels arange(64)%4"),
+                dwi=bt[0].numpy(), dce=bt[1].numpy(), masks=bt[2].numpy(), labels=bt[3].numpy(),
+                logits=out["logits"].detach().numpy(),
+                terms=np.array([out[k].item() for k in ("cls", "mask", "recon", "mimic", "total")]),
+                fusion_grad_norms=gn)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    np.savez_compressed(os.path.join(OUT, "losses.npz"), **losses_fixture())
+    np.savez_compressed(os.path.join(OUT, "encoder_small.npz"), **encoder_fixture())
+    np.savez_compressed(os.path.join(OUT, "fusion_step_small.npz"), **step_fixture())
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()
