@@ -234,6 +234,7 @@ def main():
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "size": args.size,
                    "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
         "loss": loss_val,
+        "peak_hbm_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
