@@ -212,6 +212,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
+    if loss_val is not None and loss_val != loss_val:
+        raise RuntimeError("training loss is NaN: the benchmarked step is numerically broken")
     if not args.no_roofline and rank == 0:
         roof = roofline_probe(trainer, batch, dtype)
 

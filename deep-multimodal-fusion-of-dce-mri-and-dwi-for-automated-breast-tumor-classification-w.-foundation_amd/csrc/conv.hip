@@ -45,7 +45,18 @@ struct ConvArgs {
   int Ktot;             // KH*KW*C
   int M;                // N*Ho*Wo
   int act;
+  int act_in;
   int mtiles, ntiles;
+  // A-operand prologue (FWD, single source): x <- act(x*in_ss[c] + in_ss[C+c])
+  // on every in-bounds element (padding stays zero), i.e. the producer's
+  // batch-norm apply + activation fused into this conv's loads.
+  const float* in_ss;
+  // fused batch-norm finalize: with `tickets` ([ntiles], zero at rest) the
+  // last-arriving block of each output-channel tile reduces that tile's
+  // columns of the partial-statistics slab (fixed order, double) and
+  // finalizes them into `fin`, then re-zeroes its ticket.
+  unsigned* tickets;
+  BnFin fin;
 };
 
 template <int ACT>
@@ -74,7 +85,36 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-template <typename T, bool DGRAD>
+template <int ACT>
+__device__ __forceinline__ float in_act_f(float v) {
+  if (ACT == DMF_ACT_RELU) return fmaxf(v, 0.f);
+  if (ACT == DMF_ACT_GELU) return gelu_f(v);
+  return v;
+}
+
+// x <- act(x*sc + sh) on one 16-B chunk (8 bf16 or 4 f32)
+template <typename T, int INA>
+__device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const float* sh) {
+  if constexpr (sizeof(T) == 2) {
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+      lo = in_act_f<INA>(lo * sc[2 * i] + sh[2 * i]);
+      hi = in_act_f<INA>(hi * sc[2 * i + 1] + sh[2 * i + 1]);
+      w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    u = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    float f[4] = {__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = in_act_f<INA>(f[i] * sc[i] + sh[i]);
+    u = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+}
+
+// INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
+template <typename T, bool DGRAD, int INA>
 __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   constexpr int BK = 8 * EPC;          // 8 chunks per LDS row
@@ -123,6 +163,15 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
       c -= a.C1;
       ldsrc = a.ldx2;
     }
+    float sc[EPC], sh[EPC];
+    if constexpr (INA >= 0) {
+#pragma unroll
+      for (int e = 0; e < EPC; e += 4) {
+        const float4 s4 = *(const float4*)(a.in_ss + c + e), h4 = *(const float4*)(a.in_ss + a.C + c + e);
+        sc[e] = s4.x; sc[e + 1] = s4.y; sc[e + 2] = s4.z; sc[e + 3] = s4.w;
+        sh[e] = h4.x; sh[e + 1] = h4.y; sh[e + 2] = h4.z; sh[e + 3] = h4.w;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bool ok = kok && a_ok[i];
@@ -140,6 +189,7 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
       if (ok) {
         const size_t off = ((size_t)(a_n[i] * a.H + hi) * a.W + wi) * ldsrc + c;
         ra[i] = *(const uint4*)(src + off);
+        if constexpr (INA >= 0) chunk_affine<T, INA>(ra[i], sc, sh);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
@@ -285,6 +335,50 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
       *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
     }
   }
+  if (a.tickets) {
+    // Release (every wave drains its stores, barrier, agent release fence,
+    // ticket); the block drawing the last ticket of its column tile reduces
+    // the slab for those columns after an agent acquire fence.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev = __hip_atomic_fetch_add(a.tickets + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = prev == (unsigned)(a.mtiles - 1);
+    }
+    __syncthreads();
+    if (flag[0]) {
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      const int cl = tid & 127, half = tid >> 7;
+      const int col = n0 + cl;
+      double s = 0.0, q = 0.0;
+      if (col < a.Nout) {
+#pragma unroll 4
+        for (int t = half; t < a.mtiles; t += 2) {
+          const float2 v = *(const float2*)(a.partials + ((size_t)t * a.Nout + col) * 2);
+          s += (double)v.x;
+          q += (double)v.y;
+        }
+      }
+      double* dred = (double*)(smem + 64);
+      if (half == 1) {
+        dred[cl * 2] = s;
+        dred[cl * 2 + 1] = q;
+      }
+      __syncthreads();
+      if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
+      if (tid == 0) {
+        if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
+        __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
@@ -304,17 +398,32 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const size_t lds = 2 * STAGE_BYTES;  // 64 KB; C staging (<= 128*132*4) reuses it
   const size_t lds_c = (size_t)CBM * (CBN + (dtype == DMF_BF16 ? 8 : 4)) * (dtype == DMF_BF16 ? 2 : 4);
   const size_t lds_total = lds > lds_c ? lds : lds_c;
-  if (dtype == DMF_BF16) {
-    if (dgrad)
-      hipLaunchKernelGGL((k_conv_igemm<bf16_t, true>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
-    else
-      hipLaunchKernelGGL((k_conv_igemm<bf16_t, false>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+  const dim3 g((unsigned)nblk), b(CTHREADS);
+#define DMF_CONV_LAUNCH(TT, DG, INA) hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA>), g, b, lds_total, st, a)
+  if (dgrad) {
+    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
+    else DMF_CONV_LAUNCH(float, true, -1);
+  } else if (a.in_ss == nullptr) {
+    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
+    else DMF_CONV_LAUNCH(float, false, -1);
   } else {
-    if (dgrad)
-      hipLaunchKernelGGL((k_conv_igemm<float, true>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
-    else
-      hipLaunchKernelGGL((k_conv_igemm<float, false>), dim3((unsigned)nblk), dim3(CTHREADS), lds_total, st, a);
+    DMF_CHECK_ARG(a.x2 == nullptr, "%s: input affine needs a single source", what);
+    DMF_CHECK_ARG(((uintptr_t)a.in_ss % 16) == 0, "%s: input scale/shift must be 16-byte aligned", what);
+    switch (a.act_in) {
+      case DMF_ACT_NONE:
+        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_NONE); else DMF_CONV_LAUNCH(float, false, DMF_ACT_NONE);
+        break;
+      case DMF_ACT_RELU:
+        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_RELU); else DMF_CONV_LAUNCH(float, false, DMF_ACT_RELU);
+        break;
+      case DMF_ACT_GELU:
+        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_GELU); else DMF_CONV_LAUNCH(float, false, DMF_ACT_GELU);
+        break;
+      default:
+        DMF_CHECK_ARG(false, "%s: unsupported input activation %d", what, a.act_in);
+    }
   }
+#undef DMF_CONV_LAUNCH
   DMF_LAUNCH_CHECK(what);
   return 0;
 }
@@ -354,20 +463,19 @@ using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
-extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
-                              int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
-                              const float* bias, void* y, int Ho, int Wo, int ldy, float* bn_partials, int act,
-                              void* stream) {
-  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_fwd: bad dtype %d", dtype);
-  DMF_CHECK_ARG(stride >= 1 && dil >= 1 && KH >= 1 && KW >= 1, "dmf_conv2d_fwd: bad geometry");
+static int conv_fwd_common(ConvArgs& a, int dtype, const void* x, int N, int H, int W, int Cin, int ldx,
+                           const void* x2, int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride,
+                           int pad, int dil, const float* bias, void* y, int Ho, int Wo, int ldy, int act,
+                           const float* in_ss, int in_act, const char* what) {
+  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "%s: bad dtype %d", what, dtype);
+  DMF_CHECK_ARG(stride >= 1 && dil >= 1 && KH >= 1 && KW >= 1, "%s: bad geometry", what);
   DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
-                "dmf_conv2d_fwd: output size %dx%d inconsistent with input %dx%d k%d s%d p%d d%d", Ho, Wo, H, W, KH,
+                "%s: output size %dx%d inconsistent with input %dx%d k%d s%d p%d d%d", what, Ho, Wo, H, W, KH,
                 stride, pad, dil);
-  ConvArgs a{};
-  a.x = x; a.w = w; a.bias = bias; a.y = y; a.partials = bn_partials;
+  a.x = x; a.w = w; a.bias = bias; a.y = y;
   const int epc = dtype == DMF_BF16 ? 8 : 4;
   DMF_CHECK_ARG(!x2 || (Cin2 > 0 && Cin2 % epc == 0 && ldx2 % epc == 0 && ((uintptr_t)x2 % 16) == 0),
-                "dmf_conv2d_fwd: bad second source (C2=%d ld2=%d)", Cin2, ldx2);
+                "%s: bad second source (C2=%d ld2=%d)", what, Cin2, ldx2);
   a.N = N; a.H = H; a.W = W; a.C = Cin + (x2 ? Cin2 : 0); a.ldx = ldx;
   a.x2 = x2; a.C1 = Cin; a.ldx2 = ldx2;
   a.Ho = Ho; a.Wo = Wo; a.ldy = ldy; a.Nout = Cout;
@@ -375,7 +483,41 @@ extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int
   a.Ktot = KH * KW * a.C;
   a.M = N * Ho * Wo;
   a.act = act;
+  a.in_ss = in_ss;
+  a.act_in = in_act;
+  return 0;
+}
+
+extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                              int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                              const float* bias, void* y, int Ho, int Wo, int ldy, float* bn_partials, int act,
+                              const float* in_scale_shift, int in_act, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, x2, Cin2, ldx2, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                           Ho, Wo, ldy, act, in_scale_shift, in_act, "dmf_conv2d_fwd");
+  if (rc) return rc;
+  a.partials = bn_partials;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd");
+}
+
+extern "C" int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                                 int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad,
+                                 int dil, const float* bias, void* y, int Ho, int Wo, int ldy,
+                                 const float* in_scale_shift, int in_act, float* bn_partials, unsigned* bn_tickets,
+                                 double count, double unbias_count, const float* gamma, const float* beta,
+                                 float* running_mean, float* running_var, long long* num_batches_tracked,
+                                 float momentum, float eps, float* scale_shift, float* save_mean_invstd,
+                                 void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, x2, Cin2, ldx2, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                           Ho, Wo, ldy, DMF_ACT_NONE, in_scale_shift, in_act, "dmf_conv2d_fwd_bn");
+  if (rc) return rc;
+  DMF_CHECK_ARG(bn_partials && bn_tickets && scale_shift && count > 0, "dmf_conv2d_fwd_bn: bad batch-norm args");
+  a.partials = bn_partials;
+  a.tickets = bn_tickets;
+  a.fin = BnFin{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, 1,
+                scale_shift, save_mean_invstd};
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_bn");
 }
 
 extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,

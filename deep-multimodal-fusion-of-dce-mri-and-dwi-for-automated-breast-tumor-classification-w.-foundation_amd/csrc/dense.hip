@@ -12,6 +12,8 @@
 //     (:952-973) with its backward
 //   - GatingAttention (:745-780): softmax(Linear(cat(pvec_dwi, pvec_dce,
 //     mean(mask_dwi), mean(mask_dce))))
+#include <algorithm>
+
 #include "dmf_common.h"
 #include "../../include/dmf_hip.h"
 
@@ -31,28 +33,53 @@ __device__ __forceinline__ float actf(int act, float z) {
   }
 }
 
-// C = alpha*op(A)op(B) + beta*C + bias ; then act
-__global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, float alpha,
+// C = alpha*op(A)op(B) + beta*C + bias ; then act.
+// 64x64 tile, BK=16, 256 threads (4x4 outputs each). Global loads are
+// coalesced along the operand's contiguous dimension and prefetched into
+// registers one K-step ahead. Split-K: blockIdx.z owns K range
+// [z*kchunk, (z+1)*kchunk); with gridDim.z > 1 the partial tiles are
+// atomically added into C (zeroed by the entry point) and bias/act are
+// applied by k_sgemm_finish.
+__global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, int kchunk, float alpha,
                                                const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                int ldb, float beta, float* __restrict__ C, int ldc,
                                                const float* __restrict__ bias, int act) {
-  __shared__ float As[16][65], Bs[16][65];
+  __shared__ float As[16][68], Bs[16][68];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
-      const int kk = i / 64, mm = i % 64;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  const bool split = gridDim.z > 1;
+  // load mapping: contiguous-K operands walk k fastest (16 lanes x 1 row)
+  float ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = threadIdx.x + 256 * r;
+      int kk, mm;
+      if (tA) { kk = i >> 6; mm = i & 63; } else { kk = i & 15; mm = i >> 4; }
       const int m = m0 + mm, k = k0 + kk;
-      float va = 0.f;
-      if (m < M && k < K) va = tA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k];
-      As[kk][mm] = va;
-      const int n = n0 + mm;
-      float vb = 0.f;
-      if (n < N && k < K) vb = tB ? B[(size_t)n * ldb + k] : B[(size_t)k * ldb + n];
-      Bs[kk][mm] = vb;
+      ra[r] = (m < M && k < ke) ? (tA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k]) : 0.f;
+      int kk2, nn;
+      if (tB) { kk2 = i & 15; nn = i >> 4; } else { kk2 = i >> 6; nn = i & 63; }
+      const int n = n0 + nn, k2 = k0 + kk2;
+      rb[r] = (n < N && k2 < ke) ? (tB ? B[(size_t)n * ldb + k2] : B[(size_t)k2 * ldb + n]) : 0.f;
     }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = threadIdx.x + 256 * r;
+      if (tA) As[i >> 6][i & 63] = ra[r]; else As[i & 15][i >> 4] = ra[r];
+      if (tB) Bs[i & 15][i >> 4] = rb[r]; else Bs[i >> 6][i & 63] = rb[r];
+    }
+  };
+  float acc[4][4] = {};
+  if (kb < ke) gload(kb);
+  for (int k0 = kb; k0 < ke; k0 += 16) {
     __syncthreads();
+    sstore();
+    __syncthreads();
+    if (k0 + 16 < ke) gload(k0 + 16);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       float a[4], b[4];
@@ -65,7 +92,6 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
     }
-    __syncthreads();
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -73,12 +99,27 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
       if (m < M && n < N) {
-        float v = alpha * acc[i][j];
-        if (beta != 0.f) v += beta * C[(size_t)m * ldc + n];
-        if (bias) v += bias[n];
-        C[(size_t)m * ldc + n] = actf(act, v);
+        if (split) {
+          atomicAdd(C + (size_t)m * ldc + n, alpha * acc[i][j]);
+        } else {
+          float v = alpha * acc[i][j];
+          if (beta != 0.f) v += beta * C[(size_t)m * ldc + n];
+          if (bias) v += bias[n];
+          C[(size_t)m * ldc + n] = actf(act, v);
+        }
       }
     }
+}
+
+__global__ void k_sgemm_finish(int M, int N, float* __restrict__ C, int ldc, const float* __restrict__ bias, int act) {
+  const long long total = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / N), n = (int)(i % N);
+    float v = C[(size_t)m * ldc + n];
+    if (bias) v += bias[n];
+    C[(size_t)m * ldc + n] = actf(act, v);
+  }
 }
 
 // column sums: out[n] (+)= sum_m X[m][n]
@@ -514,9 +555,21 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
                          void* stream) {
   DMF_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "dmf_sgemm: bad args");
   if (M == 0 || N == 0) return 0;
-  dim3 grid(cdiv(N, 64), cdiv(M, 64));
-  hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, (hipStream_t)stream, transA, transB, M, N, K, alpha, A, lda, B, ldb,
-                     beta, C, ldc, bias, act);
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = cdiv(N, 64) * cdiv(M, 64);
+  // split K until the grid covers the chip, keeping >= 64 K per split
+  int S = 1;
+  if (beta == 0.f && ldc == N) {
+    S = std::max(1, std::min(cdiv(512, tiles), K / 64));
+  }
+  const int kchunk = cdiv(cdiv(K, S), 16) * 16;
+  S = std::max(1, cdiv(K, kchunk));
+  dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
+  if (S > 1) hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, st);
+  hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb, beta, C,
+                     ldc, bias, act);
+  if (S > 1 && (bias || act != DMF_ACT_NONE))
+    hipLaunchKernelGGL(k_sgemm_finish, dim3(gsz((long long)M * N)), dim3(256), 0, st, M, N, C, ldc, bias, act);
   DMF_LAUNCH_CHECK("dmf_sgemm");
   return 0;
 }

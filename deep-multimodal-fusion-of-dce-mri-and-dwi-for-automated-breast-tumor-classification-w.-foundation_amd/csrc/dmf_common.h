@@ -118,6 +118,54 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return r;
 }
 
+
+// ------------------------------------------------------ batch-norm finalize
+// One channel: batch statistics (sum s, sum of squares q over `count` rows,
+// double) -> (scale, shift) of y = x*scale + shift; running-stat update with
+// momentum and the unbiased variance (n = unbias_count if > 0 else count);
+// eval mode reads the running stats. Shared by dmf_bn_finalize and the conv
+// epilogue's last-arriving-block finalizer.
+struct BnFin {
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  long long* nbt;
+  float momentum, eps;
+  double count, unbias_count;
+  int training;
+  float* ss;    // [2][C]
+  float* save;  // [2][C] mean, invstd (nullable)
+};
+
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, int C, double s, double q) {
+  float mean, var;
+  if (f.training) {
+    const double m = s / f.count;
+    double v = q / f.count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    if (f.running_mean) {
+      f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * mean;
+      const double n_ = f.unbias_count > 0.0 ? f.unbias_count : f.count;
+      const double unb = n_ > 1.0 ? v * n_ / (n_ - 1.0) : v;
+      f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unb;
+    }
+  } else {
+    mean = f.running_mean[c];
+    var = f.running_var[c];
+  }
+  const float inv = rsqrtf(var + f.eps);
+  const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+  f.ss[c] = g * inv;
+  f.ss[C + c] = b - mean * g * inv;
+  if (f.save) {
+    f.save[c] = mean;
+    f.save[C + c] = inv;
+  }
+}
+
 // ----------------------------------------------------- counter-based RNG
 // Philox-4x32-10; (seed, offset) live in device memory so captured graphs
 // draw fresh dropout masks on every replay.

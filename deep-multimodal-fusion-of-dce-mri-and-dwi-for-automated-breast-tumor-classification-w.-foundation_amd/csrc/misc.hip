@@ -10,6 +10,8 @@
 //    (64,64) of a 32x32 map, model_module.py:531-534, :707-710), bilinear
 //    resize (align_corners=False), column statistics for BN on non-conv inputs
 //  - MaskGuidedSpatialAttention (model_module.py:49-97) forward/backward
+#include <algorithm>
+
 #include "dmf_common.h"
 #include "../../include/dmf_hip.h"
 
@@ -444,16 +446,215 @@ __global__ void k_mask_attn_fwd(const T* __restrict__ f, int ldf, const T* __res
   }
 }
 
+
+// ===================================================== 8-channel vector forms
+// One thread = 8 consecutive channels of one pixel (16-B bf16 / 32-B f32
+// accesses). Used when C, the leading dimensions and the pointers allow it.
+
+// out[n][c] += scale * sum_{rows of this block} a (*b); grid (N, S), block 256.
+// Lanes: CVt channel vectors x R rows per pass; LDS tree over R; one f32
+// atomic per (block, channel). out is zeroed by the entry point.
+template <typename T>
+__global__ void __launch_bounds__(256) k_nhwc_reduce8(const T* __restrict__ a, int lda, const T* __restrict__ b,
+                                                      int ldb, int HW, int C, int rpb, float scale,
+                                                      float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int CV = C >> 3;
+  const int CVt = CV < 256 ? CV : 256;
+  const int R = 256 / CVt;
+  const int cvl = threadIdx.x % CVt, rl = threadIdx.x / CVt;
+  const int n = blockIdx.x;
+  const int p0 = blockIdx.y * rpb, p1 = min(HW, p0 + rpb);
+  for (int cvb = 0; cvb < CV; cvb += CVt) {
+    const int cv = cvb + cvl;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rl < R && cv < CV) {
+      const T* pa = a + ((long long)n * HW) * lda + cv * 8;
+      const T* pb = b ? b + ((long long)n * HW) * ldb + cv * 8 : nullptr;
+#pragma unroll 4
+      for (int p = p0 + rl; p < p1; p += R) {
+        float va[8];
+        ld8(pa + (long long)p * lda, va);
+        if (pb) {
+          float vb[8];
+          ld8(pb + (long long)p * ldb, vb);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = fmaf(va[j], vb[j], acc[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += va[j];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[j];
+    __syncthreads();
+    // thread t < CVt*8 sums channel (t) over the R row lanes
+    for (int t = threadIdx.x; t < CVt * 8; t += 256) {
+      const int v = t >> 3, j = t & 7;
+      float s = 0.f;
+      for (int r = 0; r < R; ++r) s += red[(r * CVt + v) * 8 + j];
+      const int c = (cvb + v) * 8 + j;
+      if (cvb + v < CV) atomicAdd(out + (long long)n * C + c, s * scale);
+    }
+  }
+}
+
+// per-(n,c) mean of NCHW fp32; grid (NC, S), float4 loads, one atomic per block
+__global__ void __launch_bounds__(256) k_nchw_mean4(const float* __restrict__ x, long long HW, long long chunk,
+                                                    float inv, float* __restrict__ out) {
+  __shared__ float red[16];
+  const float* p = x + (long long)blockIdx.x * HW;
+  const long long q0 = (long long)blockIdx.y * chunk, q1 = min(HW, q0 + chunk);
+  float s = 0.f;
+  for (long long i = q0 + threadIdx.x * 4; i < q1; i += 1024) {
+    const float4 v = *(const float4*)(p + i);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(out + blockIdx.x, s * inv);
+}
+
+// input staging with 16-B stores: one thread = one pixel, Cp % 8 == 0
+template <typename T>
+__global__ void k_input_prep8(const float* __restrict__ x, int N, int C, int H, int W, const float* __restrict__ gate,
+                              T* __restrict__ y, int Cp, float* __restrict__ cmean) {
+  const long long HW = (long long)H * W;
+  const long long total = (long long)N * HW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / HW, p = i - n * HW;
+    const float* src = x + n * C * HW + p;
+    float s = 0.f;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        float t = 0.f;
+        if (c < C) {
+          t = src[c * HW];
+          s += t;
+          if (gate) t *= gate[n * C + c];
+        }
+        v[j] = t;
+      }
+      st8(y + i * Cp + c0, v);
+    }
+    if (cmean) cmean[i] = s / (float)C;
+  }
+}
+
+template <typename T>
+__global__ void k_up_nearest8(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C, int r) {
+  const int CV = C >> 3;
+  const long long total = (long long)N * r * H * r * W * CV;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long long t = i / CV;
+    const int wo = (int)(t % (r * W)); t /= (r * W);
+    const int ho = (int)(t % (r * H));
+    const int n = (int)(t / (r * H));
+    float v[8];
+    ld8(x + ((size_t)(n * H + ho / r) * W + wo / r) * ldx + cv * 8, v);
+    st8(y + i * 8, v);
+  }
+}
+
+template <typename T>
+__global__ void k_maxpool8(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y, int Ho,
+                           int Wo, int ldy, int k, int s, int p) {
+  const int CV = C >> 3;
+  const long long total = (long long)N * Ho * Wo * CV;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    const long long pix = i / CV;
+    const int n = (int)(pix / (Ho * Wo));
+    const int rem = (int)(pix - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem % Wo;
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * s - p + r;
+      if (hi < 0 || hi >= H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int wi = wo * s - p + q;
+        if (wi < 0 || wi >= W) continue;
+        float v[8];
+        ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > m[j] || isnan(v[j])) m[j] = v[j];
+      }
+    }
+    st8(y + pix * ldy + cv * 8, m);
+  }
+}
+
+template <typename T>
+__global__ void k_channel_scale8(const T* __restrict__ x, int ldx, const float* __restrict__ gate,
+                                 T* __restrict__ y, int ldy, long long N, int HW, int C) {
+  const int CV = C >> 3;
+  const long long total = N * HW * CV;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / CV;
+    const int c = (int)(i - row * CV) * 8;
+    const long long n = row / HW;
+    float v[8];
+    ld8(x + row * ldx + c, v);
+    const float4 g0 = *(const float4*)(gate + n * C + c), g1 = *(const float4*)(gate + n * C + c + 4);
+    v[0] *= g0.x; v[1] *= g0.y; v[2] *= g0.z; v[3] *= g0.w;
+    v[4] *= g1.x; v[5] *= g1.y; v[6] *= g1.z; v[7] *= g1.w;
+    st8(y + row * ldy + c, v);
+  }
+}
+
+template <typename T>
+__global__ void k_mix8(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb,
+                       const float* __restrict__ wlogit, T* __restrict__ z, int ldz, long long M, int C) {
+  const float al = 1.f / (1.f + __expf(-wlogit[0]));
+  const int CV = C >> 3;
+  const long long total = M * CV;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / CV;
+    const int c = (int)(i - m * CV) * 8;
+    float va[8], vb[8];
+    ld8(a + m * lda + c, va);
+    ld8(b + m * ldb + c, vb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) va[j] = al * va[j] + (1.f - al) * vb[j];
+    st8(z + m * ldz + c, va);
+  }
+}
+
 }  // namespace dmf
 
 using namespace dmf;
+
+static inline bool a16(const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; }
+static inline bool v8ok(int C, int ld0, int ld1, const void* p0, const void* p1, const void* p2 = nullptr) {
+  return C % 8 == 0 && ld0 % 8 == 0 && ld1 % 8 == 0 && a16(p0) && a16(p1) && a16(p2);
+}
 
 extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, int W, const float* gate, void* y, int Cp,
                               float* chan_mean, void* stream) {
   DMF_CHECK_ARG(x && (y || chan_mean) && Cp >= C, "dmf_input_prep: bad args");
   const long long total = (long long)N * H * W;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
+  if (y && Cp % 8 == 0 && a16(y)) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_input_prep8<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
+                         gate, (bf16_t*)y, Cp, chan_mean);
+    else
+      hipLaunchKernelGGL(k_input_prep8<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
+                         gate, (float*)y, Cp, chan_mean);
+  } else if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_input_prep<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
                        (bf16_t*)y, Cp, chan_mean);
   else
@@ -465,7 +666,16 @@ extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, in
 
 extern "C" int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream) {
   DMF_CHECK_ARG(x && out && NC > 0 && HW > 0, "dmf_nchw_mean: bad args");
-  hipLaunchKernelGGL(k_nchw_mean, dim3(NC), dim3(256), 0, (hipStream_t)stream, x, HW, out);
+  if (HW % 4 == 0 && a16(x)) {
+    // split each plane over S blocks so the grid covers the chip; atomics into a zeroed out
+    const long long S = std::max(1LL, std::min((long long)cdiv(2048, NC), HW / 4096));
+    const long long chunk = ((HW + S - 1) / S + 1023) / 1024 * 1024;
+    hipMemsetAsync(out, 0, sizeof(float) * NC, (hipStream_t)stream);
+    hipLaunchKernelGGL(k_nchw_mean4, dim3(NC, (unsigned)cdiv(HW, chunk)), dim3(256), 0, (hipStream_t)stream, x, HW,
+                       chunk, 1.f / (float)HW, out);
+  } else {
+    hipLaunchKernelGGL(k_nchw_mean, dim3(NC), dim3(256), 0, (hipStream_t)stream, x, HW, out);
+  }
   DMF_LAUNCH_CHECK("dmf_nchw_mean");
   return 0;
 }
@@ -473,6 +683,23 @@ extern "C" int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, v
 extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C,
                                float scale, float* out, int accumulate, void* stream) {
   DMF_CHECK_ARG(a && out && N > 0 && HW > 0 && C > 0, "dmf_nhwc_reduce: bad args");
+  if (v8ok(C, lda, b ? ldb : 8, a, b)) {
+    const int CV = C / 8, CVt = CV < 256 ? CV : 256, R = 256 / CVt;
+    // rows per block: >= 4 passes of R rows, and enough blocks to cover the chip
+    int S = std::max(1, std::min(cdiv(HW, 4 * R), cdiv(2048, N)));
+    int rpb = cdiv(HW, S);
+    rpb = cdiv(rpb, R) * R;
+    S = cdiv(HW, rpb);
+    if (!accumulate) hipMemsetAsync(out, 0, sizeof(float) * N * C, (hipStream_t)stream);
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_nhwc_reduce8<bf16_t>, dim3(N, S), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
+                         (const bf16_t*)b, ldb, HW, C, rpb, scale, out);
+    else
+      hipLaunchKernelGGL(k_nhwc_reduce8<float>, dim3(N, S), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
+                         (const float*)b, ldb, HW, C, rpb, scale, out);
+    DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
+    return 0;
+  }
   dim3 grid(N, cdiv(C, 64));
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_nhwc_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
@@ -489,6 +716,16 @@ extern "C" int dmf_channel_scale(int dtype, const void* x, int ldx, const float*
   DMF_CHECK_ARG(x && gate && y, "dmf_channel_scale: bad args");
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
+  if (v8ok(C, ldx, ldy, x, y, gate)) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_channel_scale8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, ldx, gate, (bf16_t*)y, ldy, (long long)N, HW, C);
+    else
+      hipLaunchKernelGGL(k_channel_scale8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)x, ldx, gate, (float*)y, ldy, (long long)N, HW, C);
+    DMF_LAUNCH_CHECK("dmf_channel_scale");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_channel_scale<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        ldx, gate, (bf16_t*)y, ldy, (long long)N, HW, C);
@@ -503,6 +740,16 @@ extern "C" int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb
                        long long M, int C, void* stream) {
   DMF_CHECK_ARG(a && b && wlogit && z, "dmf_mix: bad args");
   if (M * C == 0) return 0;
+  if (v8ok(C, lda, ldb, a, b) && ldz % 8 == 0 && a16(z)) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_mix8<bf16_t>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a,
+                         lda, (const bf16_t*)b, ldb, wlogit, (bf16_t*)z, ldz, M, C);
+    else
+      hipLaunchKernelGGL(k_mix8<float>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
+                         (const float*)b, ldb, wlogit, (float*)z, ldz, M, C);
+    DMF_LAUNCH_CHECK("dmf_mix");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_mix<bf16_t>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
                        (const bf16_t*)b, ldb, wlogit, (bf16_t*)z, ldz, M, C);
@@ -555,6 +802,16 @@ extern "C" int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int 
   DMF_CHECK_ARG(x && y && k > 0 && s > 0, "dmf_maxpool2d: bad args");
   const long long total = (long long)N * Ho * Wo * C;
   if (total == 0) return 0;
+  if (v8ok(C, ldx, ldy, x, y)) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_maxpool8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, N, H, W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, k, s, p);
+    else
+      hipLaunchKernelGGL(k_maxpool8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)x, N, H, W, C, ldx, (float*)y, Ho, Wo, ldy, k, s, p);
+    DMF_LAUNCH_CHECK("dmf_maxpool2d");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_maxpool<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
                        W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, k, s, p);
@@ -585,6 +842,16 @@ extern "C" int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, 
   DMF_CHECK_ARG(x && y && r >= 1, "dmf_upsample_nearest: bad args");
   const long long total = (long long)N * r * r * H * W * C;
   if (total == 0) return 0;
+  if (v8ok(C, ldx, 8, x, y)) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_up_nearest8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, ldx, (bf16_t*)y, N, H, W, C, r);
+    else
+      hipLaunchKernelGGL(k_up_nearest8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)x, ldx, (float*)y, N, H, W, C, r);
+    DMF_LAUNCH_CHECK("dmf_upsample_nearest");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_up_nearest<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        ldx, (bf16_t*)y, N, H, W, C, r);

@@ -67,15 +67,12 @@ __global__ void k_bn_stage1(const float* __restrict__ part, int T, int C, int ch
 }
 
 template <typename PT>
-__global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, double count, double unbias_count,
-                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                              float* running_mean, float* running_var, long long* nbt, float momentum, float eps,
-                              int training, float* __restrict__ ss, float* __restrict__ save) {
+__global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, BnFin f) {
   __shared__ double red[4][64][2];
   const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double s = 0.0, q = 0.0;
-  if (training && c < C) {
+  if (f.training && c < C) {
     for (int t = tl; t < T; t += 4) {
       s += (double)part[((size_t)t * C + c) * 2];
       q += (double)part[((size_t)t * C + c) * 2 + 1];
@@ -85,35 +82,11 @@ __global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, double 
   red[tl][cl][1] = q;
   __syncthreads();
   if (tl == 0 && c < C) {
-    float mean, var;
-    if (training) {
-      s = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
-      q = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
-      const double m = s / count;
-      double v = q / count - m * m;
-      if (v < 0.0) v = 0.0;
-      mean = (float)m;
-      var = (float)v;
-      if (running_mean) {
-        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-        const double n_ = unbias_count > 0.0 ? unbias_count : count;
-        const double unb = n_ > 1.0 ? v * n_ / (n_ - 1.0) : v;
-        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-      }
-    } else {
-      mean = running_mean[c];
-      var = running_var[c];
-    }
-    const float inv = rsqrtf(var + eps);
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    ss[c] = g * inv;
-    ss[C + c] = b - mean * g * inv;
-    if (save) {
-      save[c] = mean;
-      save[C + c] = inv;
-    }
+    s = red[0][cl][0] + red[1][cl][0] + red[2][cl][0] + red[3][cl][0];
+    q = red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1];
+    bn_fin_channel(f, c, C, s, q);
   }
-  if (training && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  if (f.training && f.nbt && blockIdx.x == 0 && threadIdx.x == 0) *f.nbt += 1;
 }
 
 // ------------------------------------------------------ fused affine/act
@@ -341,17 +314,16 @@ extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double 
   DMF_CHECK_ARG(!training || (partials && ntiles > 0 && count > 0), "dmf_bn_finalize: training needs partials");
   DMF_CHECK_ARG(training || (running_mean && running_var), "dmf_bn_finalize: eval needs running stats");
   hipStream_t st_ = (hipStream_t)stream;
+  BnFin f{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, training,
+          scale_shift, save_mean_invstd};
   if (training && ntiles > 64) {
     DMF_CHECK_ARG(workspace, "dmf_bn_finalize: %d tiles need a workspace (dmf_bn_finalize_ws_size)", ntiles);
     const int S = (ntiles + 31) / 32;
     hipLaunchKernelGGL(k_bn_stage1, dim3(cdiv(C, 64), S), dim3(256), 0, st_, partials, ntiles, C, 32, workspace);
     hipLaunchKernelGGL(k_bn_finalize<double>, dim3(cdiv(C, 64)), dim3(256), 0, st_, (const double*)workspace, S, C,
-                       count, unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
-                       training, scale_shift, save_mean_invstd);
+                       f);
   } else {
-    hipLaunchKernelGGL(k_bn_finalize<float>, dim3(cdiv(C, 64)), dim3(256), 0, st_, partials, ntiles, C, count,
-                       unbias_count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
-                       training, scale_shift, save_mean_invstd);
+    hipLaunchKernelGGL(k_bn_finalize<float>, dim3(cdiv(C, 64)), dim3(256), 0, st_, partials, ntiles, C, f);
   }
   DMF_LAUNCH_CHECK("dmf_bn_finalize");
   return 0;

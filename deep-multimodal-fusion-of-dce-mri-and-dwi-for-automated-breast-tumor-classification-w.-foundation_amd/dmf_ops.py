@@ -147,9 +147,41 @@ class ConvGeom:
         return ho, wo
 
 
-def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=None):
+def needs_grad(*ts):
+    """True when autograd will need a backward through any of ``ts``."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+def _probe_begin():
+    probe = PROBE["conv_fwd"]
+    if probe is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return e0
+
+
+def _probe_end(e0, x, n, h, w, cxt, co, kh, kw, g, ho, wo):
+    if e0 is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record()
+    es = x.element_size()
+    k_tot = kh * kw * cxt
+    flops = 2.0 * n * ho * wo * co * k_tot
+    byts = es * (n * h * w * cxt + co * k_tot + n * ho * wo * co)
+    PROBE["conv_fwd"].append((e0, e1, flops, byts, (n, h, w, cxt, co, kh, g.stride, g.dil)))
+
+
+def _is_mfma_conv(weight, g):
+    co, ci, kh, kw = weight.shape
+    return not (co == 1 or (ci == 1 and kh == 1 and kw == 1 and g.stride == 1))
+
+
+def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=None, in_ss=None, in_act="none"):
     """Returns (y, partials|None). partials: [tiles][Cout][2] fp32.
-    x2: optional second input concatenated along channels (no copy)."""
+    x2: optional second input concatenated along channels (no copy).
+    in_ss/in_act: the producer's BN apply + activation fused into the loads."""
     n, cx, h, w, ldx = nhwc(x)
     cx2, ldx2 = 0, 0
     if x2 is not None:
@@ -167,6 +199,8 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     act_c = ACT[act]
     if x2 is not None and (co == 1 or ci == 1):
         raise RuntimeError("channel-concat input only supported on the MFMA conv path")
+    if in_ss is not None and not _is_mfma_conv(weight, g):
+        raise RuntimeError("fused input affine only supported on the MFMA conv path")
     if co == 1:
         wf = caches[0].get(weight, torch.float32, cx, 0)
         N.call("dmf_conv_cout1_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, wf.data_ptr(), _p(bias), kh, kw, g.stride,
@@ -184,22 +218,68 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
         if want_stats:
             tiles = (n * ho * wo + 127) // 128
             partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
-        probe = PROBE["conv_fwd"]
-        if probe is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        e0 = _probe_begin()
         N.call("dmf_conv2d_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
                g.stride, g.pad,
                g.dil, _p(bias), y.data_ptr(), ho, wo, ldy, _p(partials), act_c if not want_stats else N.ACT_NONE,
-               _stream())
-        if probe is not None:
-            e1.record()
-            es = x.element_size()
-            k_tot = kh * kw * (cx + cx2)
-            flops = 2.0 * n * ho * wo * co * k_tot
-            byts = es * (n * h * w * (cx + cx2) + co * k_tot + n * ho * wo * co)
-            probe.append((e0, e1, flops, byts, (n, h, w, cx + cx2, co, kh, g.stride, g.dil)))
+               _p(in_ss), ACT[in_act], _stream())
+        _probe_end(e0, x, n, h, w, cx + cx2, co, kh, kw, g, ho, wo)
     return y, partials
+
+
+FUSED_BN_MAX_MTILES = 512  # above this the tile reducer's serial slab read costs more than a launch
+
+
+def _bn_site(bn, dev):
+    """Persistent, self-cleaning per-column-tile tickets of one BatchNorm2d
+    for the conv + finalize launch (zero at rest; kept out of the state_dict)."""
+    st = bn.__dict__.get("_dmf_site")
+    if st is None or st.device != dev:
+        st = torch.zeros(max(16, (bn.num_features + 127) // 128), dtype=torch.int32, device=dev)
+        bn.__dict__["_dmf_site"] = st
+    return st
+
+
+def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None, in_act="none"):
+    """conv -> (y_raw, scale_shift, save) of the following BatchNorm2d. In
+    training mode on the MFMA path the statistics and the finalize run inside
+    the conv launch (dmf_conv2d_fwd_bn)."""
+    training = bn.training or bn.running_mean is None
+    n_, _, h_, w_, _ = nhwc(x)
+    ho_, wo_ = g.out_hw(h_, w_)
+    mtiles = (n_ * ho_ * wo_ + 127) // 128
+    if not (training and _is_mfma_conv(w, g) and mtiles <= FUSED_BN_MAX_MTILES):
+        y, part = _conv_forward_raw(x, w, b, g, caches, training, "none", x2=x2, in_ss=in_ss, in_act=in_act)
+        n, c, ho, wo, _ = nhwc(y)
+        m = n * ho * wo
+        ss, save = _bn_finalize(part, m, bn, unbias_count=m * unbias_mult if unbias_mult != 1 else 0.0)
+        return y, ss, save
+    n, cx, h, wd, ldx = nhwc(x)
+    cx2, ldx2 = 0, 0
+    if x2 is not None:
+        _, cx2, _, _, ldx2 = nhwc(x2)
+    co, ci, kh, kw = w.shape
+    ho, wo = g.out_hw(h, wd)
+    dev = x.device
+    y = empty_nhwc(n, co, ho, wo, x.dtype, dev)
+    ldy = nhwc(y)[4]
+    m = n * ho * wo
+    ss = torch.empty(2 * co, dtype=torch.float32, device=dev)
+    save = torch.empty(2 * co, dtype=torch.float32, device=dev)
+    tickets = _bn_site(bn, dev)
+    partials = torch.empty((mtiles, co, 2), dtype=torch.float32, device=dev)
+    track = bn.track_running_stats and bn.running_mean is not None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    wk = caches[0].get(w, x.dtype, cx + cx2, 0)
+    e0 = _probe_begin()
+    N.call("dmf_conv2d_fwd_bn", dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
+           g.stride, g.pad, g.dil, _p(b), y.data_ptr(), ho, wo, ldy, _p(in_ss), ACT[in_act], partials.data_ptr(),
+           tickets.data_ptr(), float(m), float(m * unbias_mult) if unbias_mult != 1 else 0.0, _p(bn.weight),
+           _p(bn.bias), _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
+           _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), ss.data_ptr(), save.data_ptr(),
+           _stream())
+    _probe_end(e0, x, n, h, wd, cx + cx2, co, kh, kw, g, ho, wo)
+    return y, ss, save
 
 
 def _col_stats(y):
@@ -356,15 +436,13 @@ class _ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x2, w, b, gamma, beta, res, xr, wr, gamma_r, beta_r, spec):
-        (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult) = spec
-        y, part = _conv_forward_raw(x, w, b, g, caches, True, "none", x2=x2)
+        (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act) = spec
+        y, ss, save = _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss, in_act=in_act)
         n, c, ho, wo, ldy = nhwc(y)
         m = n * ho * wo
-        ss, save = _bn_finalize(part, m, bn, unbias_count=m * unbias_mult if unbias_mult != 1 else 0.0)
         yr = ss_r = save_r = None
         if xr is not None:
-            yr, part_r = _conv_forward_raw(xr, wr, None, gr, caches_r, True, "none")
-            ss_r, save_r = _bn_finalize(part_r, m, bn_r)
+            yr, ss_r, save_r = _conv_bn_forward(xr, wr, None, gr, caches_r, bn_r)
             res_t, ldr = yr, nhwc(yr)[4]
         elif res is not None:
             res_t, ldr = res, nhwc(res)[4]
@@ -380,7 +458,9 @@ class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng) = ctx.saved_tensors
-        (g, caches, bn, act, p, _rng, site, gr, caches_r, bn_r, unbias_mult) = ctx.spec
+        (g, caches, bn, act, p, _rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, _ia) = ctx.spec
+        if in_ss is not None:
+            raise RuntimeError("conv_bn_act with a fused input affine is forward-only")
         dout = as_nhwc(dout)
         n, c, ho, wo, ldy = nhwc(y)
         m = n * ho * wo
@@ -427,7 +507,7 @@ def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True):
 
 
 def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0, res=None, skip=None,
-                unbias_mult=1, x2=None):
+                unbias_mult=1, x2=None, in_ss=None, in_act="none"):
     """act(bn(conv(x)) + residual) with optional dropout.
 
     ``skip`` = (x_skip, conv_skip, caches_skip, bn_skip) for a projection
@@ -445,8 +525,30 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
     else:
         xr = wr = gamma_r = beta_r = None
         gr = caches_r = bn_r = None
-    spec = (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult)
+    spec = (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act)
+    if in_ss is not None:
+        # forward-only form: x is the producer's raw conv output, its BN apply
+        # + activation run inside this conv's loads
+        if needs_grad(x, conv.weight, conv.bias, bn.weight, bn.bias, res, wr, gamma_r, beta_r):
+            raise RuntimeError("fused input affine needs a no-grad context")
+        with torch.no_grad():
+            return _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r,
+                                      beta_r, spec)
     return _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r, beta_r, spec)
+
+
+def conv_bn_stats(x, conv, caches, bn, in_ss=None, in_act="none", x2=None, unbias_mult=1):
+    """Forward-only conv + BatchNorm statistics: returns (y_raw, scale_shift).
+    The BN apply (+ activation) is deferred into the consuming conv's loads
+    (``in_ss`` of conv_bn_act / conv_bn_stats), so the activated tensor is
+    never written to HBM."""
+    if needs_grad(x, conv.weight, conv.bias, bn.weight, bn.bias):
+        raise RuntimeError("conv_bn_stats is forward-only (no autograd graph)")
+    g = ConvGeom(conv)
+    with torch.no_grad():
+        y, ss, _ = _conv_bn_forward(x, conv.weight, conv.bias, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss,
+                                    in_act=in_act)
+    return y, ss
 
 
 # ============================================================ elementwise

@@ -235,6 +235,14 @@ class Projector(nn.Module):
         unbiasing still uses the replicated element count)."""
         x = _to_compute(x, _dt(self))
         pr = self.proj
+        um = replicate * replicate
+        if not O.needs_grad(x, pr[0].weight, pr[1].weight, pr[3].weight, pr[4].weight):
+            # forward-only: the first BN + GELU run inside the second (1x1,
+            # proj_dim <= 128 outputs: one column tile, so each element is
+            # transformed once) conv's loads; the 64-channel map skips HBM
+            y, ss = O.conv_bn_stats(x, pr[0], _caches(pr[0]), pr[1], unbias_mult=um)
+            h = O.conv_bn_act(y, pr[3], _caches(pr[3]), pr[4], "gelu", unbias_mult=um, in_ss=ss, in_act="gelu")
+            return O.upsample_nearest(h, replicate)
         h = O.conv_bn_act(x, pr[0], _caches(pr[0]), pr[1], "gelu", unbias_mult=replicate * replicate)
         h = O.conv_bn_act(h, pr[3], _caches(pr[3]), pr[4], "gelu", unbias_mult=replicate * replicate)
         return O.upsample_nearest(h, replicate)
@@ -308,6 +316,8 @@ class BackboneAdapter(nn.Module):
             if self.is_transformer:
                 parts = [_tokens_to_map(f) for f in parts]
             nk = self.necks[f"f{i + 1}"]
+            if len(parts) > 2:
+                raise NotImplementedError("neck chains of more than two feature maps are not built yet")
             if len(parts) == 1:
                 h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu")
             elif len(parts) == 2:

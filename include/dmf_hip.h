@@ -55,9 +55,27 @@ int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* str
 int dmf_conv_m_tile(void);
 /* x2 (nullable): second input concatenated along channels after the Cin
  * channels of x (BackboneAdapter chain [C4, C5], model_module.py:471) */
+/* in_scale_shift (nullable, single source only): the producer's batch-norm
+ * apply + activation fused into the A loads, x <- in_act(x*ss[c] + ss[C+c])
+ * on in-bounds elements (Bottleneck conv1->bn1->relu->conv2, adapter
+ * conv->BN->GELU->conv; model_module.py:440-447). in_act is DMF_ACT_*. */
 int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
                    int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil, const float* bias,
-                   void* y, int Ho, int Wo, int ldy, float* bn_partials, int act, void* stream);
+                   void* y, int Ho, int Wo, int ldy, float* bn_partials, int act, const float* in_scale_shift,
+                   int in_act, void* stream);
+/* conv + training-mode BatchNorm2d finalize in ONE launch: every block
+ * writes its per-channel (sum, sum^2) into bn_partials [mtiles][Cout][2]
+ * and takes a ticket of its output-channel tile; the last block of each
+ * tile reduces that tile's columns (fixed order, double) into scale_shift
+ * [2][Cout] (+ save_mean_invstd, running stats, num_batches_tracked, as
+ * dmf_bn_finalize) and re-zeroes its ticket. bn_tickets: >= ceil(Cout/128)
+ * counters, zero on the first call (persistent per BatchNorm site). */
+int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
+                      int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                      const float* bias, void* y, int Ho, int Wo, int ldy, const float* in_scale_shift, int in_act,
+                      float* bn_partials, unsigned* bn_tickets, double count, double unbias_count, const float* gamma,
+                      const float* beta, float* running_mean, float* running_var, long long* num_batches_tracked,
+                      float momentum, float eps, float* scale_shift, float* save_mean_invstd, void* stream);
 int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,

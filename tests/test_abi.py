@@ -82,7 +82,7 @@ def test_argument_errors_are_reported(lib):
 def test_conv_shape_checks(lib):
     # Cin not a multiple of 8 on the MFMA path / zero batch are argument errors
     rc = lib.dmf_conv2d_fwd(1, None, 0, 8, 8, 16, 16, None, 0, 0, None, 16, 3, 3, 1, 1, 1, None, None, 8, 8, 16,
-                            None, 0, None)
+                            None, 0, None, 0, None)
     assert rc == -1
     assert lib.dmf_last_error()
 
