@@ -77,6 +77,11 @@ __device__ __forceinline__ float apply_act_rt(int act, float v) {
 
 constexpr int CBM = 128, CBN = 128, CTHREADS = 256;
 constexpr int STAGE_BYTES = (CBM + CBN) * 128;  // A + B, 128-byte rows
+// main LDS: two A/B stages, reused for the C staging tile [128][128 + 16 B pad]
+__host__ __device__ constexpr int conv_lds_main(int esize) {
+  return 2 * STAGE_BYTES > CBM * (CBN + 16 / esize) * esize ? 2 * STAGE_BYTES : CBM * (CBN + 16 / esize) * esize;
+}
+constexpr int CONV_LDS_EXTRA = 64 + 128 * 2 * 8;  // flag + reducer doubles
 
 // bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
 // an XCD; give each XCD a contiguous range of logical tiles.
@@ -114,7 +119,10 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
 }
 
 // INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
-template <typename T, bool DGRAD, int INA>
+// FASTC: C (and the concat split C1) are multiples of BK, so every K-step
+// lies inside one filter tap: the tap/channel decode is block-uniform
+// (scalar) instead of two integer divisions per lane and step.
+template <typename T, bool DGRAD, int INA, bool FASTC>
 __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   constexpr int BK = 8 * EPC;          // 8 chunks per LDS row
@@ -152,9 +160,18 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
   uint4 ra[4], rb[4];
   auto gload = [&](int kt) {
     const int k = kt * BK + q * EPC;
-    const bool kok = k < a.Ktot;
-    const int tap = kok ? k / a.C : 0;
-    int c = k - tap * a.C;
+    bool kok;
+    int tap, c;
+    if constexpr (FASTC) {
+      const int k0 = kt * BK;  // uniform
+      tap = k0 / a.C;
+      c = k0 - tap * a.C + q * EPC;
+      kok = true;
+    } else {
+      kok = k < a.Ktot;
+      tap = kok ? k / a.C : 0;
+      c = k - tap * a.C;
+    }
     const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
     const T* src = X;
     int ldsrc = a.ldx;
@@ -181,9 +198,14 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
         wi = a_w[i] * a.stride - a.pad + s * a.dil;
       } else {
         const int hn = a_h[i] + a.pad - r * a.dil, wn_ = a_w[i] + a.pad - s * a.dil;
-        ok = ok && hn >= 0 && wn_ >= 0 && (hn % a.stride) == 0 && (wn_ % a.stride) == 0;
-        hi = hn / a.stride;
-        wi = wn_ / a.stride;
+        if (a.stride == 1) {  // uniform branch: no integer division on the common path
+          hi = hn;
+          wi = wn_;
+        } else {
+          ok = ok && hn >= 0 && wn_ >= 0 && (hn % a.stride) == 0 && (wn_ % a.stride) == 0;
+          hi = hn / a.stride;
+          wi = wn_ / a.stride;
+        }
       }
       ok = ok && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
       if (ok) {
@@ -306,7 +328,14 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
         float2 v;
         v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
         v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
-        *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+        float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
+        if (a.tickets) {
+          // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
+          __hip_atomic_store((unsigned long long*)dst, *(unsigned long long*)&v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *dst = v;
+        }
       }
     }
   }
@@ -326,6 +355,18 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
         Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
       }
   __syncthreads();
+  // scratch past the C staging area: [0] last-arriver flag, [64..] reducer doubles
+  char* xtra = smem + conv_lds_main(sizeof(T));
+  if (a.tickets) {
+    // the slab stores (issued before the C staging) drain; then one ticket per block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(a.tickets + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(int*)xtra = prev == (unsigned)(a.mtiles - 1);
+    }
+    __syncthreads();
+  }
   T* Y = (T*)a.y;
   constexpr int CPR = CBN / EPC;  // chunks per row
   for (int idx = tid; idx < CBM * CPR; idx += CTHREADS) {
@@ -335,48 +376,32 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
       *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
     }
   }
-  if (a.tickets) {
-    // Release (every wave drains its stores, barrier, agent release fence,
-    // ticket); the block drawing the last ticket of its column tile reduces
-    // the slab for those columns after an agent acquire fence.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = (int*)smem;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev = __hip_atomic_fetch_add(a.tickets + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = prev == (unsigned)(a.mtiles - 1);
+  if (a.tickets && *(const int*)xtra) {
+    // last block of this column tile: reduce the slab (sc1 loads, fixed order, double)
+    const int cl = tid & 127, half = tid >> 7;
+    const int col = n0 + cl;
+    double s = 0.0, q = 0.0;
+    if (col < a.Nout) {
+#pragma unroll 4
+      for (int t = half; t < a.mtiles; t += 2) {
+        const unsigned long long u = __hip_atomic_load(
+            (const unsigned long long*)(a.partials + ((size_t)t * a.Nout + col) * 2), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        const float2 v = *(const float2*)&u;
+        s += (double)v.x;
+        q += (double)v.y;
+      }
+    }
+    double* dred = (double*)(xtra + 64);
+    if (half == 1) {
+      dred[cl * 2] = s;
+      dred[cl * 2 + 1] = q;
     }
     __syncthreads();
-    if (flag[0]) {
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      const int cl = tid & 127, half = tid >> 7;
-      const int col = n0 + cl;
-      double s = 0.0, q = 0.0;
-      if (col < a.Nout) {
-#pragma unroll 4
-        for (int t = half; t < a.mtiles; t += 2) {
-          const float2 v = *(const float2*)(a.partials + ((size_t)t * a.Nout + col) * 2);
-          s += (double)v.x;
-          q += (double)v.y;
-        }
-      }
-      double* dred = (double*)(smem + 64);
-      if (half == 1) {
-        dred[cl * 2] = s;
-        dred[cl * 2 + 1] = q;
-      }
-      __syncthreads();
-      if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
-      if (tid == 0) {
-        if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
-        __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
+    if (tid == 0) {
+      if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
+      __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -395,11 +420,15 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   a.ntiles = cdiv(a.Nout, CBN);
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
-  const size_t lds = 2 * STAGE_BYTES;  // 64 KB; C staging (<= 128*132*4) reuses it
-  const size_t lds_c = (size_t)CBM * (CBN + (dtype == DMF_BF16 ? 8 : 4)) * (dtype == DMF_BF16 ? 2 : 4);
-  const size_t lds_total = lds > lds_c ? lds : lds_c;
+  const size_t lds_total = conv_lds_main(dtype == DMF_BF16 ? 2 : 4) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
-#define DMF_CONV_LAUNCH(TT, DG, INA) hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA>), g, b, lds_total, st, a)
+  const int bk = dtype == DMF_BF16 ? 64 : 32;
+  const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
+#define DMF_CONV_LAUNCH(TT, DG, INA)                                                            \
+  do {                                                                                          \
+    if (fastc) hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, true>), g, b, lds_total, st, a);  \
+    else hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, false>), g, b, lds_total, st, a);       \
+  } while (0)
   if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);

@@ -295,11 +295,67 @@ __global__ void k_conv_cout1_wgrad(const T* __restrict__ x, int N, int H, int W,
   if (dbias_ws && blockIdx.x == 0 && threadIdx.x == 0) dbias_ws[blockIdx.y] = accb;
 }
 
+// 8-channel vector form (Cin, ldx multiples of 8): thread = one 8-channel
+// slice of one tap, positions walked incrementally (no divisions in the
+// loop), 16-B loads, several positions in flight.
+template <typename T>
+__global__ void __launch_bounds__(256) k_conv_cout1_wgrad8(const T* __restrict__ x, int N, int H, int W, int Cin,
+                                                           int ldx, const T* __restrict__ dy, int lddy, int KH, int KW,
+                                                           int stride, int pad, int dil, int Ho, int Wo, int ppsplit,
+                                                           float* __restrict__ ws, float* __restrict__ dbias_ws) {
+  const int CV = Cin >> 3;
+  const int KV = KH * KW * CV;
+  const int kv = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool kok = kv < KV;
+  const int tap = kok ? kv / CV : 0, cv = kv - tap * CV, r = tap / KW, s = tap - (tap / KW) * KW;
+  const long long M = (long long)N * Ho * Wo;
+  const long long p0 = (long long)blockIdx.y * ppsplit;
+  const long long p1 = min(M, p0 + ppsplit);
+  int n = (int)(p0 / ((long long)Ho * Wo));
+  const int rem = (int)(p0 - (long long)n * Ho * Wo);
+  int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+#pragma unroll 4
+  for (long long p = p0; p < p1; ++p) {
+    const float g = ld(dy + p * lddy);
+    accb += g;
+    const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + s * dil;
+    if (kok && hi >= 0 && hi < H && wi >= 0 && wi < W) {
+      float v[8];
+      ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(g, v[j], acc[j]);
+    }
+    if (++wo == Wo) {
+      wo = 0;
+      if (++ho == Ho) {
+        ho = 0;
+        ++n;
+      }
+    }
+  }
+  if (kok) {
+    float* o = ws + (size_t)blockIdx.y * KV * 8 + (size_t)kv * 8;
+    *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+  if (dbias_ws && blockIdx.x == 0 && threadIdx.x == 0) dbias_ws[blockIdx.y] = accb;
+}
+
 __global__ void k_sum_splits(const float* __restrict__ ws, int splits, int K, float* __restrict__ out, int accumulate) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
-  float v = 0.f;
-  for (int s = 0; s < splits; ++s) v += ws[(size_t)s * K + k];
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int s = 0;
+  for (; s + 3 < splits; s += 4) {
+    v0 += ws[(size_t)s * K + k];
+    v1 += ws[(size_t)(s + 1) * K + k];
+    v2 += ws[(size_t)(s + 2) * K + k];
+    v3 += ws[(size_t)(s + 3) * K + k];
+  }
+  for (; s < splits; ++s) v0 += ws[(size_t)s * K + k];
+  const float v = (v0 + v1) + (v2 + v3);
   out[k] = accumulate ? out[k] + v : v;
 }
 
@@ -451,8 +507,8 @@ extern "C" int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const f
 }
 
 extern "C" int dmf_conv_cout1_wgrad_splits(long long M) {
-  long long s = (M + 511) / 512;
-  if (s > 256) s = 256;
+  long long s = (M + 63) / 64;
+  if (s > 512) s = 512;
   return (int)(s < 1 ? 1 : s);
 }
 
@@ -466,7 +522,15 @@ extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int 
   const int pps = (int)((M + splits - 1) / splits);
   dim3 grid(cdiv(K, 256), splits);
   float* wsb = workspace + (size_t)splits * K;
-  if (dtype == DMF_BF16)
+  if (Cin % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0) {
+    const dim3 g8(cdiv(K / 8, 256), splits);
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_conv_cout1_wgrad8<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
+                         W, Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+    else
+      hipLaunchKernelGGL(k_conv_cout1_wgrad8<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
+                         Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+  } else if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_conv_cout1_wgrad<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
                        Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
   else

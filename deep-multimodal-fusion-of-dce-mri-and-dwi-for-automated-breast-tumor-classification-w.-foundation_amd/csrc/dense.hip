@@ -37,13 +37,13 @@ __device__ __forceinline__ float actf(int act, float z) {
 // 64x64 tile, BK=16, 256 threads (4x4 outputs each). Global loads are
 // coalesced along the operand's contiguous dimension and prefetched into
 // registers one K-step ahead. Split-K: blockIdx.z owns K range
-// [z*kchunk, (z+1)*kchunk); with gridDim.z > 1 the partial tiles are
-// atomically added into C (zeroed by the entry point) and bias/act are
-// applied by k_sgemm_finish.
+// [z*kchunk, (z+1)*kchunk); with gridDim.z > 1 each split stores its
+// partial tile into ws[z][M][N] and k_sgemm_reduce sums the splits in a
+// fixed order and applies alpha, bias and act (deterministic).
 __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, int kchunk, float alpha,
                                                const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                int ldb, float beta, float* __restrict__ C, int ldc,
-                                               const float* __restrict__ bias, int act) {
+                                               const float* __restrict__ bias, int act, float* __restrict__ ws) {
   __shared__ float As[16][68], Bs[16][68];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
       const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
       if (m < M && n < N) {
         if (split) {
-          atomicAdd(C + (size_t)m * ldc + n, alpha * acc[i][j]);
+          ws[((size_t)blockIdx.z * M + m) * N + n] = acc[i][j];
         } else {
           float v = alpha * acc[i][j];
           if (beta != 0.f) v += beta * C[(size_t)m * ldc + n];
@@ -111,12 +111,15 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
     }
 }
 
-__global__ void k_sgemm_finish(int M, int N, float* __restrict__ C, int ldc, const float* __restrict__ bias, int act) {
+__global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __restrict__ ws, float* __restrict__ C,
+                               int ldc, const float* __restrict__ bias, int act) {
   const long long total = (long long)M * N;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int m = (int)(i / N), n = (int)(i % N);
-    float v = C[(size_t)m * ldc + n];
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += ws[(size_t)z * total + i];
+    v *= alpha;
     if (bias) v += bias[n];
     C[(size_t)m * ldc + n] = actf(act, v);
   }
@@ -550,26 +553,36 @@ __global__ void k_gate_bwd(const float* __restrict__ pa, const float* __restrict
 
 using namespace dmf;
 
+// K splits used for an (M, N, K) problem: enough blocks to cover the chip,
+// >= 64 K per split (1 = no split)
+static int sgemm_splits(int M, int N, int K) {
+  const int tiles = cdiv(N, 64) * cdiv(M, 64);
+  int S = std::max(1, std::min(cdiv(512, tiles), K / 64));
+  if (S <= 1) return 1;
+  const int kchunk = cdiv(cdiv(K, S), 16) * 16;
+  return std::max(1, cdiv(K, kchunk));
+}
+
+extern "C" int dmf_sgemm_ws_size(int M, int N, int K) {
+  const int S = sgemm_splits(M, N, K);
+  return S > 1 ? S * M * N : 0;
+}
+
 extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda,
                          const float* B, int ldb, float beta, float* C, int ldc, const float* bias, int act,
-                         void* stream) {
+                         float* workspace, void* stream) {
   DMF_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "dmf_sgemm: bad args");
   if (M == 0 || N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int tiles = cdiv(N, 64) * cdiv(M, 64);
-  // split K until the grid covers the chip, keeping >= 64 K per split
-  int S = 1;
-  if (beta == 0.f && ldc == N) {
-    S = std::max(1, std::min(cdiv(512, tiles), K / 64));
-  }
-  const int kchunk = cdiv(cdiv(K, S), 16) * 16;
-  S = std::max(1, cdiv(K, kchunk));
+  int S = (workspace && beta == 0.f) ? sgemm_splits(M, N, K) : 1;
+  const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);
+  S = S > 1 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
-  if (S > 1) hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, st);
   hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb, beta, C,
-                     ldc, bias, act);
-  if (S > 1 && (bias || act != DMF_ACT_NONE))
-    hipLaunchKernelGGL(k_sgemm_finish, dim3(gsz((long long)M * N)), dim3(256), 0, st, M, N, C, ldc, bias, act);
+                     ldc, bias, act, workspace);
+  if (S > 1)
+    hipLaunchKernelGGL(k_sgemm_reduce, dim3(gsz((long long)M * N)), dim3(256), 0, st, S, M, N, alpha, workspace, C,
+                       ldc, bias, act);
   DMF_LAUNCH_CHECK("dmf_sgemm");
   return 0;
 }

@@ -199,6 +199,95 @@ __global__ void k_recon(ReconArgs a) {
   }
 }
 
+// Band form: block = (b, band of RB output rows). Per output row every
+// thread computes the loss term and its gradient g(y, x) for its columns
+// into LDS (no atomics); column threads j then gather their bilinear
+// window of g (the source column is monotonic in x), and the band's
+// contributions to its (<= RB*h/S + 2) input rows are accumulated in LDS
+// registers and added to the global gradient with one atomic per element
+// per band (<= 3 adders per element). Loss sums: one atomic per term per
+// block.
+constexpr int RECON_RB = 8;
+constexpr int RECON_MAXS = 512;
+template <typename T>
+__global__ void __launch_bounds__(256) k_recon_band(ReconArgs a) {
+  __shared__ float G[5][RECON_MAXS];
+  __shared__ float acc[5][RECON_RB + 2][64];
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int y0 = blockIdx.y * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
+  const float inv_n = 1.f / ((float)a.B * a.S * a.S);
+  int ib0, tmp;
+  float ftmp;
+  lin_r(y0, a.h, a.S, ib0, tmp, ftmp);  // first input row touched by this band
+  for (int t = threadIdx.x; t < 5 * (RECON_RB + 2) * 64; t += blockDim.x) (&acc[0][0][0])[t] = 0.f;
+  float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int y = y0; y < y1; ++y) {
+    int i0, i1;
+    float ly;
+    lin_r(y, a.h, a.S, i0, i1, ly);
+    __syncthreads();  // G reuse
+    for (int x = threadIdx.x; x < a.S; x += blockDim.x) {
+      int j0, j1;
+      float lx;
+      lin_r(x, a.w, a.S, j0, j1, lx);
+      const size_t tp = ((size_t)b * a.S + y) * a.S + x;
+      const float tAv = a.tA ? a.tA[tp] : 0.f, tBv = a.tB ? a.tB[tp] : 0.f;
+      for (int k = 0; k < a.nterms; ++k) {
+        const T* R = (const T*)a.r[k] + (size_t)b * a.h * a.w * a.ldr[k];
+        const int ld_ = a.ldr[k];
+        const float v = (1.f - ly) * ((1.f - lx) * ld(R + (i0 * a.w + j0) * ld_) + lx * ld(R + (i0 * a.w + j1) * ld_)) +
+                        ly * ((1.f - lx) * ld(R + (i1 * a.w + j0) * ld_) + lx * ld(R + (i1 * a.w + j1) * ld_));
+        float tv = a.target[k] == 0 ? tAv : (a.target[k] == 1 ? tBv : a.ca * tAv + a.cb * tBv);
+        tv = fminf(fmaxf(tv, 0.f), 1.f);
+        const float sg = sigmoid_f(v);
+        const float pp = fminf(fmaxf(sg, 0.f), 1.f);
+        const float d = pp - tv;
+        const float q = sqrtf(d * d + 1e-6f);
+        part[k] += q;
+        G[k][x] = d / q * sg * (1.f - sg) * inv_n;  // dL/dv (clamp is identity on (0,1))
+      }
+    }
+    __syncthreads();
+    // column gather: thread (k, j) sums its window of x
+    for (int t = threadIdx.x; t < a.nterms * a.w; t += blockDim.x) {
+      const int k = t / a.w, j = t % a.w;
+      // x whose source column j0 or j1 is j lie in [xl, xh)
+      int xl = (int)floorf(((float)j - 1.f + 0.5f) * a.S / a.w - 0.5f) - 1;
+      int xh = (int)ceilf(((float)j + 1.f + 0.5f) * a.S / a.w - 0.5f) + 2;
+      xl = max(xl, 0);
+      xh = min(xh, a.S);
+      float h = 0.f;
+      for (int x = xl; x < xh; ++x) {
+        int j0, j1;
+        float lx;
+        lin_r(x, a.w, a.S, j0, j1, lx);
+        const float gv = G[k][x];
+        if (j0 == j) h += (1.f - lx) * gv;
+        if (j1 == j) h += lx * gv;
+      }
+      if (a.grads[k]) {
+        acc[k][i0 - ib0][j] += (1.f - ly) * h;
+        acc[k][i1 - ib0][j] += ly * h;
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < a.nterms; ++k) {
+    const float sm = block_sum(part[k], red);
+    if (threadIdx.x == 0) atomicAdd(a.sums + k, sm);
+  }
+  int ie, jt;
+  float ft;
+  lin_r(y1 - 1, a.h, a.S, jt, ie, ft);  // last input row touched
+  const int nrows = ie - ib0 + 1;
+  for (int t = threadIdx.x; t < a.nterms * nrows * a.w; t += blockDim.x) {
+    const int k = t / (nrows * a.w), rem = t % (nrows * a.w), r = rem / a.w, j = rem % a.w;
+    const float v = acc[k][r][j];
+    if (a.grads[k] && v != 0.f) atomicAdd(a.grads[k] + ((size_t)b * a.h + ib0 + r) * a.w + j, v);
+  }
+}
+
 // ------------------------------------------------------------ mimic
 // pair i: student S_i = s + i*sstride, teacher T_i = t + i*tstride, each an
 // [HW][C] NHWC map (channel stride ld). mimic_feat_loss flattens [C,H,W] to
@@ -332,10 +421,17 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
   a.tA = tA; a.tB = tB; a.ca = ca; a.cb = cb;
   a.B = B; a.h = h; a.w = w; a.S = S;
   a.sums = sums;
-  if (dtype == DMF_BF16)
+  if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
+    const dim3 g(B, cdiv(S, RECON_RB));
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_recon_band<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(k_recon_band<float>, g, dim3(256), 0, (hipStream_t)stream, a);
+  } else if (dtype == DMF_BF16) {
     hipLaunchKernelGGL(k_recon<bf16_t>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
-  else
+  } else {
     hipLaunchKernelGGL(k_recon<float>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
+  }
   DMF_LAUNCH_CHECK("dmf_recon_loss");
   return 0;
 }

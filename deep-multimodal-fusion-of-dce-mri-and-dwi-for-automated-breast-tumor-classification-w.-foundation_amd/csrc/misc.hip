@@ -451,69 +451,97 @@ __global__ void k_mask_attn_fwd(const T* __restrict__ f, int ldf, const T* __res
 // One thread = 8 consecutive channels of one pixel (16-B bf16 / 32-B f32
 // accesses). Used when C, the leading dimensions and the pointers allow it.
 
-// out[n][c] += scale * sum_{rows of this block} a (*b); grid (N, S), block 256.
-// Lanes: CVt channel vectors x R rows per pass; LDS tree over R; one f32
-// atomic per (block, channel). out is zeroed by the entry point.
+// Stage 1 of out[n][c] (+)= scale * sum_hw a (*b) [and out_sq += scale*sum a^2]:
+// grid (N, channel groups, S row splits), block 256 = CVt channel vectors
+// (8 channels each) x R = 256/CVt row lanes; each block writes its partial
+// sums to ws[s][n][c] (and ws[S*N*C + ...] for squares). Stage 2 sums the S
+// partials in a fixed order. Deterministic, no atomics, no memset.
 template <typename T>
 __global__ void __launch_bounds__(256) k_nhwc_reduce8(const T* __restrict__ a, int lda, const T* __restrict__ b,
-                                                      int ldb, int HW, int C, int rpb, float scale,
-                                                      float* __restrict__ out) {
+                                                      int ldb, int HW, int C, int CVt, int rpb, int sq,
+                                                      float* __restrict__ ws) {
   __shared__ float red[256 * 8];
   const int CV = C >> 3;
-  const int CVt = CV < 256 ? CV : 256;
   const int R = 256 / CVt;
   const int cvl = threadIdx.x % CVt, rl = threadIdx.x / CVt;
-  const int n = blockIdx.x;
-  const int p0 = blockIdx.y * rpb, p1 = min(HW, p0 + rpb);
-  for (int cvb = 0; cvb < CV; cvb += CVt) {
-    const int cv = cvb + cvl;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (rl < R && cv < CV) {
-      const T* pa = a + ((long long)n * HW) * lda + cv * 8;
-      const T* pb = b ? b + ((long long)n * HW) * ldb + cv * 8 : nullptr;
+  const int n = blockIdx.x, N = gridDim.x;
+  const int cv = blockIdx.y * CVt + cvl;
+  const int p0 = blockIdx.z * rpb, p1 = min(HW, p0 + rpb);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float acq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rl < R && cv < CV) {
+    const T* pa = a + ((long long)n * HW) * lda + cv * 8;
+    const T* pb = b ? b + ((long long)n * HW) * ldb + cv * 8 : nullptr;
 #pragma unroll 4
-      for (int p = p0 + rl; p < p1; p += R) {
-        float va[8];
-        ld8(pa + (long long)p * lda, va);
-        if (pb) {
-          float vb[8];
-          ld8(pb + (long long)p * ldb, vb);
+    for (int p = p0 + rl; p < p1; p += R) {
+      float va[8];
+      ld8(pa + (long long)p * lda, va);
+      if (pb) {
+        float vb[8];
+        ld8(pb + (long long)p * ldb, vb);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = fmaf(va[j], vb[j], acc[j]);
-        } else {
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(va[j], vb[j], acc[j]);
+      } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += va[j];
+        for (int j = 0; j < 8; ++j) {
+          acc[j] += va[j];
+          acq[j] = fmaf(va[j], va[j], acq[j]);
         }
       }
     }
+  }
+  const size_t plane = (size_t)N * C;
+  for (int pass = 0; pass < (sq ? 2 : 1); ++pass) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[j];
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = pass ? acq[j] : acc[j];
     __syncthreads();
-    // thread t < CVt*8 sums channel (t) over the R row lanes
     for (int t = threadIdx.x; t < CVt * 8; t += 256) {
-      const int v = t >> 3, j = t & 7;
-      float s = 0.f;
-      for (int r = 0; r < R; ++r) s += red[(r * CVt + v) * 8 + j];
-      const int c = (cvb + v) * 8 + j;
-      if (cvb + v < CV) atomicAdd(out + (long long)n * C + c, s * scale);
+      const int v = t >> 3, jj = t & 7;
+      float sum = 0.f;
+      for (int r = 0; r < R; ++r) sum += red[(r * CVt + v) * 8 + jj];
+      const int c = (blockIdx.y * CVt + v) * 8 + jj;
+      if (blockIdx.y * CVt + v < CV)
+        ws[(size_t)pass * gridDim.z * plane + (size_t)blockIdx.z * plane + (size_t)n * C + c] = sum;
     }
   }
 }
 
-// per-(n,c) mean of NCHW fp32; grid (NC, S), float4 loads, one atomic per block
-__global__ void __launch_bounds__(256) k_nchw_mean4(const float* __restrict__ x, long long HW, long long chunk,
-                                                    float inv, float* __restrict__ out) {
+__global__ void k_nhwc_reduce_fin(const float* __restrict__ ws, int S, long long NC, float scale,
+                                  float* __restrict__ out, float* __restrict__ out_sq, int accumulate) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < NC * (out_sq ? 2 : 1);
+       i += (long long)gridDim.x * blockDim.x) {
+    const int pass = i >= NC;
+    const long long e = pass ? i - NC : i;
+    const float* p = ws + (size_t)pass * S * NC + e;
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += p[(size_t)z * NC];
+    float* o = pass ? out_sq + e : out + e;
+    *o = accumulate ? *o + v * scale : v * scale;
+  }
+}
+
+// per-(n,c) mean of NCHW fp32: block per plane, float4 loads, 4 in flight
+__global__ void __launch_bounds__(256) k_nchw_mean4(const float* __restrict__ x, long long HW, float inv,
+                                                    float* __restrict__ out) {
   __shared__ float red[16];
   const float* p = x + (long long)blockIdx.x * HW;
-  const long long q0 = (long long)blockIdx.y * chunk, q1 = min(HW, q0 + chunk);
-  float s = 0.f;
-  for (long long i = q0 + threadIdx.x * 4; i < q1; i += 1024) {
-    const float4 v = *(const float4*)(p + i);
-    s += (v.x + v.y) + (v.z + v.w);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  long long i = threadIdx.x * 4;
+  for (; i + 3 * 1024 < HW; i += 4 * 1024) {
+    const float4 a = *(const float4*)(p + i), b = *(const float4*)(p + i + 1024);
+    const float4 c = *(const float4*)(p + i + 2048), d = *(const float4*)(p + i + 3072);
+    s0 += (a.x + a.y) + (a.z + a.w);
+    s1 += (b.x + b.y) + (b.z + b.w);
+    s2 += (c.x + c.y) + (c.z + c.w);
+    s3 += (d.x + d.y) + (d.z + d.w);
   }
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) atomicAdd(out + blockIdx.x, s * inv);
+  for (; i < HW; i += 1024) {
+    const float4 a = *(const float4*)(p + i);
+    s0 += (a.x + a.y) + (a.z + a.w);
+  }
+  float s = block_sum((s0 + s1) + (s2 + s3), red);
+  if (threadIdx.x == 0) out[blockIdx.x] = s * inv;
 }
 
 // input staging with 16-B stores: one thread = one pixel, Cp % 8 == 0
@@ -667,12 +695,7 @@ extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, in
 extern "C" int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream) {
   DMF_CHECK_ARG(x && out && NC > 0 && HW > 0, "dmf_nchw_mean: bad args");
   if (HW % 4 == 0 && a16(x)) {
-    // split each plane over S blocks so the grid covers the chip; atomics into a zeroed out
-    const long long S = std::max(1LL, std::min((long long)cdiv(2048, NC), HW / 4096));
-    const long long chunk = ((HW + S - 1) / S + 1023) / 1024 * 1024;
-    hipMemsetAsync(out, 0, sizeof(float) * NC, (hipStream_t)stream);
-    hipLaunchKernelGGL(k_nchw_mean4, dim3(NC, (unsigned)cdiv(HW, chunk)), dim3(256), 0, (hipStream_t)stream, x, HW,
-                       chunk, 1.f / (float)HW, out);
+    hipLaunchKernelGGL(k_nchw_mean4, dim3(NC), dim3(256), 0, (hipStream_t)stream, x, HW, 1.f / (float)HW, out);
   } else {
     hipLaunchKernelGGL(k_nchw_mean, dim3(NC), dim3(256), 0, (hipStream_t)stream, x, HW, out);
   }
@@ -680,33 +703,60 @@ extern "C" int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, v
   return 0;
 }
 
+// split plan of the vector path: (CVt, groups, S, rows per split)
+static void nhwc_reduce_plan(int N, int HW, int C, int& CVt, int& groups, int& S, int& rpb) {
+  const int CV = C / 8;
+  CVt = CV < 32 ? CV : 32;
+  groups = cdiv(CV, CVt);
+  const int R = 256 / CVt;
+  // >= ~1024 blocks chip-wide, each split >= 8 passes of R rows
+  S = std::max(1, std::min(cdiv(1024, N * groups), cdiv(HW, 8 * R)));
+  rpb = cdiv(HW, S);
+  rpb = cdiv(rpb, R) * R;
+  S = cdiv(HW, rpb);
+}
+
+extern "C" int dmf_nhwc_reduce_ws_size(int N, int HW, int C) {
+  if (C % 8 != 0) return 0;
+  int CVt, groups, S, rpb;
+  nhwc_reduce_plan(N, HW, C, CVt, groups, S, rpb);
+  return 2 * S * N * C;
+}
+
 extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C,
-                               float scale, float* out, int accumulate, void* stream) {
+                               float scale, float* out, float* out_sq, int accumulate, float* workspace,
+                               void* stream) {
   DMF_CHECK_ARG(a && out && N > 0 && HW > 0 && C > 0, "dmf_nhwc_reduce: bad args");
-  if (v8ok(C, lda, b ? ldb : 8, a, b)) {
-    const int CV = C / 8, CVt = CV < 256 ? CV : 256, R = 256 / CVt;
-    // rows per block: >= 4 passes of R rows, and enough blocks to cover the chip
-    int S = std::max(1, std::min(cdiv(HW, 4 * R), cdiv(2048, N)));
-    int rpb = cdiv(HW, S);
-    rpb = cdiv(rpb, R) * R;
-    S = cdiv(HW, rpb);
-    if (!accumulate) hipMemsetAsync(out, 0, sizeof(float) * N * C, (hipStream_t)stream);
+  DMF_CHECK_ARG(!(b && out_sq), "dmf_nhwc_reduce: out_sq is for the plain (b == NULL) form");
+  hipStream_t st = (hipStream_t)stream;
+  if (workspace && v8ok(C, lda, b ? ldb : 8, a, b)) {
+    int CVt, groups, S, rpb;
+    nhwc_reduce_plan(N, HW, C, CVt, groups, S, rpb);
+    const dim3 g8(N, groups, S);
     if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_nhwc_reduce8<bf16_t>, dim3(N, S), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
-                         (const bf16_t*)b, ldb, HW, C, rpb, scale, out);
+      hipLaunchKernelGGL(k_nhwc_reduce8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)a, lda, (const bf16_t*)b, ldb,
+                         HW, C, CVt, rpb, out_sq ? 1 : 0, workspace);
     else
-      hipLaunchKernelGGL(k_nhwc_reduce8<float>, dim3(N, S), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
-                         (const float*)b, ldb, HW, C, rpb, scale, out);
+      hipLaunchKernelGGL(k_nhwc_reduce8<float>, g8, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, HW,
+                         C, CVt, rpb, out_sq ? 1 : 0, workspace);
+    const long long nc = (long long)N * C;
+    hipLaunchKernelGGL(k_nhwc_reduce_fin, dim3(gsz(nc * (out_sq ? 2 : 1))), dim3(256), 0, st, workspace, S, nc, scale,
+                       out, out_sq, accumulate);
     DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
     return 0;
   }
   dim3 grid(N, cdiv(C, 64));
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_nhwc_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
-                       (const bf16_t*)b, ldb, HW, C, scale, out, accumulate);
-  else
-    hipLaunchKernelGGL(k_nhwc_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
-                       (const float*)b, ldb, HW, C, scale, out, accumulate);
+  for (int pass = 0; pass < (out_sq ? 2 : 1); ++pass) {
+    const void* bb = pass ? a : b;
+    const int ldbb = pass ? lda : ldb;
+    float* o = pass ? out_sq : out;
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_nhwc_reduce<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)a, lda, (const bf16_t*)bb,
+                         ldbb, HW, C, scale, o, accumulate);
+    else
+      hipLaunchKernelGGL(k_nhwc_reduce<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)bb, ldbb,
+                         HW, C, scale, o, accumulate);
+  }
   DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
   return 0;
 }

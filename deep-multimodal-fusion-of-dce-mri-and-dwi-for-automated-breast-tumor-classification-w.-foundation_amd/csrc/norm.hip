@@ -89,6 +89,37 @@ __global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, BnFin f
   if (f.training && f.nbt && blockIdx.x == 0 && threadIdx.x == 0) *f.nbt += 1;
 }
 
+// single-launch finalize for T <= 1024 tiles: block of 1024 threads =
+// 64 channels x 16 tile lanes, each lane summing T/16 tiles (double)
+__global__ void __launch_bounds__(1024) k_bn_finalize_wide(const float* __restrict__ part, int T, int C, BnFin f) {
+  __shared__ double red[16][64][2];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int t = tl; t < T; t += 16) {
+      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      s += (double)v.x;
+      q += (double)v.y;
+    }
+  }
+  red[tl][cl][0] = s;
+  red[tl][cl][1] = q;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    s = 0.0;
+    q = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s += red[i][cl][0];
+      q += red[i][cl][1];
+    }
+    bn_fin_channel(f, c, C, s, q);
+  }
+  if (f.nbt && blockIdx.x == 0 && threadIdx.x == 0) *f.nbt += 1;
+}
+
 // ------------------------------------------------------ fused affine/act
 // y = drop(act(x*sa + ba + [res*sr + br | res]))
 template <typename T>
@@ -303,7 +334,7 @@ static inline int grid_for(long long n, int block = 256) {
 using namespace dmf;
 
 extern "C" int dmf_bn_finalize_ws_size(int ntiles, int C) {
-  return ntiles <= 64 ? 0 : ((ntiles + 31) / 32) * C * 2;
+  return ntiles <= 1024 ? 0 : ((ntiles + 31) / 32) * C * 2;
 }
 
 extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, double unbias_count,
@@ -316,7 +347,9 @@ extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double 
   hipStream_t st_ = (hipStream_t)stream;
   BnFin f{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, training,
           scale_shift, save_mean_invstd};
-  if (training && ntiles > 64) {
+  if (training && ntiles > 64 && ntiles <= 1024) {
+    hipLaunchKernelGGL(k_bn_finalize_wide, dim3(cdiv(C, 64)), dim3(1024), 0, st_, partials, ntiles, C, f);
+  } else if (training && ntiles > 64) {
     DMF_CHECK_ARG(workspace, "dmf_bn_finalize: %d tiles need a workspace (dmf_bn_finalize_ws_size)", ntiles);
     const int S = (ntiles + 31) / 32;
     hipLaunchKernelGGL(k_bn_stage1, dim3(cdiv(C, 64), S), dim3(256), 0, st_, partials, ntiles, C, 32, workspace);

@@ -101,6 +101,7 @@ class FusionTrainer:
             self._setup_bucket()
         self._exchange_and_update()
         self.lm.global_step += 1
+        self.loss = loss.detach()
         return loss
 
     # ----------------------------------------------------------- graphs

@@ -131,6 +131,24 @@ class WeightCache:
         return out
 
 
+def _sgemm(tA, tB, M, N_, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act, stream):
+    """dmf_sgemm with its split-K workspace (deterministic ordered reduce)."""
+    wsn = N.load().dmf_sgemm_ws_size(M, N_, K) if beta == 0.0 else 0
+    ws = torch.empty(wsn, dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device())) \
+        if wsn > 0 else None
+    N.call("dmf_sgemm", tA, tB, M, N_, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act, _p(ws), stream)
+
+
+def _nhwc_reduce(a, b, scale, out, out_sq=None, accumulate=0):
+    """out[n][c] (+)= scale * sum_hw a*(b or 1) [out_sq: scale * sum_hw a^2]."""
+    n, c, h, w, lda = nhwc(a)
+    ldb = nhwc(b)[4] if b is not None else 0
+    wsn = N.load().dmf_nhwc_reduce_ws_size(n, h * w, c)
+    ws = torch.empty(wsn, dtype=torch.float32, device=a.device) if wsn > 0 else None
+    N.call("dmf_nhwc_reduce", dt(a), a.data_ptr(), lda, _p(b), ldb, n, h * w, c, float(scale), out.data_ptr(),
+           _p(out_sq), accumulate, _p(ws), _stream())
+
+
 # =================================================================== conv
 class ConvGeom:
     __slots__ = ("stride", "pad", "dil", "kh", "kw")
@@ -227,7 +245,7 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     return y, partials
 
 
-FUSED_BN_MAX_MTILES = 512  # above this the tile reducer's serial slab read costs more than a launch
+FUSED_BN_MAX_MTILES = 32  # the tile reducer reads mtiles slab rows serially: only pays for small problems
 
 
 def _bn_site(bn, dev):
@@ -587,8 +605,7 @@ def spatial_mean(x):
     """AdaptiveAvgPool2d(1) -> fp32 [N][C] (forward only helper)."""
     n, c, h, w, ld = nhwc(x)
     out = torch.empty((n, c), dtype=torch.float32, device=x.device)
-    N.call("dmf_nhwc_reduce", dt(x), x.data_ptr(), ld, None, 0, n, h * w, c, 1.0 / (h * w), out.data_ptr(), 0,
-           _stream())
+    _nhwc_reduce(x, None, 1.0 / (h * w), out)
     return out
 
 
@@ -622,7 +639,7 @@ class _LinearFn(torch.autograd.Function):
         nout = w.shape[0]
         y = torch.empty((r, nout), dtype=torch.float32, device=x.device)
         wc = w.detach().contiguous()
-        N.call("dmf_sgemm", 0, 1, r, nout, k, 1.0, x.data_ptr(), k, wc.data_ptr(), k, 0.0, y.data_ptr(), nout, _p(b),
+        _sgemm(0, 1, r, nout, k, 1.0, x.data_ptr(), k, wc.data_ptr(), k, 0.0, y.data_ptr(), nout, _p(b),
                N.ACT_NONE, _stream())
         pre = y
         if act != "none":
@@ -649,11 +666,11 @@ class _LinearFn(torch.autograd.Function):
         wc = w.detach().contiguous()
         if ctx.needs_input_grad[0]:
             dx = torch.empty((r, k), dtype=torch.float32, device=x.device)
-            N.call("dmf_sgemm", 0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
+            _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
                    None, N.ACT_NONE, _stream())
         if ctx.needs_input_grad[1]:
             dw = torch.empty((nout, k), dtype=torch.float32, device=x.device)
-            N.call("dmf_sgemm", 1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 0.0, dw.data_ptr(), k,
+            _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 0.0, dw.data_ptr(), k,
                    None, N.ACT_NONE, _stream())
             dw = dw.view_as(w)
         if b is not None and ctx.needs_input_grad[2]:
@@ -681,12 +698,12 @@ class _SEFn(torch.autograd.Function):
         pooled = spatial_mean(x)
         mid = w1.shape[0]
         hpre = torch.empty((n, mid), dtype=torch.float32, device=x.device)
-        N.call("dmf_sgemm", 0, 1, n, mid, c, 1.0, pooled.data_ptr(), c, w1.detach().reshape(mid, c).contiguous()
+        _sgemm(0, 1, n, mid, c, 1.0, pooled.data_ptr(), c, w1.detach().reshape(mid, c).contiguous()
                .data_ptr(), c, 0.0, hpre.data_ptr(), mid, _p(b1), N.ACT_NONE, _stream())
         hact = torch.empty_like(hpre)
         _act_f32(hpre, hact, "gelu")
         z2 = torch.empty((n, c), dtype=torch.float32, device=x.device)
-        N.call("dmf_sgemm", 0, 1, n, c, mid, 1.0, hact.data_ptr(), mid, w2.detach().reshape(c, mid).contiguous()
+        _sgemm(0, 1, n, c, mid, 1.0, hact.data_ptr(), mid, w2.detach().reshape(c, mid).contiguous()
                .data_ptr(), mid, 0.0, z2.data_ptr(), c, _p(b2), N.ACT_NONE, _stream())
         gate = torch.empty_like(z2)
         _act_f32(z2, gate, "sigmoid")
@@ -705,32 +722,31 @@ class _SEFn(torch.autograd.Function):
         mid = w1.shape[0]
         dev = x.device
         dg = torch.empty((n, c), dtype=torch.float32, device=dev)
-        N.call("dmf_nhwc_reduce", dt(x), dy.data_ptr(), nhwc(dy)[4], x.data_ptr(), ld, n, h * w, c, 1.0,
-               dg.data_ptr(), 0, _stream())
+        _nhwc_reduce(as_nhwc(dy), x, 1.0, dg)
         # through sigmoid: dz2 = dg * g * (1 - g)
         dz2 = torch.empty_like(dg)
         N.call("dmf_sig_grad_f32", dg.data_ptr(), gate.data_ptr(), dz2.data_ptr(), dg.numel(), _stream())
         w2m = w2.detach().reshape(c, mid).contiguous()
         w1m = w1.detach().reshape(mid, c).contiguous()
         dw2 = torch.empty((c, mid), dtype=torch.float32, device=dev)
-        N.call("dmf_sgemm", 1, 0, c, mid, n, 1.0, dz2.data_ptr(), c, hact.data_ptr(), mid, 0.0, dw2.data_ptr(), mid,
+        _sgemm(1, 0, c, mid, n, 1.0, dz2.data_ptr(), c, hact.data_ptr(), mid, 0.0, dw2.data_ptr(), mid,
                None, N.ACT_NONE, _stream())
         db2 = torch.empty(c, dtype=torch.float32, device=dev)
         N.call("dmf_colsum_f32", dz2.data_ptr(), c, n, c, db2.data_ptr(), 0, _stream())
         dh = torch.empty((n, mid), dtype=torch.float32, device=dev)
-        N.call("dmf_sgemm", 0, 0, n, mid, c, 1.0, dz2.data_ptr(), c, w2m.data_ptr(), mid, 0.0, dh.data_ptr(), mid,
+        _sgemm(0, 0, n, mid, c, 1.0, dz2.data_ptr(), c, w2m.data_ptr(), mid, 0.0, dh.data_ptr(), mid,
                None, N.ACT_NONE, _stream())
         dh1 = torch.empty_like(dh)
         N.call("dmf_act_grad_f32", dh.data_ptr(), hpre.data_ptr(), dh1.data_ptr(), dh.numel(), N.ACT_GELU, _stream())
         dw1 = torch.empty((mid, c), dtype=torch.float32, device=dev)
-        N.call("dmf_sgemm", 1, 0, mid, c, n, 1.0, dh1.data_ptr(), mid, pooled.data_ptr(), c, 0.0, dw1.data_ptr(), c,
+        _sgemm(1, 0, mid, c, n, 1.0, dh1.data_ptr(), mid, pooled.data_ptr(), c, 0.0, dw1.data_ptr(), c,
                None, N.ACT_NONE, _stream())
         db1 = torch.empty(mid, dtype=torch.float32, device=dev)
         N.call("dmf_colsum_f32", dh1.data_ptr(), mid, n, mid, db1.data_ptr(), 0, _stream())
         dx = None
         if ctx.needs_input_grad[0]:
             dpooled = torch.empty((n, c), dtype=torch.float32, device=dev)
-            N.call("dmf_sgemm", 0, 0, n, c, mid, 1.0, dh1.data_ptr(), mid, w1m.data_ptr(), c, 0.0, dpooled.data_ptr(),
+            _sgemm(0, 0, n, c, mid, 1.0, dh1.data_ptr(), mid, w1m.data_ptr(), c, 0.0, dpooled.data_ptr(),
                    c, None, N.ACT_NONE, _stream())
             dx = empty_nhwc(n, c, h, w, x.dtype, dev)
             N.call("dmf_channel_affine", dt(x), dy.data_ptr(), nhwc(dy)[4], gate.data_ptr(), dpooled.data_ptr(),
@@ -838,10 +854,7 @@ class _GNMixFn(torch.autograd.Function):
                n * h * w, c, _stream())
         mean = torch.empty((n, c), dtype=torch.float32, device=a.device)
         m2 = torch.empty((n, c), dtype=torch.float32, device=a.device)
-        N.call("dmf_nhwc_reduce", dt(z), z.data_ptr(), ldz, None, 0, n, h * w, c, 1.0 / (h * w), mean.data_ptr(), 0,
-               _stream())
-        N.call("dmf_nhwc_reduce", dt(z), z.data_ptr(), ldz, z.data_ptr(), ldz, n, h * w, c, 1.0 / (h * w),
-               m2.data_ptr(), 0, _stream())
+        _nhwc_reduce(z, None, 1.0 / (h * w), mean, out_sq=m2)
         y = empty_nhwc(n, c, h, w, a.dtype, a.device)
         N.call("dmf_gn_apply", dt(z), z.data_ptr(), ldz, mean.data_ptr(), m2.data_ptr(), gamma.data_ptr(),
                beta.data_ptr(), float(eps), y.data_ptr(), nhwc(y)[4], n, h * w, c, _stream())

@@ -139,8 +139,13 @@ int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* 
 int dmf_input_prep(int dtype, const float* x, int N, int C, int H, int W, const float* gate, void* y, int Cp,
                    float* chan_mean, void* stream);
 int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream);
+/* out[n][c] (+)= scale * sum_hw a*(b or 1); out_sq (nullable, b == NULL only)
+ * also gets scale * sum_hw a^2 in the same pass. workspace (nullable):
+ * dmf_nhwc_reduce_ws_size(N, HW, C) floats enable the chip-wide split form
+ * (partials + ordered combine, deterministic). */
+int dmf_nhwc_reduce_ws_size(int N, int HW, int C);
 int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C, float scale,
-                    float* out, int accumulate, void* stream);
+                    float* out, float* out_sq, int accumulate, float* workspace, void* stream);
 int dmf_channel_scale(int dtype, const void* x, int ldx, const float* gate, void* y, int ldy, int N, int HW, int C,
                       void* stream);
 int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb, const float* wlogit, void* z, int ldz,
@@ -184,8 +189,12 @@ int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, con
  * (:745-780), _to_tokens (:903-917), CrossAttentionBlock (:799-818: MHA +
  * LayerNorm/Linear FFN), gated combine + bilinear upsample-add (:952-973);
  * nn.Linear layers (classifier, SE excitations) via dmf_sgemm. */
+/* workspace (nullable): dmf_sgemm_ws_size(M, N, K) floats enable a
+ * deterministic split-K (partial tiles + ordered reduce) for small-output,
+ * long-K problems; without it (or with beta != 0) one pass over K. */
+int dmf_sgemm_ws_size(int M, int N, int K);
 int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
-              int ldb, float beta, float* C, int ldc, const float* bias, int act, void* stream);
+              int ldb, float beta, float* C, int ldc, const float* bias, int act, float* workspace, void* stream);
 int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream);
 int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
 int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream);

@@ -72,9 +72,9 @@ def test_argument_errors_are_reported(lib):
         N.call("dmf_bn_finalize", None, 0, 0, 1.0, 1.0, None, None, None, None, None, 0.1, 1e-5, 1, None, None,
                None, None)
     # large-T training finalize without a workspace is refused
-    assert lib.dmf_bn_finalize_ws_size(64, 128) == 0
-    assert lib.dmf_bn_finalize_ws_size(65, 128) == 3 * 128 * 2
-    rc = lib.dmf_bn_finalize(ctypes.c_void_p(16), 100, 8, 1.0, 1.0, None, None, None, None, None, 0.1, 1e-5, 1,
+    assert lib.dmf_bn_finalize_ws_size(1024, 128) == 0
+    assert lib.dmf_bn_finalize_ws_size(1025, 128) == 33 * 128 * 2
+    rc = lib.dmf_bn_finalize(ctypes.c_void_p(16), 2000, 8, 1.0, 1.0, None, None, None, None, None, 0.1, 1e-5, 1,
                              ctypes.c_void_p(16), None, None, None)
     assert rc == -1 and b"workspace" in lib.dmf_last_error()
 

@@ -168,7 +168,7 @@ def test_encoder_backward_parity_all_trainable():
     dozen training-mode BNs) the backbone grads are ill-conditioned: the fp32
     CPU oracle itself is 2-5 % away from a float64 evaluation. So the bar is
     relative to float64 truth: the HIP grads must be no further from it than
-    3x the fp32 oracle's own error (+1e-3)."""
+    3x the fp32 oracle's own error (+1e-3), in relative L2 norm per tensor."""
     P = PR.small_parameters(dropout=0.0)
     enc, ref, _ = build_pair(P, "dwi", 14, 41)
     ref64 = copy.deepcopy(ref).double()
@@ -188,9 +188,9 @@ def test_encoder_backward_parity_all_trainable():
             continue
         assert p1.grad is not None, n
         truth = p3.grad.float()
-        scale = max(1e-6, truth.abs().max().item())
-        e_mine = (p1.grad.float().cpu().reshape(truth.shape) - truth).abs().max().item() / scale
-        e_ref = (p2.grad - truth).abs().max().item() / scale
+        scale = max(1e-12, truth.norm().item())
+        e_mine = (p1.grad.float().cpu().reshape(truth.shape) - truth).norm().item() / scale
+        e_ref = (p2.grad - truth).norm().item() / scale
         if e_mine > 3 * e_ref + 1e-3:
             bad[n] = (round(e_mine, 5), round(e_ref, 5))
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
