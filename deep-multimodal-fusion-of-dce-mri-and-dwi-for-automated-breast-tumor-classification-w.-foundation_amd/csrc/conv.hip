@@ -118,6 +118,299 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
   }
 }
 
+// one LDS stage of A/B fragments -> 4x4 MFMA fragments per wave (64x64)
+template <typename T>
+__device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[4][4], int wm, int wn, int lane) {
+  const char* Bs = As + CBM * 128;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 4 + fg;
+    uint4 av[4], bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + fr;
+      av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wn * 64 + j * 16 + fr;
+      bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
+    }
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
+                                                              0, 0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float fa = __uint_as_float(((const uint32_t*)&av[i])[e]);
+            const float fb = __uint_as_float(((const uint32_t*)&bv[j])[e]);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, acc[i][j], 0, 0, 0);
+          }
+    }
+  }
+}
+
+// bias / activation or BN partial statistics, LDS-staged 16-B stores
+template <typename T>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[4][4], char* smem, int tid, int mt,
+                                              int nt, int m0, int n0) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const bool has_bias = a.bias != nullptr;
+  const bool stats = a.partials != nullptr;
+  float* red = (float*)smem;  // [2 wm][128 cols][2] floats = 2 KB
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + fr;
+    const float bsv = (has_bias && col < a.Nout) ? a.bias[col] : 0.f;
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
+        float v = acc[i][j][r] + bsv;
+        if (stats && row < a.M) { s += v; ss += v * v; }
+        if (!stats) v = apply_act_rt(a.act, v);
+        acc[i][j][r] = v;
+      }
+    }
+    if (stats) {
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
+      if (fg == 0) {
+        const int lc = wn * 64 + j * 16 + fr;
+        red[(wm * 128 + lc) * 2 + 0] = s;
+        red[(wm * 128 + lc) * 2 + 1] = ss;
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    if (tid < 128) {
+      const int col = n0 + tid;
+      if (col < a.Nout) {
+        float2 v;
+        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
+        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
+        float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
+        if (a.tickets) {
+          // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
+          __hip_atomic_store((unsigned long long*)dst, *(unsigned long long*)&v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *dst = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // stage C tile through LDS: [128 rows][128 + pad] of T
+  constexpr int CPAD = 16 / sizeof(T);
+  constexpr int CST = CBN + CPAD;
+  T* Cs = (T*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + fg * 4 + r;
+        const int col = wn * 64 + j * 16 + fr;
+        Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
+      }
+  __syncthreads();
+  // scratch past the C staging area: [0] last-arriver flag, [64..] reducer doubles
+  char* xtra = smem + conv_lds_main(sizeof(T));
+  if (a.tickets) {
+    // the slab stores (issued before the C staging) drain; then one ticket per block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(a.tickets + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(int*)xtra = prev == (unsigned)(a.mtiles - 1);
+    }
+    __syncthreads();
+  }
+  T* Y = (T*)a.y;
+  constexpr int CPR = CBN / EPC;  // chunks per row
+  for (int idx = tid; idx < CBM * CPR; idx += CTHREADS) {
+    const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
+    const int m = m0 + row, n = n0 + chn * EPC;
+    if (m < a.M && n < a.Nout) {
+      *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
+    }
+  }
+  if (a.tickets && *(const int*)xtra) {
+    // last block of this column tile: reduce the slab (sc1 loads, fixed order, double)
+    const int cl = tid & 127, half = tid >> 7;
+    const int col = n0 + cl;
+    double s = 0.0, q = 0.0;
+    if (col < a.Nout) {
+#pragma unroll 4
+      for (int t = half; t < a.mtiles; t += 2) {
+        const unsigned long long u = __hip_atomic_load(
+            (const unsigned long long*)(a.partials + ((size_t)t * a.Nout + col) * 2), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        const float2 v = *(const float2*)&u;
+        s += (double)v.x;
+        q += (double)v.y;
+      }
+    }
+    double* dred = (double*)(xtra + 64);
+    if (half == 1) {
+      dred[cl * 2] = s;
+      dred[cl * 2 + 1] = q;
+    }
+    __syncthreads();
+    if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
+    if (tid == 0) {
+      if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
+      __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ------------------------------------------------ forward, buffer-load form
+// FWD with C (and C1) multiples of BK and no input prologue. Every load is a
+// raw buffer load with a 32-bit per-lane offset: out-of-range lanes (M/N
+// edges, zero padding) get an offset past the buffer and read zeros from the
+// range check -- no branches, no 64-bit address math. The K-step's tap and
+// channel offsets are block-uniform (SGPR soffset). PADCHK = false for 1x1,
+// stride-1, pad-0 convs (no per-row bounds at all).
+constexpr unsigned BUF_OOB = 0x80000000u;
+constexpr int BUF_FLAGS = 0x00020000;
+
+template <typename T, bool PADCHK, bool DUAL>
+__global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
+  constexpr int ES = sizeof(T);
+  constexpr int EPC = 16 / ES;
+  constexpr int BK = 8 * EPC;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nblk = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, nblk);
+  const int mt = lin / a.ntiles, nt = lin % a.ntiles;
+  const int m0 = mt * CBM, n0 = nt * CBN;
+  const int q = tid & 7, rbase = tid >> 3;
+
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, (int)((long long)a.N * a.H * a.W * a.ldx * ES), BUF_FLAGS);
+  const __amdgpu_buffer_rsrc_t rx2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x2 ? a.x2 : a.x), 0, (int)((long long)a.N * a.H * a.W * (a.x2 ? a.ldx2 : a.ldx) * ES),
+      BUF_FLAGS);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.w), 0, (int)((long long)a.Nout * a.Ktot * ES), BUF_FLAGS);
+
+  // per-row origin (element offsets; may be negative for padded rows)
+  int h0[4], w0[4], b1[4], b2[4];
+  bool mok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rbase + 32 * i;
+    mok[i] = m < a.M;
+    const int mm = mok[i] ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    const int n = mm / hw, rem = mm - (mm / hw) * hw;
+    const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+    h0[i] = ho * a.stride - a.pad;
+    w0[i] = wo * a.stride - a.pad;
+    const int pix = (n * a.H + h0[i]) * a.W + w0[i];
+    b1[i] = pix * a.ldx + q * EPC;
+    b2[i] = pix * a.ldx2 + q * EPC;
+  }
+  unsigned vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + rbase + 32 * i;
+    vb[i] = n < a.Nout ? (unsigned)((n * a.Ktot + q * EPC) * ES) : BUF_OOB;
+  }
+  const int nk = a.Ktot / BK;
+
+  // two register sets: tile kt+1 is in flight while tile kt+2 is issued
+  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
+  auto gload = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
+    const int k0 = kt * BK;  // uniform
+    const int tap = k0 / a.C;
+    int c0 = k0 - tap * a.C;
+    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
+    const int rd = r * a.dil, sd = s * a.dil;
+    // block-uniform source choice as a branch, so each path keeps its descriptor in SGPRs
+    if (DUAL && c0 >= a.C1) {
+      const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b2[i] + toff) * ES) : BUF_OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx2, vo, 0, 0));
+      }
+    } else {
+      const int toff = (rd * a.W + sd) * a.ldx + c0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b1[i] + toff) * ES) : BUF_OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, vb[i], k0 * ES, 0));
+  };
+  auto lds_store = [&](int stage, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
+    char* base = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + 32 * i;
+      *(uint4*)(base + row * 128 + ((q ^ (row & 7)) << 4)) = ra[i];
+      *(uint4*)(base + CBM * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // Loads are issued unconditionally (tile index clamped at the tail) so the
+  // loop body has no branches around them: the compiler's vmcnt then counts
+  // exactly one tile still in flight at each LDS write.
+  gload(0, ra0, rb0);
+  gload(nk > 1 ? 1 : 0, ra1, rb1);
+  lds_store(0, ra0, rb0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // even step: LDS stage 0 holds tile kt, ra1/rb1 carry tile kt+1
+    gload(min(kt + 2, nk - 1), ra0, rb0);
+    conv_mma<T>(smem, acc, wm, wn, lane);
+    lds_store(1, ra1, rb1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    // odd step: stage 1 holds tile kt+1, ra0/rb0 carry tile kt+2
+    gload(min(kt + 3, nk - 1), ra1, rb1);
+    conv_mma<T>(smem + STAGE_BYTES, acc, wm, wn, lane);
+    lds_store(0, ra0, rb0);
+    __syncthreads();
+  }
+  conv_epilogue<T>(a, acc, smem, tid, mt, nt, m0, n0);
+}
+
 // INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
 // FASTC: C (and the concat split C1) are multiples of BK, so every K-step
 // lies inside one filter tap: the tap/channel decode is block-uniform
@@ -246,164 +539,23 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
   lds_store(0);
   __syncthreads();
 
-  const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const char* As = smem + cur * STAGE_BYTES;
-    const char* Bs = As + CBM * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 4 + fg;
-      uint4 av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + fr;
-        av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wn * 64 + j * 16 + fr;
-        bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
-      }
-      if constexpr (sizeof(T) == 2) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                *(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float fa = __uint_as_float(((const uint32_t*)&av[i])[e]);
-              const float fb = __uint_as_float(((const uint32_t*)&bv[j])[e]);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, acc[i][j], 0, 0, 0);
-            }
-      }
-    }
+    conv_mma<T>(smem + cur * STAGE_BYTES, acc, wm, wn, lane);
     if (kt + 1 < nk) lds_store(cur ^ 1);
     __syncthreads();
   }
+  conv_epilogue<T>(a, acc, smem, tid, mt, nt, m0, n0);
+}
 
-  // ------------------------------------------------------------ epilogue
-  const bool has_bias = a.bias != nullptr;
-  const bool stats = a.partials != nullptr;
-  float* red = (float*)smem;  // [2 wm][128 cols][2] floats = 2 KB
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + fr;
-    const float bsv = (has_bias && col < a.Nout) ? a.bias[col] : 0.f;
-    float s = 0.f, ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
-        float v = acc[i][j][r] + bsv;
-        if (stats && row < a.M) { s += v; ss += v * v; }
-        if (!stats) v = apply_act_rt(a.act, v);
-        acc[i][j][r] = v;
-      }
-    }
-    if (stats) {
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
-      if (fg == 0) {
-        const int lc = wn * 64 + j * 16 + fr;
-        red[(wm * 128 + lc) * 2 + 0] = s;
-        red[(wm * 128 + lc) * 2 + 1] = ss;
-      }
-    }
-  }
-  if (stats) {
-    __syncthreads();
-    if (tid < 128) {
-      const int col = n0 + tid;
-      if (col < a.Nout) {
-        float2 v;
-        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
-        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
-        float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
-        if (a.tickets) {
-          // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
-          __hip_atomic_store((unsigned long long*)dst, *(unsigned long long*)&v, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          *dst = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // stage C tile through LDS: [128 rows][128 + pad] of T
-  constexpr int CPAD = 16 / sizeof(T);
-  constexpr int CST = CBN + CPAD;
-  T* Cs = (T*)smem;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * 64 + i * 16 + fg * 4 + r;
-        const int col = wn * 64 + j * 16 + fr;
-        Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
-      }
-  __syncthreads();
-  // scratch past the C staging area: [0] last-arriver flag, [64..] reducer doubles
-  char* xtra = smem + conv_lds_main(sizeof(T));
-  if (a.tickets) {
-    // the slab stores (issued before the C staging) drain; then one ticket per block
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(a.tickets + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *(int*)xtra = prev == (unsigned)(a.mtiles - 1);
-    }
-    __syncthreads();
-  }
-  T* Y = (T*)a.y;
-  constexpr int CPR = CBN / EPC;  // chunks per row
-  for (int idx = tid; idx < CBM * CPR; idx += CTHREADS) {
-    const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
-    const int m = m0 + row, n = n0 + chn * EPC;
-    if (m < a.M && n < a.Nout) {
-      *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
-    }
-  }
-  if (a.tickets && *(const int*)xtra) {
-    // last block of this column tile: reduce the slab (sc1 loads, fixed order, double)
-    const int cl = tid & 127, half = tid >> 7;
-    const int col = n0 + cl;
-    double s = 0.0, q = 0.0;
-    if (col < a.Nout) {
-#pragma unroll 4
-      for (int t = half; t < a.mtiles; t += 2) {
-        const unsigned long long u = __hip_atomic_load(
-            (const unsigned long long*)(a.partials + ((size_t)t * a.Nout + col) * 2), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        const float2 v = *(const float2*)&u;
-        s += (double)v.x;
-        q += (double)v.y;
-      }
-    }
-    double* dred = (double*)(xtra + 64);
-    if (half == 1) {
-      dred[cl * 2] = s;
-      dred[cl * 2 + 1] = q;
-    }
-    __syncthreads();
-    if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
-    if (tid == 0) {
-      if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
-      __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+#include <cstdlib>
+static bool fast_disabled() {
+  static const int v = [] {
+    const char* e = std::getenv("DMF_CONV_LEGACY");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
 }
 
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
@@ -433,7 +585,24 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
   } else if (a.in_ss == nullptr) {
-    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
+    const long long xbytes = (long long)a.N * a.H * a.W * a.ldx * (dtype == DMF_BF16 ? 2 : 4);
+    const long long x2bytes = a.x2 ? (long long)a.N * a.H * a.W * a.ldx2 * (dtype == DMF_BF16 ? 2 : 4) : 0;
+    const long long wbytes = (long long)a.Nout * a.Ktot * (dtype == DMF_BF16 ? 2 : 4);
+    const bool bufok = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31) &&
+                       (long long)a.N * a.H * a.W * (a.ldx > a.ldx2 ? a.ldx : a.ldx2) < (1LL << 30);
+    if (bufok && !fast_disabled()) {
+      const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+      const bool dual = a.x2 != nullptr;
+      if (dtype == DMF_BF16) {
+        if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, true, true>), g, b, lds_total, st, a);
+        else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, false, false>), g, b, lds_total, st, a);
+        else hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, true, false>), g, b, lds_total, st, a);
+      } else {
+        if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<float, true, true>), g, b, lds_total, st, a);
+        else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<float, false, false>), g, b, lds_total, st, a);
+        else hipLaunchKernelGGL((k_conv_fwd_buf<float, true, false>), g, b, lds_total, st, a);
+      }
+    } else if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
     else DMF_CONV_LAUNCH(float, false, -1);
   } else {
     DMF_CHECK_ARG(a.x2 == nullptr, "%s: input affine needs a single source", what);
