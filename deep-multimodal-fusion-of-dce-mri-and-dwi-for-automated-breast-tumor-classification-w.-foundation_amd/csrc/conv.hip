@@ -77,11 +77,11 @@ __device__ __forceinline__ float apply_act_rt(int act, float v) {
 
 constexpr int CBM = 128, CBN = 128, CTHREADS = 256;
 constexpr int STAGE_BYTES = (CBM + CBN) * 128;  // A + B, 128-byte rows
-// main LDS: two A/B stages, reused for the C staging tile [128][128 + 16 B pad]
-__host__ __device__ constexpr int conv_lds_main(int esize) {
-  return 2 * STAGE_BYTES > CBM * (CBN + 16 / esize) * esize ? 2 * STAGE_BYTES : CBM * (CBN + 16 / esize) * esize;
+// main LDS: two A/B stages, reused for the C staging tile [BM][BN + 16 B pad]
+__host__ __device__ constexpr int conv_lds_main(int esize, int bm = CBM, int bn = CBN) {
+  return 2 * (bm + bn) * 128 > bm * (bn + 16 / esize) * esize ? 2 * (bm + bn) * 128 : bm * (bn + 16 / esize) * esize;
 }
-constexpr int CONV_LDS_EXTRA = 64 + 128 * 2 * 8;  // flag + reducer doubles
+constexpr int CONV_LDS_EXTRA = 64 + CTHREADS * 2 * 8;  // flag + reducer doubles
 
 // bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
 // an XCD; give each XCD a contiguous range of logical tiles.
@@ -118,39 +118,42 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
   }
 }
 
-// one LDS stage of A/B fragments -> 4x4 MFMA fragments per wave (64x64)
-template <typename T>
-__device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[4][4], int wm, int wn, int lane) {
-  const char* Bs = As + CBM * 128;
+// one LDS stage of A/B fragments -> (BM/32)x(BN/32) MFMA fragments per wave
+// (2x2 waves, each a (BM/2)x(BN/2) sub-tile)
+template <typename T, int BM = CBM, int BN = CBN>
+__device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / 32][BN / 32], int wm, int wn,
+                                         int lane) {
+  constexpr int FM = BM / 32, FN = BN / 32;
+  const char* Bs = As + BM * 128;
   const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int ch = kk * 4 + fg;
-    uint4 av[4], bv[4];
+    uint4 av[FM], bv[FN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wm * 64 + i * 16 + fr;
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * (BM / 2) + i * 16 + fr;
       av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = wn * 64 + j * 16 + fr;
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * (BN / 2) + j * 16 + fr;
       bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
     }
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
                                                               0, 0);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < FN; ++j) {
             const float fa = __uint_as_float(((const uint32_t*)&av[i])[e]);
             const float fb = __uint_as_float(((const uint32_t*)&bv[j])[e]);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, acc[i][j], 0, 0, 0);
@@ -160,26 +163,27 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[4][4], i
 }
 
 // bias / activation or BN partial statistics, LDS-staged 16-B stores
-template <typename T>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[4][4], char* smem, int tid, int mt,
-                                              int nt, int m0, int n0) {
+template <typename T, int BM = CBM, int BN = CBN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32], char* smem,
+                                              int tid, int mt, int nt, int m0, int n0) {
+  constexpr int FM = BM / 32, FN = BN / 32;
   constexpr int EPC = 16 / sizeof(T);
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int fr = lane & 15, fg = lane >> 4;
   const bool has_bias = a.bias != nullptr;
   const bool stats = a.partials != nullptr;
-  float* red = (float*)smem;  // [2 wm][128 cols][2] floats = 2 KB
+  float* red = (float*)smem;  // [2 wm][BN cols][2] floats
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + fr;
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 16 + fr;
     const float bsv = (has_bias && col < a.Nout) ? a.bias[col] : 0.f;
     float s = 0.f, ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
+        const int row = m0 + wm * (BM / 2) + i * 16 + fg * 4 + r;
         float v = acc[i][j][r] + bsv;
         if (stats && row < a.M) { s += v; ss += v * v; }
         if (!stats) v = apply_act_rt(a.act, v);
@@ -190,20 +194,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
       if (fg == 0) {
-        const int lc = wn * 64 + j * 16 + fr;
-        red[(wm * 128 + lc) * 2 + 0] = s;
-        red[(wm * 128 + lc) * 2 + 1] = ss;
+        const int lc = wn * (BN / 2) + j * 16 + fr;
+        red[(wm * BN + lc) * 2 + 0] = s;
+        red[(wm * BN + lc) * 2 + 1] = ss;
       }
     }
   }
   if (stats) {
     __syncthreads();
-    if (tid < 128) {
+    if (tid < BN) {
       const int col = n0 + tid;
       if (col < a.Nout) {
         float2 v;
-        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
-        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
+        v.x = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
+        v.y = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
         float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
         if (a.tickets) {
           // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
@@ -218,21 +222,21 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   __syncthreads();
   // stage C tile through LDS: [128 rows][128 + pad] of T
   constexpr int CPAD = 16 / sizeof(T);
-  constexpr int CST = CBN + CPAD;
+  constexpr int CST = BN + CPAD;
   T* Cs = (T*)smem;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * 64 + i * 16 + fg * 4 + r;
-        const int col = wn * 64 + j * 16 + fr;
+        const int row = wm * (BM / 2) + i * 16 + fg * 4 + r;
+        const int col = wn * (BN / 2) + j * 16 + fr;
         Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
       }
   __syncthreads();
   // scratch past the C staging area: [0] last-arriver flag, [64..] reducer doubles
-  char* xtra = smem + conv_lds_main(sizeof(T));
+  char* xtra = smem + conv_lds_main(sizeof(T), BM, BN);
   if (a.tickets) {
     // the slab stores (issued before the C staging) drain; then one ticket per block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -244,8 +248,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     __syncthreads();
   }
   T* Y = (T*)a.y;
-  constexpr int CPR = CBN / EPC;  // chunks per row
-  for (int idx = tid; idx < CBM * CPR; idx += CTHREADS) {
+  constexpr int CPR = BN / EPC;  // chunks per row
+  for (int idx = tid; idx < BM * CPR; idx += CTHREADS) {
     const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
     const int m = m0 + row, n = n0 + chn * EPC;
     if (m < a.M && n < a.Nout) {
@@ -254,12 +258,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   }
   if (a.tickets && *(const int*)xtra) {
     // last block of this column tile: reduce the slab (sc1 loads, fixed order, double)
-    const int cl = tid & 127, half = tid >> 7;
+    constexpr int NP = CTHREADS / BN;  // tile-row lanes per column
+    const int cl = tid % BN, part = tid / BN;
     const int col = n0 + cl;
     double s = 0.0, q = 0.0;
     if (col < a.Nout) {
 #pragma unroll 4
-      for (int t = half; t < a.mtiles; t += 2) {
+      for (int t = part; t < a.mtiles; t += NP) {
         const unsigned long long u = __hip_atomic_load(
             (const unsigned long long*)(a.partials + ((size_t)t * a.Nout + col) * 2), __ATOMIC_RELAXED,
             __HIP_MEMORY_SCOPE_AGENT);
@@ -269,12 +274,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       }
     }
     double* dred = (double*)(xtra + 64);
-    if (half == 1) {
-      dred[cl * 2] = s;
-      dred[cl * 2 + 1] = q;
-    }
+    dred[(part * BN + cl) * 2] = s;
+    dred[(part * BN + cl) * 2 + 1] = q;
     __syncthreads();
-    if (half == 0 && col < a.Nout) bn_fin_channel(a.fin, col, a.Nout, s + dred[cl * 2], q + dred[cl * 2 + 1]);
+    if (part == 0 && col < a.Nout) {
+      for (int pp = 1; pp < NP; ++pp) {
+        s += dred[(pp * BN + cl) * 2];
+        q += dred[(pp * BN + cl) * 2 + 1];
+      }
+      bn_fin_channel(a.fin, col, a.Nout, s, q);
+    }
     if (tid == 0) {
       if (nt == 0 && a.fin.training && a.fin.nbt) *a.fin.nbt += 1;
       __hip_atomic_store(a.tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -292,8 +301,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int BUF_FLAGS = 0x00020000;
 
-template <typename T, bool PADCHK, bool DUAL>
-__global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
+template <typename T, bool PADCHK, bool DUAL, int BM, int BN>
+__global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN <= 64 * 128) ? 3 : 2)) k_conv_fwd_buf(ConvArgs a) {
+  constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per K-step
+  constexpr int SB = (BM + BN) * 128;        // LDS stage bytes
   constexpr int ES = sizeof(T);
   constexpr int EPC = 16 / ES;
   constexpr int BK = 8 * EPC;
@@ -304,7 +315,7 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
   const int nblk = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, nblk);
   const int mt = lin / a.ntiles, nt = lin % a.ntiles;
-  const int m0 = mt * CBM, n0 = nt * CBN;
+  const int m0 = mt * BM, n0 = nt * BN;
   const int q = tid & 7, rbase = tid >> 3;
 
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -316,10 +327,10 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
       const_cast<void*>(a.w), 0, (int)((long long)a.Nout * a.Ktot * ES), BUF_FLAGS);
 
   // per-row origin (element offsets; may be negative for padded rows)
-  int h0[4], w0[4], b1[4], b2[4];
-  bool mok[4];
+  int h0[RA], w0[RA], b1[RA], b2[RA];
+  bool mok[RA];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RA; ++i) {
     const int m = m0 + rbase + 32 * i;
     mok[i] = m < a.M;
     const int mm = mok[i] ? m : 0;
@@ -332,17 +343,17 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
     b1[i] = pix * a.ldx + q * EPC;
     b2[i] = pix * a.ldx2 + q * EPC;
   }
-  unsigned vb[4];
+  unsigned vb[RB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RB; ++i) {
     const int n = n0 + rbase + 32 * i;
     vb[i] = n < a.Nout ? (unsigned)((n * a.Ktot + q * EPC) * ES) : BUF_OOB;
   }
   const int nk = a.Ktot / BK;
 
   // two register sets: tile kt+1 is in flight while tile kt+2 is issued
-  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
-  auto gload = [&](int kt, uint4 (&ra)[4], uint4 (&rb)[4]) {
+  uint4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
+  auto gload = [&](int kt, uint4 (&ra)[RA], uint4 (&rb)[RB]) {
     const int k0 = kt * BK;  // uniform
     const int tap = k0 / a.C;
     int c0 = k0 - tap * a.C;
@@ -352,7 +363,7 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
     if (DUAL && c0 >= a.C1) {
       const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < RA; ++i) {
         bool ok = mok[i];
         if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
         const unsigned vo = ok ? (unsigned)((b2[i] + toff) * ES) : BUF_OOB;
@@ -361,7 +372,7 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
     } else {
       const int toff = (rd * a.W + sd) * a.ldx + c0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < RA; ++i) {
         bool ok = mok[i];
         if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
         const unsigned vo = ok ? (unsigned)((b1[i] + toff) * ES) : BUF_OOB;
@@ -369,46 +380,62 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_buf(ConvArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < RB; ++i)
       rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, vb[i], k0 * ES, 0));
   };
-  auto lds_store = [&](int stage, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
-    char* base = smem + stage * STAGE_BYTES;
+  auto lds_store = [&](int stage, const uint4 (&ra)[RA], const uint4 (&rb)[RB]) {
+    char* base = smem + stage * SB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RA; ++i) {
       const int row = rbase + 32 * i;
       *(uint4*)(base + row * 128 + ((q ^ (row & 7)) << 4)) = ra[i];
-      *(uint4*)(base + CBM * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int row = rbase + 32 * i;
+      *(uint4*)(base + BM * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
     }
   };
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[RA][RB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < RA; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < RB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // Loads are issued unconditionally (tile index clamped at the tail) so the
   // loop body has no branches around them: the compiler's vmcnt then counts
   // exactly one tile still in flight at each LDS write.
+  if (nk <= 2) {  // short K (1x1 over <= 128 channels): no pipeline to fill
+    gload(0, ra0, rb0);
+    if (nk == 2) gload(1, ra1, rb1);
+    lds_store(0, ra0, rb0);
+    if (nk == 2) lds_store(1, ra1, rb1);
+    __syncthreads();
+    conv_mma<T, BM, BN>(smem, acc, wm, wn, lane);
+    if (nk == 2) conv_mma<T, BM, BN>(smem + SB, acc, wm, wn, lane);
+    __syncthreads();
+    conv_epilogue<T, BM, BN>(a, acc, smem, tid, mt, nt, m0, n0);
+    return;
+  }
   gload(0, ra0, rb0);
-  gload(nk > 1 ? 1 : 0, ra1, rb1);
+  gload(1, ra1, rb1);
   lds_store(0, ra0, rb0);
   __syncthreads();
   for (int kt = 0; kt < nk; kt += 2) {
     // even step: LDS stage 0 holds tile kt, ra1/rb1 carry tile kt+1
     gload(min(kt + 2, nk - 1), ra0, rb0);
-    conv_mma<T>(smem, acc, wm, wn, lane);
+    conv_mma<T, BM, BN>(smem, acc, wm, wn, lane);
     lds_store(1, ra1, rb1);
     __syncthreads();
     if (kt + 1 >= nk) break;
     // odd step: stage 1 holds tile kt+1, ra0/rb0 carry tile kt+2
     gload(min(kt + 3, nk - 1), ra1, rb1);
-    conv_mma<T>(smem + STAGE_BYTES, acc, wm, wn, lane);
+    conv_mma<T, BM, BN>(smem + SB, acc, wm, wn, lane);
     lds_store(0, ra0, rb0);
     __syncthreads();
   }
-  conv_epilogue<T>(a, acc, smem, tid, mt, nt, m0, n0);
+  conv_epilogue<T, BM, BN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
 // INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
@@ -558,6 +585,31 @@ static bool fast_disabled() {
   return v != 0;
 }
 
+// Which kernel/tile a forward launch uses. The buffer-load kernel needs C
+// (and C1) multiples of BK, no input prologue and < 2 GiB operands. Tile:
+// BN = 64 when Cout <= 64 (no wasted MFMA columns), BM = 64 when 128-row
+// tiles would leave fewer than ~2 blocks per CU.
+struct ConvPlan {
+  bool buf;
+  int bm, bn;
+};
+static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
+  ConvPlan p{false, CBM, CBN};
+  if (dgrad || a.in_ss != nullptr || fast_disabled()) return p;
+  const int es = dtype == DMF_BF16 ? 2 : 4;
+  const int bk = dtype == DMF_BF16 ? 64 : 32;
+  const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
+  const long long xbytes = (long long)a.N * a.H * a.W * a.ldx * es;
+  const long long x2bytes = a.x2 ? (long long)a.N * a.H * a.W * a.ldx2 * es : 0;
+  const long long wbytes = (long long)a.Nout * a.Ktot * es;
+  p.buf = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31);
+  if (!p.buf) return p;
+  p.bn = a.Nout <= 64 ? 64 : 128;
+  const long long blocks128 = (long long)cdiv(a.M, 128) * cdiv(a.Nout, p.bn);
+  p.bm = blocks128 < 512 ? 64 : 128;
+  return p;
+}
+
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
   const int epc = dtype == DMF_BF16 ? 8 : 4;
   DMF_CHECK_ARG(a.C % epc == 0 && a.ldx % epc == 0, "%s: input channels (%d) and stride (%d) must be multiples of %d",
@@ -568,11 +620,13 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
                 "%s: pointers must be 16-byte aligned", what);
   DMF_CHECK_ARG(a.M > 0 && a.Nout > 0 && a.Ktot > 0, "%s: empty problem (M=%d N=%d K=%d)", what, a.M, a.Nout,
                 a.Ktot);
-  a.mtiles = cdiv(a.M, CBM);
-  a.ntiles = cdiv(a.Nout, CBN);
+  const ConvPlan plan = conv_plan(dtype, dgrad, a);
+  a.mtiles = cdiv(a.M, plan.bm);
+  a.ntiles = cdiv(a.Nout, plan.bn);
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
-  const size_t lds_total = conv_lds_main(dtype == DMF_BF16 ? 2 : 4) + CONV_LDS_EXTRA;
+  const int es = dtype == DMF_BF16 ? 2 : 4;
+  const size_t lds_total = conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
   const int bk = dtype == DMF_BF16 ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
@@ -581,28 +635,36 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     if (fastc) hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, true>), g, b, lds_total, st, a);  \
     else hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, false>), g, b, lds_total, st, a);       \
   } while (0)
+#define DMF_BUF_LAUNCH(TT, BM, BN)                                                                           \
+  do {                                                                                                       \
+    if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<TT, true, true, BM, BN>), g, b, lds_total, st, a);          \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, BM, BN>), g, b, lds_total, st, a);  \
+    else hipLaunchKernelGGL((k_conv_fwd_buf<TT, true, false, BM, BN>), g, b, lds_total, st, a);              \
+  } while (0)
   if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
-  } else if (a.in_ss == nullptr) {
-    const long long xbytes = (long long)a.N * a.H * a.W * a.ldx * (dtype == DMF_BF16 ? 2 : 4);
-    const long long x2bytes = a.x2 ? (long long)a.N * a.H * a.W * a.ldx2 * (dtype == DMF_BF16 ? 2 : 4) : 0;
-    const long long wbytes = (long long)a.Nout * a.Ktot * (dtype == DMF_BF16 ? 2 : 4);
-    const bool bufok = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31) &&
-                       (long long)a.N * a.H * a.W * (a.ldx > a.ldx2 ? a.ldx : a.ldx2) < (1LL << 30);
-    if (bufok && !fast_disabled()) {
-      const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-      const bool dual = a.x2 != nullptr;
-      if (dtype == DMF_BF16) {
-        if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, true, true>), g, b, lds_total, st, a);
-        else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, false, false>), g, b, lds_total, st, a);
-        else hipLaunchKernelGGL((k_conv_fwd_buf<bf16_t, true, false>), g, b, lds_total, st, a);
-      } else {
-        if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<float, true, true>), g, b, lds_total, st, a);
-        else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<float, false, false>), g, b, lds_total, st, a);
-        else hipLaunchKernelGGL((k_conv_fwd_buf<float, true, false>), g, b, lds_total, st, a);
+  } else if (plan.buf) {
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const bool dual = a.x2 != nullptr;
+    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
+    if (dtype == DMF_BF16) {
+      switch (cfg) {
+        case 3: DMF_BUF_LAUNCH(bf16_t, 128, 128); break;
+        case 2: DMF_BUF_LAUNCH(bf16_t, 128, 64); break;
+        case 1: DMF_BUF_LAUNCH(bf16_t, 64, 128); break;
+        default: DMF_BUF_LAUNCH(bf16_t, 64, 64); break;
       }
-    } else if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
+    } else {
+      switch (cfg) {
+        case 3: DMF_BUF_LAUNCH(float, 128, 128); break;
+        case 2: DMF_BUF_LAUNCH(float, 128, 64); break;
+        case 1: DMF_BUF_LAUNCH(float, 64, 128); break;
+        default: DMF_BUF_LAUNCH(float, 64, 64); break;
+      }
+    }
+  } else if (a.in_ss == nullptr) {
+    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
     else DMF_CONV_LAUNCH(float, false, -1);
   } else {
     DMF_CHECK_ARG(a.x2 == nullptr, "%s: input affine needs a single source", what);
@@ -621,6 +683,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
         DMF_CHECK_ARG(false, "%s: unsupported input activation %d", what, a.act_in);
     }
   }
+#undef DMF_BUF_LAUNCH
 #undef DMF_CONV_LAUNCH
   DMF_LAUNCH_CHECK(what);
   return 0;
@@ -660,6 +723,17 @@ __global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, 
 using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
+
+// rows of the BN partial-statistics slab a forward launch of this shape writes
+extern "C" int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2,
+                                         int Cout, int KH, int KW, int Ho, int Wo, int has_in_affine) {
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = Cin + Cin2; a.ldx = ldx; a.C1 = Cin; a.ldx2 = ldx2;
+  a.x2 = Cin2 > 0 ? (const void*)16 : nullptr;
+  a.in_ss = has_in_affine ? (const float*)16 : nullptr;
+  a.Nout = Cout; a.KH = KH; a.KW = KW; a.Ktot = KH * KW * a.C; a.M = N * Ho * Wo;
+  return cdiv(a.M, conv_plan(dtype, false, a).bm);
+}
 
 static int conv_fwd_common(ConvArgs& a, int dtype, const void* x, int N, int H, int W, int Cin, int ldx,
                            const void* x2, int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride,

@@ -488,6 +488,86 @@ __global__ void k_combine_bwd_low(const T* __restrict__ dy, int lddy, int B, int
   }
 }
 
+// 8-channel vector forms (C, strides multiples of 8, 16-B aligned)
+// dg[n][0..1]: block of 1024 threads per sample, 16-B loads
+template <typename T>
+__global__ void __launch_bounds__(1024) k_combine_bwd_gate8(const T* __restrict__ dy, int lddy,
+                                                            const T* __restrict__ a, const T* __restrict__ b, int ldm,
+                                                            int HW, int C, float* __restrict__ dg) {
+  __shared__ float red[16];
+  const int n = blockIdx.x;
+  const int CV = C >> 3;
+  float s0 = 0.f, s1 = 0.f;
+  const long long base = (long long)n * HW;
+  for (long long t = threadIdx.x; t < (long long)HW * CV; t += blockDim.x) {
+    const long long pix = base + t / CV;
+    const int c = (int)(t % CV) * 8;
+    float d[8], va[8], vb[8];
+    ld8(dy + pix * lddy + c, d);
+    ld8(a + pix * ldm + c, va);
+    ld8(b + pix * ldm + c, vb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0 = fmaf(d[j], va[j], s0);
+      s1 = fmaf(d[j], vb[j], s1);
+    }
+  }
+  s0 = block_sum(s0, red);
+  s1 = block_sum(s1, red);
+  if (threadIdx.x == 0) {
+    dg[2 * n] = s0;
+    dg[2 * n + 1] = s1;
+  }
+}
+
+// dlow[n][i][j][c..c+8]: loop only over the output rows/columns whose
+// bilinear source interval touches (i, j)
+template <typename T>
+__global__ void k_combine_bwd_low8(const T* __restrict__ dy, int lddy, int B, int H, int W, int C, int Hp, int Wp,
+                                   float* __restrict__ dlow) {
+  const int CV = C >> 3;
+  const long long total = (long long)B * Hp * Wp * CV;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    long long r = t / CV;
+    const int j = (int)(r % Wp); r /= Wp;
+    const int i = (int)(r % Hp);
+    const int n = (int)(r / Hp);
+    const int hl = max(0, (int)floorf(((float)i - 0.5f) * H / Hp - 0.5f) - 1);
+    const int hh = min(H, (int)ceilf(((float)i + 1.5f) * H / Hp - 0.5f) + 2);
+    const int wl = max(0, (int)floorf(((float)j - 0.5f) * W / Wp - 0.5f) - 1);
+    const int wh = min(W, (int)ceilf(((float)j + 1.5f) * W / Wp - 0.5f) + 2);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int h = hl; h < hh; ++h) {
+      int h0, h1;
+      float lh;
+      lin_w(h, Hp, H, h0, h1, lh);
+      float wgh = 0.f;
+      if (h0 == i) wgh += 1.f - lh;
+      if (h1 == i) wgh += lh;
+      if (wgh == 0.f) continue;
+      for (int w = wl; w < wh; ++w) {
+        int w0, w1;
+        float lw;
+        lin_w(w, Wp, W, w0, w1, lw);
+        float ww = 0.f;
+        if (w0 == j) ww += 1.f - lw;
+        if (w1 == j) ww += lw;
+        if (ww == 0.f) continue;
+        float v[8];
+        ld8(dy + ((size_t)(n * H + h) * W + w) * lddy + cv * 8, v);
+        const float wt = wgh * ww;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(wt, v[k], acc[k]);
+      }
+    }
+    float* o = dlow + (size_t)t * 8;
+    *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
 // ---------------------------------------------------------------- gating
 // x = [pv_dwi (C), pv_dce (C), conf_dwi, conf_dce]; g = softmax(W x + b), 2 outputs
 __global__ void k_gate_fwd(const float* __restrict__ pa, const float* __restrict__ pb, const float* __restrict__ ca,
@@ -727,7 +807,29 @@ extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const
   DMF_CHECK_ARG(dy && p_dwi && p_dce && gates, "dmf_fusion_combine_bwd: bad args");
   const long long total = (long long)B * H * W * C;
   hipStream_t st_ = (hipStream_t)stream;
-  if (dtype == DMF_BF16) {
+  const bool v8 = C % 8 == 0 && lddy % 8 == 0 && ld % 8 == 0 && ((uintptr_t)dy % 16) == 0 &&
+                  ((uintptr_t)p_dwi % 16) == 0 && ((uintptr_t)p_dce % 16) == 0;
+  if (v8 && dtype == DMF_BF16) {
+    if (dp_dwi || dp_dce)
+      hipLaunchKernelGGL(k_combine_bwd_maps<bf16_t>, dim3(gsz(total)), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
+                         gates, H * W, C, total, (bf16_t*)dp_dwi, (bf16_t*)dp_dce, ldd);
+    if (dgates)
+      hipLaunchKernelGGL(k_combine_bwd_gate8<bf16_t>, dim3(B), dim3(1024), 0, st_, (const bf16_t*)dy, lddy,
+                         (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, H * W, C, dgates);
+    if (dlowres)
+      hipLaunchKernelGGL(k_combine_bwd_low8<bf16_t>, dim3(gsz((long long)B * Hp * Wp * C / 8)), dim3(256), 0, st_,
+                         (const bf16_t*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
+  } else if (v8) {
+    if (dp_dwi || dp_dce)
+      hipLaunchKernelGGL(k_combine_bwd_maps<float>, dim3(gsz(total)), dim3(256), 0, st_, (const float*)dy, lddy, gates,
+                         H * W, C, total, (float*)dp_dwi, (float*)dp_dce, ldd);
+    if (dgates)
+      hipLaunchKernelGGL(k_combine_bwd_gate8<float>, dim3(B), dim3(1024), 0, st_, (const float*)dy, lddy,
+                         (const float*)p_dwi, (const float*)p_dce, ld, H * W, C, dgates);
+    if (dlowres)
+      hipLaunchKernelGGL(k_combine_bwd_low8<float>, dim3(gsz((long long)B * Hp * Wp * C / 8)), dim3(256), 0, st_,
+                         (const float*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
+  } else if (dtype == DMF_BF16) {
     if (dp_dwi || dp_dce)
       hipLaunchKernelGGL(k_combine_bwd_maps<bf16_t>, dim3(gsz(total)), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
                          gates, H * W, C, total, (bf16_t*)dp_dwi, (bf16_t*)dp_dce, ldd);

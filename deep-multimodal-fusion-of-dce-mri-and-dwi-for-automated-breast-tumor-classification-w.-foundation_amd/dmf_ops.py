@@ -234,7 +234,8 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     else:
         wk = caches[0].get(weight, x.dtype, cx + cx2, 0)
         if want_stats:
-            tiles = (n * ho * wo + 127) // 128
+            tiles = N.load().dmf_conv2d_fwd_stat_tiles(dtc, n, h, w, cx, ldx, cx2, ldx2, co, kh, kw, ho, wo,
+                                                       1 if in_ss is not None else 0)
             partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
         e0 = _probe_begin()
         N.call("dmf_conv2d_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
@@ -263,9 +264,11 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
     training mode on the MFMA path the statistics and the finalize run inside
     the conv launch (dmf_conv2d_fwd_bn)."""
     training = bn.training or bn.running_mean is None
-    n_, _, h_, w_, _ = nhwc(x)
+    n_, cx_, h_, w_, ldx_ = nhwc(x)
+    cx2_, ldx2_ = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
     ho_, wo_ = g.out_hw(h_, w_)
-    mtiles = (n_ * ho_ * wo_ + 127) // 128
+    mtiles = N.load().dmf_conv2d_fwd_stat_tiles(dt(x), n_, h_, w_, cx_, ldx_, cx2_, ldx2_, w.shape[0], w.shape[2],
+                                                w.shape[3], ho_, wo_, 1 if in_ss is not None else 0)
     if not (training and _is_mfma_conv(w, g) and mtiles <= FUSED_BN_MAX_MTILES):
         y, part = _conv_forward_raw(x, w, b, g, caches, training, "none", x2=x2, in_ss=in_ss, in_act=in_act)
         n, c, ho, wo, _ = nhwc(y)

@@ -53,6 +53,10 @@ int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* str
  * FeatureDownAlign (:386-390), FusionModel.proj_in_* / reduce (:857-862,
  * :788-792), PatchEmbed.proj (transformer_model.py:17-22). */
 int dmf_conv_m_tile(void);
+/* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
+ * for this shape (the launcher picks 64- or 128-row tiles per shape) */
+int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2, int Cout, int KH,
+                              int KW, int Ho, int Wo, int has_in_affine);
 /* x2 (nullable): second input concatenated along channels after the Cin
  * channels of x (BackboneAdapter chain [C4, C5], model_module.py:471) */
 /* in_scale_shift (nullable, single source only): the producer's batch-norm

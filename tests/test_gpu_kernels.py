@@ -32,6 +32,9 @@ CONV_CASES = [
     (2, 16, 32, 32, 64, 7, 2, 3, 1),
     (2, 256, 8, 8, 512, 1, 2, 0, 1),
     (3, 8, 9, 9, 8, 3, 1, 1, 1),
+    # large enough for the 128-row tiles of the buffer-load forward kernel
+    (64, 64, 32, 32, 128, 3, 1, 1, 1),
+    (64, 128, 32, 32, 64, 1, 1, 0, 1),
 ]
 
 

@@ -168,7 +168,7 @@ def test_encoder_backward_parity_all_trainable():
     dozen training-mode BNs) the backbone grads are ill-conditioned: the fp32
     CPU oracle itself is 2-5 % away from a float64 evaluation. So the bar is
     relative to float64 truth: the HIP grads must be no further from it than
-    3x the fp32 oracle's own error (+1e-3), in relative L2 norm per tensor."""
+    3x the fp32 oracle's own error (+5e-3), in relative L2 norm per tensor."""
     P = PR.small_parameters(dropout=0.0)
     enc, ref, _ = build_pair(P, "dwi", 14, 41)
     ref64 = copy.deepcopy(ref).double()
