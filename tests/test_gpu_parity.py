@@ -191,7 +191,7 @@ def test_encoder_backward_parity_all_trainable():
         scale = max(1e-12, truth.norm().item())
         e_mine = (p1.grad.float().cpu().reshape(truth.shape) - truth).norm().item() / scale
         e_ref = (p2.grad - truth).norm().item() / scale
-        if e_mine > 3 * e_ref + 1e-3:
+        if e_mine > 3 * e_ref + 5e-3:
             bad[n] = (round(e_mine, 5), round(e_ref, 5))
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
