@@ -438,6 +438,226 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
   conv_epilogue<T, BM, BN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
+// ---------------------------------------- forward, persistent buffer-load form
+// 128x128 tiles, gridDim = resident blocks; each block walks its tiles as ONE
+// flat stream of K-steps, so the two-tile register pipeline runs across tile
+// boundaries: the loads of the next tile's first K-steps are in flight while
+// the finished tile's epilogue (bias/act or BN partials, C staging in row
+// passes through the free LDS stage, 16-B stores) runs. Used when a launch
+// needs more than one round of blocks; no fused BN finalize (tickets).
+template <typename T>
+__device__ __forceinline__ void conv_epilogue_stage(const ConvArgs& a, f32x4_t (&acc)[4][4], char* st, int tid,
+                                                    int mt, int m0, int n0) {
+  constexpr int ES = sizeof(T);
+  constexpr int EPC = 16 / ES;
+  constexpr int RP = ES == 2 ? 64 : 32;  // rows per staging pass (fits a 32 KB stage)
+  constexpr int CST = 128 + 16 / ES;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const bool stats = a.partials != nullptr;
+  float* red = (float*)st;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + fr;
+    const float bsv = (a.bias != nullptr && col < a.Nout) ? a.bias[col] : 0.f;
+    float s = 0.f, ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
+        float v = acc[i][j][r] + bsv;
+        if (stats && row < a.M) { s += v; ss += v * v; }
+        if (!stats) v = apply_act_rt(a.act, v);
+        acc[i][j][r] = v;
+      }
+    }
+    if (stats) {
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
+      if (fg == 0) {
+        const int lc = wn * 64 + j * 16 + fr;
+        red[(wm * 128 + lc) * 2 + 0] = s;
+        red[(wm * 128 + lc) * 2 + 1] = ss;
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    if (tid < 128) {
+      const int col = n0 + tid;
+      if (col < a.Nout) {
+        float2 v;
+        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
+        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
+        *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+      }
+    }
+  }
+  T* Cs = (T*)st;
+  T* Y = (T*)a.y;
+#pragma unroll
+  for (int pass = 0; pass < 128 / RP; ++pass) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((wm * 64 + i * 16) / RP != pass) continue;  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * 64 + i * 16 + fg * 4 + r - pass * RP;
+          const int col = wn * 64 + j * 16 + fr;
+          Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = 128 / EPC;
+#pragma unroll
+    for (int idx = tid; idx < RP * CPR; idx += CTHREADS) {
+      const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
+      const int m = m0 + pass * RP + row, n = n0 + chn * EPC;
+      if (m < a.M && n < a.Nout) *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
+    }
+  }
+}
+
+template <typename T, bool PADCHK, bool DUAL>
+__global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_pers(ConvArgs a) {
+  constexpr int ES = sizeof(T);
+  constexpr int EPC = 16 / ES;
+  constexpr int BK = 8 * EPC;
+  constexpr int SB = 256 * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int q = tid & 7, rbase = tid >> 3;
+  const int nk = a.Ktot / BK;
+  // tiles of this block: XCD x = blockIdx % 8 owns a contiguous range of logical tiles
+  const int T_ = a.mtiles * a.ntiles, G = gridDim.x;
+  const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int gx = G / 8 + (x < G % 8 ? 1 : 0);  // blocks on this XCD
+  const int r0 = (int)((long long)T_ * x / 8), r1 = (int)((long long)T_ * (x + 1) / 8);
+  const int cnt = jb < (r1 - r0) ? (r1 - r0 - jb + gx - 1) / gx : 0;
+  if (cnt == 0) return;
+  const int S = cnt * nk;  // flat K-steps of this block
+
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.x), 0, (int)((long long)a.N * a.H * a.W * a.ldx * ES), BUF_FLAGS);
+  const __amdgpu_buffer_rsrc_t rx2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(DUAL ? a.x2 : a.x), 0, (int)((long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES),
+      BUF_FLAGS);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.w), 0, (int)((long long)a.Nout * a.Ktot * ES), BUF_FLAGS);
+
+  // loader state: row metadata of the tile being loaded
+  int ltile = -1;
+  int h0[4], w0[4], b1[4], b2[4];
+  bool mok[4];
+  unsigned vb[4];
+  auto set_tile = [&](int li) {
+    const int lin = r0 + jb + li * gx;
+    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+    const int m0 = mt * 128, n0 = nt * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + rbase + 32 * i;
+      mok[i] = m < a.M;
+      const int mm = mok[i] ? m : 0;
+      const int hw = a.Ho * a.Wo;
+      const int n = mm / hw, rem = mm - (mm / hw) * hw;
+      const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+      h0[i] = ho * a.stride - a.pad;
+      w0[i] = wo * a.stride - a.pad;
+      const int pix = (n * a.H + h0[i]) * a.W + w0[i];
+      b1[i] = pix * a.ldx + q * EPC;
+      b2[i] = DUAL ? pix * a.ldx2 + q * EPC : 0;
+      const int nn = n0 + rbase + 32 * i;
+      vb[i] = nn < a.Nout ? (unsigned)((nn * a.Ktot + q * EPC) * ES) : BUF_OOB;
+    }
+  };
+  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
+  auto gload = [&](int sidx, uint4 (&ra)[4], uint4 (&rb)[4]) {
+    const int li = sidx / nk, kt = sidx - (sidx / nk) * nk;  // uniform
+    if (li != ltile) {
+      set_tile(li);
+      ltile = li;
+    }
+    const int k0 = kt * BK;
+    const int tap = k0 / a.C;
+    const int c0 = k0 - tap * a.C;
+    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
+    const int rd = r * a.dil, sd = s * a.dil;
+    if (DUAL && c0 >= a.C1) {
+      const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b2[i] + toff) * ES) : BUF_OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx2, vo, 0, 0));
+      }
+    } else {
+      const int toff = (rd * a.W + sd) * a.ldx + c0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b1[i] + toff) * ES) : BUF_OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, vb[i], k0 * ES, 0));
+  };
+  auto lds_store = [&](char* base, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + 32 * i;
+      *(uint4*)(base + row * 128 + ((q ^ (row & 7)) << 4)) = ra[i];
+      *(uint4*)(base + 128 * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
+    }
+  };
+  f32x4_t acc[4][4];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  // after computing flat step sidx from stage `st`: a finished tile's epilogue
+  // runs in that stage (free once every wave is past the next barrier)
+  auto finish = [&](int sidx, char* st) {
+    if (sidx - (sidx / nk) * nk != nk - 1) return;  // uniform
+    const int lin = r0 + jb + (sidx / nk) * gx;
+    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+    conv_epilogue_stage<T>(a, acc, st, tid, mt, mt * 128, nt * 128);
+    zero_acc();
+    __syncthreads();
+  };
+
+  zero_acc();
+  gload(0, ra0, rb0);
+  gload(min(1, S - 1), ra1, rb1);
+  lds_store(smem, ra0, rb0);
+  __syncthreads();
+  for (int sidx = 0; sidx < S; sidx += 2) {
+    gload(min(sidx + 2, S - 1), ra0, rb0);
+    conv_mma<T>(smem, acc, wm, wn, lane);
+    lds_store(smem + SB, ra1, rb1);
+    __syncthreads();
+    finish(sidx, smem);
+    if (sidx + 1 >= S) break;
+    gload(min(sidx + 3, S - 1), ra1, rb1);
+    conv_mma<T>(smem + SB, acc, wm, wn, lane);
+    lds_store(smem, ra0, rb0);
+    __syncthreads();
+    finish(sidx + 1, smem + SB);
+  }
+}
+
 // INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
 // FASTC: C (and the concat split C1) are multiples of BK, so every K-step
 // lies inside one filter tap: the tap/channel decode is block-uniform
@@ -577,6 +797,13 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
 }
 
 #include <cstdlib>
+static bool pers_disabled() {
+  static const int v = [] {
+    const char* e = std::getenv("DMF_CONV_NOPERS");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
+}
 static bool fast_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_LEGACY");
@@ -648,7 +875,31 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const bool dual = a.x2 != nullptr;
     const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
-    if (dtype == DMF_BF16) {
+    int ncu = 256;
+    {
+      static int cached = 0;
+      if (!cached) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cached <= 0) cached = 256;
+      }
+      ncu = cached;
+    }
+    const long long resident = 2LL * ncu;
+    // persistent form: measured to pay for 1x1 (plain) convs only
+    if (cfg == 3 && plain && !dual && a.tickets == nullptr && nblk > resident && !pers_disabled()) {
+      const dim3 gp((unsigned)resident);
+#define DMF_PERS_LAUNCH(TT)                                                                         \
+  do {                                                                                              \
+    if (dual) hipLaunchKernelGGL((k_conv_fwd_pers<TT, true, true>), gp, b, lds_total, st, a);       \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_pers<TT, false, false>), gp, b, lds_total, st, a); \
+    else hipLaunchKernelGGL((k_conv_fwd_pers<TT, true, false>), gp, b, lds_total, st, a);           \
+  } while (0)
+      if (dtype == DMF_BF16) DMF_PERS_LAUNCH(bf16_t);
+      else DMF_PERS_LAUNCH(float);
+#undef DMF_PERS_LAUNCH
+    } else if (dtype == DMF_BF16) {
       switch (cfg) {
         case 3: DMF_BUF_LAUNCH(bf16_t, 128, 128); break;
         case 2: DMF_BUF_LAUNCH(bf16_t, 128, 64); break;

@@ -35,6 +35,9 @@ CONV_CASES = [
     # large enough for the 128-row tiles of the buffer-load forward kernel
     (64, 64, 32, 32, 128, 3, 1, 1, 1),
     (64, 128, 32, 32, 64, 1, 1, 0, 1),
+    # more blocks than resident slots: the persistent forward kernel
+    (64, 128, 32, 32, 256, 1, 1, 0, 1),
+    (48, 64, 32, 32, 256, 3, 1, 1, 1),
 ]
 
 
