@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 ROOT=$(pwd)
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -rf > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $OUT/tests.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $OUT/tests.log; exit 1; }
   tail -3 $OUT/tests.log
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
