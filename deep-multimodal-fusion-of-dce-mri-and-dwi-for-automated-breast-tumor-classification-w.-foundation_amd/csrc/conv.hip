@@ -797,10 +797,12 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
 }
 
 #include <cstdlib>
+// persistent 1x1 form: opt-in (DMF_CONV_PERS=1); measured slower than the
+// one-tile-per-block launch on the hot path's shapes (tools/conv_sweep.sh)
 static bool pers_disabled() {
   static const int v = [] {
-    const char* e = std::getenv("DMF_CONV_NOPERS");
-    return e && e[0] == '1' ? 1 : 0;
+    const char* e = std::getenv("DMF_CONV_PERS");
+    return e && e[0] == '1' ? 0 : 1;
   }();
   return v != 0;
 }

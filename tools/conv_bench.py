@@ -47,10 +47,16 @@ def run_shape(shape, reps, stats, dtype=torch.bfloat16):
         for _ in range(3):
             O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
         torch.cuda.synchronize()
+        # replay R launches from a hipGraph: GPU time only (no Python launch overhead)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(reps):
+                O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
+        graph.replay()
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(reps):
-            O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
+        graph.replay()
         e1.record()
         torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
@@ -64,11 +70,18 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--nostats", action="store_true")
+    ap.add_argument("--from", dest="src", default="", help="bench.py DMF_CONV_DUMP jsonl: every distinct shape, with counts")
     a = ap.parse_args()
-    sel = [int(i) for i in a.only.split(",")] if a.only else range(len(SHAPES))
+    shapes = SHAPES
+    if a.src:
+        import collections
+        import json
+        cnt = collections.Counter(tuple(json.loads(l)["shape"]) for l in open(a.src))
+        shapes = sorted(cnt.items(), key=lambda kv: -kv[1] * kv[0][0] * kv[0][1] * kv[0][2] * kv[0][3] * kv[0][4] * kv[0][5] ** 2 / kv[0][6] ** 2)
+    sel = [int(i) for i in a.only.split(",")] if a.only else range(len(shapes))
     tot_ms = 0.0
     for i in sel:
-        shape, cnt = SHAPES[i]
+        shape, cnt = shapes[i]
         ms, tf = run_shape(shape, a.reps, not a.nostats)
         tot_ms += ms * cnt
         print(f"{i:2d} {str(shape):38s} x{cnt:2d} {ms * 1e3:8.1f} us {tf:7.1f} TF/s", flush=True)
