@@ -99,6 +99,10 @@ def roofline_probe(trainer, batch, dtype):
     recs = []
     O.PROBE["conv_fwd"] = recs
     torch.cuda.synchronize()
+    # park the GPU behind a spin kernel while the host enqueues the eager step,
+    # so the per-launch events bracket back-to-back GPU execution (no host gaps)
+    if hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(int(os.environ.get("DMF_PROBE_SLEEP_CYCLES", 1_000_000_000)))
     trainer.eager_step(batch)
     torch.cuda.synchronize()
     O.PROBE["conv_fwd"] = None
@@ -117,20 +121,38 @@ def roofline_probe(trainer, batch, dtype):
                                     "tflops": round(r[2] / (t * 1e-3) / 1e12, 1)}) + "\n")
     peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
     achieved = flops / (ms * 1e-3) / 1e12
+    traffic = pmc_traffic()
     return {
-        "kernel": "k_conv_igemm<%s, false>" % ("unsigned short" if dtype == torch.bfloat16 else "float"),
+        "kernel": "conv2d forward (k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm, %s)" %
+                  ("bf16" if dtype == torch.bfloat16 else "f32"),
         "bound": "mfma",
         "achieved": round(achieved, 2),
         "peak": peak,
         "unit": "TFLOP/s",
         "frac": round(achieved / peak, 4),
-        "traffic": None,
+        "traffic": traffic["traffic_mb_per_launch"] if traffic else None,
+        "traffic_unit": "MB per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, " +
+                        (traffic["source"] if traffic else "no PMC summary") + ")",
         "launches_per_step": n,
         "avg_launch_us": round(ms * 1e3 / n, 2),
         "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
         "algorithmic_mb_per_launch": round(byt / n / 1e6, 2),
         "hbm_gbs_per_launch_avg": round(byt / (ms * 1e-3) / 1e9, 1),
     }
+
+
+def pmc_traffic():
+    """HBM bytes per conv-forward launch from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from two
+    rocprofv3 --pmc passes of this bench on an MI355X)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(files[-1], ROOT)
+    return d
 
 
 def cpu_baseline(args, P_fn):

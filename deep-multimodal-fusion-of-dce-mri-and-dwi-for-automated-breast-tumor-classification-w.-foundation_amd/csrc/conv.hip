@@ -22,6 +22,8 @@
 // partials[mtile][co][2], reduced deterministically by dmf_bn_finalize), then
 // an LDS-staged, 16-B coalesced store with an output channel stride (so
 // producers can write straight into a channel slice of a concat buffer).
+#include <algorithm>
+
 #include "dmf_common.h"
 #include "../../include/dmf_hip.h"
 
@@ -120,10 +122,10 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
 
 // one LDS stage of A/B fragments -> (BM/32)x(BN/32) MFMA fragments per wave
 // (2x2 waves, each a (BM/2)x(BN/2) sub-tile)
-template <typename T, int BM = CBM, int BN = CBN>
-__device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / 32][BN / 32], int wm, int wn,
-                                         int lane) {
-  constexpr int FM = BM / 32, FN = BN / 32;
+template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2>
+__device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16 * WMW)][BN / (16 * WNW)], int wm,
+                                         int wn, int lane) {
+  constexpr int FM = BM / (16 * WMW), FN = BN / (16 * WNW);
   const char* Bs = As + BM * 128;
   const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
@@ -132,12 +134,12 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / 32]
     uint4 av[FM], bv[FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int row = wm * (BM / 2) + i * 16 + fr;
+      const int row = wm * (BM / WMW) + i * 16 + fr;
       av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int col = wn * (BN / 2) + j * 16 + fr;
+      const int col = wn * (BN / WNW) + j * 16 + fr;
       bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
     }
     if constexpr (sizeof(T) == 2) {
@@ -163,27 +165,28 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / 32]
 }
 
 // bias / activation or BN partial statistics, LDS-staged 16-B stores
-template <typename T, int BM = CBM, int BN = CBN>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / 32][BN / 32], char* smem,
-                                              int tid, int mt, int nt, int m0, int n0) {
-  constexpr int FM = BM / 32, FN = BN / 32;
+template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / (16 * WMW)][BN / (16 * WNW)],
+                                              char* smem, int tid, int mt, int nt, int m0, int n0) {
+  constexpr int FM = BM / (16 * WMW), FN = BN / (16 * WNW);
+  constexpr int NT = 64 * WMW * WNW;
   constexpr int EPC = 16 / sizeof(T);
   const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNW, wn = wid % WNW;
   const int fr = lane & 15, fg = lane >> 4;
   const bool has_bias = a.bias != nullptr;
   const bool stats = a.partials != nullptr;
   float* red = (float*)smem;  // [2 wm][BN cols][2] floats
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 16 + fr;
+    const int col = n0 + wn * (BN / WNW) + j * 16 + fr;
     const float bsv = (has_bias && col < a.Nout) ? a.bias[col] : 0.f;
     float s = 0.f, ss = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 16 + fg * 4 + r;
+        const int row = m0 + wm * (BM / WMW) + i * 16 + fg * 4 + r;
         float v = acc[i][j][r] + bsv;
         if (stats && row < a.M) { s += v; ss += v * v; }
         if (!stats) v = apply_act_rt(a.act, v);
@@ -194,7 +197,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
       if (fg == 0) {
-        const int lc = wn * (BN / 2) + j * 16 + fr;
+        const int lc = wn * (BN / WNW) + j * 16 + fr;
         red[(wm * BN + lc) * 2 + 0] = s;
         red[(wm * BN + lc) * 2 + 1] = ss;
       }
@@ -205,9 +208,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     if (tid < BN) {
       const int col = n0 + tid;
       if (col < a.Nout) {
-        float2 v;
-        v.x = red[tid * 2 + 0] + red[(BN + tid) * 2 + 0];
-        v.y = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
+        float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < WMW; ++q) {
+          v.x += red[(q * BN + tid) * 2 + 0];
+          v.y += red[(q * BN + tid) * 2 + 1];
+        }
         float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
         if (a.tickets) {
           // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
@@ -230,8 +236,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / 2) + i * 16 + fg * 4 + r;
-        const int col = wn * (BN / 2) + j * 16 + fr;
+        const int row = wm * (BM / WMW) + i * 16 + fg * 4 + r;
+        const int col = wn * (BN / WNW) + j * 16 + fr;
         Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
       }
   __syncthreads();
@@ -249,7 +255,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   }
   T* Y = (T*)a.y;
   constexpr int CPR = BN / EPC;  // chunks per row
-  for (int idx = tid; idx < BM * CPR; idx += CTHREADS) {
+  for (int idx = tid; idx < BM * CPR; idx += NT) {
     const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
     const int m = m0 + row, n = n0 + chn * EPC;
     if (m < a.M && n < a.Nout) {
@@ -258,7 +264,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   }
   if (a.tickets && *(const int*)xtra) {
     // last block of this column tile: reduce the slab (sc1 loads, fixed order, double)
-    constexpr int NP = CTHREADS / BN;  // tile-row lanes per column
+    constexpr int NP = NT / BN;  // tile-row lanes per column
     const int cl = tid % BN, part = tid / BN;
     const int col = n0 + cl;
     double s = 0.0, q = 0.0;
@@ -353,12 +359,17 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
 
   // two register sets: tile kt+1 is in flight while tile kt+2 is issued
   uint4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
+  // K cursor (filter row, column, channel): gload() runs in K order (the
+  // clamped tail re-issues only feed registers that are never stored)
+  int cr = 0, cs = 0, cc = 0;
   auto gload = [&](int kt, uint4 (&ra)[RA], uint4 (&rb)[RB]) {
     const int k0 = kt * BK;  // uniform
-    const int tap = k0 / a.C;
-    int c0 = k0 - tap * a.C;
-    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
-    const int rd = r * a.dil, sd = s * a.dil;
+    const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
+    cc += BK;
+    if (cc == a.C) {
+      cc = 0;
+      if (++cs == a.KW) { cs = 0; ++cr; }
+    }
     // block-uniform source choice as a branch, so each path keeps its descriptor in SGPRs
     if (DUAL && c0 >= a.C1) {
       const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
@@ -436,6 +447,145 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
     __syncthreads();
   }
   conv_epilogue<T, BM, BN>(a, acc, smem, tid, mt, nt, m0, n0);
+}
+
+// ------------------------------------------- forward, LDS-DMA wide form (bf16)
+// 256x128 block tile, 8 waves (4x2) of 64x64 each (4x4 MFMA fragments, 32
+// v_mfma_f32_16x16x32_bf16 per wave per K-step, two waves per SIMD), BK = 64,
+// one workgroup per CU. A and B tiles go global -> LDS directly (buffer_load_dwordx4 ... lds:
+// no VGPR staging, no ds_write pass) into a 3-deep ring of [256+128 rows][128
+// B] stages, two tiles in flight across the single raw s_barrier of each
+// K-step (counted vmcnt, never 0 in the loop). The LDS-DMA writes each wave-
+// instruction's 64 x 16 B linearly (8 rows x 128 B), so the conv_mma XOR
+// swizzle (chunk ^ row&7) is applied on the SOURCE side: lane l fetches
+// logical chunk (l&7) ^ (l>>3) of its row. Zero padding and the M tail are
+// buffer range-check zeros (offset past the buffer). Requires C (and C1) %
+// 64 == 0, Nout % 128 == 0, no input prologue.
+constexpr int WBM = 256, WBN = 128, WSTAGE = (WBM + WBN) * 128, WNSTAGE = 3;
+constexpr int WWM = 4, WWN = 2, WTHREADS = 64 * WWM * WWN;  // 8 waves of 64x64: two per SIMD
+constexpr int WLDS = WNSTAGE * WSTAGE;  // 147456 B: also holds the C staging tile
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i_t buf_rsrc(const void* p, long long bytes) {
+  const unsigned long long u = (unsigned long long)p;
+  return v4i_t{(int)(unsigned)u, (int)(unsigned)(u >> 32), (int)bytes, BUF_FLAGS};
+}
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff(+soff) to LDS
+// [lds, lds + 1 KiB). Inline asm so the compiler neither tracks it (it would
+// drain vmcnt(0) before every ds_read it cannot disambiguate) nor reorders it
+// across LDS accesses; m0 is saved and restored.
+__device__ __forceinline__ void dma16(v4i_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+               : "memory");
+}
+
+template <bool PADCHK, bool DUAL>
+__global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
+  constexpr int ES = 2, EPC = 8, BK = 64;
+  constexpr int NW = WTHREADS / 64;
+  constexpr int NA = WBM / 8 / NW;  // A row-groups (8 rows) per wave: 4
+  constexpr int NB = WBN / 8 / NW;  // B row-groups per wave: 2
+  static_assert(NA + NB == 6, "vmcnt counts below assume 6 DMA per wave per K-step");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WWN, wn = wid % WWN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lin / a.ntiles, nt = lin % a.ntiles;
+  const int m0 = mt * WBM, n0 = nt * WBN;
+  const int lr = lane >> 3;        // row within an 8-row group
+  const int lc = (lane & 7) ^ lr;  // logical 16-B chunk this lane fetches (source-side swizzle)
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  const v4i_t rx = buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * ES);
+  const v4i_t rx2 = buf_rsrc(DUAL ? a.x2 : a.x, (long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES);
+  const v4i_t rw = buf_rsrc(a.w, (long long)a.Nout * a.Ktot * ES);
+
+  // this lane's A rows: wid*(NA*8) + i*8 + lr
+  int h0[NA], w0[NA], b1[NA], b2[NA];
+  bool mok[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + wid * (NA * 8) + i * 8 + lr;
+    mok[i] = m < a.M;
+    const int mm = mok[i] ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    const int n = mm / hw, rem = mm - (mm / hw) * hw;
+    const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+    h0[i] = ho * a.stride - a.pad;
+    w0[i] = wo * a.stride - a.pad;
+    const int pix = (n * a.H + h0[i]) * a.W + w0[i];
+    b1[i] = pix * a.ldx + lc * EPC;
+    b2[i] = DUAL ? pix * a.ldx2 + lc * EPC : 0;
+  }
+  unsigned vb[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + wid * (NB * 8) + i * 8 + lr;  // Nout % 128 == 0: always in range
+    vb[i] = (unsigned)((n * a.Ktot + lc * EPC) * ES);
+  }
+  const int nk = a.Ktot / BK;
+
+  // K cursor (filter row r, column s, channel c0) advanced without divisions: issue() runs in K order
+  int cr = 0, cs = 0, cc = 0;
+  auto issue = [&](int kt, int stage) {
+    const unsigned As = lds0 + stage * WSTAGE;
+    const unsigned Bs = As + WBM * 128;
+    const int k0 = kt * BK;  // uniform
+    const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
+    cc += BK;
+    if (cc == a.C) {
+      cc = 0;
+      if (++cs == a.KW) { cs = 0; ++cr; }
+    }
+    if (DUAL && c0 >= a.C1) {
+      const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b2[i] + toff) * ES) : BUF_OOB;
+        dma16(rx2, vo, 0, As + (wid * (NA * 8) + i * 8) * 128);
+      }
+    } else {
+      const int toff = (rd * a.W + sd) * a.ldx + c0;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        bool ok = mok[i];
+        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
+        const unsigned vo = ok ? (unsigned)((b1[i] + toff) * ES) : BUF_OOB;
+        dma16(rx, vo, 0, As + (wid * (NA * 8) + i * 8) * 128);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dma16(rw, vb[i], (unsigned)(k0 * ES), Bs + (wid * (NB * 8) + i * 8) * 128);
+  };
+
+  f32x4_t acc[WBM / (16 * WWM)][WBN / (16 * WWN)];
+#pragma unroll
+  for (int i = 0; i < WBM / (16 * WWM); ++i)
+#pragma unroll
+    for (int j = 0; j < WBN / (16 * WWN); ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ring: tile kt lives in stage kt % 3; tiles kt+1 and kt+2 in flight while kt is computed
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire this wave's DMA of tile kt (tile kt+1's 6 may stay in flight); the barrier then
+    // publishes every wave's part of tile kt and orders the refill of stage (kt+2)%3 after
+    // every wave's reads of tile kt-1 (retired by lgkmcnt(0))
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);
+    conv_mma<bf16_t, WBM, WBN, WWM, WWN>(smem + st * WSTAGE, acc, wm, wn, lane);
+    st = st == 2 ? 0 : st + 1;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  conv_epilogue<bf16_t, WBM, WBN, WWM, WWN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
 // ---------------------------------------- forward, persistent buffer-load form
@@ -820,10 +970,18 @@ static bool fast_disabled() {
 // tiles would leave fewer than ~2 blocks per CU.
 struct ConvPlan {
   bool buf;
+  bool wide;  // k_conv_fwd_wide (LDS-DMA, 256x128)
   int bm, bn;
 };
+static bool wide_disabled() {
+  static const int v = [] {
+    const char* e = std::getenv("DMF_CONV_WIDE");
+    return e && e[0] == '0' ? 1 : 0;
+  }();
+  return v != 0;
+}
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, CBM, CBN};
+  ConvPlan p{false, false, CBM, CBN};
   if (dgrad || a.in_ss != nullptr || fast_disabled()) return p;
   const int es = dtype == DMF_BF16 ? 2 : 4;
   const int bk = dtype == DMF_BF16 ? 64 : 32;
@@ -833,6 +991,14 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const long long wbytes = (long long)a.Nout * a.Ktot * es;
   p.buf = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31);
   if (!p.buf) return p;
+  // wide LDS-DMA tile: bf16, whole 128-column tiles, long enough K, >= one block per CU
+  if (dtype == DMF_BF16 && !wide_disabled() && a.Nout % WBN == 0 && a.Ktot >= 512 &&
+      (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= 256) {
+    p.wide = true;
+    p.bm = WBM;
+    p.bn = WBN;
+    return p;
+  }
   p.bn = a.Nout <= 64 ? 64 : 128;
   const long long blocks128 = (long long)cdiv(a.M, 128) * cdiv(a.Nout, p.bn);
   p.bm = blocks128 < 512 ? 64 : 128;
@@ -855,7 +1021,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = dtype == DMF_BF16 ? 2 : 4;
-  const size_t lds_total = conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
+  const size_t lds_total = plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
   const int bk = dtype == DMF_BF16 ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
@@ -873,6 +1039,12 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
+  } else if (plan.wide) {
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const dim3 bw(WTHREADS);
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_wide<true, true>), g, bw, lds_total, st, a);
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_wide<false, false>), g, bw, lds_total, st, a);
+    else hipLaunchKernelGGL((k_conv_fwd_wide<true, false>), g, bw, lds_total, st, a);
   } else if (plan.buf) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const bool dual = a.x2 != nullptr;

@@ -72,6 +72,41 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     assert torch.allclose(cd.bias.grad.cpu(), gy.sum((0, 2, 3)), rtol=rtol, atol=atol * gy.abs().sum((0, 2, 3)).max())
 
 
+# shapes that take the 256x128 LDS-DMA forward kernel (bf16, Cout % 128 == 0,
+# K >= 512, >= 256 blocks): dilated 3x3 with zero padding and an M tail, a
+# plain 1x1, and the neck's channel-concat (two-source) 3x3
+WIDE_CASES = [
+    # (N, Cin, H, W, Cout, k, pad, dil, Cin2)
+    (33, 256, 32, 32, 256, 3, 2, 2, 0),
+    (33, 512, 32, 32, 512, 1, 0, 1, 0),
+    (32, 128, 32, 32, 256, 3, 1, 1, 384),
+]
+
+
+@pytest.mark.parametrize("case", WIDE_CASES)
+def test_conv_wide_forward_and_bn_stats(case):
+    n, ci, h, w, co, k, p, d, ci2 = case
+    torch.manual_seed(5)
+    conv = nn.Conv2d(ci + ci2, co, k, padding=p, dilation=d, bias=False)
+    bn = nn.BatchNorm2d(co)
+    a = torch.randn(n, ci, h, w).bfloat16().float()
+    b = torch.randn(n, ci2, h, w).bfloat16().float() if ci2 else None
+    wq = conv.weight.detach().bfloat16().float()
+    xin = torch.cat([a, b], 1) if ci2 else a
+    with torch.no_grad():
+        raw = F.conv2d(xin, wq, None, 1, p, d)
+        ref = F.relu(bn(raw))
+    cd, bd = copy.deepcopy(conv).to(DEV), nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        y = O.conv_bn_act(_to_dev(a, torch.bfloat16), cd, (O.WeightCache(), O.WeightCache()), bd, "relu",
+                          x2=_to_dev(b, torch.bfloat16) if ci2 else None)
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 3e-2 * ref.abs().max().item(), err
+    # batch statistics (running stats after one momentum-0.1 update), tolerance for bf16 outputs
+    assert torch.allclose(bd.running_mean.cpu(), bn.running_mean, rtol=1e-2, atol=1e-3 * raw.abs().max().item())
+    assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv_dual_source(dtype):
     torch.manual_seed(1)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the conv-forward kernels from two rocprofv3
+--pmc passes (FETCH_SIZE, WRITE_SIZE; KB per dispatch). gfx950 correction
+(MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per 128-B request
+of wide streaming reads -> x2. WRITE_SIZE is exact for 16-B/lane stores.
+
+    python tools/pmc_traffic.py gpurun_out/pmc1 [--match REGEX]
+"""
+import argparse
+import csv
+import json
+import re
+
+
+def load(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--match", default=r"k_conv_fwd_wide|k_conv_fwd_buf|k_conv_fwd_pers|k_conv_igemm<unsigned short, false")
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    fe = load(f"{a.dir}/FETCH_SIZE/run_counter_collection.csv")
+    wr = load(f"{a.dir}/WRITE_SIZE/run_counter_collection.csv")
+    rx = re.compile(a.match)
+    f_k = [v for _, n, v in fe if rx.search(n)]
+    w_k = [v for _, n, v in wr if rx.search(n)]
+    n = min(len(f_k), len(w_k))
+    fetch = 2.0 * sum(f_k[:n]) * 1024 / n
+    write = sum(w_k[:n]) * 1024 / n
+    print(f"launches {n}: fetch {fetch / 1e6:.2f} MB (x2 corrected), write {write / 1e6:.2f} MB, "
+          f"traffic {(fetch + write) / 1e6:.2f} MB per launch")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"kernels": a.match, "launches": n, "fetch_mb_per_launch": round(fetch / 1e6, 2),
+                       "write_mb_per_launch": round(write / 1e6, 2),
+                       "traffic_mb_per_launch": round((fetch + write) / 1e6, 2),
+                       "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is"}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
