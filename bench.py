@@ -92,33 +92,35 @@ def synthetic_batch(B, S, device, seed, cd=14, cc=6):
 
 
 def roofline_probe(trainer, batch, dtype):
-    """Per-launch HIP-event timing of the dominant kernel (implicit-GEMM conv
-    forward) over one eager step, on the stream the kernels run on."""
+    """Average launch duration of the dominant kernel family (implicit-GEMM
+    conv forward): one eager step records every conv-forward C-ABI launch
+    (entry point, arguments, buffers); the recorded launches are then captured
+    into a hipGraph and replayed on the stream they run on, with HIP events
+    around the replay -- GPU time only, no host launch gaps."""
     import dmf_ops as O
 
     recs = []
     O.PROBE["conv_fwd"] = recs
     torch.cuda.synchronize()
-    # park the GPU behind a spin kernel while the host enqueues the eager step,
-    # so the per-launch events bracket back-to-back GPU execution (no host gaps)
-    if hasattr(torch.cuda, "_sleep"):
-        torch.cuda._sleep(int(os.environ.get("DMF_PROBE_SLEEP_CYCLES", 1_000_000_000)))
     trainer.eager_step(batch)
     torch.cuda.synchronize()
     O.PROBE["conv_fwd"] = None
     if not recs:
         return None
-    flops = sum(r[2] for r in recs)
-    byt = sum(r[3] for r in recs)
-    times = [r[0].elapsed_time(r[1]) for r in recs]
-    ms = sum(times)
+    flops = sum(r["flops"] for r in recs)
+    byt = sum(r["bytes"] for r in recs)
     n = len(recs)
+    avg_ms, per = O.probe_replay(recs)
+    ms = avg_ms * n
     dump = os.environ.get("DMF_CONV_DUMP")
     if dump:
         with open(dump, "w") as f:
-            for r, t in zip(recs, times):
-                f.write(json.dumps({"shape": r[4], "ms": round(t, 4), "gflop": round(r[2] / 1e9, 3),
-                                    "tflops": round(r[2] / (t * 1e-3) / 1e12, 1)}) + "\n")
+            for shp, cnt, t in per:
+                fl = next(r["flops"] for r in recs if r["shape"] == shp)
+                for _ in range(cnt):
+                    f.write(json.dumps({"shape": shp, "ms": round(t, 4), "gflop": round(fl / 1e9, 3),
+                                        "tflops": round(fl / (t * 1e-3) / 1e12, 1)}) + "\n")
+    recs.clear()
     peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = pmc_traffic()

@@ -170,25 +170,20 @@ def needs_grad(*ts):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
-def _probe_begin():
+def _conv_launch(fn, args, keep, x, n, h, w, cxt, co, kh, kw, g, ho, wo):
+    """One MFMA conv-forward C-ABI call (``args`` without the trailing stream).
+    With bench.py's probe armed, the call is also recorded -- entry point,
+    arguments, the tensors they point into (kept alive) and the algorithmic
+    flops/bytes -- so the probe can replay the same launches GPU-only."""
+    N.call(fn, *args, _stream())
     probe = PROBE["conv_fwd"]
-    if probe is None:
-        return None
-    e0 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    return e0
-
-
-def _probe_end(e0, x, n, h, w, cxt, co, kh, kw, g, ho, wo):
-    if e0 is None:
-        return
-    e1 = torch.cuda.Event(enable_timing=True)
-    e1.record()
-    es = x.element_size()
-    k_tot = kh * kw * cxt
-    flops = 2.0 * n * ho * wo * co * k_tot
-    byts = es * (n * h * w * cxt + co * k_tot + n * ho * wo * co)
-    PROBE["conv_fwd"].append((e0, e1, flops, byts, (n, h, w, cxt, co, kh, g.stride, g.dil)))
+    if probe is not None:
+        es = x.element_size()
+        k_tot = kh * kw * cxt
+        flops = 2.0 * n * ho * wo * co * k_tot
+        byts = es * (n * h * w * cxt + co * k_tot + n * ho * wo * co)
+        probe.append({"fn": fn, "args": args, "keep": keep, "flops": flops, "bytes": byts,
+                      "shape": (n, h, w, cxt, co, kh, g.stride, g.dil)})
 
 
 def _is_mfma_conv(weight, g):
@@ -237,12 +232,11 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
             tiles = N.load().dmf_conv2d_fwd_stat_tiles(dtc, n, h, w, cx, ldx, cx2, ldx2, co, kh, kw, ho, wo,
                                                        1 if in_ss is not None else 0)
             partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
-        e0 = _probe_begin()
-        N.call("dmf_conv2d_fwd", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
-               g.stride, g.pad,
-               g.dil, _p(bias), y.data_ptr(), ho, wo, ldy, _p(partials), act_c if not want_stats else N.ACT_NONE,
-               _p(in_ss), ACT[in_act], _stream())
-        _probe_end(e0, x, n, h, w, cx + cx2, co, kh, kw, g, ho, wo)
+        _conv_launch("dmf_conv2d_fwd",
+                     (dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw, g.stride,
+                      g.pad, g.dil, _p(bias), y.data_ptr(), ho, wo, ldy, _p(partials),
+                      act_c if not want_stats else N.ACT_NONE, _p(in_ss), ACT[in_act]),
+                     (x, x2, wk, bias, y, partials, in_ss), x, n, h, w, cx + cx2, co, kh, kw, g, ho, wo)
     return y, partials
 
 
@@ -292,14 +286,15 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
     track = bn.track_running_stats and bn.running_mean is not None
     mom = bn.momentum if bn.momentum is not None else 0.1
     wk = caches[0].get(w, x.dtype, cx + cx2, 0)
-    e0 = _probe_begin()
-    N.call("dmf_conv2d_fwd_bn", dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw,
-           g.stride, g.pad, g.dil, _p(b), y.data_ptr(), ho, wo, ldy, _p(in_ss), ACT[in_act], partials.data_ptr(),
-           tickets.data_ptr(), float(m), float(m * unbias_mult) if unbias_mult != 1 else 0.0, _p(bn.weight),
-           _p(bn.bias), _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
-           _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), ss.data_ptr(), save.data_ptr(),
-           _stream())
-    _probe_end(e0, x, n, h, wd, cx + cx2, co, kh, kw, g, ho, wo)
+    _conv_launch("dmf_conv2d_fwd_bn",
+                 (dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw, g.stride,
+                  g.pad, g.dil, _p(b), y.data_ptr(), ho, wo, ldy, _p(in_ss), ACT[in_act], partials.data_ptr(),
+                  tickets.data_ptr(), float(m), float(m * unbias_mult) if unbias_mult != 1 else 0.0, _p(bn.weight),
+                  _p(bn.bias), _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
+                  _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), ss.data_ptr(),
+                  save.data_ptr()),
+                 (x, x2, wk, b, y, in_ss, partials, tickets, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                  bn.num_batches_tracked, ss, save), x, n, h, wd, cx + cx2, co, kh, kw, g, ho, wo)
     return y, ss, save
 
 
@@ -1521,6 +1516,39 @@ def mimic_pairs(feats, npairs=2):
 
 
 # bench.py's roofline probe: when PROBE["conv_fwd"] is a list, every MFMA conv
-# forward launch appends (start_event, end_event, flops, bytes, shape) -- events
-# are recorded on the stream the kernel is launched on.
+# forward launch appends its record (see _conv_launch).
 PROBE = {"conv_fwd": None}
+
+
+def probe_replay(recs, reps=3):
+    """GPU-only average duration (ms) of the recorded conv-forward launches:
+    the same C-ABI calls, same buffers, captured into one hipGraph and
+    replayed, HIP events around the replay on the capture stream. Returns
+    (avg_ms_per_launch, per-shape list of (shape, ms)) -- the per-shape times
+    come from one graph per shape group."""
+    def capture(items):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for r in items:
+                N.call(r["fn"], *r["args"], _stream())
+        return graph
+
+    def timed(graph):
+        graph.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    total = timed(capture(recs))
+    per = []
+    groups = {}
+    for r in recs:
+        groups.setdefault(r["shape"], []).append(r)
+    for shp, items in groups.items():
+        per.append((shp, len(items), timed(capture(items)) / len(items)))
+    return total / len(recs), per
