@@ -199,11 +199,18 @@ def main():
     args = parse()
     rank, local_rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), \
         int(os.environ.get("WORLD_SIZE", 1))
+    # one process per GPU over RCCL ("nccl"). DMF_DIST_BACKEND=gloo with
+    # DMF_BENCH_SHARE_GPU=1 rehearses the multi-rank control flow on a 1-GPU box.
+    dev_idx = local_rank % torch.cuda.device_count() if os.environ.get("DMF_BENCH_SHARE_GPU") == "1" else local_rank
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_idx)
+        backend = os.environ.get("DMF_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", dev_idx)
     import parameters as PR
     from dmf_dp import FusionTrainer
 
@@ -238,7 +245,8 @@ def main():
     loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
     if loss_val is not None and loss_val != loss_val:
         raise RuntimeError("training loss is NaN: the benchmarked step is numerically broken")
-    if not args.no_roofline and rank == 0:
+    if not args.no_roofline:
+        # every rank: the probe's eager step contains the gradient all-reduce
         roof = roofline_probe(trainer, batch, dtype)
 
     vols = args.batch * world * args.steps
