@@ -1054,8 +1054,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
       static int cached = 0;
       if (!cached) {
         int dev = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
         if (cached <= 0) cached = 256;
       }
       ncu = cached;

@@ -29,18 +29,6 @@ __device__ __forceinline__ float act_grad(int act, float z) {
   }
 }
 
-// keep-mask for 4 consecutive elements starting at flat index e (multiple of 4)
-__device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int site, unsigned long long e,
-                                              float p, bool keep[4]) {
-  const unsigned long long seed = rng[0], off = rng[1];
-  uint32_t r[4];
-  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)(e >> 2), (uint32_t)(e >> 34), (uint32_t)site,
-         (uint32_t)off, r);
-  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) keep[i] = r[i] >= thr;
-}
-
 // ---------------------------------------------------------- bn finalize
 // partials [T][C][2] -> mean/invstd, per-channel affine (scale, shift), and
 // running-stat update. Block: 64 channels x 4 tile lanes.

@@ -1,0 +1,257 @@
+"""Token-stream ops of the hybrid TransformerStage (configuration 5) on the
+bf16 MFMA GEMM (csrc/gemm.hip) and the token kernels (csrc/tokens.hip).
+
+Reference: ``code/transformer_model.py`` -- PatchEmbed :7-32 (conv k=s=patch,
+then LayerNorm over tokens), TransformerBlock :68-81 (pre-LN, LayerScale
+gamma, residual), MultiHeadSelfAttention :83-116 (qkv Linear, softmax(q k^T *
+scale), attn_drop, P v, proj, proj_drop), MLP :118-134 (fc1, GELU, drop,
+fc2, drop).
+
+A whole TransformerBlock is ONE autograd node (`_BlockFn`): the forward is 6
+GEMM launches + softmax/dropout + 2 LayerNorms with every bias / GELU /
+dropout / LayerScale / residual fused into a GEMM epilogue, and the backward
+is written out by hand (13 GEMMs, the dropout masks re-drawn from the Philox
+snapshot instead of stored). Residual stream: f32 [B*N, E]; GEMM operands:
+bf16; accumulation and weight grads: f32.
+"""
+from __future__ import annotations
+
+import torch
+
+import dmf_native as N
+import dmf_ops as O
+
+F32, BF16 = N.F32, N.BF16
+
+
+def _s():
+    return N.stream_ptr()
+
+
+def gemm(out, a, b, M, Nn, K, ta=0, tb=0, lda=None, ldb=None, ldc=None, batch=(1, 1), sa=(0, 0), sb=(0, 0),
+         sc=(0, 0), a_off=0, b_off=0, c_off=0, bias=None, act="none", colscale=None, res=None, aux=None, pre=None,
+         dropout_p=0.0, rng=None, site=0, dbias=None, alpha=1.0):
+    """out[z] = epilogue(alpha * op(A[z]) op(B[z])) -- see include/dmf_hip.h dmf_gemm_bf16.
+    Offsets are in elements of the operand's dtype."""
+    N.require_cuda(out, a, b)
+    assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+    esz_c = out.element_size()
+    N.call("dmf_gemm_bf16", F32 if out.dtype == torch.float32 else BF16, int(ta), int(tb), int(M), int(Nn), int(K),
+           float(alpha), a.data_ptr() + 2 * a_off, int(lda), int(sa[0]), int(sa[1]),
+           b.data_ptr() + 2 * b_off, int(ldb), int(sb[0]), int(sb[1]),
+           out.data_ptr() + esz_c * c_off, int(ldc), int(sc[0]), int(sc[1]), int(batch[0]), int(batch[1]),
+           O._p(bias), O.ACT[act], O._p(colscale), O._p(res), int(res.stride(0)) if res is not None else 0,
+           O._p(aux), int(aux.stride(0)) if aux is not None else 0,
+           O._p(pre), int(pre.stride(0)) if pre is not None else 0,
+           float(dropout_p), O._p(rng), int(site), O._p(dbias), _s())
+    return out
+
+
+def cast_bf16(x):
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    N.call("dmf_cast_bf16", x.data_ptr(), x.numel(), y.data_ptr(), _s())
+    return y
+
+
+def cast_f32(x):
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    N.call("dmf_cast_f32", x.data_ptr(), x.numel(), y.data_ptr(), _s())
+    return y
+
+
+def ln_fwd(x2d, gamma, beta, eps, out_dtype):
+    r, e = x2d.shape
+    y = torch.empty((r, e), dtype=out_dtype, device=x2d.device)
+    save = torch.empty(2 * r, dtype=torch.float32, device=x2d.device)
+    N.call("dmf_tok_layernorm_fwd", O.dt(x2d), x2d.data_ptr(), x2d.stride(0), r, e, gamma.data_ptr(),
+           beta.data_ptr(), float(eps), O.dt(y), y.data_ptr(), e, save.data_ptr(), _s())
+    return y, save
+
+
+def ln_bwd(dy, x2d, save, gamma, dres, dgamma, dbeta):
+    r, e = x2d.shape
+    dx = dres if dres is not None else torch.empty((r, e), dtype=torch.float32, device=dy.device)
+    N.call("dmf_tok_layernorm_bwd", dy.data_ptr(), O.dt(x2d), x2d.data_ptr(), x2d.stride(0), save.data_ptr(), r, e,
+           gamma.data_ptr(), O._p(dres), dx.data_ptr(), O._p(dgamma), O._p(dbeta), _s())
+    return dx
+
+
+# ------------------------------------------------------------- patch embed
+class _TokLNFn(torch.autograd.Function):
+    """LayerNorm over the channels of NHWC-stored conv output viewed as
+    tokens [B, h*w, E] (PatchEmbed :26-31: flatten(2).transpose(1,2), norm)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, eps):
+        b, e, h, w = y.shape
+        x2d = y.permute(0, 2, 3, 1).reshape(b * h * w, e)  # NHWC storage: a view
+        out, save = ln_fwd(x2d, gamma, beta, eps, torch.float32)
+        ctx.save_for_backward(x2d, save, gamma)
+        ctx.shape = (b, e, h, w)
+        ctx.ydtype = y.dtype
+        return out.view(b, h * w, e)
+
+    @staticmethod
+    def backward(ctx, dt):
+        x2d, save, gamma = ctx.saved_tensors
+        b, e, h, w = ctx.shape
+        dgamma = torch.zeros_like(gamma)
+        dbeta = torch.zeros_like(gamma)
+        dx = ln_bwd(dt.reshape(-1, e).contiguous().float(), x2d, save, gamma, None, dgamma, dbeta)
+        if ctx.ydtype == torch.bfloat16:
+            dx = cast_bf16(dx)
+        dy = dx.view(b, h, w, e).permute(0, 3, 1, 2)  # NCHW logical, NHWC storage
+        return dy, dgamma, dbeta, None
+
+
+def patch_tokens_layernorm(y, ln):
+    return _TokLNFn.apply(y, ln.weight, ln.bias, ln.eps)
+
+
+class _TokensToMapFn(torch.autograd.Function):
+    """tokens f32 [B, N, E] -> NCHW-logical, NHWC-stored map in the compute
+    dtype (TokensToFeatureMap :34-52: transpose(1,2).reshape)."""
+
+    @staticmethod
+    def forward(ctx, t, h, w, dtype):
+        b, n, e = t.shape
+        o = cast_bf16(t) if dtype == torch.bfloat16 else t.contiguous().clone()
+        return o.view(b, h, w, e).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dm):
+        b, e, h, w = dm.shape
+        d = dm.permute(0, 2, 3, 1).contiguous()
+        d = cast_f32(d) if d.dtype == torch.bfloat16 else d
+        return d.view(b, h * w, e), None, None, None
+
+
+def tokens_to_map(t, h, w, dtype):
+    return _TokensToMapFn.apply(t, h, w, dtype)
+
+
+# ------------------------------------------------------- transformer block
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cfg, rng, ln1w, ln1b, qkvw, qkvb, projw, projb, ln2w, ln2b, fc1w, fc1b, fc2w, fc2b, g1, g2):
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites = cfg
+        s_attn, s_proj, s_m1, s_m2 = sites
+        b, n, e = x.shape
+        r, d, hid = b * n, e // heads, fc1w.shape[0]
+        dev = x.device
+        x = x.contiguous().view(r, e)
+        wq, wp, w1, w2 = cast_bf16(qkvw), cast_bf16(projw), cast_bf16(fc1w), cast_bf16(fc2w)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        # attention branch: x1 = x + drop(proj(attn(ln1(x)))) * g1
+        ln1, save1 = ln_fwd(x, ln1w, ln1b, eps1, torch.bfloat16)
+        qkv = gemm(torch.empty((r, 3 * e), **bf), ln1, wq, r, 3 * e, e, lda=e, ldb=e, ldc=3 * e, bias=qkvb)
+        S = torch.empty((b, heads, n, n), **f32)
+        gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * 3 * e, d),
+             sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
+        P = torch.empty((b, heads, n, n), **bf)
+        Pd = torch.empty((b, heads, n, n), **bf) if p_attn > 0 else P
+        N.call("dmf_softmax_dropout", S.data_ptr(), n, b * heads * n, n, float(d ** -0.5), float(p_attn), O._p(rng),
+               int(s_attn), P.data_ptr(), Pd.data_ptr(), n, _s())
+        del S
+        o = gemm(torch.empty((r, e), **bf), Pd, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads),
+                 sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
+        y1 = torch.empty((r, e), **bf)
+        x1 = gemm(torch.empty((r, e), **f32), o, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=projb, colscale=g1, res=x,
+                  aux=y1, dropout_p=p_proj, rng=rng, site=s_proj)
+        # MLP branch: x2 = x1 + drop(fc2(drop(gelu(fc1(ln2(x1)))))) * g2
+        ln2, save2 = ln_fwd(x1, ln2w, ln2b, eps2, torch.bfloat16)
+        hpre = torch.empty((r, hid), **bf)
+        h = gemm(torch.empty((r, hid), **bf), ln2, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=fc1b, act="gelu",
+                 aux=hpre, dropout_p=p_mlp, rng=rng, site=s_m1)
+        y2 = torch.empty((r, e), **bf)
+        x2 = gemm(torch.empty((r, e), **f32), h, w2, r, e, hid, lda=hid, ldb=hid, ldc=e, bias=fc2b, colscale=g2,
+                  res=x1, aux=y2, dropout_p=p_mlp, rng=rng, site=s_m2)
+        ctx.save_for_backward(x, ln1, save1, qkv, P, Pd, o, y1, x1, ln2, save2, hpre, h, y2, wq, wp, w1, w2,
+                              ln1w, ln2w, g1, g2, rng)
+        ctx.cfg = cfg
+        ctx.dims = (b, n, e, heads, d, hid)
+        return x2.view(b, n, e)
+
+    @staticmethod
+    def backward(ctx, dx2):
+        (x, ln1, save1, qkv, P, Pd, o, y1, x1, ln2, save2, hpre, h, y2, wq, wp, w1, w2,
+         ln1w, ln2w, g1, g2, rng) = ctx.saved_tensors
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites = ctx.cfg
+        s_attn, s_proj, s_m1, s_m2 = sites
+        b, n, e, heads, d, hid = ctx.dims
+        r = b * n
+        dev = x.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        def z(*s):
+            return torch.zeros(s, **f32)
+
+        dln1w, dln1b, dqkvw, dqkvb, dprojw, dprojb = z(e), z(e), z(3 * e, e), z(3 * e), z(e, e), z(e)
+        dln2w, dln2b, dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2 = z(e), z(e), z(hid, e), z(hid), z(e, hid), z(e), z(e), z(e)
+        dx2 = dx2.contiguous().view(r, e).float()
+        # ---- MLP branch
+        dy2 = torch.empty((r, e), **bf)
+        N.call("dmf_tok_scale_dropout_bwd", dx2.data_ptr(), y2.data_ptr(), r, e, g2.data_ptr(), float(p_mlp),
+               O._p(rng), int(s_m2), dy2.data_ptr(), dg2.data_ptr(), dfc2b.data_ptr(), _s())
+        gemm(dfc2w, dy2, h, e, hid, r, ta=1, tb=1, lda=e, ldb=hid, ldc=hid)
+        dpre = gemm(torch.empty((r, hid), **bf), dy2, w2, r, hid, e, tb=1, lda=e, ldb=hid, ldc=hid, act="gelu",
+                    pre=hpre, dropout_p=p_mlp, rng=rng, site=s_m1, dbias=dfc1b)
+        gemm(dfc1w, dpre, ln2, hid, e, r, ta=1, tb=1, lda=hid, ldb=e, ldc=e)
+        dln2 = gemm(torch.empty((r, e), **f32), dpre, w1, r, e, hid, tb=1, lda=hid, ldb=e, ldc=e)
+        del dpre
+        dx1 = ln_bwd(dln2, x1, save2, ln2w, dx2.clone(), dln2w, dln2b)
+        # ---- attention branch
+        dy1 = torch.empty((r, e), **bf)
+        N.call("dmf_tok_scale_dropout_bwd", dx1.data_ptr(), y1.data_ptr(), r, e, g1.data_ptr(), float(p_proj),
+               O._p(rng), int(s_proj), dy1.data_ptr(), dg1.data_ptr(), dprojb.data_ptr(), _s())
+        gemm(dprojw, dy1, o, e, e, r, ta=1, tb=1, lda=e, ldb=e, ldc=e)
+        do = gemm(torch.empty((r, e), **bf), dy1, wp, r, e, e, tb=1, lda=e, ldb=e, ldc=e)
+        dPd = torch.empty((b, heads, n, n), **f32)
+        gemm(dPd, do, qkv, n, n, d, lda=e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * e, d), sb=(n * 3 * e, d),
+             sc=(heads * n * n, n * n), b_off=2 * e)
+        dqkv = torch.empty((r, 3 * e), **bf)
+        # dV = Pd^T dO
+        gemm(dqkv, Pd, do, n, d, n, ta=1, tb=1, lda=n, ldb=e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
+             sb=(n * e, d), sc=(n * 3 * e, d), c_off=2 * e)
+        dS = torch.empty((b, heads, n, n), **bf)
+        N.call("dmf_softmax_dropout_bwd", P.data_ptr(), n, dPd.data_ptr(), n, b * heads * n, n, float(d ** -0.5),
+               float(p_attn), O._p(rng), int(s_attn), dS.data_ptr(), n, _s())
+        del dPd
+        # dQ = dS K, dK = dS^T Q
+        gemm(dqkv, dS, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
+             sb=(n * 3 * e, d), sc=(n * 3 * e, d), b_off=e)
+        gemm(dqkv, dS, qkv, n, d, n, ta=1, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads),
+             sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * 3 * e, d), c_off=e)
+        del dS
+        gemm(dqkvw, dqkv, ln1, 3 * e, e, r, ta=1, tb=1, lda=3 * e, ldb=e, ldc=e)
+        N.call("dmf_colsum_bf16", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), _s())
+        dln1 = gemm(torch.empty((r, e), **f32), dqkv, wq, r, e, 3 * e, tb=1, lda=3 * e, ldb=e, ldc=e)
+        dx = ln_bwd(dln1, x, save1, ln1w, dx1, dln1w, dln1b)
+        return (dx.view(b, n, e), None, None, dln1w, dln1b, dqkvw, dqkvb, dprojw, dprojb, dln2w, dln2b,
+                dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2)
+
+
+def transformer_block(x, blk, rng, sites):
+    """TransformerBlock.forward (transformer_model.py:78-81) as one node."""
+    training = blk.training
+    at, mlp = blk.attn, blk.mlp
+    p_attn = float(at.attn_drop.p) if training else 0.0
+    p_proj = float(at.proj_drop.p) if training else 0.0
+    p_mlp = float(mlp.drop.p) if training else 0.0
+    if rng is None and (p_attn > 0 or p_proj > 0 or p_mlp > 0):
+        raise RuntimeError("transformer dropout requested without an rng snapshot")
+    e = x.shape[-1]
+    if e % 256 or e > 1024 or at.head_dim % 8:
+        raise ValueError(f"TransformerBlock: embed_dim {e} must be a multiple of 256 (<= 1024), head_dim % 8 == 0")
+    if x.shape[1] % 8:
+        raise ValueError(f"TransformerBlock: token count {x.shape[1]} must be a multiple of 8")
+    if at.qkv.bias is None:
+        raise ValueError("TransformerBlock: qkv_bias=False is not supported by the fused path")
+    cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites))
+    return _BlockFn.apply(x, cfg, rng, blk.norm1.weight, blk.norm1.bias, at.qkv.weight, at.qkv.bias, at.proj.weight,
+                          at.proj.bias, blk.norm2.weight, blk.norm2.bias, mlp.fc1.weight, mlp.fc1.bias,
+                          mlp.fc2.weight, mlp.fc2.bias, blk.gamma1, blk.gamma2)

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 import dmf_ops as O
+import dmf_tokens as D
 
 
 def _caches(conv):
@@ -36,9 +37,8 @@ class PatchEmbed(nn.Module):
         dt = getattr(self, "compute_dtype", torch.bfloat16)
         x = O.as_nhwc(x.to(dt))
         y = O.conv2d(x, self.proj, _caches(self.proj))           # [B, E, h, w] NHWC
-        b, e, h, w = y.shape
-        tokens = y.permute(0, 2, 3, 1).reshape(b, h * w, e).float()  # NHWC storage == token order
-        return O.layer_norm(tokens, self.norm), (h, w)
+        h, w = y.shape[-2:]
+        return D.patch_tokens_layernorm(y, self.norm), (h, w)    # NHWC storage == token order
 
 
 class TokensToFeatureMap(nn.Module):
@@ -101,10 +101,15 @@ class TransformerBlock(nn.Module):
         self.mlp = MLP(embed_dim)
         self.gamma1 = nn.Parameter(init_scale * torch.ones(embed_dim))
         self.gamma2 = nn.Parameter(init_scale * torch.ones(embed_dim))
+        # Philox sites: attn_drop, proj_drop, MLP drop after GELU, MLP drop after fc2
+        self._sites = tuple(O.RNG.new_site() for _ in range(4))
 
     def forward(self, x):
-        x = O.layerscale_residual(x, self.attn(O.layer_norm(x, self.norm1)), self.gamma1)
-        return O.layerscale_residual(x, self.mlp(O.layer_norm(x, self.norm2)), self.gamma2)
+        rng = None
+        if self.training:
+            cur = O.RNG_CURRENT[0]
+            rng = cur if cur is not None else O.RNG.snapshot(x.device)
+        return D.transformer_block(x.float(), self, rng, self._sites)
 
 
 class TransformerEncoder(nn.Module):
@@ -131,4 +136,4 @@ class TransformerStage(nn.Module):
         tokens, hw = self.patch_embed(x)
         tokens = self.transformer(tokens)
         dt = getattr(self, "compute_dtype", torch.bfloat16)
-        return self.tokens_to_map(tokens, hw).to(dt)
+        return D.tokens_to_map(tokens, hw[0], hw[1], dt)

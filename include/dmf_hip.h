@@ -255,6 +255,57 @@ int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, 
 int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul, void* dst,
                       int ldd, void* stream);
 
+/* ------------------------------------------ batched bf16 GEMM, attention
+ * Hybrid TransformerStage, configuration 5 (transformer_model.py:68-134):
+ * nn.Linear (qkv, proj, fc1, fc2) forward/backward and the
+ * MultiHeadSelfAttention core at 576 tokens (:83-116) as GEMMs.
+ *   op(A)[m][k] = ta ? A[k*lda+m] : A[m*lda+k]; op(B)[k][n] = tb ? B[k*ldb+n] : B[n*ldb+k]
+ *   z = z1*batch2 + z2, operand offset z1*s?1 + z2*s?2 (elements; aux/pre use C's).
+ * Fused epilogue, in order (each step optional):
+ *   t = alpha * sum_k op(A) op(B) + bias[n]
+ *   aux[m][n] = bf16(t)                         (pre-activation saved for backward)
+ *   pre == NULL: t = dropout(act(t), p)         (forward; Philox index z*M*N + m*N + n at `site`)
+ *   pre != NULL: t = dropout_mask(t) * act'(pre[m][n])   (gradient of that forward)
+ *   t *= colscale[n]; t += res[m][n] (f32, unbatched; may alias C); C = t; dbias[n] += t
+ * A, B bf16; C f32 or bf16 (out_dtype). */
+int dmf_gemm_bf16(int out_dtype, int ta, int tb, int M, int N, int K, float alpha, const void* A, int lda,
+                  long long sA1, long long sA2, const void* B, int ldb, long long sB1, long long sB2, void* C,
+                  int ldc, long long sC1, long long sC2, int batch1, int batch2, const float* bias, int act,
+                  const float* colscale, const float* res, int ldr, void* aux, int ldaux, const void* pre, int ldpre,
+                  float dropout_p, const unsigned long long* rng, int site, float* dbias, void* stream);
+/* attention probabilities (transformer_model.py:104-110): per row of L f32
+ * scores, probs = softmax(scale * s) (bf16, kept for backward) and
+ * probs_dropped = dropout(probs, p) (bf16, the P operand of P v); Philox
+ * element index row*L + col at dropout site `site`. */
+int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
+                        const unsigned long long* rng, int site, void* probs, void* probs_dropped, int ldp,
+                        void* stream);
+/* dscores = scale * P * (g - sum(P g)), g = dropout_mask(dprobs_dropped) (bf16 out) */
+int dmf_softmax_dropout_bwd(const void* probs, int ldp, const float* dprobs_dropped, int ldg, long long rows, int L,
+                            float scale, float dropout_p, const unsigned long long* rng, int site, void* dscores,
+                            int lds, void* stream);
+
+/* token-stream kernels (transformer_model.py:29, :71-80, :115, :133); rows R = B*N,
+ * E % 256 == 0 and E <= 1024. LayerNorm: y bf16, save = (mean, rstd) per row. */
+int dmf_tok_layernorm_fwd(int x_dtype, const void* x, int ldx, long long R, int E, const float* gamma,
+                          const float* beta, float eps, int y_dtype, void* y, int ldy, float* save, void* stream);
+/* dx (f32) = LN'(dy) (+ dres; dx may alias dres); dgamma/dbeta accumulated (nullable) */
+int dmf_tok_layernorm_bwd(const float* dy, int x_dtype, const void* x, int ldx, const float* save, long long R,
+                          int E, const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta,
+                          void* stream);
+/* backward of out = res + dropout(y) * gamma: dy (bf16) = mask * gamma * gout,
+ * dgamma += sum gout * dropout(y), dbias += sum dy (accumulated, nullable) */
+int dmf_tok_scale_dropout_bwd(const float* gout, const void* yaux, long long R, int E, const float* gamma,
+                              float dropout_p, const unsigned long long* rng, int site, void* dy, float* dgamma,
+                              float* dbias, void* stream);
+int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, void* stream);
+int dmf_cast_bf16(const float* x, long long n, void* y, void* stream);
+int dmf_cast_f32(const void* x, long long n, float* y, void* stream);
+/* keep[i] (0/1) of element i at dropout site `site` -- the mask every fused
+ * dropout of this library draws (test/inspection helper; n % 4 == 0) */
+int dmf_dropout_keep_mask(const unsigned long long* rng, int site, long long n, float p, unsigned char* keep,
+                          void* stream);
+
 /* ------------------------------------------------------------ optimizer
  * torch.optim.AdamW as built by LightningFusionOptimizerFactory
  * (selector_helpers.py:632-685, :617-629) -- multi-tensor, one launch. */

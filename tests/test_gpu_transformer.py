@@ -1,0 +1,304 @@
+"""Configuration 5 (hybrid TransformerStage, transformer_model.py:7-175):
+the bf16 MFMA GEMM with its fused epilogues, softmax+dropout, the token
+LayerNorm / LayerScale-dropout kernels, one TransformerBlock forward+backward
+(eval mode against the CPU oracle; train mode with dropout against a torch
+fp32 restatement that uses the library's own Philox keep-masks), and the
+hybrid encoder end to end.
+
+Tolerance: every GEMM operand is bf16 (fp32 accumulation), so outputs are
+compared as max|ours - ref| <= tol * max(1, max|ref|) with tol = 2e-2 for
+single GEMMs and 3e-2 for a whole block / gradient."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dmf_native as N
+import dmf_ops as O
+import dmf_tokens as D
+import model_module as MM
+import parameters as PR
+import transformer_model as TM
+from oracle import model as OM
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _close(a, b, tol, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = (a - b).abs().max().item()
+    assert err <= tol * max(1.0, b.abs().max().item()), f"{what}: max err {err:.3e} (ref max {b.abs().max():.3e})"
+
+
+GEMM_CASES = [
+    # (ta, tb, M, N, K, out dtype)
+    (0, 0, 200, 136, 72, torch.float32),
+    (0, 1, 256, 128, 96, torch.bfloat16),
+    (1, 0, 136, 264, 48, torch.float32),
+    (1, 1, 64, 72, 520, torch.float32),
+    (0, 0, 1030, 512, 512, torch.bfloat16),
+]
+
+
+@pytest.mark.parametrize("case", GEMM_CASES)
+def test_gemm_bf16_plain(case):
+    ta, tb, M, Nn, K, odt = case
+    g = torch.Generator().manual_seed(M + Nn + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((K, Nn) if tb else (Nn, K), generator=g)
+    bias = torch.randn(Nn, generator=g)
+    ref = (_bf(A).t() if ta else _bf(A)) @ (_bf(B) if tb else _bf(B).t()) + bias
+    Ad, Bd = A.to(DEV, torch.bfloat16), B.to(DEV, torch.bfloat16)
+    C = torch.empty((M, Nn), dtype=odt, device=DEV)
+    D.gemm(C, Ad, Bd, M, Nn, K, ta=ta, tb=tb, lda=A.shape[1], ldb=B.shape[1], ldc=Nn, bias=bias.to(DEV))
+    _close(C, ref, 1e-2, "gemm")
+
+
+def test_gemm_bf16_batched_offsets():
+    """attention-style operands: heads are column slices of packed rows"""
+    b, h, n, d = 2, 3, 40, 16
+    g = torch.Generator().manual_seed(1)
+    qkv = torch.randn(b, n, 3 * h * d, generator=g)
+    e = h * d
+    S = torch.empty((b, h, n, n), device=DEV)
+    qd = qkv.to(DEV, torch.bfloat16)
+    D.gemm(S, qd, qd, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, h), sa=(n * 3 * e, d), sb=(n * 3 * e, d),
+           sc=(h * n * n, n * n), b_off=e)
+    q = _bf(qkv[..., :e]).view(b, n, h, d).transpose(1, 2)
+    k = _bf(qkv[..., e:2 * e]).view(b, n, h, d).transpose(1, 2)
+    _close(S, q @ k.transpose(-1, -2), 1e-2, "QK^T")
+    # P V with V^T-free layout (tb=1) into a column slice
+    P = torch.softmax(torch.randn(b, h, n, n, generator=g), -1)
+    o = torch.zeros((b * n, e), dtype=torch.bfloat16, device=DEV)
+    D.gemm(o, P.to(DEV, torch.bfloat16), qd, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, h),
+           sa=(h * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
+    v = _bf(qkv[..., 2 * e:]).view(b, n, h, d).transpose(1, 2)
+    ref = (_bf(P) @ v).transpose(1, 2).reshape(b * n, e)
+    _close(o, ref, 1e-2, "PV")
+
+
+def test_gemm_epilogues():
+    """aux + gelu + dropout forward, its gradient epilogue with dbias, and
+    LayerScale + residual (f32) -- masks from dmf_dropout_keep_mask"""
+    M, Nn, K, p = 96, 256, 64, 0.25
+    g = torch.Generator().manual_seed(2)
+    A, W, bias = torch.randn(M, K, generator=g), torch.randn(Nn, K, generator=g) * 0.2, torch.randn(Nn, generator=g)
+    rng = O.RNG.snapshot(DEV)
+    site = O.RNG.new_site()
+    keep = torch.empty(M * Nn, dtype=torch.uint8, device=DEV)
+    N.call("dmf_dropout_keep_mask", rng.data_ptr(), site, M * Nn, p, keep.data_ptr(), N.stream_ptr())
+    mk = keep.cpu().float().view(M, Nn) / (1 - p)
+    Ad, Wd = A.to(DEV, torch.bfloat16), W.to(DEV, torch.bfloat16)
+    aux = torch.empty((M, Nn), dtype=torch.bfloat16, device=DEV)
+    out = torch.empty((M, Nn), dtype=torch.bfloat16, device=DEV)
+    D.gemm(out, Ad, Wd, M, Nn, K, lda=K, ldb=K, ldc=Nn, bias=bias.to(DEV), act="gelu", aux=aux, dropout_p=p,
+           rng=rng, site=site)
+    pre = _bf(A) @ _bf(W).t() + bias
+    _close(aux, pre, 1e-2, "aux")
+    _close(out, F.gelu(pre) * mk, 2e-2, "gelu+dropout")
+    # gradient epilogue: dpre = mask(dh) * gelu'(pre), dbias = colsum(dpre)
+    dh = torch.randn(M, 128, generator=g)
+    W2 = torch.randn(128, Nn, generator=g) * 0.1   # dh @ W2 -> [M, Nn]  (tb=1 on W2 [128][Nn])
+    dpre = torch.empty((M, Nn), dtype=torch.bfloat16, device=DEV)
+    dbias = torch.zeros(Nn, device=DEV)
+    D.gemm(dpre, dh.to(DEV, torch.bfloat16), W2.to(DEV, torch.bfloat16), M, Nn, 128, tb=1, lda=128, ldb=Nn, ldc=Nn,
+           act="gelu", pre=aux, dropout_p=p, rng=rng, site=site, dbias=dbias)
+    pre_b = _bf(pre)
+    x_ = pre_b.clone().requires_grad_(True)
+    F.gelu(x_).backward(torch.ones_like(x_))
+    ref = (_bf(dh) @ _bf(W2)) * mk * x_.grad
+    _close(dpre, ref, 2e-2, "grad epilogue")
+    _close(dbias, ref.sum(0), 2e-2, "dbias")
+    # LayerScale + residual into f32
+    res = torch.randn(M, Nn, generator=g)
+    gam = torch.rand(Nn, generator=g)
+    out32 = torch.empty((M, Nn), device=DEV)
+    D.gemm(out32, Ad, Wd, M, Nn, K, lda=K, ldb=K, ldc=Nn, bias=bias.to(DEV), colscale=gam.to(DEV), res=res.to(DEV))
+    _close(out32, res + pre * gam, 1e-2, "layerscale residual")
+
+
+def test_softmax_dropout_fwd_bwd():
+    rows, L, p, scale = 300, 72, 0.2, 0.125
+    g = torch.Generator().manual_seed(3)
+    S = torch.randn(rows, L, generator=g) * 4
+    rng = O.RNG.snapshot(DEV)
+    site = O.RNG.new_site()
+    Sd = S.to(DEV)
+    P = torch.empty((rows, L), dtype=torch.bfloat16, device=DEV)
+    Pd = torch.empty_like(P)
+    N.call("dmf_softmax_dropout", Sd.data_ptr(), L, rows, L, scale, p, rng.data_ptr(), site, P.data_ptr(),
+           Pd.data_ptr(), L, N.stream_ptr())
+    keep = torch.empty(rows * L, dtype=torch.uint8, device=DEV)
+    N.call("dmf_dropout_keep_mask", rng.data_ptr(), site, rows * L, p, keep.data_ptr(), N.stream_ptr())
+    mk = keep.cpu().float().view(rows, L) / (1 - p)
+    ref = torch.softmax(S * scale, -1)
+    _close(P, ref, 1e-2, "probs")
+    _close(Pd, ref * mk, 1e-2, "dropped probs")
+    G = torch.randn(rows, L, generator=g)
+    dS = torch.empty((rows, L), dtype=torch.bfloat16, device=DEV)
+    N.call("dmf_softmax_dropout_bwd", P.data_ptr(), L, G.to(DEV).data_ptr(), L, rows, L, scale, p, rng.data_ptr(),
+           site, dS.data_ptr(), L, N.stream_ptr())
+    s_ = S.clone().requires_grad_(True)
+    (torch.softmax(s_ * scale, -1) * mk).backward(G)
+    _close(dS, s_.grad, 2e-2, "dscores")
+
+
+def test_token_layernorm_and_scale_dropout():
+    R, E, p = 70, 512, 0.3
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(R, E, generator=g) * 2 + 0.5
+    gam, bet = 1 + 0.1 * torch.randn(E, generator=g), 0.1 * torch.randn(E, generator=g)
+    y, save = D.ln_fwd(x.to(DEV), gam.to(DEV), bet.to(DEV), 1e-5, torch.bfloat16)
+    xr = x.clone().requires_grad_(True)
+    gr, br = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (E,), gr, br, 1e-5)
+    _close(y, yr, 1e-2, "ln fwd")
+    dy = torch.randn(R, E, generator=g)
+    dres = torch.randn(R, E, generator=g)
+    yr.backward(dy)
+    dg, db = torch.zeros(E, device=DEV), torch.zeros(E, device=DEV)
+    dx = D.ln_bwd(dy.to(DEV), x.to(DEV), save, gam.to(DEV), dres.to(DEV).clone(), dg, db)
+    _close(dx, xr.grad + dres, 1e-3, "ln dx")
+    _close(dg, gr.grad, 1e-3, "ln dgamma")
+    _close(db, br.grad, 1e-3, "ln dbeta")
+    # out = res + drop(y) * gamma  backward
+    yb = torch.randn(R, E, generator=g)
+    rng = O.RNG.snapshot(DEV)
+    site = O.RNG.new_site()
+    keep = torch.empty(R * E, dtype=torch.uint8, device=DEV)
+    N.call("dmf_dropout_keep_mask", rng.data_ptr(), site, R * E, p, keep.data_ptr(), N.stream_ptr())
+    mk = keep.cpu().float().view(R, E) / (1 - p)
+    ydev = yb.to(DEV, torch.bfloat16)
+    dyo = torch.empty((R, E), dtype=torch.bfloat16, device=DEV)
+    dgam, dbias = torch.zeros(E, device=DEV), torch.zeros(E, device=DEV)
+    N.call("dmf_tok_scale_dropout_bwd", dy.to(DEV).data_ptr(), ydev.data_ptr(), R, E, gam.to(DEV).data_ptr(), p,
+           rng.data_ptr(), site, dyo.data_ptr(), dgam.data_ptr(), dbias.data_ptr(), N.stream_ptr())
+    _close(dyo, dy * mk * gam, 1e-2, "branch dy")
+    _close(dgam, (dy * mk * _bf(yb)).sum(0), 1e-3, "dgamma")
+    _close(dbias, (dy * mk * gam).sum(0), 1e-3, "dbias")
+
+
+def _masked_block_ref(blk, x, masks, p):
+    """transformer_model.py:78-134 in fp32 with explicit keep masks (1/(1-p) scaled)."""
+    b, n, e = x.shape
+    at, ml = blk.attn, blk.mlp
+    hh, d = at.num_heads, at.head_dim
+    h1 = blk.norm1(x)
+    q, k, v = at.qkv(h1).reshape(b, n, 3, hh, d).permute(2, 0, 3, 1, 4)
+    a = torch.softmax((q @ k.transpose(-2, -1)) * at.scale, dim=-1) * masks[0]
+    y = at.proj((a @ v).transpose(1, 2).reshape(b, n, e)) * masks[1]
+    x = x + y * blk.gamma1
+    hm = F.gelu(ml.fc1(blk.norm2(x))) * masks[2]
+    return x + ml.fc2(hm) * masks[3] * blk.gamma2
+
+
+def _block_pair(e, heads, seed):
+    torch.manual_seed(seed)
+    ref = OM.TransformerBlock(e, heads)
+    for m in ref.modules():
+        if isinstance(m, torch.nn.LayerNorm):
+            m.weight.data = 1 + 0.1 * torch.randn(e)
+            m.bias.data = 0.1 * torch.randn(e)
+    ref.gamma1.data = 0.5 + torch.rand(e)
+    ref.gamma2.data = 0.5 + torch.rand(e)
+    ours = TM.TransformerBlock(e, heads)
+    ours.load_state_dict(ref.state_dict())
+    return ours.to(DEV), ref
+
+
+def _grads(mod):
+    return {n: p.grad for n, p in mod.named_parameters()}
+
+
+def test_block_eval_parity_vs_oracle():
+    b, n, e, heads = 2, 64, 256, 4
+    ours, ref = _block_pair(e, heads, 5)
+    ours.eval()
+    ref.eval()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(b, n, e, generator=g)
+    gy = torch.randn(b, n, e, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(gy)
+    xd = x.to(DEV).requires_grad_(True)
+    y = ours(xd)
+    y.backward(gy.to(DEV))
+    _close(y, yr, 3e-2, "block out")
+    _close(xd.grad, xr.grad, 3e-2, "dx")
+    gr = _grads(ref)
+    for name, gd in _grads(ours).items():
+        _close(gd, gr[name], 3e-2, name)
+
+
+def test_block_train_dropout_vs_masked_restatement():
+    b, n, e, heads, p = 2, 48, 256, 4, 0.1
+    ours, ref = _block_pair(e, heads, 7)
+    ours.train()
+    ref.train()
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(b, n, e, generator=g)
+    gy = torch.randn(b, n, e, generator=g)
+    rng = O.RNG.snapshot(DEV)
+    hid = ours.mlp.fc1.out_features
+    shapes = [(b * heads * n * n, (b, heads, n, n)), (b * n * e, (b, n, e)), (b * n * hid, (b, n, hid)),
+              (b * n * e, (b, n, e))]
+    masks = []
+    for site, (cnt, shp) in zip(ours._sites, shapes):
+        keep = torch.empty(cnt, dtype=torch.uint8, device=DEV)
+        N.call("dmf_dropout_keep_mask", rng.data_ptr(), site, cnt, p, keep.data_ptr(), N.stream_ptr())
+        masks.append(keep.cpu().float().view(shp) / (1 - p))
+    xr = x.clone().requires_grad_(True)
+    yr = _masked_block_ref(ref, xr, masks, p)
+    yr.backward(gy)
+    xd = x.to(DEV).requires_grad_(True)
+    y = D.transformer_block(xd, ours, rng, ours._sites)
+    y.backward(gy.to(DEV))
+    _close(y, yr, 3e-2, "block out (dropout)")
+    _close(xd.grad, xr.grad, 3e-2, "dx (dropout)")
+    gr = _grads(ref)
+    for name, gd in _grads(ours).items():
+        _close(gd, gr[name], 3e-2, name)
+    # same snapshot -> same masks -> same output
+    with torch.no_grad():
+        y2 = D.transformer_block(x.to(DEV), ours, rng, ours._sites)
+    assert torch.equal(y2, y.detach())
+
+
+def test_hybrid_encoder_forward_backward():
+    """ModelMaskHeadBackbone with use_hybrid_transformer (model_module.py:564-579,
+    :701-703) against the oracle, eval mode, f32 convs + bf16 transformer GEMMs."""
+    P = PR.small_parameters(channels=(16, 32, 64), input_size=64, dropout=0.0, use_backbone=False)
+    mp = P["dwi_model_parameters"]
+    mp["use_hybrid_transformer"] = True
+    mp["transformer_embed_dim"] = 256
+    mp["transformer_depth"] = 2
+    mp["transformer_heads"] = 4
+    mp["mask_stage"] = "f2"
+    torch.manual_seed(9)
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", copy.deepcopy(P), None), True)
+    ref = OM.ModelMaskHeadBackbone("dwi", copy.deepcopy(P), None)
+    ref.load_state_dict(enc.state_dict())
+    MM.set_compute_dtype(enc, torch.float32)
+    enc = enc.to(DEV).eval()
+    ref.eval()
+    g = torch.Generator().manual_seed(10)
+    x = (0.5 + torch.randn(2, 14, 64, 64, generator=g) / 6).clamp(0, 1)
+    lo, aux, mp_ = enc(x.to(DEV))
+    lr_, auxr, mpr = ref(x)
+    _close(lo, lr_, 3e-2, "logits")
+    _close(aux["raw_feats"][2], auxr["raw_feats"][2], 3e-2, "f3")
+    (aux["raw_feats"][2].float().square().mean()).backward()
+    (auxr["raw_feats"][2].square().mean()).backward()
+    gr = dict(ref.named_parameters())
+    for name, prm in enc.named_parameters():
+        if name.startswith("transformer.") and prm.grad is not None:
+            _close(prm.grad, gr[name].grad, 5e-2, name)
