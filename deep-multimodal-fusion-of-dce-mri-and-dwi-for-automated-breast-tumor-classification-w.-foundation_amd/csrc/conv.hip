@@ -361,14 +361,17 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
   uint4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
   // K cursor (filter row, column, channel): gload() runs in K order (the
   // clamped tail re-issues only feed registers that are never stored)
+  // Channel chunk outer, filter tap inner: the KH*KW consecutive K-steps of
+  // one 64-channel chunk re-read the same input rows (shifted by a tap), so
+  // the im2col gather hits L2 instead of re-streaming the input per tap.
   int cr = 0, cs = 0, cc = 0;
   auto gload = [&](int kt, uint4 (&ra)[RA], uint4 (&rb)[RB]) {
-    const int k0 = kt * BK;  // uniform
+    (void)kt;
     const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
-    cc += BK;
-    if (cc == a.C) {
-      cc = 0;
-      if (++cs == a.KW) { cs = 0; ++cr; }
+    const int k0 = (cr * a.KW + cs) * a.C + c0;  // uniform
+    if (++cs == a.KW) {
+      cs = 0;
+      if (++cr == a.KH) { cr = 0; cc += BK; }
     }
     // block-uniform source choice as a branch, so each path keeps its descriptor in SGPRs
     if (DUAL && c0 >= a.C1) {
@@ -530,16 +533,17 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
   const int nk = a.Ktot / BK;
 
   // K cursor (filter row r, column s, channel c0) advanced without divisions: issue() runs in K order
+  // channel chunk outer, tap inner (see k_conv_fwd_buf): L2 reuse of the gather
   int cr = 0, cs = 0, cc = 0;
   auto issue = [&](int kt, int stage) {
+    (void)kt;
     const unsigned As = lds0 + stage * WSTAGE;
     const unsigned Bs = As + WBM * 128;
-    const int k0 = kt * BK;  // uniform
     const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
-    cc += BK;
-    if (cc == a.C) {
-      cc = 0;
-      if (++cs == a.KW) { cs = 0; ++cr; }
+    const int k0 = (cr * a.KW + cs) * a.C + c0;  // uniform
+    if (++cs == a.KW) {
+      cs = 0;
+      if (++cr == a.KH) { cr = 0; cc += BK; }
     }
     if (DUAL && c0 >= a.C1) {
       const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
