@@ -122,7 +122,7 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
 
 // one LDS stage of A/B fragments -> (BM/32)x(BN/32) MFMA fragments per wave
 // (2x2 waves, each a (BM/2)x(BN/2) sub-tile)
-template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2>
+template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2, bool PRIO = false>
 __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16 * WMW)][BN / (16 * WNW)], int wm,
                                          int wn, int lane) {
   constexpr int FM = BM / (16 * WMW), FN = BN / (16 * WNW);
@@ -143,12 +143,14 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16
       bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
     }
     if constexpr (sizeof(T) == 2) {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
                                                               0, 0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -592,6 +594,152 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
   conv_epilogue<bf16_t, WBM, WBN, WWM, WWN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
+// --------------------------------------- forward, LDS-DMA square form (bf16)
+// 256x256 block tile, 8 waves (2 M x 4 N) of 128x64 each (8x4 MFMA
+// fragments, 64 v_mfma_f32_16x16x32_bf16 per wave per K-step), BK = 64, one
+// workgroup per CU, two 64 KiB LDS stages. A K-step stages 64 KiB per CU for
+// twice the MFMA work of the 256x128 form (32 B per MFMA-cycle instead of
+// 47): on the 256x128 form the per-CU load path, not the matrix pipe, was the
+// bound (SQ PMC: 43 % MFMA busy, 36 % of wave time parked in waitcnt /
+// barrier). The next tile's 8 LDS-DMA pieces per wave are issued between
+// the current tile's MFMA groups, right after the one barrier per K-step
+// that retires the current tile (vmcnt(0): only it is in flight) and frees
+// the other stage. Requires Nout % 256 == 0 plus the wide form's conditions.
+constexpr int QBM = 256, QBN = 256, QSTAGE = (QBM + QBN) * 128;
+constexpr int QWM = 2, QWN = 4, QTHREADS = 64 * QWM * QWN;
+constexpr int QLDS_MAIN = 2 * QSTAGE > QBM * (QBN + 8) * 2 ? 2 * QSTAGE : QBM * (QBN + 8) * 2;
+constexpr int QLDS = QLDS_MAIN + 64 + QTHREADS * 2 * 8;  // + epilogue flag and reducer doubles
+
+// VAR bit 0: waves 4-7 at static priority 1; bit 1: s_setprio around each MFMA group
+template <bool PADCHK, bool DUAL, int VAR>
+__global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
+  constexpr int ES = 2, EPC = 8, BK = 64;
+  constexpr int NW = QTHREADS / 64;
+  constexpr int NA = QBM / 8 / NW;  // A row-groups (8 rows) per wave: 4
+  constexpr int NB = QBN / 8 / NW;  // B row-groups per wave: 4
+  constexpr int FM = QBM / (16 * QWM), FN = QBN / (16 * QWN);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / QWN, wn = wid % QWN;
+  if constexpr (VAR & 1) {
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lin / a.ntiles, nt = lin % a.ntiles;
+  const int m0 = mt * QBM, n0 = nt * QBN;
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;  // source-side swizzle (see k_conv_fwd_wide)
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  const v4i_t rx = buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * ES);
+  const v4i_t rx2 = buf_rsrc(DUAL ? a.x2 : a.x, (long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES);
+  const v4i_t rw = buf_rsrc(a.w, (long long)a.Nout * a.Ktot * ES);
+
+  int h0[NA], w0[NA], b1[NA], b2[NA];
+  bool mok[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + wid * (NA * 8) + i * 8 + lr;
+    mok[i] = m < a.M;
+    const int mm = mok[i] ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    const int n = mm / hw, rem = mm - (mm / hw) * hw;
+    const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+    h0[i] = ho * a.stride - a.pad;
+    w0[i] = wo * a.stride - a.pad;
+    const int pix = (n * a.H + h0[i]) * a.W + w0[i];
+    b1[i] = pix * a.ldx + lc * EPC;
+    b2[i] = DUAL ? pix * a.ldx2 + lc * EPC : 0;
+  }
+  unsigned vb[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + wid * (NB * 8) + i * 8 + lr;  // Nout % 256 == 0: always in range
+    vb[i] = (unsigned)((n * a.Ktot + lc * EPC) * ES);
+  }
+  const int nk = a.Ktot / BK;
+
+  // K cursor: channel chunk outer, tap inner. prep() fixes one K-step's
+  // source, tap offset and weight offset; piece(p) issues DMA piece p of it.
+  int cr = 0, cs = 0, cc = 0;
+  bool p_hi = false;
+  int p_toff = 0, p_rd = 0, p_sd = 0;
+  unsigned p_koff = 0, p_As = 0, p_Bs = 0;
+  auto prep = [&](int stage) {
+    const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
+    p_koff = (unsigned)(((cr * a.KW + cs) * a.C + c0) * ES);
+    if (++cs == a.KW) {
+      cs = 0;
+      if (++cr == a.KH) { cr = 0; cc += BK; }
+    }
+    p_hi = DUAL && c0 >= a.C1;
+    p_toff = p_hi ? (rd * a.W + sd) * a.ldx2 + (c0 - a.C1) : (rd * a.W + sd) * a.ldx + c0;
+    p_rd = rd;
+    p_sd = sd;
+    p_As = lds0 + stage * QSTAGE;
+    p_Bs = p_As + QBM * 128;
+  };
+  auto piece = [&](int p) {
+    if (p < NA) {
+      bool ok = mok[p];
+      if (PADCHK) ok = ok && (unsigned)(h0[p] + p_rd) < (unsigned)a.H && (unsigned)(w0[p] + p_sd) < (unsigned)a.W;
+      const unsigned vo = ok ? (unsigned)(((p_hi ? b2[p] : b1[p]) + p_toff) * ES) : BUF_OOB;
+      dma16(p_hi ? rx2 : rx, vo, 0, p_As + (wid * (NA * 8) + p * 8) * 128);
+    } else {
+      const int i = p - NA;
+      dma16(rw, vb[i], p_koff, p_Bs + (wid * (NB * 8) + i * 8) * 128);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  prep(0);
+#pragma unroll
+  for (int p = 0; p < NA + NB; ++p) piece(p);
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt is the only DMA in flight: retire it; the barrier publishes every wave's part
+    // and orders the refill of the other stage after every wave's reads of tile kt-1
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const bool more = kt + 1 < nk;
+    if (more) prep((kt + 1) & 1);
+    const char* As = smem + (kt & 1) * QSTAGE;
+    const char* Bs = As + QBM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fg;
+      uint4 av[FM], bv[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * (QBN / QWN) + j * 16 + fr;
+        bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * (QBM / QWM) + i * 16 + fr;
+        av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
+        if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
+                                                              0, 0);
+        if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  conv_epilogue<bf16_t, QBM, QBN, QWM, QWN>(a, acc, smem, tid, mt, nt, m0, n0);
+}
+
 // ---------------------------------------- forward, persistent buffer-load form
 // 128x128 tiles, gridDim = resident blocks; each block walks its tiles as ONE
 // flat stream of K-steps, so the two-tile register pipeline runs across tile
@@ -975,8 +1123,11 @@ static bool fast_disabled() {
 struct ConvPlan {
   bool buf;
   bool wide;  // k_conv_fwd_wide (LDS-DMA, 256x128)
+  bool sq;    // k_conv_fwd_sq (LDS-DMA, 256x256)
   int bm, bn;
 };
+// runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
+static int g_sq_enable = 1, g_sq_var = 1;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -985,7 +1136,7 @@ static bool wide_disabled() {
   return v != 0;
 }
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, false, CBM, CBN};
+  ConvPlan p{false, false, false, CBM, CBN};
   if (dgrad || a.in_ss != nullptr || fast_disabled()) return p;
   const int es = dtype == DMF_BF16 ? 2 : 4;
   const int bk = dtype == DMF_BF16 ? 64 : 32;
@@ -995,6 +1146,16 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const long long wbytes = (long long)a.Nout * a.Ktot * es;
   p.buf = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31);
   if (!p.buf) return p;
+  // square LDS-DMA tile: whole 256-column tiles and >= one block per CU
+  // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
+  // bound at one 256x256 block per CU and stays on the 256x128 form)
+  if (dtype == DMF_BF16 && !wide_disabled() && g_sq_enable && a.Nout % QBN == 0 &&
+      (a.KH * a.KW > 1 ? a.Ktot >= 512 : a.Ktot >= 2048) && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= 256) {
+    p.wide = p.sq = true;
+    p.bm = QBM;
+    p.bn = QBN;
+    return p;
+  }
   // wide LDS-DMA tile: bf16, whole 128-column tiles, long enough K, >= one block per CU
   if (dtype == DMF_BF16 && !wide_disabled() && a.Nout % WBN == 0 && a.Ktot >= 512 &&
       (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= 256) {
@@ -1025,7 +1186,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = dtype == DMF_BF16 ? 2 : 4;
-  const size_t lds_total = plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
+  const size_t lds_total = plan.sq ? (size_t)QLDS : plan.wide ? (size_t)WLDS
+                                                            : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
   const int bk = dtype == DMF_BF16 ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
@@ -1043,6 +1205,22 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
+  } else if (plan.sq) {
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const dim3 bq(QTHREADS);
+#define DMF_SQ(V)                                                                                      \
+  do {                                                                                                 \
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, V>), g, bq, lds_total, st, a);   \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_sq<false, false, V>), g, bq, lds_total, st, a);     \
+    else hipLaunchKernelGGL((k_conv_fwd_sq<true, false, V>), g, bq, lds_total, st, a);                 \
+  } while (0)
+    switch (g_sq_var) {
+      case 1: DMF_SQ(1); break;
+      case 2: DMF_SQ(2); break;
+      case 3: DMF_SQ(3); break;
+      default: DMF_SQ(0); break;
+    }
+#undef DMF_SQ
   } else if (plan.wide) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 bw(WTHREADS);
@@ -1152,6 +1330,14 @@ __global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, 
 using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
+
+extern "C" int dmf_conv_tune(int key, int value) {
+  switch (key) {
+    case 0: g_sq_enable = value != 0; return 0;
+    case 1: DMF_CHECK_ARG(value >= 0 && value < 4, "dmf_conv_tune: square-tile variant %d", value); g_sq_var = value; return 0;
+    default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
+  }
+}
 
 // rows of the BN partial-statistics slab a forward launch of this shape writes
 extern "C" int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2,

@@ -53,6 +53,9 @@ int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* str
  * FeatureDownAlign (:386-390), FusionModel.proj_in_* / reduce (:857-862,
  * :788-792), PatchEmbed.proj (transformer_model.py:17-22). */
 int dmf_conv_m_tile(void);
+/* forward-conv tuning knobs (benchmarks / A-B runs): key 0 = 256x256 LDS-DMA
+ * tile on (1, default) / off; key 1 = its scheduling variant 0..3 */
+int dmf_conv_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */
 int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2, int Cout, int KH,

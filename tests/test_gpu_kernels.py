@@ -80,6 +80,12 @@ WIDE_CASES = [
     (33, 256, 32, 32, 256, 3, 2, 2, 0),
     (33, 512, 32, 32, 512, 1, 0, 1, 0),
     (32, 128, 32, 32, 256, 3, 1, 1, 384),
+    # 256x256 square-tile LDS-DMA kernel (Cout % 256 == 0, >= 256 blocks):
+    # padded dilated 3x3 with an M tail, channel-concat 3x3, plain 1x1
+    (65, 64, 31, 31, 512, 3, 2, 2, 0),
+    (36, 64, 31, 31, 512, 3, 1, 1, 64),
+    (34, 512, 32, 32, 1024, 1, 0, 1, 0),
+    (34, 2048, 32, 32, 512, 1, 0, 1, 0),
 ]
 
 

@@ -65,13 +65,54 @@ def run_shape(shape, reps, stats, dtype=torch.bfloat16):
     return ms, flops / (ms * 1e-3) / 1e12
 
 
+def _shapes(src):
+    import collections
+    import json
+    cnt = collections.Counter(tuple(json.loads(l)["shape"]) for l in open(src))
+    return sorted(cnt.items(), key=lambda kv: -kv[1] * kv[0][0] * kv[0][1] * kv[0][2] * kv[0][3] * kv[0][4] *
+                  kv[0][5] ** 2 / kv[0][6] ** 2)
+
+
+def ab(a):
+    """Interleaved A/B of tuning variants (cdna_hip_programming.md 5.4 rule 24):
+    per shape, rounds x variants, median time per variant."""
+    import statistics
+
+    import dmf_native as N
+    variants = [[tuple(int(t) for t in kv.split(":")) for kv in grp.split(",") if kv] for grp in a.tunes.split(";")]
+    shapes = _shapes(a.src) if a.src else SHAPES
+    sel = [int(i) for i in a.only.split(",")] if a.only else range(len(shapes))
+    tot = [0.0] * len(variants)
+    print("variants:", variants)
+    for i in sel:
+        shape, cnt = shapes[i]
+        times = [[] for _ in variants]
+        for _ in range(a.rounds):
+            for vi, var in enumerate(variants):
+                for k, v in var:
+                    N.call("dmf_conv_tune", k, v)
+                times[vi].append(run_shape(shape, a.reps, not a.nostats)[0])
+        med = [statistics.median(t) for t in times]
+        for vi in range(len(variants)):
+            tot[vi] += med[vi] * cnt
+        print(f"{i:2d} {str(shape):38s} x{cnt:2d} " + " ".join(f"{m * 1e3:8.1f}" for m in med) + " us", flush=True)
+    print("weighted totals (ms):", " ".join(f"{t:.3f}" for t in tot))
+    for k, v in variants[0]:
+        N.call("dmf_conv_tune", k, v)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--nostats", action="store_true")
     ap.add_argument("--from", dest="src", default="", help="bench.py DMF_CONV_DUMP jsonl: every distinct shape, with counts")
+    ap.add_argument("--tunes", default="", help="A/B variants, e.g. '0:0;0:1,1:0;0:1,1:1' (dmf_conv_tune key:value "
+                                                "lists), timed interleaved in this process")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
+    if a.tunes:
+        return ab(a)
     shapes = SHAPES
     if a.src:
         import collections
