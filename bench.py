@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--mode", choices=["A", "B"], default="A")
+    ap.add_argument("--config", type=int, choices=[3, 5], default=3,
+                    help="5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -157,6 +159,14 @@ def pmc_traffic():
     return d
 
 
+def _cpu_params(PR, args):
+    P = PR.default_parameters()
+    if args.config == 5:
+        P["dwi_model_parameters"]["use_hybrid_transformer"] = True
+    P["dwi_model_parameters"]["input_size"] = args.size
+    return P
+
+
 def cpu_baseline(args, P_fn):
     """fp32 CPU oracle (same eager op sequence as the reference) on a bounded
     sample: cpu-batch volumes at SxS, mode A step, 1 warm-up + cpu-steps timed."""
@@ -216,6 +226,12 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     P = PR.default_parameters()
+    if args.config == 5:
+        # hybrid CNN -> Transformer stage (E=512, depth 6, 4 heads, patch 2;
+        # parameters_generate.py:71-75) in place of block3, S=384 (576 tokens per volume)
+        P["dwi_model_parameters"]["use_hybrid_transformer"] = True
+        if args.size == 256:
+            args.size = 384
     P["dwi_model_parameters"]["input_size"] = args.size
     lm = build(P, device, dtype, args.mode, seed=0)
     trainer = FusionTrainer(lm, world=world, use_graph=not args.no_graph)
@@ -263,7 +279,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (config-3 recipe: DWI clamp(0.5+N/6), DCE U[0,1), disc masks); random-init weights",
-        "config": {"workload": f"fusion training step, config 3, mode {args.mode} "
+        "config": {"workload": f"fusion training step, config {args.config}, mode {args.mode} "
                                f"({'encoders frozen, train-mode' if args.mode == 'A' else 'all trainable'})",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "size": args.size,
                    "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
@@ -273,7 +289,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(args, PR.default_parameters)
+            out["cpu_baseline"] = cpu_baseline(args, lambda: _cpu_params(PR, args))
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
