@@ -166,6 +166,8 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16
   }
 }
 
+constexpr int BUF_FLAGS_EP = 0x00020000;  // buffer descriptor word 3 (as BUF_FLAGS below)
+
 // bias / activation or BN partial statistics, LDS-staged 16-B stores
 template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / (16 * WMW)][BN / (16 * WNW)],
@@ -271,14 +273,29 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     const int col = n0 + cl;
     double s = 0.0, q = 0.0;
     if (col < a.Nout) {
-#pragma unroll 4
-      for (int t = part; t < a.mtiles; t += NP) {
-        const unsigned long long u = __hip_atomic_load(
-            (const unsigned long long*)(a.partials + ((size_t)t * a.Nout + col) * 2), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        const float2 v = *(const float2*)&u;
-        s += (double)v.x;
-        q += (double)v.y;
+      // sc1 buffer loads (the slab was stored write-through), 8 independent
+      // loads in flight per batch; fixed summation order (deterministic)
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          a.partials, 0, (int)((long long)a.mtiles * a.Nout * 8), BUF_FLAGS_EP);
+      const unsigned stride = (unsigned)(NP * a.Nout * 8);
+      unsigned off = (unsigned)((part * a.Nout + col) * 8);
+      int t = part;
+      for (; t + 7 * NP < a.mtiles; t += 8 * NP) {
+        uint2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rp, off + u * stride, 0, 16));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          s += (double)__uint_as_float(v[u].x);
+          q += (double)__uint_as_float(v[u].y);
+        }
+        off += 8 * stride;
+      }
+      for (; t < a.mtiles; t += NP, off += stride) {
+        const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rp, off, 0, 16));
+        s += (double)__uint_as_float(v.x);
+        q += (double)__uint_as_float(v.y);
       }
     }
     double* dred = (double*)(xtra + 64);

@@ -993,3 +993,86 @@ extern "C" int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* 
   DMF_LAUNCH_CHECK("dmf_mask_attn_fwd");
   return 0;
 }
+
+// ------------------------------------------------ adaptive average pooling
+// nn.AdaptiveAvgPool2d((Ho, Wo)) on NHWC (model_module.py:534 proj_pool when
+// the map size does not divide proj_dim, e.g. 48 -> 64 at S=384): output bin
+// i covers input rows [floor(i*H/Ho), ceil((i+1)*H/Ho)). One thread per
+// (output pixel, channel); the backward gathers, per input pixel, the bins
+// that contain it (no atomics).
+namespace dmf {
+__device__ __forceinline__ int ap_lo(int i, int in, int out) { return (int)(((long long)i * in) / out); }
+__device__ __forceinline__ int ap_hi(int i, int in, int out) { return (int)(((long long)(i + 1) * in + out - 1) / out); }
+
+template <typename T>
+__global__ void k_adaptive_avgpool(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int N, int H, int W,
+                                   int C, int Ho, int Wo) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long p = e / C;
+    const int j = (int)(p % Wo), i = (int)((p / Wo) % Ho), n = (int)(p / ((long long)Wo * Ho));
+    const int h0 = ap_lo(i, H, Ho), h1 = ap_hi(i, H, Ho), w0 = ap_lo(j, W, Wo), w1 = ap_hi(j, W, Wo);
+    float s = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) s += ld(x + ((size_t)(n * H + h) * W + w) * ldx + c);
+    st(y + p * ldy + c, s / (float)((h1 - h0) * (w1 - w0)));
+  }
+}
+
+template <typename T>
+__global__ void k_adaptive_avgpool_bwd(const T* __restrict__ dy, int lddy, T* __restrict__ dx, int lddx, int N, int H,
+                                       int W, int C, int Ho, int Wo) {
+  const long long total = (long long)N * H * W * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long p = e / C;
+    const int w = (int)(p % W), h = (int)((p / W) % H), n = (int)(p / ((long long)W * H));
+    // candidate output bins: floor(h*Ho/H) - 1 .. ceil((h+1)*Ho/H) (clamped)
+    const int i0 = max(0, (int)(((long long)h * Ho) / H) - 1), i1 = min(Ho, (int)(((long long)(h + 1) * Ho + H - 1) / H) + 1);
+    const int j0 = max(0, (int)(((long long)w * Wo) / W) - 1), j1 = min(Wo, (int)(((long long)(w + 1) * Wo + W - 1) / W) + 1);
+    float s = 0.f;
+    for (int i = i0; i < i1; ++i) {
+      const int a0 = ap_lo(i, H, Ho), a1 = ap_hi(i, H, Ho);
+      if (h < a0 || h >= a1) continue;
+      for (int j = j0; j < j1; ++j) {
+        const int b0 = ap_lo(j, W, Wo), b1 = ap_hi(j, W, Wo);
+        if (w < b0 || w >= b1) continue;
+        s += ld(dy + ((size_t)(n * Ho + i) * Wo + j) * lddy + c) / (float)((a1 - a0) * (b1 - b0));
+      }
+    }
+    st(dx + p * lddx + c, s);
+  }
+}
+}  // namespace dmf
+
+extern "C" int dmf_adaptive_avgpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho,
+                                      int Wo, int ldy, void* stream) {
+  DMF_CHECK_ARG(x && y && N > 0 && H > 0 && W > 0 && C > 0 && Ho > 0 && Wo > 0, "dmf_adaptive_avgpool2d: bad args");
+  const long long total = (long long)N * Ho * Wo * C;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_adaptive_avgpool<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ldx, (bf16_t*)y, ldy, N, H, W, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL(k_adaptive_avgpool<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)x, ldx, (float*)y, ldy, N, H, W, C, Ho, Wo);
+  DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d");
+  return 0;
+}
+
+extern "C" int dmf_adaptive_avgpool2d_bwd(int dtype, const void* dy, int N, int Ho, int Wo, int C, int lddy, void* dx,
+                                          int H, int W, int lddx, void* stream) {
+  DMF_CHECK_ARG(dy && dx && N > 0 && H > 0 && W > 0 && C > 0 && Ho > 0 && Wo > 0,
+                "dmf_adaptive_avgpool2d_bwd: bad args");
+  const long long total = (long long)N * H * W * C;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_adaptive_avgpool_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, N, H, W, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL(k_adaptive_avgpool_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, lddy, (float*)dx, lddx, N, H, W, C, Ho, Wo);
+  DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d_bwd");
+  return 0;
+}

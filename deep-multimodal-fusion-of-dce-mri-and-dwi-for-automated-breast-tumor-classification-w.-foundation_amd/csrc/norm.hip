@@ -78,15 +78,23 @@ __global__ void k_bn_finalize(const PT* __restrict__ part, int T, int C, BnFin f
 }
 
 // single-launch finalize for T <= 1024 tiles: block of 1024 threads =
-// 64 channels x 16 tile lanes, each lane summing T/16 tiles (double)
+// 16 channels x 64 tile lanes (T/64 independent loads per lane, then a
+// fixed-order LDS tree in double) -- C/16 blocks, so even C = 64 spreads
+// over 4 CUs and a lane waits for at most a few loads (latency-bound launch)
 __global__ void __launch_bounds__(1024) k_bn_finalize_wide(const float* __restrict__ part, int T, int C, BnFin f) {
-  __shared__ double red[16][64][2];
-  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double red[64][16][2];
+  const int cl = threadIdx.x & 15, tl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double s = 0.0, q = 0.0;
   if (c < C) {
-#pragma unroll 4
-    for (int t = tl; t < T; t += 16) {
+    int t = tl;
+    for (; t + 64 < T; t += 128) {
+      const float2 v0 = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      const float2 v1 = *(const float2*)(part + ((size_t)(t + 64) * C + c) * 2);
+      s += (double)v0.x + (double)v1.x;
+      q += (double)v0.y + (double)v1.y;
+    }
+    if (t < T) {
       const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
       s += (double)v.x;
       q += (double)v.y;
@@ -95,16 +103,15 @@ __global__ void __launch_bounds__(1024) k_bn_finalize_wide(const float* __restri
   red[tl][cl][0] = s;
   red[tl][cl][1] = q;
   __syncthreads();
-  if (tl == 0 && c < C) {
-    s = 0.0;
-    q = 0.0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s += red[i][cl][0];
-      q += red[i][cl][1];
+  for (int w = 32; w > 0; w >>= 1) {
+    if (tl < w) {
+      red[tl][cl][0] += red[tl + w][cl][0];
+      red[tl][cl][1] += red[tl + w][cl][1];
     }
-    bn_fin_channel(f, c, C, s, q);
+    __syncthreads();
   }
+  if (tl == 0 && c < C) bn_fin_channel(f, c, C, red[0][cl][0], red[0][cl][1]);
   if (f.nbt && blockIdx.x == 0 && threadIdx.x == 0) *f.nbt += 1;
 }
 
@@ -152,15 +159,15 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
                               const T* __restrict__ res, int ldr, const float* __restrict__ ssr, float p,
                               const unsigned long long* rng, int site, T* __restrict__ y, int ldy, long long M,
                               int C) {
-  const int cv = C >> 3;
-  const long long total = M * cv;
+  // 32-bit index math (the host routes M*C/8 >= 2^31 to k_affine_act)
+  const unsigned cv = (unsigned)C >> 3;
+  const unsigned total = (unsigned)(M * cv);
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long m = i / cv;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned m = i / cv;
     const int c0 = (int)(i - m * cv) << 3;
     float v[8], r[8];
-    ld8(x + m * ldx + c0, v);
+    ld8(x + (size_t)m * ldx + c0, v);
     if (ssa) {
       const float4 s0 = *(const float4*)(ssa + c0), s1 = *(const float4*)(ssa + c0 + 4);
       const float4 b0 = *(const float4*)(ssa + C + c0), b1 = *(const float4*)(ssa + C + c0 + 4);
@@ -168,7 +175,7 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
       v[4] = v[4] * s1.x + b1.x; v[5] = v[5] * s1.y + b1.y; v[6] = v[6] * s1.z + b1.z; v[7] = v[7] * s1.w + b1.w;
     }
     if (res) {
-      ld8(res + m * ldr + c0, r);
+      ld8(res + (size_t)m * ldr + c0, r);
       if (ssr) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = r[k] * ssr[c0 + k] + ssr[C + c0 + k];
@@ -184,14 +191,14 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
     }
     if (p > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+      dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * sc : 0.f;
-      dropout_keep4(rng, site, (unsigned long long)(m * C + c0 + 4), p, keep);
+      dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * sc : 0.f;
     }
-    st8(y + m * ldy + c0, v);
+    st8(y + (size_t)m * ldy + c0, v);
   }
 }
 
@@ -336,7 +343,7 @@ extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double 
   BnFin f{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, training,
           scale_shift, save_mean_invstd};
   if (training && ntiles > 64 && ntiles <= 1024) {
-    hipLaunchKernelGGL(k_bn_finalize_wide, dim3(cdiv(C, 64)), dim3(1024), 0, st_, partials, ntiles, C, f);
+    hipLaunchKernelGGL(k_bn_finalize_wide, dim3(cdiv(C, 16)), dim3(1024), 0, st_, partials, ntiles, C, f);
   } else if (training && ntiles > 64) {
     DMF_CHECK_ARG(workspace, "dmf_bn_finalize: %d tiles need a workspace (dmf_bn_finalize_ws_size)", ntiles);
     const int S = (ntiles + 31) / 32;
@@ -358,7 +365,7 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_affine_act: dropout needs rng state");
   DMF_CHECK_ARG(dropout_p < 1.f, "dmf_affine_act: dropout p must be < 1");
   if (M == 0) return 0;
-  const bool vec8 = C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!res || ldr % 8 == 0) &&
+  const bool vec8 = C % 8 == 0 && M * (C / 8) < (1LL << 31) && ldx % 8 == 0 && ldy % 8 == 0 && (!res || ldr % 8 == 0) &&
                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0) &&
                     (!scale_shift || ((uintptr_t)scale_shift % 16) == 0);
   if (vec8) {

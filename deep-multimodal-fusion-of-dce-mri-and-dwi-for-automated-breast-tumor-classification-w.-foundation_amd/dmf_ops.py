@@ -240,7 +240,7 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     return y, partials
 
 
-FUSED_BN_MAX_MTILES = 32  # the tile reducer reads mtiles slab rows serially: only pays for small problems
+FUSED_BN_MAX_MTILES = 32  # measured: at larger slabs every block's drain-before-ticket costs more than a finalize launch
 
 
 def _bn_site(bn, dev):
@@ -914,6 +914,33 @@ class _UpNearestFn(torch.autograd.Function):
         return dx, None
 
 
+class _AdaptivePoolFn(torch.autograd.Function):
+    """nn.AdaptiveAvgPool2d((ho, wo)) on an NHWC map (any ratio)."""
+
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        n, c, h, w, ld = nhwc(x)
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        N.call("dmf_adaptive_avgpool2d", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4],
+               _stream())
+        ctx.shape = (n, c, h, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.shape
+        dy = as_nhwc(dy)
+        _, _, ho, wo, lddy = nhwc(dy)
+        dx = empty_nhwc(n, c, h, w, dy.dtype, dy.device)
+        N.call("dmf_adaptive_avgpool2d_bwd", dt(dy), dy.data_ptr(), n, ho, wo, c, lddy, dx.data_ptr(), h, w,
+               nhwc(dx)[4], _stream())
+        return dx, None, None
+
+
+def adaptive_avgpool(x, ho, wo):
+    return _AdaptivePoolFn.apply(x, ho, wo)
+
+
 def upsample_nearest(x, r):
     return x if r == 1 else _UpNearestFn.apply(x, r)
 
@@ -1370,6 +1397,8 @@ class _ReconFn(torch.autograd.Function):
         k = len(maps)
         r0 = maps[0]
         b, _, h, w = r0.shape
+        if any(tuple(m.shape) != tuple(r0.shape) for m in maps):
+            raise ValueError("recon maps of one dmf_recon_loss launch must share [B,1,h,w] (use recon_terms)")
         s = tA.shape[-1] if tA is not None else tB.shape[-1]
         dev = r0.device
         prepared = []
@@ -1418,8 +1447,18 @@ class _ReconFn(torch.autograd.Function):
 
 def recon_terms(maps, sels, tA, tB=None, ca=0.0, cb=0.0):
     """Charbonnier recon terms for up to 5 single-channel maps; sel 0 -> tA,
-    1 -> tB, 2 -> ca*tA + cb*tB."""
-    return _ReconFn.apply(tA, tB, ca, cb, tuple(sels), *maps)
+    1 -> tB, 2 -> ca*tA + cb*tB. Maps of different sizes (config 5: the
+    encoders' 48x48 r1/r2 beside the fused 24x24 map) go to one launch per size."""
+    shapes = [tuple(m.shape) for m in maps]
+    if len(set(shapes)) == 1:
+        return _ReconFn.apply(tA, tB, ca, cb, tuple(sels), *maps)
+    out = [None] * len(maps)
+    for shp in dict.fromkeys(shapes):
+        idx = [i for i, s_ in enumerate(shapes) if s_ == shp]
+        v = _ReconFn.apply(tA, tB, ca, cb, tuple(sels[i] for i in idx), *[maps[i] for i in idx])
+        for j, i in enumerate(idx):
+            out[i] = v[j]
+    return torch.stack(out)
 
 
 class _MimicFn(torch.autograd.Function):

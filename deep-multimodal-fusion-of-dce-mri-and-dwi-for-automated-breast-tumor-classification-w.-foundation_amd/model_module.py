@@ -434,7 +434,8 @@ class ModelMaskHeadBackbone(nn.Module):
         h, w = f.shape[-2], f.shape[-1]
         if h == w and self.proj_dim % h == 0:
             return proj(f, replicate=self.proj_dim // h)
-        raise NotImplementedError(f"proj_pool from {tuple(f.shape[-2:])} to {self.proj_dim} is not built")
+        # general ratio (e.g. 48 -> 64 at S=384): materialize the pooled map
+        return proj(O.adaptive_avgpool(_to_compute(f, _dt(self)), self.proj_dim, self.proj_dim))
 
     def _stage_input(self, x):
         dt = _dt(self)

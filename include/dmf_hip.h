@@ -168,6 +168,11 @@ int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int 
                       int lddy, void* dx, int lddx, int k, int s, int p, void* stream);
 int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, int r,
                          void* stream);
+/* nn.AdaptiveAvgPool2d((Ho, Wo)) on NHWC, any ratio (proj_pool, model_module.py:534) */
+int dmf_adaptive_avgpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo,
+                           int ldy, void* stream);
+int dmf_adaptive_avgpool2d_bwd(int dtype, const void* dy, int N, int Ho, int Wo, int C, int lddy, void* dx, int H,
+                               int W, int lddx, void* stream);
 int dmf_upsample_nearest_bwd(int dtype, const void* dy, void* dx, int N, int H, int W, int C, int r, void* stream);
 int dmf_bilinear(int dtype, const void* x, int N, int Hi, int Wi, int C, int ldx, void* y, int Ho, int Wo, int ldy,
                  void* stream);

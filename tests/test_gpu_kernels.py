@@ -362,3 +362,41 @@ def test_recon_and_mimic_match_oracle():
     om.backward()
     assert abs(om.item() - refm.item()) < 1e-5
     assert torch.allclose(pd.grad.cpu(), pr.grad, atol=1e-6)
+
+
+@pytest.mark.parametrize("hw_out", [(64, 64), (20, 28)])
+def test_adaptive_avgpool_any_ratio(hw_out):
+    """proj_pool (model_module.py:534) at S=384: AdaptiveAvgPool2d 48 -> 64 (and a shrinking ratio)."""
+    torch.manual_seed(12)
+    x = torch.randn(2, 16, 48, 48)
+    xr = x.clone().requires_grad_(True)
+    ref = F.adaptive_avg_pool2d(xr, hw_out)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    xd = _to_dev(x, torch.float32).requires_grad_(True)
+    y = O.adaptive_avgpool(xd, *hw_out)
+    assert torch.allclose(y.cpu(), ref.detach(), atol=1e-5, rtol=1e-5)
+    y.backward(_to_dev(g, torch.float32))
+    assert torch.allclose(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_fused_recon_mixed_map_sizes():
+    """config 5: encoder recon maps 8x8 beside a 4x4 fused map (48x48 / 24x24 at
+    S=384) -- one launch per size, same value and grads as the oracle's three
+    compute_recon_list_loss calls (train_fusion.py:281-285)."""
+    torch.manual_seed(13)
+    from oracle import losses as L
+    import train_fusion as TF
+
+    dimg, cimg = torch.rand(2, 4, 32, 32), torch.rand(2, 3, 32, 32)
+    maps = [torch.randn(2, 1, 8, 8) for _ in range(4)] + [torch.randn(2, 1, 4, 4)]
+    ref_in = [m.clone().requires_grad_(True) for m in maps]
+    ref = (L.recon_list_loss(ref_in[0:2], dimg) + L.recon_list_loss(ref_in[2:4], cimg)
+           + L.recon_list_loss([ref_in[4]], torch.cat([dimg, cimg], 1))) / 3
+    ref.backward()
+    dev_in = [_to_dev(m, torch.float32).requires_grad_(True) for m in maps]
+    out = TF.fused_recon_losses(dev_in[0:2], dev_in[2:4], dev_in[4], dimg.to(DEV), cimg.to(DEV))
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-5
+    for a, b in zip(dev_in, ref_in):
+        assert torch.allclose(a.grad.cpu(), b.grad, atol=1e-6, rtol=1e-4)

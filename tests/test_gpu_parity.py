@@ -218,3 +218,45 @@ def test_bf16_full_width_training_steps_finite(mode):
     for n, buf in lm.named_buffers():
         if buf.dtype.is_floating_point:
             assert torch.isfinite(buf).all().item(), n
+
+
+def test_fusion_step_config5_hybrid_mode_b():
+    """Config 5 (hybrid TransformerStage, model_module.py:564-579 / :701-703) at a
+    reduced size that keeps its shape regime: S=192 -> f2 24x24 -> 144 tokens,
+    f3 12x12, proj_pool 24 -> 64 (non-integer ratio), fused recon map 12x12
+    beside 24x24 encoder maps. Everything trainable (mode B). Convs in the f32
+    parity mode; the transformer GEMMs are bf16, so the tolerance is the bf16
+    one (3e-2 relative on the loss, 5e-2 of the max on grads)."""
+    P = PR.small_parameters(channels=(16, 32, 64), input_size=192, dropout=0.0)
+    mp = P["dwi_model_parameters"]
+    mp["use_hybrid_transformer"] = True
+    mp["transformer_embed_dim"] = 256
+    mp["transformer_depth"] = 2
+    mp["transformer_heads"] = 4
+    P["backbone_freeze_on_start"] = False
+    dwi_m, dwi_r, P1 = build_pair(P, "dwi", 14, 31)
+    dce_m, dce_r, _ = build_pair(P, "dce", 6, 32)
+    P = P1
+    fm, fr = _fusion_pair(P, 33)
+    for m in (dwi_m, dce_m, fm, dwi_r, dce_r, fr):
+        for mod in m.modules():
+            if hasattr(mod, "p") and isinstance(getattr(mod, "p"), float):
+                mod.p = 0.0  # transformer dropouts: compare deterministic paths
+    train_labels = torch.arange(64) % 4
+    crit = get_classification_loss(P, train_labels, "fusion", DEV)
+    lm = TF.LightningFusionModel(dwi_m, dce_m, fm, P, crit)
+    lm.train()
+    for m in (dwi_r, dce_r, fr):
+        m.train()
+    bt = batch(4, 192, 17)
+    loss = lm.training_step(tuple(t.to(DEV) for t in bt))
+    loss.backward()
+    cw = OL.class_weights_from_labels(train_labels)
+    ref = OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, cw, epoch=0)
+    ref["total"].backward()
+    assert abs(loss.item() - ref["total"].item()) < 3e-2 * max(1, abs(ref["total"].item()))
+    named = dict(dwi_r.named_parameters())
+    for n, p1 in dwi_m.named_parameters():
+        if n.startswith("transformer.") and named[n].grad is not None:
+            g2 = named[n].grad
+            assert (p1.grad.cpu().reshape(g2.shape) - g2).abs().max() <= 5e-2 * max(1e-3, g2.abs().max().item()), n
