@@ -1317,6 +1317,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
 // torch Conv2d weight [Cout][Cin][KH][KW] (fp32 master) ->
 //   mode 0: [Cout][KH][KW][CinP]   (forward B operand, zero-padded channels)
 //   mode 1: [CinP][KH][KW][Cout]   (dgrad B operand)
+//   mode 2: [CinP][KH][KW][Cout] with the taps flipped (r -> KH-1-r, s -> KW-1-s):
+//           a stride-1 dgrad is then a forward conv of dY (pad' = dil*(K-1) - pad)
 template <typename T>
 __global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, int Cout, int Cin, int CinP, int KH,
                               int KW, int mode) {
@@ -1336,6 +1338,10 @@ __global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, 
       s = (int)(t % KW); t /= KW;
       r = (int)(t % KH);
       ci = (int)(t / KH);
+    }
+    if (mode == 2) {
+      r = KH - 1 - r;
+      s = KW - 1 - s;
     }
     const float v = ci < Cin ? w[(((long long)co * Cin + ci) * KH + r) * KW + s] : 0.f;
     out[i] = Cvt<T>::store(v);
@@ -1444,7 +1450,7 @@ extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo
 
 extern "C" int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW,
                                     int mode, void* stream) {
-  DMF_CHECK_ARG(CinP >= Cin && (mode == 0 || mode == 1), "dmf_conv_weight_prep: bad args");
+  DMF_CHECK_ARG(CinP >= Cin && mode >= 0 && mode <= 2, "dmf_conv_weight_prep: bad args");
   const long long total = (long long)Cout * CinP * KH * KW;
   const int grid = (int)(total < 65536 * 256LL ? cdiv(total, 256) : 65536);
   if (dtype == DMF_BF16)

@@ -179,6 +179,195 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
       }
 }
 
+// bf16 weight gradient on transposed LDS reads. Both operands stay pixel-major
+// in LDS exactly as they arrive from HBM (16-B channel vectors, one 256-B row
+// per pixel per 128-channel sub-image), and the MFMA fragments, which want 8
+// consecutive pixels per lane, are gathered with ds_read_b64_tr_b16 (two
+// 4-pixel x 16-channel blocks per fragment). Sub-image byte layout: 256-B rows
+// with the 16-B chunk XOR (((row&3)<<2)|((row>>2)&3)), conflict-free for the
+// 16x16x32 transposed reads. Register-staged double buffer, one barrier per
+// 64-pixel K-step; each thread walks its gather rows' (n,ho,wo) incrementally.
+typedef short v4s_w __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_w lds_v4s_w;
+
+__device__ __forceinline__ int wtr_off(int row, int ch) {
+  return (row << 8) + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+template <int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_wgrad_tr(WgArgs a) {
+  constexpr int T = 64 * WM * WN;
+  constexpr int BM = 64 * WM, BN = 64 * WN, BK = 64;
+  constexpr int SUB = BK * 256;                      // one 128-channel sub-image
+  constexpr int STAGE = (BM / 128 + BN / 128) * SUB;  // A sub-images, then B
+  constexpr int CPRA = BM / 8, RPPA = T / CPRA, PA = BK / RPPA;
+  constexpr int CPRB = BN / 8, RPPB = T / CPRB, PB = BK / RPPB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x % a.ntiles;
+  const int co0 = mt * BM, k0 = nt * BN;
+  const int p_begin = blockIdx.y * a.pix_per_split;
+  const int p_end = min(a.M, p_begin + a.pix_per_split);
+  const bf16_t* __restrict__ DY = (const bf16_t*)a.dy;
+
+  // A loader: chunk of dY row (channels co0 + 8*ca ..)
+  const int ca = tid % CPRA, ra = tid / CPRA;
+  const int cocol = co0 + ca * 8;
+  const bool cook = cocol < a.Cout;
+  // B loader: chunk column -> (tap, ci, source), fixed per thread
+  const int cb = tid % CPRB, rb = tid / CPRB;
+  const int kcol = k0 + cb * 8;
+  const bool kok = kcol < a.Ktot;
+  const int tap = kok ? kcol / a.Cin : 0;
+  int ci = kcol - tap * a.Cin;
+  const bf16_t* xsrc = (const bf16_t*)a.x;
+  int ldxs = a.ldx;
+  if (ci >= a.C1) {
+    xsrc = (const bf16_t*)a.x2;
+    ci -= a.C1;
+    ldxs = a.ldx2;
+  }
+  const int roff = (tap / a.KW) * a.dil - a.pad, soff = (tap % a.KW) * a.dil - a.pad;
+  // gather-row cursors (n, ho, wo) of this thread's B rows at the current K-step
+  int bn_[PB], bho[PB], bwo[PB];
+  {
+    const int hw = a.Ho * a.Wo;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int p = p_begin + rb + i * RPPB;
+      bn_[i] = p / hw;
+      const int rem = p - bn_[i] * hw;
+      bho[i] = rem / a.Wo;
+      bwo[i] = rem - bho[i] * a.Wo;
+    }
+  }
+  const int dho = BK / a.Wo, dwo = BK % a.Wo;
+
+  uint4 sa[PA], sb[PB];
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int p = kb + ra + i * RPPA;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (cook && p < p_end) v = *(const uint4*)(DY + (size_t)p * a.lddy + cocol);
+      sa[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int p = kb + rb + i * RPPB;
+      const int hi = bho[i] * a.stride + roff, wi = bwo[i] * a.stride + soff;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kok && p < p_end && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
+        v = *(const uint4*)(xsrc + ((size_t)(bn_[i] * a.H + hi) * a.W + wi) * ldxs + ci);
+      sb[i] = v;
+      // advance this row's cursor by one K-step
+      int wo = bwo[i] + dwo, ho = bho[i] + dho, n = bn_[i];
+      if (wo >= a.Wo) { wo -= a.Wo; ++ho; }
+      while (ho >= a.Ho) { ho -= a.Ho; ++n; }
+      bwo[i] = wo; bho[i] = ho; bn_[i] = n;
+    }
+  };
+  auto lds_store = [&](int stage) {
+    char* S = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int cc = ca * 8;
+      *(uint4*)(S + (cc >> 7) * SUB + wtr_off(ra + i * RPPA, (cc & 127) >> 3)) = sa[i];
+    }
+    char* SB = S + (BM / 128) * SUB;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int cc = cb * 8;
+      *(uint4*)(SB + (cc >> 7) * SUB + wtr_off(rb + i * RPPB, (cc & 127) >> 3)) = sb[i];
+    }
+  };
+
+  f32x4_w acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p_end - p_begin + BK - 1) / BK;
+  if (nk > 0) {
+    gload(p_begin);
+    lds_store(0);
+  }
+  __syncthreads();
+  // transposed-read lane roles: group g, block row q, 4-column quarter p4
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(p_begin + (kt + 1) * BK);
+    const char* SA = smem + cur * STAGE;
+    const char* SB = SA + (BM / 128) * SUB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_w af[4], bfr[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int cl = wm * 64 + i * 16;
+          const char* pa = SA + (cl >> 7) * SUB + wtr_off(row, ((cl & 127) >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pa);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cl = wn * 64 + j * 16;
+          const char* pb = SB + (cl >> 7) * SUB + wtr_off(row, ((cl & 127) >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lds_store(cur ^ 1);
+    __syncthreads();
+  }
+  float* slab = a.ws + (size_t)blockIdx.y * a.Cout * a.Ktot;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * 64 + i * 16 + fg * 4 + e;
+        const int k = k0 + wn * 64 + j * 16 + fr;
+        if (co < a.Cout && k < a.Ktot) slab[(size_t)co * a.Ktot + k] = acc[i][j][e];
+      }
+}
+
+// Gate gradient of a channel-gated conv input y = x * gate[n][c] (the SE
+// block in front of the backbone stem, model_module.py:584-591) from the
+// per-sample weight-gradient slabs G_n = sum_{pixels of n} dY (x) im2col(y):
+//   sum_hw dL/dy[n,c,h,w] * y[n,c,h,w] = sum_{co,r,s} W[co][c][r][s] * G_n[co][(r,s,c)]
+// so dgate[n][c] = that / gate[n][c]; the stem's input gradient is never formed.
+__global__ void k_gate_grad_wslab(const float* __restrict__ ws, int Cout, int C, int CinP, int KK,
+                                  const float* __restrict__ w, const float* __restrict__ gate,
+                                  float* __restrict__ dgate) {
+  __shared__ float red[16];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const float* slab = ws + (size_t)n * Cout * KK * CinP;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < Cout * KK; i += blockDim.x) {
+    const int co = i / KK, t = i - co * KK;
+    acc += w[((size_t)co * C + c) * KK + t] * slab[((size_t)co * KK + t) * CinP + c];
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) dgate[(size_t)n * C + c] = acc / gate[(size_t)n * C + c];
+}
+
 // sum slabs, reorder [Cout][KH][KW][CinP] -> torch [Cout][Cin][KH][KW], accumulate
 __global__ void k_wgrad_reduce(const float* __restrict__ ws, int splits, int Cout, int Cin, int CinP, int KH, int KW,
                                float* __restrict__ dw, int accumulate) {
@@ -418,15 +607,29 @@ static inline int gsz(long long n) {
 
 using namespace dmf;
 
+static int wgrad_tr_enabled() {
+  static int v = [] {
+    const char* e = std::getenv("DMF_WGRAD_TR");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
+}
+
 extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M) {
-  (void)dtype;
   const long long tiles = (long long)cdiv(Cout, 128) * cdiv((long long)KH * KW * Cin, 128);
-  long long want = (1024 + tiles - 1) / tiles;      // aim for ~1024 blocks
+  // transposed-read kernel: ~2 resident blocks per CU, and every split costs
+  // a Cout x K fp32 slab round trip, so aim for one wave of 512 blocks
+  const long long target = (dtype == DMF_BF16 && wgrad_tr_enabled()) ? 512 : 1024;
+  long long want = (target + tiles - 1) / tiles;
   long long maxs = (M + 1023) / 1024;              // >= 1024 pixels per split
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   if (want > 512) want = 512;
   return (int)want;
+}
+
+extern "C" int dmf_conv2d_wgrad_pixel_step(int dtype) {
+  return dtype == DMF_BF16 ? 64 : 32;
 }
 
 extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
@@ -451,11 +654,15 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
   a.mtiles = cdiv(Cout, 128);
   a.ntiles = cdiv(a.Ktot, 128);
   a.splits = splits;
-  const int bk = 8 * epc;
+  const int bk = dtype == DMF_BF16 ? 64 : 8 * epc;
   a.pix_per_split = cdiv(cdiv(a.M, splits), bk) * bk;
   dim3 grid(a.mtiles * a.ntiles, splits);
   const size_t lds = 2 * 2 * 128 * 128;
-  if (dtype == DMF_BF16)
+  DMF_CHECK_ARG((uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && (!x2 || (uintptr_t)x2 % 16 == 0),
+                "dmf_conv2d_wgrad: pointers must be 16-byte aligned");
+  if (dtype == DMF_BF16 && wgrad_tr_enabled())
+    hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+  else if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_conv_wgrad<bf16_t>, grid, dim3(256), lds, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(k_conv_wgrad<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
@@ -470,6 +677,16 @@ extern "C" int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int C
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, workspace, splits, Cout, Cin,
                      CinP, KH, KW, dw, accumulate);
   DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");
+  return 0;
+}
+
+extern "C" int dmf_conv2d_wgrad_gate(const float* workspace, int N, int Cout, int Cin, int CinP, int KH, int KW,
+                                     const float* w, const float* gate, float* dgate, void* stream) {
+  DMF_CHECK_ARG(workspace && w && gate && dgate && N > 0 && Cin > 0 && CinP >= Cin,
+                "dmf_conv2d_wgrad_gate: bad args");
+  hipLaunchKernelGGL(k_gate_grad_wslab, dim3(Cin, N), dim3(256), 0, (hipStream_t)stream, workspace, Cout, Cin, CinP,
+                     KH * KW, w, gate, dgate);
+  DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_gate");
   return 0;
 }
 

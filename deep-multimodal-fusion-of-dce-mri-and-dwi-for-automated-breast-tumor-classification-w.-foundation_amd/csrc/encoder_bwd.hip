@@ -52,9 +52,11 @@ __device__ __forceinline__ void ma_stats(const MaskAttnB& P, const float* stats,
   rs = rsqrtf(fmaxf(mw2 * mm2 - mu * mu, 0.f) + P.eps);
 }
 
-// pass 1: block per sample, one wave per pixel at a time.
+// pass 1: grid (sample, 64-pixel slice), one wave per pixel at a time.
 // grads layout: [hid] dw1, [hid] dgn_w, [hid] dgn_b, [hid] dw2, [1] db2, [1] dgamma
-// ws: dhh [N][HW][hid], then S [N][2]
+// ws: dhh [N][HW][hid], then S [N][slices][2] (per-slice partial sums, summed
+// in order by pass 2)
+constexpr int MA_PIX = 64;
 template <typename T>
 __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* __restrict__ f, int ldf,
                                  const T* __restrict__ m, MaskAttnB P, const float* __restrict__ stats, int HW, int C,
@@ -68,7 +70,8 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
   ma_stats(P, stats, n, HW, mu, rs);
   float a_gw = 0.f, a_gb = 0.f, a_w2 = 0.f;  // lane c < hid
   float a_db2 = 0.f, a_dgam = 0.f, a_s1 = 0.f, a_s2 = 0.f;
-  for (int p = wid; p < HW; p += 4) {
+  const int p_end = min(HW, (int)(blockIdx.y + 1) * MA_PIX);
+  for (int p = blockIdx.y * MA_PIX + wid; p < p_end; p += 4) {
     const long long pix = (long long)n * HW + p;
     const float mv = ld(m + pix);
     // recompute forward for this pixel (every lane computes the scalar z)
@@ -78,11 +81,25 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
     const float A = fminf(fmaxf(s, 1e-4f), 1.f - 1e-4f);
     const float gam = P.gamma[0];
     float gsum = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float d = ld(dout + pix * lddo + c);
-      const float fv = ld(f + pix * ldf + c);
-      gsum += d * fv;
-      st(df + pix * lddf + c, d * (1.f + gam * A));
+    if (sizeof(T) == 2 && (C & 7) == 0 && ((lddo | ldf | lddf) & 7) == 0) {
+      for (int c = lane * 8; c < C; c += 512) {
+        float d[8], fv[8];
+        ld8(dout + pix * lddo + c, d);
+        ld8(f + pix * ldf + c, fv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          gsum += d[e] * fv[e];
+          d[e] *= 1.f + gam * A;
+        }
+        st8(df + pix * lddf + c, d);
+      }
+    } else {
+      for (int c = lane; c < C; c += 64) {
+        const float d = ld(dout + pix * lddo + c);
+        const float fv = ld(f + pix * ldf + c);
+        gsum += d * fv;
+        st(df + pix * lddf + c, d * (1.f + gam * A));
+      }
     }
     gsum = wave_sum(gsum);
     const float dA = gsum * gam;
@@ -132,8 +149,8 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
       for (int k = 0; k < 4; ++k) t[k] += sw[w][k];
     atomicAdd(grads + 4 * P.hid, t[0]);
     atomicAdd(grads + 4 * P.hid + 1, t[1]);
-    S[2 * n] = t[2];
-    S[2 * n + 1] = t[3];
+    S[2 * ((size_t)n * gridDim.y + blockIdx.y)] = t[2];
+    S[2 * ((size_t)n * gridDim.y + blockIdx.y) + 1] = t[3];
   }
 }
 
@@ -148,9 +165,15 @@ __global__ void k_mask_attn_bwd2(const T* __restrict__ m, MaskAttnB P, const flo
   float mu, rs;
   ma_stats(P, stats, n, HW, mu, rs);
   const float G = (float)P.hid * HW;
-  const float m1 = S[2 * n] / G, m2 = S[2 * n + 1] / G;
+  float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < (int)gridDim.y; ++j) {
+    s1 += S[2 * ((size_t)n * gridDim.y + j)];
+    s2 += S[2 * ((size_t)n * gridDim.y + j) + 1];
+  }
+  const float m1 = s1 / G, m2 = s2 / G;
   float a_w1 = 0.f;
-  for (int p = wid; p < HW; p += 4) {
+  const int p_end = min(HW, (int)(blockIdx.y + 1) * MA_PIX);
+  for (int p = blockIdx.y * MA_PIX + wid; p < p_end; p += 4) {
     const long long pix = (long long)n * HW + p;
     const float mv = ld(m + pix);
     float contrib = 0.f;
@@ -191,6 +214,10 @@ extern "C" int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, i
   return 0;
 }
 
+extern "C" int dmf_mask_attn_bwd_ws_size(int N, int HW, int hidden) {
+  return (int)((long long)N * HW * hidden + 2LL * N * cdiv(HW, MA_PIX));
+}
+
 extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int ldf, const void* m, int N,
                                  int HW, int C, const float* w1, const float* gn_w, const float* gn_b, const float* w2,
                                  const float* b2, const float* gamma, int hidden, float eps, const float* stats,
@@ -202,15 +229,16 @@ extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const vo
   float* dhh = workspace;
   float* S = workspace + (size_t)N * HW * hidden;
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(N, cdiv(HW, MA_PIX));
   if (dtype == DMF_BF16) {
-    hipLaunchKernelGGL(k_mask_attn_bwd1<bf16_t>, dim3(N), dim3(256), 0, s, (const bf16_t*)dout, lddo, (const bf16_t*)f,
+    hipLaunchKernelGGL(k_mask_attn_bwd1<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, lddo, (const bf16_t*)f,
                        ldf, (const bf16_t*)m, P, stats, HW, C, (bf16_t*)df, lddf, dhh, S, grads);
-    hipLaunchKernelGGL(k_mask_attn_bwd2<bf16_t>, dim3(N), dim3(256), 0, s, (const bf16_t*)m, P, stats, HW, dhh, S,
+    hipLaunchKernelGGL(k_mask_attn_bwd2<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)m, P, stats, HW, dhh, S,
                        (bf16_t*)dm, grads);
   } else {
-    hipLaunchKernelGGL(k_mask_attn_bwd1<float>, dim3(N), dim3(256), 0, s, (const float*)dout, lddo, (const float*)f,
+    hipLaunchKernelGGL(k_mask_attn_bwd1<float>, grid, dim3(256), 0, s, (const float*)dout, lddo, (const float*)f,
                        ldf, (const float*)m, P, stats, HW, C, (float*)df, lddf, dhh, S, grads);
-    hipLaunchKernelGGL(k_mask_attn_bwd2<float>, dim3(N), dim3(256), 0, s, (const float*)m, P, stats, HW, dhh, S,
+    hipLaunchKernelGGL(k_mask_attn_bwd2<float>, grid, dim3(256), 0, s, (const float*)m, P, stats, HW, dhh, S,
                        (float*)dm, grads);
   }
   DMF_LAUNCH_CHECK("dmf_mask_attn_bwd");

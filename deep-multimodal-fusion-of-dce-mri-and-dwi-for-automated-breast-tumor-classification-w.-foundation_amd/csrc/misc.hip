@@ -244,6 +244,53 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int 
   }
 }
 
+// 8 channels per thread (16-B loads): the window argmax recompute per candidate
+// output reads 16-B vectors instead of scalars
+template <typename T>
+__global__ void k_maxpool_bwd8(const T* __restrict__ x, int N, int H, int W, int C, int ldx, const T* __restrict__ dy,
+                               int Ho, int Wo, int lddy, T* __restrict__ dx, int lddx, int k, int s, int p) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * H * W * C8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const long long pix = i / C8;
+    const int n = (int)(pix / (H * W));
+    const int rem = (int)(pix - (long long)n * H * W);
+    const int h = rem / W, w = rem % W;
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
+    const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        float m[8];
+        int am[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { m[e] = -INFINITY; am[e] = -1; }
+        for (int r = 0; r < k; ++r) {
+          const int hi = ho * s - p + r;
+          if (hi < 0 || hi >= H) continue;
+          for (int q = 0; q < k; ++q) {
+            const int wi = wo * s - p + q;
+            if (wi < 0 || wi >= W) continue;
+            float v[8];
+            ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + c, v);
+            const int pos = hi * W + wi;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (v[e] > m[e] || (isnan(v[e]) && !isnan(m[e]))) { m[e] = v[e]; am[e] = pos; }
+          }
+        }
+        float d[8];
+        ld8(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy + c, d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (am[e] == rem) g[e] += d[e];
+      }
+    st8(dx + pix * lddx + c, g);
+  }
+}
+
 // ----------------------------------------------------------- resampling
 template <typename T>
 __global__ void k_up_nearest(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C, int r) {
@@ -877,6 +924,16 @@ extern "C" int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, 
   DMF_CHECK_ARG(x && dy && dx, "dmf_maxpool2d_bwd: bad args");
   const long long total = (long long)N * H * W * C;
   if (total == 0) return 0;
+  if (v8ok(C, ldx, lddy, x, dy, dx) && lddx % 8 == 0) {
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_maxpool_bwd8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, N, H, W, C, ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, k, s, p);
+    else
+      hipLaunchKernelGGL(k_maxpool_bwd8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)x, N, H, W, C, ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, k, s, p);
+    DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_maxpool_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        N, H, W, C, ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, k, s, p);

@@ -317,6 +317,153 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dz, int lddz, const T* __re
   }
 }
 
+// Fused activation/dropout backward + BatchNorm backward column reduction:
+// dz (= k_act_bwd's output) is written once and the per-tile BN partials
+// (sum dz, sum dz*xhat) of the same 256-row tile come out of the same pass
+// (k_bn_bwd_reduce would re-read dz and x). Block = 32 row lanes x 8 channel
+// lanes of 8 channels (64 channels), 16-B accesses; x is the BN input (the
+// raw conv output), z = x*ssa + shift (+ residual) recomputed for act'.
+template <typename T, int ACT>
+__global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy, int lddy, const T* __restrict__ x,
+                                                        int ldx, const float* __restrict__ ssa,
+                                                        const T* __restrict__ res, int ldr,
+                                                        const float* __restrict__ ssr, float p,
+                                                        const unsigned long long* rng, int site,
+                                                        const float* __restrict__ save, T* __restrict__ dz, int lddz,
+                                                        long long M, int C, float* __restrict__ part) {
+  __shared__ float red[32][65 * 2];
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.y * 64 + cl * 8;
+  const long long r0 = (long long)blockIdx.x * 256;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (c0 < C) {
+    float mean[8], inv[8], a[8], b[8], ra[8], rb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mean[e] = save[c0 + e];
+      inv[e] = save[C + c0 + e];
+      a[e] = ssa[c0 + e];
+      b[e] = ssa[C + c0 + e];
+      ra[e] = ssr ? ssr[c0 + e] : 1.f;
+      rb[e] = ssr ? ssr[C + c0 + e] : 0.f;
+    }
+    for (int r = rl; r < 256; r += 32) {
+      const long long m = r0 + r;
+      if (m >= M) break;
+      float g[8], xv[8];
+      ld8(dy + m * lddy + c0, g);
+      ld8(x + m * ldx + c0, xv);
+      if (p > 0.f) {
+        bool keep[4];
+        dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] = keep[k] ? g[k] * sc : 0.f;
+        dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[4 + k] = keep[k] ? g[4 + k] * sc : 0.f;
+      }
+      if (ACT != DMF_ACT_NONE) {
+        float z[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = xv[e] * a[e] + b[e];
+        if (res) {
+          float rv[8];
+          ld8(res + m * ldr + c0, rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) z[e] += rv[e] * ra[e] + rb[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] *= act_grad(ACT, z[e]);
+      }
+      st8(dz + m * lddz + c0, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += g[e];
+        q[e] += g[e] * (xv[e] - mean[e]) * inv[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[rl][(cl * 8 + e) * 2] = s[e];
+    red[rl][(cl * 8 + e) * 2 + 1] = q[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int c = threadIdx.x >> 1, w = threadIdx.x & 1;
+    float t = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < 32; ++r) t += red[r][c * 2 + w];
+    const int cg = blockIdx.y * 64 + c;
+    if (cg < C) part[((size_t)blockIdx.x * C + cg) * 2 + w] = t;
+  }
+}
+
+// BN backward apply, 8 channels per thread: dx = A*dz + Cc*x + B
+template <typename T>
+__global__ void k_bn_bwd_apply8(const T* __restrict__ dz, int lddz, const T* __restrict__ x, int ldx,
+                                const float* __restrict__ coef, T* __restrict__ dx, int lddx, long long M, int C) {
+  const unsigned cv = (unsigned)C >> 3;
+  const unsigned total = (unsigned)(M * cv);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned m = i / cv;
+    const int c0 = (int)(i - m * cv) << 3;
+    float g[8], xv[8];
+    ld8(dz + (size_t)m * lddz + c0, g);
+    ld8(x + (size_t)m * ldx + c0, xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = coef[c0 + e] * g[e] + coef[C + c0 + e] * xv[e] + coef[2 * C + c0 + e];
+    st8(dx + (size_t)m * lddx + c0, g);
+  }
+}
+
+// dmf_bn_bwd_finalize for many tiles: 16 channels x 64 tile lanes per block
+__global__ void __launch_bounds__(1024) k_bn_bwd_finalize_wide(const float* __restrict__ part, int T, int C,
+                                                               double count, int training,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ save, float* dgamma,
+                                                               float* dbeta, float* __restrict__ coef) {
+  __shared__ double red[64][16][2];
+  const int cl = threadIdx.x & 15, tl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int t = tl; t < T; t += 64) {
+      const float2 v = *(const float2*)(part + ((size_t)t * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
+  red[tl][cl][0] = s;
+  red[tl][cl][1] = q;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    if (tl < o) {
+      red[tl][cl][0] += red[tl + o][cl][0];
+      red[tl][cl][1] += red[tl + o][cl][1];
+    }
+    __syncthreads();
+  }
+  if (tl == 0 && c < C) {
+    s = red[0][cl][0];
+    q = red[0][cl][1];
+    if (dbeta) dbeta[c] += (float)s;
+    if (dgamma) dgamma[c] += (float)q;
+    if (coef) {
+      const double g = gamma ? gamma[c] : 1.0;
+      const double mean = save[c], inv = save[C + c];
+      const double A = g * inv;
+      const double Cc = training ? -g * inv * inv * q / count : 0.0;
+      const double B = training ? -g * inv * s / count - Cc * mean : 0.0;
+      coef[c] = (float)A;
+      coef[C + c] = (float)Cc;
+      coef[2 * C + c] = (float)B;
+    }
+  }
+}
+
 static inline int grid_for(long long n, int block = 256) {
   long long g = (n + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -451,8 +598,12 @@ extern "C" int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, dou
                                    float* coef, void* stream) {
   DMF_CHECK_ARG(partials && ntiles > 0 && C > 0, "dmf_bn_bwd_finalize: bad args");
   DMF_CHECK_ARG(!coef || save_mean_invstd, "dmf_bn_bwd_finalize: coef needs saved stats");
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C,
-                     count, training, gamma, save_mean_invstd, dgamma, dbeta, coef);
+  if (ntiles > 64)
+    hipLaunchKernelGGL(k_bn_bwd_finalize_wide, dim3(cdiv(C, 16)), dim3(1024), 0, (hipStream_t)stream, partials, ntiles,
+                       C, count, training, gamma, save_mean_invstd, dgamma, dbeta, coef);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, partials, ntiles, C,
+                       count, training, gamma, save_mean_invstd, dgamma, dbeta, coef);
   DMF_LAUNCH_CHECK("dmf_bn_bwd_finalize");
   return 0;
 }
@@ -461,6 +612,18 @@ extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void*
                                 void* dx, int lddx, long long M, int C, void* stream) {
   DMF_CHECK_ARG(dz && x && coef && dx, "dmf_bn_bwd_apply: bad args");
   if (M == 0) return 0;
+  if (C % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && lddx % 8 == 0 && M * (C / 8) < (1LL << 31) &&
+      ((uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx) % 16 == 0) {
+    const int g8 = grid_for(M * (C / 8));
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_bn_bwd_apply8<bf16_t>, dim3(g8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz,
+                         lddz, (const bf16_t*)x, ldx, coef, (bf16_t*)dx, lddx, M, C);
+    else
+      hipLaunchKernelGGL(k_bn_bwd_apply8<float>, dim3(g8), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
+                         (const float*)x, ldx, coef, (float*)dx, lddx, M, C);
+    DMF_LAUNCH_CHECK("dmf_bn_bwd_apply");
+    return 0;
+  }
   const int g = grid_for(M * C);
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_bn_bwd_apply<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
@@ -469,5 +632,46 @@ extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void*
     hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
                        (const float*)x, ldx, coef, (float*)dx, lddx, M, C);
   DMF_LAUNCH_CHECK("dmf_bn_bwd_apply");
+  return 0;
+}
+
+extern "C" int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, int ldx,
+                                     const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
+                                     int act, float dropout_p, const unsigned long long* rng, int site,
+                                     const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
+                                     float* partials, void* stream) {
+  DMF_CHECK_ARG(dy && x && scale_shift && save_mean_invstd && dz && partials && M > 0 && C > 0,
+                "dmf_act_bwd_bn_reduce: bad args");
+  DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_act_bwd_bn_reduce: dropout needs rng state");
+  const bool vec8 = C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
+                    ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz)) % 16 == 0;
+  if (!vec8) {
+    int rc = dmf_act_bwd(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng, site,
+                         dz, lddz, M, C, stream);
+    if (rc) return rc;
+    return dmf_bn_bwd_reduce(dtype, dz, lddz, x, ldx, save_mean_invstd, M, C, partials, stream);
+  }
+  const long long tiles = (M + 255) / 256;
+  DMF_CHECK_ARG(tiles < 65536LL * 32768LL, "dmf_act_bwd_bn_reduce: too many rows");
+  dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
+  hipStream_t s = (hipStream_t)stream;
+#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials)
+  if (dtype == DMF_BF16) {
+    switch (act) {
+      case DMF_ACT_RELU: DMF_ABR(bf16_t, DMF_ACT_RELU); break;
+      case DMF_ACT_GELU: DMF_ABR(bf16_t, DMF_ACT_GELU); break;
+      case DMF_ACT_SIGMOID: DMF_ABR(bf16_t, DMF_ACT_SIGMOID); break;
+      default: DMF_ABR(bf16_t, DMF_ACT_NONE);
+    }
+  } else {
+    switch (act) {
+      case DMF_ACT_RELU: DMF_ABR(float, DMF_ACT_RELU); break;
+      case DMF_ACT_GELU: DMF_ABR(float, DMF_ACT_GELU); break;
+      case DMF_ACT_SIGMOID: DMF_ABR(float, DMF_ACT_SIGMOID); break;
+      default: DMF_ABR(float, DMF_ACT_NONE);
+    }
+  }
+#undef DMF_ABR
+  DMF_LAUNCH_CHECK("dmf_act_bwd_bn_reduce");
   return 0;
 }

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 
 import torch
 
@@ -240,6 +241,7 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     return y, partials
 
 
+DGRAD_AS_FWD = os.environ.get("DMF_DGRAD_FWD", "1") != "0"
 FUSED_BN_MAX_MTILES = 32  # measured: at larger slabs every block's drain-before-ticket costs more than a finalize launch
 
 
@@ -307,9 +309,11 @@ def _col_stats(y):
     return part
 
 
-def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None):
+def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None, gate_holder=None):
     """Returns (dx, dw, db) -- with x2 given, dx is (dx, dx2) (views into one
-    concat-gradient buffer)."""
+    concat-gradient buffer). gate_holder: x is the channel-gated network
+    input (_InputFn); its gradient is then only needed for the gate, which
+    comes from per-sample weight-gradient slabs (dx is a zero placeholder)."""
     n, cx, h, w, ldx = nhwc(x)
     cx2, ldx2 = 0, 0
     if x2 is not None:
@@ -321,6 +325,24 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
     dev = x.device
     dx = dw = db = None
     m = n * ho * wo
+    if (gate_holder is not None and need_dx and x2 is None and _is_mfma_conv(weight, g)
+            and (ho * wo) % N.load().dmf_conv2d_wgrad_pixel_step(dtc) == 0):
+        gate = gate_holder["gate"]
+        ws = torch.empty(n * co * kh * kw * cx, dtype=torch.float32, device=dev)
+        N.call("dmf_conv2d_wgrad", dtc, x.data_ptr(), n, h, w, cx, ldx, None, 0, 0, dy.data_ptr(), ho, wo, co,
+               lddy, kh, kw, g.stride, g.pad, g.dil, n, ws.data_ptr(), _stream())
+        wf = weight.detach().float().contiguous()
+        dgate = torch.empty((n, ci), dtype=torch.float32, device=dev)
+        N.call("dmf_conv2d_wgrad_gate", ws.data_ptr(), n, co, ci, cx, kh, kw, wf.data_ptr(), gate.data_ptr(),
+               dgate.data_ptr(), _stream())
+        gate_holder["dgate"] = dgate
+        if need_dw:
+            dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dev)
+            N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), n, co, ci, cx, kh, kw, dw.data_ptr(), 0, _stream())
+        if need_db:
+            db = _colsum_nhwc(dy)
+        dx = torch.zeros((), dtype=x.dtype, device=dev).expand(n, cx, h, w)
+        return dx, dw, db
     if need_dx:
         dx = empty_nhwc(n, cx + cx2, h, w, x.dtype, dev)
         _, _, _, _, lddx = nhwc(dx)
@@ -332,6 +354,13 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
             wf = weight.detach().reshape(co).contiguous()
             N.call("dmf_conv_cin1_dgrad", dtc, dy.data_ptr(), lddy, wf.data_ptr(), dx.data_ptr(), lddx, n * h * w, co,
                    _stream())
+        elif g.stride == 1 and g.dil * (kh - 1) >= g.pad and kh == kw and DGRAD_AS_FWD:
+            # stride 1: dX = conv(dY, flipped W^T, pad' = dil*(k-1) - pad), so the
+            # dgrad runs on the forward kernels (LDS-DMA tiles included)
+            wt = caches[1].get(weight, x.dtype, cx + cx2, 2)
+            N.call("dmf_conv2d_fwd", dtc, dy.data_ptr(), n, ho, wo, co, lddy, None, 0, 0, wt.data_ptr(), cx + cx2,
+                   kh, kw, 1, g.dil * (kh - 1) - g.pad, g.dil, None, dx.data_ptr(), h, w, lddx, None, N.ACT_NONE,
+                   None, N.ACT_NONE, _stream())
         else:
             wt = caches[1].get(weight, x.dtype, cx + cx2, 1)
             N.call("dmf_conv2d_dgrad", dtc, dy.data_ptr(), n, ho, wo, co, lddy, wt.data_ptr(), cx + cx2, kh, kw,
@@ -454,6 +483,7 @@ class _ConvBNActFn(torch.autograd.Function):
     def forward(ctx, x, x2, w, b, gamma, beta, res, xr, wr, gamma_r, beta_r, spec):
         (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act) = spec
         y, ss, save = _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss, in_act=in_act)
+        ctx.gate_holder = x.__dict__.get("_dmf_gate")
         n, c, ho, wo, ldy = nhwc(y)
         m = n * ho * wo
         yr = ss_r = save_r = None
@@ -484,14 +514,19 @@ class _ConvBNActFn(torch.autograd.Function):
         res_t = yr if yr is not None else res
         ldr = nhwc(res_t)[4] if res_t is not None else 0
         dz = empty_nhwc(n, c, ho, wo, y.dtype, y.device)
-        N.call("dmf_act_bwd", dtc, dout.data_ptr(), nhwc(dout)[4], y.data_ptr(), ldy, ss.data_ptr(), _p(res_t), ldr,
-               _p(ss_r), ACT[act], float(p), _p(rng), site, dz.data_ptr(), nhwc(dz)[4], m, c, _stream())
         need = ctx.needs_input_grad
         dgamma = torch.zeros_like(bn.weight) if need[4] else None
         dbeta = torch.zeros_like(bn.bias) if need[5] else None
-        dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training)
+        # act/dropout backward and the BN column partials in one pass
+        tiles = N.load().dmf_bn_bwd_tiles(m)
+        part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
+        N.call("dmf_act_bwd_bn_reduce", dtc, dout.data_ptr(), nhwc(dout)[4], y.data_ptr(), ldy, ss.data_ptr(),
+               _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
+               nhwc(dz)[4], m, c, part.data_ptr(), _stream())
+        dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
         need_dx = need[0] or (x2 is not None and need[1])
-        dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2)
+        dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2,
+                                    gate_holder=ctx.gate_holder)
         dx2 = None
         if x2 is not None and dx is not None:
             dx, dx2 = dx
@@ -506,13 +541,16 @@ class _ConvBNActFn(torch.autograd.Function):
         return dx, dx2, dw, db, dgamma, dbeta, dres, dxr, dwr, dgr, dbr, None
 
 
-def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True):
+def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True, part=None):
+    """BatchNorm2d backward from dz; part: column partials already
+    produced (dmf_act_bwd_bn_reduce)."""
     n, c, h, w, ldy = nhwc(y)
     m = n * h * w
     tiles = (m + 255) // 256
-    part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
-    N.call("dmf_bn_bwd_reduce", dt(y), dz.data_ptr(), nhwc(dz)[4], y.data_ptr(), ldy, save.data_ptr(), m, c,
-           part.data_ptr(), _stream())
+    if part is None:
+        part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
+        N.call("dmf_bn_bwd_reduce", dt(y), dz.data_ptr(), nhwc(dz)[4], y.data_ptr(), ldy, save.data_ptr(), m, c,
+               part.data_ptr(), _stream())
     coef = torch.empty(3 * c, dtype=torch.float32, device=y.device)
     N.call("dmf_bn_bwd_finalize", part.data_ptr(), tiles, c, float(m), 1 if training else 0, _p(bn.weight),
            save.data_ptr(), _p(dgamma), _p(dbeta), coef.data_ptr(), _stream())
@@ -781,6 +819,11 @@ class _InputFn(torch.autograd.Function):
                cmean.data_ptr(), _stream())
         ctx.save_for_backward(x)
         ctx.mark_non_differentiable(cmean)
+        # the consuming conv (the backbone stem) may deliver the gate gradient
+        # directly (_conv_backward gate_holder) instead of d(x*gate)
+        ctx.holder = {"gate": g} if g is not None else None
+        if g is not None:
+            y.__dict__["_dmf_gate"] = ctx.holder
         return y, cmean
 
     @staticmethod
@@ -789,10 +832,15 @@ class _InputFn(torch.autograd.Function):
         dgate = None
         if ctx.needs_input_grad[1]:
             n, c, h, w = x.shape
+            pre = ctx.holder.pop("dgate", None) if ctx.holder is not None else None
+            if pre is not None and dy is not None and all(st == 0 for st in dy.stride()):
+                return None, pre, None  # the stem was the only consumer
             dy = as_nhwc(dy)
             dgate = torch.empty((n, c), dtype=torch.float32, device=x.device)
             N.call("dmf_gate_grad_nchw", dt(dy), dy.data_ptr(), nhwc(dy)[4], x.data_ptr(), n, c, h * w,
                    dgate.data_ptr(), _stream())
+            if pre is not None:
+                dgate = dgate + pre
         return None, dgate, None
 
 
@@ -1008,7 +1056,7 @@ class _MaskAttnFn(torch.autograd.Function):
         df = empty_nhwc(n, c, h, w, f.dtype, dev)
         dm = empty_nhwc(n, 1, h, w, f.dtype, dev)
         grads = torch.zeros(4 * hid + 2, dtype=torch.float32, device=dev)  # dw1, dgn_w, dgn_b, dw2, db2, dgamma
-        ws = torch.empty(n * h * w * hid + 2 * n, dtype=torch.float32, device=dev)
+        ws = torch.empty(N.load().dmf_mask_attn_bwd_ws_size(n, h * w, hid), dtype=torch.float32, device=dev)
         N.call("dmf_mask_attn_bwd", dt(f), dout.data_ptr(), nhwc(dout)[4], f.data_ptr(), ldf, m.data_ptr(), n, h * w,
                c, w1.detach().reshape(hid).contiguous().data_ptr(), gn_w.data_ptr(), gn_b.data_ptr(),
                w2.detach().reshape(hid).contiguous().data_ptr(), b2.data_ptr(), gamma.data_ptr(), hid,

@@ -19,6 +19,8 @@
  *                 `ld*` arguments are channel strides (elements per pixel)
  *   conv weights: forward  [Cout][KH][KW][CinP]  (dmf_conv_weight_prep mode 0)
  *                 dgrad    [CinP][KH][KW][Cout]  (mode 1)
+ *                 dgrad as a forward conv of dY (stride 1): mode 1 with the
+ *                 filter taps flipped (mode 2)
  *                 gradients are produced in torch layout [Cout][Cin][KH][KW]
  *   BN partials : float [tiles][C][2] (sum, sum of squares)
  *   scale_shift : float [2][C] (y = x*scale + shift)
@@ -93,6 +95,15 @@ int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int
                      int dil, int splits, float* workspace, void* stream);
 int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int Cout, int Cin, int CinP, int KH, int KW,
                             float* dw, int accumulate, void* stream);
+/* gate gradient of a channel-gated conv input y = x*gate[N][Cin] from
+ * per-sample weight-gradient slabs (dmf_conv2d_wgrad with splits = N and
+ * Ho*Wo a multiple of dmf_conv2d_wgrad_pixel_step): dgate[n][c] =
+ * sum_{co,r,s} W[co][c][r][s] * slab_n[co][r][s][c] / gate[n][c], w the fp32
+ * torch-layout weight (SE input gate, model_module.py:584-591) */
+int dmf_conv2d_wgrad_gate(const float* workspace, int N, int Cout, int Cin, int CinP, int KH, int KW, const float* w,
+                          const float* gate, float* dgate, void* stream);
+/* pixels per K-step of dmf_conv2d_wgrad (splits cover whole multiples of it) */
+int dmf_conv2d_wgrad_pixel_step(int dtype);
 /* single-output-channel convs: ReconHead.conv[3] (model_module.py:117),
  * MaskHeadResize.out (:187); weights [KH][KW][Cin] fp32 */
 int dmf_conv_cout1_fwd(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const float* w,
@@ -136,6 +147,15 @@ int dmf_bn_bwd_finalize(const float* partials, int ntiles, int C, double count, 
                         const float* save_mean_invstd, float* dgamma, float* dbeta, float* coef, void* stream);
 int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void* x, int ldx, const float* coef, void* dx,
                      int lddx, long long M, int C, void* stream);
+/* dmf_act_bwd + dmf_bn_bwd_reduce in one pass: dz = act/dropout backward of
+ * y = drop(act(x*scale_shift + residual)) written once, plus the BN column
+ * partials [dmf_bn_bwd_tiles(M)][C][2] of x (the BN input) with the saved
+ * (mean, invstd); ResNetLite/Bottleneck conv->BN->act backward
+ * (model_module.py:259-280, timm Bottleneck) */
+int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+                          const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
+                          const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz, int lddz,
+                          long long M, int C, float* partials, void* stream);
 int dmf_col_stats_tiles(long long M);
 int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
 
@@ -187,7 +207,9 @@ int dmf_gate_grad_nchw(int dtype, const void* dy, int lddy, const float* x, int 
 int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* m, int N, int HW, int C, const float* w1,
                       const float* gn_w, const float* gn_b, const float* w2, const float* b2, const float* gamma,
                       int hidden, float eps, float* stats, void* out, int ldo, void* A_out, void* stream);
-/* workspace: N*HW*hidden + 2*N floats; grads (accumulated):
+/* floats of the dmf_mask_attn_bwd workspace */
+int dmf_mask_attn_bwd_ws_size(int N, int HW, int hidden);
+/* workspace: dmf_mask_attn_bwd_ws_size floats; grads (accumulated):
  * [hidden] dw1, [hidden] dgn_w, [hidden] dgn_b, [hidden] dw2, [1] db2, [1] dgamma */
 int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int ldf, const void* m, int N, int HW,
                       int C, const float* w1, const float* gn_w, const float* gn_b, const float* w2, const float* b2,

@@ -113,6 +113,53 @@ def test_conv_wide_forward_and_bn_stats(case):
     assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
 
 
+# bf16 backward at the encoder's shapes: the weight gradient on the
+# transposed-LDS-read kernel (pixel splits, tap-crossing K tiles, M tails,
+# the neck's two-source input) and the stride-1 input gradient as a forward
+# conv of dY with flipped taps (the LDS-DMA tiles); stride 2 keeps the gather
+BWD_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, dil, Cin2)
+    (8, 256, 32, 32, 256, 3, 1, 2, 2, 0),
+    (9, 512, 32, 32, 512, 1, 1, 0, 1, 0),
+    (4, 128, 32, 32, 256, 3, 1, 1, 1, 384),
+    (4, 64, 33, 31, 128, 3, 2, 1, 1, 0),
+    (3, 64, 20, 20, 64, 3, 1, 4, 4, 0),
+    (2, 72, 17, 19, 40, 3, 1, 1, 1, 0),
+    (16, 2048, 16, 16, 512, 1, 1, 0, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", BWD_CASES)
+def test_conv_backward_bf16(case):
+    n, ci, h, w, co, k, s, p, d, ci2 = case
+    torch.manual_seed(6)
+    q = lambda t: t.bfloat16().float()
+    a = q(torch.randn(n, ci, h, w))
+    b = q(torch.randn(n, ci2, h, w)) if ci2 else None
+    conv = nn.Conv2d(ci + ci2, co, k, stride=s, padding=p, dilation=d, bias=False)
+    wq = q(conv.weight.detach())
+    xin = (torch.cat([a, b], 1) if ci2 else a).double().requires_grad_(True)
+    wr = wq.double().requires_grad_(True)
+    yr = F.conv2d(xin, wr, None, s, p, d)
+    gy = q(torch.randn(yr.shape))
+    yr.backward(gy.double())
+    cd = copy.deepcopy(conv).to(DEV)
+    with torch.no_grad():
+        cd.weight.copy_(wq)
+    g = O.ConvGeom(cd)
+    xd = _to_dev(a, torch.bfloat16)
+    x2d = _to_dev(b, torch.bfloat16) if ci2 else None
+    dx, dw, _ = O._conv_backward(xd, cd.weight, None, g, (O.WeightCache(), O.WeightCache()),
+                                 _to_dev(gy, torch.bfloat16), True, True, False, x2=x2d)
+    if ci2:
+        dx = torch.cat([dx[0].float(), dx[1].float()], 1)
+    ref_dx, ref_dw = xin.grad.float(), wr.grad.float()
+    err_x = (dx.float().cpu() - ref_dx).abs().max().item()
+    assert err_x <= 1e-2 * ref_dx.abs().max().item(), err_x
+    err_w = (dw.cpu() - ref_dw).abs().max().item()
+    assert err_w <= 1e-3 * ref_dw.abs().max().item(), err_w
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv_dual_source(dtype):
     torch.manual_seed(1)
@@ -400,3 +447,41 @@ def test_fused_recon_mixed_map_sizes():
     assert abs(out.item() - ref.item()) < 1e-5
     for a, b in zip(dev_in, ref_in):
         assert torch.allclose(a.grad.cpu(), b.grad, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mask_attention_backward_sliced(dtype):
+    """MaskGuidedSpatialAttention (model_module.py:49-97) forward + backward at
+    the f2 shape (32x32 = 16 slices of 64 pixels per sample) vs the oracle."""
+    import oracle.model as OM
+    torch.manual_seed(7)
+    ref_m = OM.MaskGuidedSpatialAttention(256, 1, 16)
+    with torch.no_grad():
+        ref_m.gamma.fill_(0.3)
+        ref_m.mask_processor[1].weight.uniform_(0.5, 1.5)
+        ref_m.mask_processor[1].bias.uniform_(-0.5, 0.5)
+    f = torch.randn(3, 256, 32, 32)
+    m = torch.randn(3, 1, 32, 32)
+    if dtype == torch.bfloat16:
+        f, m = f.bfloat16().float(), m.bfloat16().float()
+    fr, mr = f.clone().requires_grad_(True), m.clone().requires_grad_(True)
+    out_r, a_r = ref_m(fr, mr)
+    g = torch.randn_like(out_r)
+    if dtype == torch.bfloat16:
+        g = g.bfloat16().float()
+    out_r.backward(g)
+    dev_m = copy.deepcopy(ref_m).to(DEV)
+    dev_m.zero_grad(set_to_none=True)
+    fd = _to_dev(f, dtype).requires_grad_(True)
+    md = _to_dev(m, dtype).requires_grad_(True)
+    out, a = O.mask_attention(fd, md, dev_m)
+    out.backward(_to_dev(g, dtype))
+    tol = 2e-4 if dtype == torch.float32 else 3e-2
+
+    def close(x, y, t):
+        return (x.float().cpu() - y).abs().max().item() <= t * max(1.0, y.abs().max().item())
+    assert close(out, out_r.detach(), tol)
+    assert close(fd.grad, fr.grad, tol)
+    assert close(md.grad, mr.grad, 5 * tol)
+    for p_dev, p_ref in zip(dev_m.parameters(), ref_m.parameters()):
+        assert close(p_dev.grad, p_ref.grad, 5 * tol), (p_dev.grad, p_ref.grad)
