@@ -610,7 +610,7 @@ using namespace dmf;
 static int wgrad_tr_enabled() {
   static int v = [] {
     const char* e = std::getenv("DMF_WGRAD_TR");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '0' ? 0 : (e && e[0] == '2' ? 2 : 1);
   }();
   return v;
 }
@@ -660,7 +660,12 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
   const size_t lds = 2 * 2 * 128 * 128;
   DMF_CHECK_ARG((uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && (!x2 || (uintptr_t)x2 % 16 == 0),
                 "dmf_conv2d_wgrad: pointers must be 16-byte aligned");
-  if (dtype == DMF_BF16 && wgrad_tr_enabled())
+  if (dtype == DMF_BF16 && wgrad_tr_enabled() == 2 && a.Ktot >= 256) {
+    // 128 x 256 tile, 8 waves: half the operand re-reads per flop
+    a.ntiles = cdiv(a.Ktot, 256);
+    grid = dim3(a.mtiles * a.ntiles, splits);
+    hipLaunchKernelGGL((k_conv_wgrad_tr<2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+  } else if (dtype == DMF_BF16 && wgrad_tr_enabled())
     hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
   else if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_conv_wgrad<bf16_t>, grid, dim3(256), lds, (hipStream_t)stream, a);

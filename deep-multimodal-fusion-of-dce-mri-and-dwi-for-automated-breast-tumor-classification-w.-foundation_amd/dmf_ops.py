@@ -309,11 +309,24 @@ def _col_stats(y):
     return part
 
 
-def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None, gate_holder=None):
+def grad_sink(p):
+    """p.grad as the in-place accumulation target of a gradient kernel: the
+    conv/BN backward kernels add straight into it (their accumulate mode) and
+    hand autograd None, so there is no AccumulateGrad add and no zero fill
+    per parameter. Allocated zeroed on first use."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    return p.grad
+
+
+def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None, gate_holder=None,
+                   dw_sink=False):
     """Returns (dx, dw, db) -- with x2 given, dx is (dx, dx2) (views into one
     concat-gradient buffer). gate_holder: x is the channel-gated network
     input (_InputFn); its gradient is then only needed for the gate, which
-    comes from per-sample weight-gradient slabs (dx is a zero placeholder)."""
+    comes from per-sample weight-gradient slabs (dx is a zero placeholder).
+    dw_sink: the MFMA weight gradient accumulates into weight.grad
+    (grad_sink) and dw comes back None."""
     n, cx, h, w, ldx = nhwc(x)
     cx2, ldx2 = 0, 0
     if x2 is not None:
@@ -337,8 +350,10 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
                dgate.data_ptr(), _stream())
         gate_holder["dgate"] = dgate
         if need_dw:
-            dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dev)
-            N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), n, co, ci, cx, kh, kw, dw.data_ptr(), 0, _stream())
+            dwt = grad_sink(weight) if dw_sink else torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dev)
+            N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), n, co, ci, cx, kh, kw, dwt.data_ptr(),
+                   1 if dw_sink else 0, _stream())
+            dw = None if dw_sink else dwt
         if need_db:
             db = _colsum_nhwc(dy)
         dx = torch.zeros((), dtype=x.dtype, device=dev).expand(n, cx, h, w)
@@ -394,9 +409,11 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
                 ws = torch.empty(splits * co * kh * kw * ct, dtype=torch.float32, device=dev)
                 N.call("dmf_conv2d_wgrad", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, dy.data_ptr(), ho,
                        wo, co, lddy, kh, kw, g.stride, g.pad, g.dil, splits, ws.data_ptr(), _stream())
-                dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dev)
-                N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), splits, co, ci, ct, kh, kw, dw.data_ptr(), 0,
-                       _stream())
+                dwt = grad_sink(weight) if dw_sink else torch.empty((co, ci, kh, kw), dtype=torch.float32,
+                                                                      device=dev)
+                N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), splits, co, ci, ct, kh, kw, dwt.data_ptr(),
+                       1 if dw_sink else 0, _stream())
+                dw = None if dw_sink else dwt
             if need_db:
                 db = _colsum_nhwc(dy)
     return dx, dw, db
@@ -515,8 +532,8 @@ class _ConvBNActFn(torch.autograd.Function):
         ldr = nhwc(res_t)[4] if res_t is not None else 0
         dz = empty_nhwc(n, c, ho, wo, y.dtype, y.device)
         need = ctx.needs_input_grad
-        dgamma = torch.zeros_like(bn.weight) if need[4] else None
-        dbeta = torch.zeros_like(bn.bias) if need[5] else None
+        dgamma = grad_sink(bn.weight) if need[4] else None
+        dbeta = grad_sink(bn.bias) if need[5] else None
         # act/dropout backward and the BN column partials in one pass
         tiles = N.load().dmf_bn_bwd_tiles(m)
         part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
@@ -526,19 +543,20 @@ class _ConvBNActFn(torch.autograd.Function):
         dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
         need_dx = need[0] or (x2 is not None and need[1])
         dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2,
-                                    gate_holder=ctx.gate_holder)
+                                    gate_holder=ctx.gate_holder, dw_sink=True)
         dx2 = None
         if x2 is not None and dx is not None:
             dx, dx2 = dx
         dres = dxr = dwr = dgr = dbr = None
         if xr is not None:
-            dgr = torch.zeros_like(bn_r.weight) if need[9] else None
-            dbr = torch.zeros_like(bn_r.bias) if need[10] else None
+            dgr = grad_sink(bn_r.weight) if need[9] else None
+            dbr = grad_sink(bn_r.bias) if need[10] else None
             dyr = _bn_backward(dz, yr, save_r, bn_r, dgr, dbr, training=bn_r.training)
-            dxr, dwr, _ = _conv_backward(xr, wr, None, gr, caches_r, dyr, need[7], need[8], False)
+            dxr, dwr, _ = _conv_backward(xr, wr, None, gr, caches_r, dyr, need[7], need[8], False, dw_sink=True)
         elif res is not None and need[6]:
             dres = dz
-        return dx, dx2, dw, db, dgamma, dbeta, dres, dxr, dwr, dgr, dbr, None
+        # gamma/beta (and the MFMA conv weights) were accumulated in place (grad_sink)
+        return dx, dx2, dw, db, None, None, dres, dxr, dwr, None, None, None
 
 
 def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True, part=None):
