@@ -10,6 +10,8 @@ reconstruction terms of one step share a single launch.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -87,6 +89,42 @@ class LightningFusionModel(nn.Module):
     def forward(self, dwi_feats, dce_feats, dwi_mask=None, dce_mask=None):
         return self.fusion_model(dwi_feats, dce_feats, dwi_mask, dce_mask)
 
+    # ------------------------------------------------------------- encoders
+    def _encode(self, dwi_inputs, dce_inputs):
+        """The two encoder forwards (train_fusion.py:227-230). They are
+        independent until FusionModel, so on the GPU the DCE encoder runs on a
+        second HIP stream beside the DWI one (a fork/join that a captured
+        hipGraph keeps as two branches): the small, latency-bound launches
+        and the tails of one encoder overlap the other's. The dropout Philox
+        snapshots are taken up front in the sequential order (DWI, DCE), so
+        the masks match a sequential run; autograd replays each encoder's
+        backward on the stream its forward ran on."""
+        if not (dwi_inputs.is_cuda and PARALLEL_ENCODERS):
+            return self.dwi_model(dwi_inputs), self.dce_model(dce_inputs)
+        main = torch.cuda.current_stream(dwi_inputs.device)
+        side = self.__dict__.get("_side_stream")
+        if side is None or side.device != dwi_inputs.device:
+            side = torch.cuda.Stream(dwi_inputs.device)
+            self.__dict__["_side_stream"] = side
+        snap_dwi = O.RNG.snapshot(dwi_inputs.device) if self.dwi_model.training else None
+        snap_dce = O.RNG.snapshot(dwi_inputs.device) if self.dce_model.training else None
+        side.wait_stream(main)
+        prev = O.RNG_CURRENT[0]
+        try:
+            O.RNG_CURRENT[0] = snap_dwi
+            out_dwi = self.dwi_model(dwi_inputs)
+            O.RNG_CURRENT[0] = snap_dce
+            with torch.cuda.stream(side):
+                dce_inputs.record_stream(side)
+                if snap_dce is not None:
+                    snap_dce.record_stream(side)
+                out_dce = self.dce_model(dce_inputs)
+        finally:
+            O.RNG_CURRENT[0] = prev
+        main.wait_stream(side)
+        _record_tree(out_dce, main)
+        return out_dwi, out_dce
+
     # ---------------------------------------------------------------- step
     def _shared_step(self, batch, phase="train", return_preds=False):
         """train_fusion.py:204-321."""
@@ -104,8 +142,7 @@ class LightningFusionModel(nn.Module):
             masks_batch = masks_batch.to(dev, non_blocking=True)
         aux_w = max(0.0, 1 - self.current_epoch / self.aux_loss_limit) if self.use_aux_loss_sched else 1.0
 
-        _, dwi_aux, dwi_mask_pred = self.dwi_model(dwi_inputs)
-        _, dce_aux, dce_mask_pred = self.dce_model(dce_inputs)
+        (_, dwi_aux, dwi_mask_pred), (_, dce_aux, dce_mask_pred) = self._encode(dwi_inputs, dce_inputs)
         logits, fused_mask_logits, aux = self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask_pred,
                                                       dce_mask_pred)
 
@@ -174,6 +211,23 @@ class LightningFusionModel(nn.Module):
 
 
 # ------------------------------------------------------------------ helpers
+PARALLEL_ENCODERS = os.environ.get("DMF_PAR_ENC", "1") != "0"
+
+
+def _record_tree(obj, stream):
+    """record_stream on every CUDA tensor of a nested encoder output (made
+    on the side stream, consumed on stream)."""
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record_tree(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record_tree(v, stream)
+
+
 def compute_recon_list_loss(recon_list, input_img):
     """train_fusion.py:709-744 (2-D): mean over the valid maps of
     recon_image_loss(bilinear(r -> input size), channel-mean(input))."""
