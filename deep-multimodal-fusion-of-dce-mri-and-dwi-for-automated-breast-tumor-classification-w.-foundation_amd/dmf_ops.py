@@ -1556,6 +1556,79 @@ class _MimicFn(torch.autograd.Function):
 
 
 # the Philox snapshot shared by the dropout sites of one top-level forward
+# ------------------------------------------------------ concurrent branches
+PARALLEL_BRANCHES = os.environ.get("DMF_PAR_ENC", "1") != "0"
+
+
+def record_tree(obj, stream):
+    """record_stream on every CUDA tensor of a nested output made on one
+    stream and consumed on stream. Skipped while a hipGraph is being
+    captured: there record_stream on graph-pool blocks of a nested branch
+    has crashed capture end (measured, ROCm 7.2), and the fork/join events plus
+    the references the branch holds until its join already order every
+    reuse."""
+    if torch.cuda.is_current_stream_capturing():
+        return
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            record_tree(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            record_tree(v, stream)
+
+
+SIDE_STREAMS = []
+ORIGIN_STREAM = [None]  # the stream the concurrent region forked from (train_fusion._encode)
+
+
+def side_stream(owner, name, device):
+    """A HIP stream owned by owner (created once per device)."""
+    key = "_dmf_stream_" + name
+    st = owner.__dict__.get(key)
+    if st is None or st.device != device:
+        st = torch.cuda.Stream(device)
+        owner.__dict__[key] = st
+        SIDE_STREAMS.append(st)
+    return st
+
+
+
+
+
+def branch(owner, name, fn, *inputs):
+    """Run fn() (an off-critical-path branch reading inputs) on a side
+    stream forked from the current one. Returns (out, join) -- call join()
+    before the branch outputs are consumed on the current stream."""
+    dev = inputs[0].device
+    if not (PARALLEL_BRANCHES and inputs[0].is_cuda):
+        out = fn()
+        return out, (lambda: out)
+    main = torch.cuda.current_stream(dev)
+    origin = ORIGIN_STREAM[0]
+    if origin is not None and origin != main:
+        # already on a branch: a fork from a forked stream crashes
+        # hipStreamEndCapture when the step is captured (measured, ROCm 7.2;
+        # with or without record_stream, joined directly or transitively)
+        out = fn()
+        return out, (lambda: out)
+    side = side_stream(owner, name, dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        record_tree(list(inputs), side)
+        out = fn()
+
+    def join():
+        main.wait_stream(side)
+        record_tree(out, main)
+        del keep[:]
+        return out
+    keep = list(inputs)  # alive until the join (stands in for record_stream under capture)
+    return out, join
+
+
 RNG_CURRENT = [None]
 
 

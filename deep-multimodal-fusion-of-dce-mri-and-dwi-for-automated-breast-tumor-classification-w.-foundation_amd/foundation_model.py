@@ -143,7 +143,11 @@ class ResNet50OS8(nn.Module):
         y, _ = O.input_stage(x, dt, None)
         return y
 
-    def forward(self, x):
+    supports_feature_callback = True
+
+    def forward(self, x, on_feature=None):
+        """on_feature(i, feats): called as soon as out_indices map i is
+        produced (lets a consumer start on C2 while layer2..4 still run)."""
         if x.shape[1] == self.in_chans or x.dtype != self.compute_dtype:
             x = self.stage_input(x)
         x = O.conv_bn_act(x, self.conv1, _caches(self.conv1), self.bn1, "relu")
@@ -153,6 +157,8 @@ class ResNet50OS8(nn.Module):
             for blk in getattr(self, f"layer{i}"):
                 x = blk(x)
             feats.append(x)
+            if on_feature is not None:
+                on_feature(i - 1, feats)
         return feats
 
 
@@ -174,8 +180,12 @@ class _DisabledWrapper(nn.Module):
         except AttributeError:
             return getattr(self._modules["_orig_mod"], name)
 
-    def forward(self, x):
-        return self._orig_mod(x)
+    @property
+    def supports_feature_callback(self):
+        return getattr(self._orig_mod, "supports_feature_callback", False)
+
+    def forward(self, x, **kw):
+        return self._orig_mod(x, **kw)
 
 
 # --------------------------------------------------------- weight plumbing

@@ -11,6 +11,7 @@ are NCHW-shaped tensors with NHWC storage in the model's compute dtype
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass
 
 import torch
@@ -308,24 +309,51 @@ class BackboneAdapter(nn.Module):
             self.necks[f"f{i + 1}"] = nn.Sequential(nn.Conv2d(cin, co, 3, padding=1), nn.BatchNorm2d(co), nn.GELU(),
                                                    nn.Conv2d(co, co, 3, padding=1), nn.BatchNorm2d(co), nn.GELU())
 
+    def _neck(self, i, feats):
+        parts = [feats[j] for j in self.selected_indices_chains[i]]
+        if self.is_transformer:
+            parts = [_tokens_to_map(f) for f in parts]
+        nk = self.necks[f"f{i + 1}"]
+        if len(parts) == 1:
+            h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu")
+        elif len(parts) == 2:
+            h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu", x2=parts[1])
+        else:
+            raise NotImplementedError("neck chains of more than two feature maps are not built yet")
+        return O.conv_bn_act(h, nk[3], _caches(nk[3]), nk[4], "gelu")
+
     def forward(self, x):
-        feats = self.backbone(x)
-        outs = []
-        for i, chain in enumerate(self.selected_indices_chains):
-            parts = [feats[j] for j in chain]
-            if self.is_transformer:
-                parts = [_tokens_to_map(f) for f in parts]
-            nk = self.necks[f"f{i + 1}"]
-            if len(parts) > 2:
-                raise NotImplementedError("neck chains of more than two feature maps are not built yet")
-            if len(parts) == 1:
-                h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu")
-            elif len(parts) == 2:
-                h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu", x2=parts[1])
-            else:
-                raise NotImplementedError("neck chains of more than two feature maps are not built yet")
-            outs.append(O.conv_bn_act(h, nk[3], _caches(nk[3]), nk[4], "gelu"))
+        chains = self.selected_indices_chains
+        if not (PARALLEL_NECKS and x.is_cuda and getattr(self.backbone, "supports_feature_callback", False)):
+            feats = self.backbone(x)
+            outs = [self._neck(i, feats) for i in range(len(chains))]
+            return outs[0], outs[1], outs[2]
+        # a neck chain whose maps are all out starts on a side stream while the
+        # backbone's deeper layers still run; the last chain stays on this stream
+        outs, joins = [None] * len(chains), {}
+
+        def on_feature(k, feats):
+            for i, chain in enumerate(chains):
+                if i != len(chains) - 1 and i not in joins and max(chain) == k:
+                    outs[i], joins[i] = O.branch(self, f"neck{i}", lambda i=i: self._neck(i, feats),
+                                                 *[feats[j] for j in chain])
+
+        feats = self.backbone(x, on_feature=on_feature)
+        for i in range(len(chains)):
+            if i in joins:
+                outs[i] = joins[i]()
+            elif outs[i] is None:
+                outs[i] = self._neck(i, feats)
         return outs[0], outs[1], outs[2]
+
+
+PARALLEL_NECKS = os.environ.get("DMF_PAR_NECK", "0") != "0"  # opt-in: measured slower (r01w)
+PARALLEL_PROJ = os.environ.get("DMF_PAR_PROJ", "0") != "0"  # opt-in: measured slower (r01w)
+
+
+def _inline_branch(owner, name, fn, *inputs):
+    out = fn()
+    return out, (lambda: out)
 
 
 def _tokens_to_map(f):
@@ -468,6 +496,12 @@ class ModelMaskHeadBackbone(nn.Module):
                 f1_aligned = self.f1_to_f2(f1)
                 mask_pred = self.mask_head(O.act_nhwc(f2, "none", res=f1_aligned))
                 f2, mask_attn_map = self.mask_spatial_attention(f2, mask_pred)
+            # the four projectors (their outputs only feed aux["proj_pairs"]) run
+            # on a side stream beside block3 / the transformer stage
+            (p1, p2, p1_r, p2_r), join_proj = (O.branch if PARALLEL_PROJ else _inline_branch)(
+                self, "proj", lambda: (self._projector(self.proj_f1, f1), self._projector(self.proj_f2, f2),
+                                       self._projector(self.proj_r1, r1), self._projector(self.proj_r2, r2)),
+                f1, f2, r1, r2)
             if not self.use_hybrid_transformer:
                 f3_in = O.gn_mix(f3_b, f2, self.f3_weight, self.norm_f3) if self.use_backbone else f2
                 f3, _ = self.block3(f3_in)
@@ -477,11 +511,8 @@ class ModelMaskHeadBackbone(nn.Module):
                     f3, mask_attn_map = self.mask_spatial_attention(f3, mask_pred)
             else:
                 f3 = O.conv2d(self.transformer(f2), self.trans_out_proj, _caches(self.trans_out_proj))
-            p1 = self._projector(self.proj_f1, f1)
-            p2 = self._projector(self.proj_f2, f2)
-            p1_r = self._projector(self.proj_r1, r1)
-            p2_r = self._projector(self.proj_r2, r2)
             logits = self.classification_head(f3)
+            p1, p2, p1_r, p2_r = join_proj()
         aux = {"raw_feats": [f1, f2, f3], "recon_feats": [r1, r2], "proj_pairs": [p1, p1_r, p2, p2_r],
                "mask_attn_map": mask_attn_map, "mod_attn_map": mod_attn_map}
         return logits, aux, mask_pred

@@ -10,8 +10,6 @@ reconstruction terms of one step share a single launch.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
@@ -110,19 +108,19 @@ class LightningFusionModel(nn.Module):
         snap_dce = O.RNG.snapshot(dwi_inputs.device) if self.dce_model.training else None
         side.wait_stream(main)
         prev = O.RNG_CURRENT[0]
+        O.ORIGIN_STREAM[0] = main
         try:
             O.RNG_CURRENT[0] = snap_dwi
             out_dwi = self.dwi_model(dwi_inputs)
             O.RNG_CURRENT[0] = snap_dce
             with torch.cuda.stream(side):
-                dce_inputs.record_stream(side)
-                if snap_dce is not None:
-                    snap_dce.record_stream(side)
+                O.record_tree([dce_inputs, snap_dce], side)
                 out_dce = self.dce_model(dce_inputs)
         finally:
             O.RNG_CURRENT[0] = prev
+            O.ORIGIN_STREAM[0] = None
         main.wait_stream(side)
-        _record_tree(out_dce, main)
+        O.record_tree(out_dce, main)
         return out_dwi, out_dce
 
     # ---------------------------------------------------------------- step
@@ -211,21 +209,7 @@ class LightningFusionModel(nn.Module):
 
 
 # ------------------------------------------------------------------ helpers
-PARALLEL_ENCODERS = os.environ.get("DMF_PAR_ENC", "1") != "0"
-
-
-def _record_tree(obj, stream):
-    """record_stream on every CUDA tensor of a nested encoder output (made
-    on the side stream, consumed on stream)."""
-    if isinstance(obj, torch.Tensor):
-        if obj.is_cuda:
-            obj.record_stream(stream)
-    elif isinstance(obj, dict):
-        for v in obj.values():
-            _record_tree(v, stream)
-    elif isinstance(obj, (list, tuple)):
-        for v in obj:
-            _record_tree(v, stream)
+PARALLEL_ENCODERS = O.PARALLEL_BRANCHES
 
 
 def compute_recon_list_loss(recon_list, input_img):
