@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--mode", choices=["A", "B"], default="A")
+    ap.add_argument("--patch-embed", choices=["fp8", "bf16"], default="fp8",
+                    help="config 5: PatchEmbed.proj on e4m3 MFMA (default) or the bf16 conv engine")
     ap.add_argument("--config", type=int, choices=[3, 5], default=3,
                     help="5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
@@ -127,7 +129,7 @@ def roofline_probe(trainer, batch, dtype):
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = pmc_traffic()
     return {
-        "kernel": "conv2d forward (k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm, %s)" %
+        "kernel": "conv2d forward (k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm, %s)" %
                   ("bf16" if dtype == torch.bfloat16 else "f32"),
         "bound": "mfma",
         "achieved": round(achieved, 2),
@@ -230,6 +232,8 @@ def main():
         # hybrid CNN -> Transformer stage (E=512, depth 6, 4 heads, patch 2;
         # parameters_generate.py:71-75) in place of block3, S=384 (576 tokens per volume)
         P["dwi_model_parameters"]["use_hybrid_transformer"] = True
+        # config 5 names an fp8-e4m3 MFMA patch-embed (bf16 elsewhere)
+        P["dwi_model_parameters"]["patch_embed_fp8"] = args.patch_embed == "fp8" and dtype == torch.bfloat16
         if args.size == 256:
             args.size = 384
     P["dwi_model_parameters"]["input_size"] = args.size
@@ -282,7 +286,9 @@ def main():
         "config": {"workload": f"fusion training step, config {args.config}, mode {args.mode} "
                                f"({'encoders frozen, train-mode' if args.mode == 'A' else 'all trainable'})",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "size": args.size,
-                   "parallelism": f"dp{world}", "hipgraph": not args.no_graph},
+                   "parallelism": f"dp{world}", "hipgraph": not args.no_graph,
+                   **({"patch_embed": args.patch_embed if args.dtype == "bf16" else "f32"}
+                      if args.config == 5 else {})},
         "loss": loss_val,
         "peak_hbm_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
         "roofline": roof,

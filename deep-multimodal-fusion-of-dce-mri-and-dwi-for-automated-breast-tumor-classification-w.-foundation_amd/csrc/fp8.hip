@@ -1,0 +1,217 @@
+// fp8 (OCP e4m3fn) patch-embed GEMM of configuration 5: PatchEmbed.proj, a
+// conv with kernel = stride = patch (transformer_model.py:7-32), as
+//   tokens[m][e] = rs[m] * ws[e] * sum_k q8(x)[m][k] * q8(W)[e][k] + bias[e]
+// m = (n, ho, wo) token, k = (r, s, c) patch element (the conv engine's
+// [Cout][KH][KW][CinP] order). Activations are scaled per token row and the
+// weights per output channel so each row's max maps to 448 (e4m3 max), then
+// packed with v_cvt_pk_fp8_f32; the GEMM runs v_mfma_f32_16x16x32_fp8_fp8
+// (fp32 accumulation) and the scales are applied in the epilogue. The
+// backward stays bf16 (the straight-through estimate through the
+// quantisation, like fp8 training recipes keep it).
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+typedef __attribute__((ext_vector_type(4))) float f8_f32x4;
+
+__device__ __forceinline__ uint2 pack8_e4m3(const float v[8]) {
+  int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], w0, true);
+  int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], w1, true);
+  return make_uint2((unsigned)w0, (unsigned)w1);
+}
+
+// one wave per token row: gather the P x P patch from NHWC bf16, row amax,
+// scale, pack (8 elements per lane per pass; C % 8 == 0 so a chunk never
+// crosses a tap)
+__global__ void __launch_bounds__(256) k_patch_quant(const bf16_t* __restrict__ x, int H, int W, int C, int ldx, int P,
+                                                     int Ho, int Wo, uint8_t* __restrict__ q, int ldq,
+                                                     float* __restrict__ rscale, long long M) {
+  const int lane = threadIdx.x & 63;
+  const long long m = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;  // wave-uniform
+  const int K = P * P * C;
+  const int hw = Ho * Wo;
+  const int n = (int)(m / hw), rem = (int)(m - (long long)n * hw);
+  const int ho = rem / Wo, wo = rem - ho * Wo;
+  auto src = [&](int k) {
+    const int tap = k / C, c = k - tap * C;
+    const int r = tap / P, s = tap - (tap / P) * P;
+    return x + ((size_t)(n * H + ho * P + r) * W + wo * P + s) * ldx + c;
+  };
+  float amax = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    float v[8];
+    ld8(src(k), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+  }
+  amax = wave_max(amax);
+  const float sc = amax > 0.f ? 448.f / amax : 1.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    float v[8];
+    ld8(src(k), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= sc;
+    *(uint2*)(q + (size_t)m * ldq + k) = pack8_e4m3(v);
+  }
+  if (lane == 0) rscale[m] = amax > 0.f ? amax / 448.f : 1.f;
+}
+
+// one wave per output channel: torch conv weight [E][C][P][P] (fp32) ->
+// e4m3 rows [E][(r,s,c)], per-channel scale
+__global__ void __launch_bounds__(256) k_weight_quant(const float* __restrict__ w, int E, int C, int P,
+                                                      uint8_t* __restrict__ q, float* __restrict__ cscale) {
+  const int lane = threadIdx.x & 63;
+  const int e_ = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e_ >= E) return;
+  const int K = P * P * C;
+  auto at = [&](int k) {
+    const int tap = k / C, c = k - tap * C;
+    const int r = tap / P, s = tap - (tap / P) * P;
+    return w[(((size_t)e_ * C + c) * P + r) * P + s];
+  };
+  float amax = 0.f;
+  for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf(at(k)));
+  amax = wave_max(amax);
+  const float sc = amax > 0.f ? 448.f / amax : 1.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = at(k + e) * sc;
+    *(uint2*)(q + (size_t)e_ * K + k) = pack8_e4m3(v);
+  }
+  if (lane == 0) cscale[e_] = amax > 0.f ? amax / 448.f : 1.f;
+}
+
+// C[m][n] (bf16) = as[m] * bs[n] * sum_k A[m][k] B[n][k] + bias[n]; A, B e4m3
+// K-contiguous rows. 128x128 tile, 256 threads (2x2 waves of 64x64 = 4x4
+// 16x16x32 fragments), K-step 128 (one 128-B LDS row per operand row, 16-B
+// chunks XOR-swizzled by row&7), register-staged double buffer.
+constexpr int F8BM = 128, F8BN = 128, F8BK = 128;
+constexpr int F8STAGE = (F8BM + F8BN) * F8BK;
+
+__global__ void __launch_bounds__(256, 2) k_gemm_fp8(const uint8_t* __restrict__ A, int lda,
+                                                     const float* __restrict__ as, const uint8_t* __restrict__ B,
+                                                     int ldb, const float* __restrict__ bs,
+                                                     const float* __restrict__ bias, bf16_t* __restrict__ Cm, int ldc,
+                                                     int M, int N, int K, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int mt = blockIdx.x / ntiles, nt = blockIdx.x % ntiles;
+  const int m0 = mt * F8BM, n0 = nt * F8BN;
+  // loader: 128 rows x 8 chunks per operand; thread -> chunk tid&7 of rows tid>>3 + 32i
+  const int lq = tid & 7, lr = tid >> 3;
+  uint4 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = lr + 32 * i, k = k0 + lq * 16;
+      ra[i] = (m0 + r < M && k < K) ? *(const uint4*)(A + (size_t)(m0 + r) * lda + k) : make_uint4(0, 0, 0, 0);
+      rb[i] = (n0 + r < N && k < K) ? *(const uint4*)(B + (size_t)(n0 + r) * ldb + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](char* S) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = lr + 32 * i;
+      *(uint4*)(S + row * 128 + ((lq ^ (row & 7)) << 4)) = ra[i];
+      *(uint4*)(S + F8BM * 128 + row * 128 + ((lq ^ (row & 7)) << 4)) = rb[i];
+    }
+  };
+  f8_f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f8_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (K + F8BK - 1) / F8BK;
+  gload(0);
+  lstore(smem);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* S = smem + (kt & 1) * F8STAGE;
+    if (kt + 1 < nk) gload((kt + 1) * F8BK);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ch = kk * 2 + (fg >> 1), half = (fg & 1) * 8;
+      long av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        av[i] = *(const long*)(S + row * 128 + ((ch ^ (row & 7)) << 4) + half);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + fr;
+        bv[j] = *(const long*)(S + F8BM * 128 + col * 128 + ((ch ^ (col & 7)) << 4) + half);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(smem + ((kt + 1) & 1) * F8STAGE);
+    __syncthreads();
+  }
+  // epilogue: D[4*fg + e][fr] of each 16x16 fragment
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + fr;
+    if (n >= N) continue;
+    const float sb = bs[n], bb = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * 64 + i * 16 + fg * 4 + e;
+        if (m < M) Cm[(size_t)m * ldc + n] = f2bf(acc[i][j][e] * as[m] * sb + bb);
+      }
+  }
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" int dmf_patch_quant_fp8(const void* x, int N, int H, int W, int C, int ldx, int P, void* q, int ldq,
+                                   float* row_scale, void* stream) {
+  DMF_CHECK_ARG(x && q && row_scale && N > 0 && P > 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0,
+                "dmf_patch_quant_fp8: bad args (C=%d ldx=%d)", C, ldx);
+  DMF_CHECK_ARG(H % P == 0 && W % P == 0 && ldq >= P * P * C && ldq % 8 == 0 && ((uintptr_t)q % 8) == 0,
+                "dmf_patch_quant_fp8: bad geometry (H=%d W=%d P=%d ldq=%d)", H, W, P, ldq);
+  const int Ho = H / P, Wo = W / P;
+  const long long M = (long long)N * Ho * Wo;
+  hipLaunchKernelGGL(k_patch_quant, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, H, W, C, ldx, P, Ho, Wo, (uint8_t*)q, ldq, row_scale, M);
+  DMF_LAUNCH_CHECK("dmf_patch_quant_fp8");
+  return 0;
+}
+
+extern "C" int dmf_weight_quant_fp8(const float* w, int E, int C, int P, void* q, float* col_scale, void* stream) {
+  DMF_CHECK_ARG(w && q && col_scale && E > 0 && C > 0 && P > 0 && (P * P * C) % 8 == 0,
+                "dmf_weight_quant_fp8: bad args");
+  hipLaunchKernelGGL(k_weight_quant, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, (hipStream_t)stream, w, E, C, P,
+                     (uint8_t*)q, col_scale);
+  DMF_LAUNCH_CHECK("dmf_weight_quant_fp8");
+  return 0;
+}
+
+extern "C" int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const float* a_scale, const void* B, int ldb,
+                            const float* b_scale, const float* bias, void* C, int ldc, void* stream) {
+  DMF_CHECK_ARG(A && B && C && a_scale && b_scale && M > 0 && N > 0 && K > 0, "dmf_gemm_fp8: bad args");
+  DMF_CHECK_ARG(K % 16 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
+                "dmf_gemm_fp8: K (%d) and row strides must be multiples of 16 bytes", K);
+  const int ntiles = cdiv(N, F8BN);
+  const long long blocks = (long long)cdiv(M, F8BM) * ntiles;
+  DMF_CHECK_ARG(blocks < (1LL << 31), "dmf_gemm_fp8: grid too large");
+  hipLaunchKernelGGL(k_gemm_fp8, dim3((unsigned)blocks), dim3(256), (size_t)2 * F8STAGE, (hipStream_t)stream,
+                     (const uint8_t*)A, lda, a_scale, (const uint8_t*)B, ldb, b_scale, bias, (bf16_t*)C, ldc, M, N, K,
+                     ntiles);
+  DMF_LAUNCH_CHECK("dmf_gemm_fp8");
+  return 0;
+}

@@ -106,6 +106,55 @@ class _TokLNFn(torch.autograd.Function):
         return dy, dgamma, dbeta, None
 
 
+class _PatchEmbedFp8Fn(torch.autograd.Function):
+    """PatchEmbed.proj (conv k = s = P, transformer_model.py:17-22) forward on
+    the e4m3 MFMA GEMM (per-token / per-channel scales, csrc/fp8.hip); the
+    backward is the bf16 conv backward of the same conv (straight-through
+    through the quantisation)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, conv, caches):
+        n, c, h, w, ldx = O.nhwc(x)
+        p = conv.kernel_size[0]
+        e = weight.shape[0]
+        ho, wo = h // p, w // p
+        m, k = n * ho * wo, p * p * c
+        dev = x.device
+        q = torch.empty((m, k), dtype=torch.uint8, device=dev)
+        rs = torch.empty(m, dtype=torch.float32, device=dev)
+        N.call("dmf_patch_quant_fp8", x.data_ptr(), n, h, w, c, ldx, p, q.data_ptr(), k, rs.data_ptr(), _s())
+        wq = torch.empty((e, k), dtype=torch.uint8, device=dev)
+        cs = torch.empty(e, dtype=torch.float32, device=dev)
+        wc = weight.detach().float().contiguous()
+        N.call("dmf_weight_quant_fp8", wc.data_ptr(), e, c, p, wq.data_ptr(), cs.data_ptr(), _s())
+        y = O.empty_nhwc(n, e, ho, wo, torch.bfloat16, dev)
+        N.call("dmf_gemm_fp8", m, e, k, q.data_ptr(), k, rs.data_ptr(), wq.data_ptr(), k, cs.data_ptr(),
+               O._p(bias), y.data_ptr(), O.nhwc(y)[4], _s())
+        ctx.save_for_backward(x, weight, bias)
+        ctx.conv, ctx.caches = conv, caches
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dx, dw, db = O._conv_backward(x, weight, bias, O.ConvGeom(ctx.conv), ctx.caches, dy, need[0], need[1],
+                                      bias is not None and need[2])
+        return dx, dw, db, None, None
+
+
+def patch_embed_fp8(x, conv, caches):
+    """NHWC bf16 x -> NHWC bf16 patch-embed conv output via e4m3 MFMA."""
+    p = conv.kernel_size[0]
+    if (conv.kernel_size[0] != conv.kernel_size[1] or conv.stride[0] != p or conv.stride[1] != p
+            or conv.padding[0] != 0 or conv.dilation[0] != 1 or x.dtype != torch.bfloat16):
+        raise ValueError("patch_embed_fp8: needs a bf16 input and a conv with kernel == stride, no padding")
+    _, c, h, w, _ = O.nhwc(x)
+    if c % 8 or h % p or w % p or (p * p * c) % 16:
+        raise ValueError(f"patch_embed_fp8: unsupported shape C={c} H={h} W={w} P={p}")
+    return _PatchEmbedFp8Fn.apply(x, conv.weight, conv.bias, conv, caches)
+
+
 def patch_tokens_layernorm(y, ln):
     return _TokLNFn.apply(y, ln.weight, ln.bias, ln.eps)
 

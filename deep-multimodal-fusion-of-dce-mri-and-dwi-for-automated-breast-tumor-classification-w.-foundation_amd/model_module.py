@@ -425,6 +425,7 @@ class ModelMaskHeadBackbone(nn.Module):
                                                 depth=mp["transformer_depth"], heads=mp["transformer_heads"],
                                                 patch_size=mp["transformer_patch_size"], dim=self.dim)
             self.trans_out_proj = nn.Conv2d(mp["transformer_embed_dim"], c3, kernel_size=1)
+            self.transformer.patch_embed.use_fp8 = bool(mp.get("patch_embed_fp8", False))
 
         self.modality_attention = None
         if self.enable_modality_attention:

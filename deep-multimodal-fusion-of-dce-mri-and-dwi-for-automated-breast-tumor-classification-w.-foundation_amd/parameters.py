@@ -33,6 +33,7 @@ def default_parameters():
         "transformer_patch_size": 2,                    # :73
         "transformer_depth": 6,                         # :74
         "transformer_embed_dim": 512,                   # :75
+        "patch_embed_fp8": False,                       # build option (config 5): PatchEmbed.proj on e4m3 MFMA
         "dropout": 0.2,                                 # :77
         "channels": (128, 256, 512),                    # :82
         "repeat_blocks": (1, 1, 1),                     # :83

@@ -33,10 +33,17 @@ class PatchEmbed(nn.Module):
         self.norm = nn.LayerNorm(embed_dim)
         self.proj = nn.Conv2d(in_ch, embed_dim, kernel_size=patch_size, stride=patch_size)
 
+    # config 5 (BASELINE.json configs[4]): the projection on e4m3 MFMA; set by
+    # TransformerStage from parameters "patch_embed_fp8" (bf16 compute only)
+    use_fp8 = False
+
     def forward(self, x):
         dt = getattr(self, "compute_dtype", torch.bfloat16)
         x = O.as_nhwc(x.to(dt))
-        y = O.conv2d(x, self.proj, _caches(self.proj))           # [B, E, h, w] NHWC
+        if self.use_fp8 and dt == torch.bfloat16:
+            y = D.patch_embed_fp8(x, self.proj, _caches(self.proj))
+        else:
+            y = O.conv2d(x, self.proj, _caches(self.proj))       # [B, E, h, w] NHWC
         h, w = y.shape[-2:]
         return D.patch_tokens_layernorm(y, self.norm), (h, w)    # NHWC storage == token order
 

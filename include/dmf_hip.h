@@ -336,6 +336,21 @@ int dmf_cast_f32(const void* x, long long n, float* y, void* stream);
 int dmf_dropout_keep_mask(const unsigned long long* rng, int site, long long n, float p, unsigned char* keep,
                           void* stream);
 
+/* ------------------------------------------------- fp8 patch embed (cfg 5)
+ * PatchEmbed.proj (conv, kernel = stride = P; transformer_model.py:7-32) on
+ * OCP e4m3 MFMA (v_mfma_f32_16x16x32_fp8_fp8, fp32 accumulation).
+ * dmf_patch_quant_fp8: NHWC bf16 x [N][H][W][ldx] -> q [N*(H/P)*(W/P)][ldq]
+ *   e4m3 patch rows in (r, s, c) order, row_scale[m] = amax_m / 448.
+ * dmf_weight_quant_fp8: torch weight [E][C][P][P] fp32 -> q [E][P*P*C] e4m3,
+ *   col_scale[e] = amax_e / 448.
+ * dmf_gemm_fp8: C (bf16) [M][ldc] = a_scale[m] * b_scale[n] * A[m].B[n] + bias[n]
+ *   (A [M][lda], B [N][ldb], K-contiguous e4m3; K, lda, ldb multiples of 16). */
+int dmf_patch_quant_fp8(const void* x, int N, int H, int W, int C, int ldx, int P, void* q, int ldq,
+                        float* row_scale, void* stream);
+int dmf_weight_quant_fp8(const float* w, int E, int C, int P, void* q, float* col_scale, void* stream);
+int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const float* a_scale, const void* B, int ldb,
+                 const float* b_scale, const float* bias, void* C, int ldc, void* stream);
+
 /* ------------------------------------------------------------ optimizer
  * torch.optim.AdamW as built by LightningFusionOptimizerFactory
  * (selector_helpers.py:632-685, :617-629) -- multi-tensor, one launch. */

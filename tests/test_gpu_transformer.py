@@ -302,3 +302,51 @@ def test_hybrid_encoder_forward_backward():
     for name, prm in enc.named_parameters():
         if name.startswith("transformer.") and prm.grad is not None:
             _close(prm.grad, gr[name].grad, 5e-2, name)
+
+
+def test_patch_embed_fp8_matches_quantised_reference():
+    """Config 5's fp8 patch-embed (PatchEmbed.proj, transformer_model.py:17-22,
+    on e4m3 MFMA): the quantiser must produce OCP e4m3fn bytes identical to
+    torch.float8_e4m3fn's cast of the scaled rows, and the GEMM must match the
+    fp32 product of the dequantised operands (fp32 accumulation order only);
+    the bf16 backward is the conv engine's."""
+    import dmf_native as N
+    import dmf_tokens as D
+    torch.manual_seed(11)
+    n, c, h, w, e, p = 3, 256, 12, 10, 512, 2
+    conv = torch.nn.Conv2d(c, e, p, stride=p).to(DEV)
+    x = torch.randn(n, c, h, w, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    # reference quantisation (per token row / per output channel, amax -> 448)
+    xr = x.float().permute(0, 2, 3, 1).reshape(n, h // p, p, w // p, p, c).permute(0, 1, 3, 2, 4, 5)
+    xr = xr.reshape(n * (h // p) * (w // p), p * p * c).cpu()
+    rs = xr.abs().amax(1).clamp_min(1e-30) / 448.0
+    xq = (xr / rs[:, None]).to(torch.float8_e4m3fn)
+    wr = conv.weight.detach().float().permute(0, 2, 3, 1).reshape(e, -1).cpu()
+    cs = wr.abs().amax(1) / 448.0
+    wq = (wr / cs[:, None]).to(torch.float8_e4m3fn)
+    # the kernel's bytes
+    m, k = xr.shape
+    q = torch.empty((m, k), dtype=torch.uint8, device=DEV)
+    rsd = torch.empty(m, dtype=torch.float32, device=DEV)
+    N.call("dmf_patch_quant_fp8", x.data_ptr(), n, h, w, c, c, p, q.data_ptr(), k, rsd.data_ptr(),
+           N.stream_ptr())
+    torch.cuda.synchronize()
+    mism = (q.cpu() != xq.view(torch.uint8)).float().mean().item()
+    assert mism < 1e-3, mism  # ties may round differently; the format and the scaling must agree
+    assert torch.allclose(rsd.cpu(), rs, rtol=1e-6)
+    ref = (xq.float() * rs[:, None]) @ (wq.float() * cs[:, None]).t() + conv.bias.detach().float().cpu()
+    xd = x.clone().requires_grad_(True)
+    y = D.patch_embed_fp8(xd, conv, (O.WeightCache(), O.WeightCache()))
+    got = y.float().permute(0, 2, 3, 1).reshape(m, e).cpu()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+    # and the fp8 projection stays close to the exact conv
+    exact = torch.nn.functional.conv2d(x.float(), conv.weight, conv.bias, stride=p)
+    rel = (y.float() - exact).abs().max().item() / exact.abs().max().item()
+    assert rel < 0.08, rel
+    # backward: bf16 conv engine
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr2 = x.float().detach().requires_grad_(True)
+    torch.nn.functional.conv2d(xr2, conv.weight.detach(), None, stride=p).backward(g.float())
+    assert (xd.grad.float() - xr2.grad).abs().max().item() <= 3e-2 * xr2.grad.abs().max().item()
