@@ -95,6 +95,49 @@ def synthetic_batch(B, S, device, seed, cd=14, cc=6):
     return tuple(t.to(device) for t in (dwi, dce, masks, labels))
 
 
+# t_roof(fwd, B=32, bf16, S=256) = sum_k max(F_k / 2.5 PF, B_k / 8 TB/s)
+# over the DWI + DCE encoder forward kernels (algorithmic F and B per kernel)
+T_ROOF_ENC_FWD_MS_B32 = 2.69
+
+
+def encoder_forward_probe(trainer, batch, args):
+    """The north-star line: the fused DCE+DWI feature-extraction
+    forward (both encoders, a1-a10, train-mode BN as in the step) timed alone
+    from a hipGraph replay, against the survey's step roofline t_roof."""
+    lm = trainer.lm
+    dwi, dce = batch[0], batch[1]
+    with torch.no_grad():
+        for _ in range(2):
+            lm._encode(dwi, dce)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            lm._encode(dwi, dce)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            lm._encode(dwi, dce)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    out = {"ms": round(ms, 3), "volumes_per_s": round(args.batch / (ms * 1e-3), 1),
+           "what": "DWI + DCE encoder forward (a1-a10), hipGraph replay, train-mode BN"}
+    if args.config == 3 and args.size == 256 and args.dtype == "bf16":
+        t_roof = T_ROOF_ENC_FWD_MS_B32 * args.batch / 32
+        out.update({"t_roof_ms": round(t_roof, 3), "frac": round(t_roof / ms, 4),
+                    "roof": "SURVEY 8(d): sum_k max(F_k / 2.5 PFLOP/s, B_k / 8 TB/s)"})
+    return out
+
+
 def roofline_probe(trainer, batch, dtype):
     """Average launch duration of the dominant kernel family (implicit-GEMM
     conv forward): one eager step records every conv-forward C-ABI launch
@@ -268,6 +311,7 @@ def main():
     if not args.no_roofline:
         # every rank: the probe's eager step contains the gradient all-reduce
         roof = roofline_probe(trainer, batch, dtype)
+    enc = encoder_forward_probe(trainer, batch, args) if (rank == 0 and not args.no_roofline) else None
 
     vols = args.batch * world * args.steps
     out = {
@@ -293,6 +337,8 @@ def main():
         "peak_hbm_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
         "roofline": roof,
     }
+    if enc is not None:
+        out["encoder_forward"] = enc
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args, lambda: _cpu_params(PR, args))

@@ -1145,6 +1145,9 @@ struct ConvPlan {
 };
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
+// 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
+// 3 buf 128x64, 4 buf 64x64, 5 wide 256x128, 6 square 256x256 (only where legal)
+static int g_force = 0;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1163,6 +1166,17 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const long long wbytes = (long long)a.Nout * a.Ktot * es;
   p.buf = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31);
   if (!p.buf) return p;
+  if (g_force) {
+    const bool wide_ok = dtype == DMF_BF16 && a.Nout % WBN == 0 && a.Ktot >= 512;
+    const bool sq_ok = dtype == DMF_BF16 && a.Nout % QBN == 0 && a.Ktot >= 512;
+    if (g_force == 6 && sq_ok) { p.wide = p.sq = true; p.bm = QBM; p.bn = QBN; return p; }
+    if (g_force == 5 && wide_ok) { p.wide = true; p.bm = WBM; p.bn = WBN; return p; }
+    if (g_force >= 1 && g_force <= 4) {
+      p.bm = (g_force == 1 || g_force == 3) ? 128 : 64;
+      p.bn = (g_force == 1 || g_force == 2) ? 128 : 64;
+      return p;
+    }
+  }
   // square LDS-DMA tile: whole 256-column tiles and >= one block per CU
   // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
   // bound at one 256x256 block per CU and stays on the 256x128 form)
@@ -1358,6 +1372,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
   switch (key) {
     case 0: g_sq_enable = value != 0; return 0;
     case 1: DMF_CHECK_ARG(value >= 0 && value < 4, "dmf_conv_tune: square-tile variant %d", value); g_sq_var = value; return 0;
+    case 2: DMF_CHECK_ARG(value >= 0 && value <= 6, "dmf_conv_tune: forced tile %d", value); g_force = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

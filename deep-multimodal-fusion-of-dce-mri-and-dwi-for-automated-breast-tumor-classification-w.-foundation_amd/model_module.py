@@ -349,6 +349,7 @@ class BackboneAdapter(nn.Module):
 
 PARALLEL_NECKS = os.environ.get("DMF_PAR_NECK", "0") != "0"  # opt-in: measured slower (r01w)
 PARALLEL_PROJ = os.environ.get("DMF_PAR_PROJ", "0") != "0"  # opt-in: measured slower (r01w)
+PARALLEL_DEAD = os.environ.get("DMF_PAR_DEAD", "1") != "0"
 
 
 def _inline_branch(owner, name, fn, *inputs):
@@ -627,10 +628,14 @@ class FusionModel(nn.Module):
             p_dwi = self._proj(self.proj_in_dwi, raw_feats_dwi[-1])
             p_dce = self._proj(self.proj_in_dce, raw_feats_dce[-1])
             # Q4: reduce + refine are computed (BN running stats move in train
-            # mode) but never reach an output -- as in the reference (:935-940)
-            reduced = self.fusion_conv_reduce(p_dwi, x2=p_dce)
-            residual, _ = self.refine(reduced)
-            _refined = O.act_nhwc(reduced, "gelu", res=residual)
+            # mode) but never reach an output -- as in the reference (:935-940).
+            # Off the critical path: a side stream overlaps it with the rest of
+            # the fusion forward.
+            def _dead():
+                reduced = self.fusion_conv_reduce(p_dwi, x2=p_dce)
+                residual, _ = self.refine(reduced)
+                return O.act_nhwc(reduced, "gelu", res=residual)
+            _refined, join_dead = (O.branch if PARALLEL_DEAD else _inline_branch)(self, "dead", _dead, p_dwi, p_dce)
             pvec_dwi = O.gap(p_dwi)
             pvec_dce = O.gap(p_dce)
             gating_weights = self.gating(pvec_dwi, pvec_dce, dwi_mask=dwi_mask_pred, dce_mask=dce_mask_pred)
@@ -648,6 +653,7 @@ class FusionModel(nn.Module):
             logits = O.linear(O.gap(fused_refined), cl.weight, cl.bias)
             recon_fused = self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None
             proj_fused = self.projF(fused_refined)
+            join_dead()
         aux = {"proj_fused": proj_fused, "recon_fused": recon_fused, "gating_weights": gating_weights,
                "attn_weights": attn_weights, "p_dwi": p_dwi, "p_dce": p_dce}
         return logits, fused_mask_logits, aux
