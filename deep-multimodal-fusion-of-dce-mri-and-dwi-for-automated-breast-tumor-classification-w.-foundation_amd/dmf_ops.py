@@ -587,7 +587,9 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
     element count used for the running-variance correction (a map that the
     reference evaluates after a nearest 2x upsample has 4x the elements)."""
     g = ConvGeom(conv)
-    p = float(dropout_p) if bn.training else 0.0
+    # the caller decides (its nn.Dropout modules' flags): MC dropout keeps BN
+    # in eval with dropout on (train_fusion.py:479-481)
+    p = float(dropout_p)
     if p > 0 and rng is None:
         raise RuntimeError("dropout requested without an rng snapshot")
     if skip is not None:

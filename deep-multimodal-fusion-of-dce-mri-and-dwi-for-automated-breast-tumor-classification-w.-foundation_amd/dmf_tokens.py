@@ -286,11 +286,12 @@ class _BlockFn(torch.autograd.Function):
 
 def transformer_block(x, blk, rng, sites):
     """TransformerBlock.forward (transformer_model.py:78-81) as one node."""
-    training = blk.training
     at, mlp = blk.attn, blk.mlp
-    p_attn = float(at.attn_drop.p) if training else 0.0
-    p_proj = float(at.proj_drop.p) if training else 0.0
-    p_mlp = float(mlp.drop.p) if training else 0.0
+    # the nn.Dropout modules' own flags (train() / eval() set them with the
+    # block's; MC dropout turns on only these, train_fusion.py:445-449)
+    p_attn = float(at.attn_drop.p) if at.attn_drop.training else 0.0
+    p_proj = float(at.proj_drop.p) if at.proj_drop.training else 0.0
+    p_mlp = float(mlp.drop.p) if mlp.drop.training else 0.0
     if rng is None and (p_attn > 0 or p_proj > 0 or p_mlp > 0):
         raise RuntimeError("transformer dropout requested without an rng snapshot")
     e = x.shape[-1]

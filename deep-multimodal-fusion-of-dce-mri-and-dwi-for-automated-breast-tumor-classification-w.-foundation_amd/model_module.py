@@ -193,19 +193,22 @@ class ResNetLiteBlock_withRecon(nn.Module):
 
     def forward(self, x):
         x = _to_compute(x, _dt(self))
-        p = self.p if self.training else 0.0
-        rng = _rng(x.device) if p > 0 else None
+        # dropout follows the nn.Dropout modules' flags (train()/eval() set them
+        # with the block's; MC dropout turns on only them, train_fusion.py:445-449)
+        p_out = self.p if self.dropout.training else 0.0
+        rng = _rng(x.device) if (p_out > 0 or any(b[3].training for b in self.bottlenecks)) and self.p > 0 else None
         h = x
         last = len(self.bottlenecks) - 1
         for i, b in enumerate(self.bottlenecks):
             site_a, site_b = self._sites[i]
+            p = self.p if b[3].training else 0.0
             h = O.conv_bn_act(h, b[0], _caches(b[0]), b[1], "gelu", dropout_p=p, rng=rng, site=site_a)
             h = O.conv_bn_act(h, b[4], _caches(b[4]), b[5], "gelu")
             if i < last:
                 h = O.conv_bn_act(h, b[7], _caches(b[7]), b[8], "none")
             else:
                 # act(bn(conv(h)) + identity) -> dropout, fused in one pass
-                kw = dict(dropout_p=p, rng=rng, site=site_b)
+                kw = dict(dropout_p=p_out, rng=rng, site=site_b)
                 if self.skip is not None:
                     kw["skip"] = (x, self.skip[0], _caches(self.skip[0]), self.skip[1])
                 else:

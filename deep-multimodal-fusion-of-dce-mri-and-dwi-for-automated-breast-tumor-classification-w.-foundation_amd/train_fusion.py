@@ -104,8 +104,11 @@ class LightningFusionModel(nn.Module):
         if side is None or side.device != dwi_inputs.device:
             side = torch.cuda.Stream(dwi_inputs.device)
             self.__dict__["_side_stream"] = side
-        snap_dwi = O.RNG.snapshot(dwi_inputs.device) if self.dwi_model.training else None
-        snap_dce = O.RNG.snapshot(dwi_inputs.device) if self.dce_model.training else None
+        # one snapshot per encoder whenever it draws dropout masks (train mode,
+        # or MC dropout with only the Dropout modules on): the two streams then
+        # never advance the shared Philox state concurrently
+        snap_dwi = O.RNG.snapshot(dwi_inputs.device) if _draws_dropout(self.dwi_model) else None
+        snap_dce = O.RNG.snapshot(dwi_inputs.device) if _draws_dropout(self.dce_model) else None
         side.wait_stream(main)
         prev = O.RNG_CURRENT[0]
         O.ORIGIN_STREAM[0] = main
@@ -199,17 +202,130 @@ class LightningFusionModel(nn.Module):
         _, dce_aux, dce_mask = self.dce_model(dce_inputs)
         return self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask, dce_mask)
 
+    # ---- test-time MC dropout x TTA (train_fusion.py:445-632) -------------
+    def enable_dropout(self, model):
+        """train_fusion.py:445-449."""
+        for m in model.modules():
+            if isinstance(m, nn.Dropout):
+                m.train()
+
+    def set_batchnorm_eval(self, model):
+        """train_fusion.py:455-459."""
+        for m in model.modules():
+            if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d, nn.SyncBatchNorm)):
+                m.eval()
+
+    def _get_module_train_states(self, model):
+        return {m: m.training for m in model.modules()}
+
+    def _restore_module_train_states(self, model, states):
+        for m, was_training in states.items():
+            m.train(was_training)
+
+    def mc_enable(self, model):
+        """train_fusion.py:479-481: Dropout on, BatchNorm in eval."""
+        self.enable_dropout(model)
+        self.set_batchnorm_eval(model)
+
+    @torch.no_grad()
+    def _replicated_forward(self, dwi_list, dce_list, chunk):
+        """One batched forward over replicas of the batch (TTA views x MC
+        passes, concatenated along the batch axis): BN is per-sample in eval
+        mode and every replica row draws its own Philox dropout mask (the mask
+        index runs over the batch rows), so R replicas of B volumes cost
+        ceil(R*B/chunk) encoder+fusion launches instead of R sequential
+        forwards. Returns (softmax probs [R, B, K], gating [R, B, 2])."""
+        b = dwi_list[0].shape[0]
+        r = len(dwi_list)
+        per = max(1, chunk // b)
+        probs, gates = [], []
+        for i in range(0, r, per):
+            x_dwi = torch.cat(dwi_list[i:i + per], 0)
+            x_dce = torch.cat(dce_list[i:i + per], 0)
+            (_, dwi_aux, dwi_mask), (_, dce_aux, dce_mask) = self._encode(x_dwi, x_dce)
+            logits, _, aux = self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask, dce_mask)
+            probs.append(torch.softmax(logits.float(), dim=1).view(-1, b, logits.shape[1]))
+            gw = aux["gating_weights"]
+            gates.append(gw.float().reshape(-1, b, gw.shape[-1]) if gw is not None else None)
+        gating = torch.cat(gates, 0) if all(g is not None for g in gates) else None
+        return torch.cat(probs, 0), gating, dwi_aux, dce_aux
+
+    def predict_mc_dropout(self, dwi_inputs, dce_inputs, masks=None, passes=20, chunk=256):
+        """train_fusion.py:484-537: passes stochastic forwards (encoders'
+        Dropout on, BN eval) -> mean / std of the softmax, mean gating; the
+        passes run batched (_replicated_forward). The reference's
+        masks-given branch feeds encoder *logits* back into the encoders
+        (:500-503) and cannot run; it is not reproduced."""
+        st_dwi = self._get_module_train_states(self.dwi_model)
+        st_dce = self._get_module_train_states(self.dce_model)
+        self.mc_enable(self.dwi_model)
+        self.mc_enable(self.dce_model)
+        try:
+            probs, gating, dwi_aux, dce_aux = self._replicated_forward([dwi_inputs] * passes, [dce_inputs] * passes,
+                                                                       chunk)
+        finally:
+            self._restore_module_train_states(self.dwi_model, st_dwi)
+            self._restore_module_train_states(self.dce_model, st_dce)
+        mean_gating = gating.mean(0).cpu() if gating is not None else None
+        return probs.mean(0), probs.std(0), {"gating_weights": mean_gating, "dwi_aux": dwi_aux, "dce_aux": dce_aux}
+
+    def predict_tta(self, dwi_inputs, dce_inputs, masks=None, transforms=None, chunk=256):
+        """train_fusion.py:541-587: one forward per flip (identity, lr, ud,
+        lr+ud; train.py:916-923) -> mean / std of the softmax, mean gating;
+        the views run batched. As in the reference the aux of the fusion
+        output has no dwi_aux / dce_aux keys, so those stay None."""
+        transforms = transforms if transforms is not None else self.transforms_list
+        probs, gating, _, _ = self._replicated_forward([t(x=dwi_inputs) for t in transforms],
+                                                       [t(x=dce_inputs) for t in transforms], chunk)
+        mean_gating = gating.mean(0).cpu() if gating is not None else None
+        return probs.mean(0), probs.std(0), {"gating_weights": mean_gating, "dwi_aux": None, "dce_aux": None}
+
+    def predict_tta_mc(self, dwi_inputs, dce_inputs, masks=None, transforms=None, passes=10, chunk=256):
+        """train_fusion.py:591-632: per flip, the MC mean of passes
+        stochastic forwards; then mean / std over the flips. All
+        len(transforms) x passes forwards run batched."""
+        transforms = transforms if transforms is not None else self.transforms_list
+        st_dwi = self._get_module_train_states(self.dwi_model)
+        st_dce = self._get_module_train_states(self.dce_model)
+        self.mc_enable(self.dwi_model)
+        self.mc_enable(self.dce_model)
+        try:
+            views_dwi = [t(x=dwi_inputs) for t in transforms for _ in range(passes)]
+            views_dce = [t(x=dce_inputs) for t in transforms for _ in range(passes)]
+            probs, gating, dwi_aux, dce_aux = self._replicated_forward(views_dwi, views_dce, chunk)
+        finally:
+            self._restore_module_train_states(self.dwi_model, st_dwi)
+            self._restore_module_train_states(self.dce_model, st_dce)
+        nt = len(transforms)
+        per_t = probs.view(nt, passes, *probs.shape[1:]).mean(1)
+        mean_gating = None
+        if gating is not None:
+            mean_gating = gating.view(nt, passes, *gating.shape[1:]).mean(1).mean(0).cpu()
+        return per_t.mean(0), per_t.std(0), {"gating_weights": mean_gating, "dwi_aux": dwi_aux, "dce_aux": dce_aux}
+
     @torch.no_grad()
     def predict_custom(self, batch, mode="normal", mc_passes=10):
+        """train_fusion.py:682-701."""
         dwi = batch[0].to(self.device)
         dce = batch[1].to(self.device)
+        masks = batch[2] if len(batch) == 4 else None
         if mode == "normal":
-            return self.forward_from_inputs(dwi, dce)
-        raise NotImplementedError(f"predict mode {mode!r} (TTA / MC-dropout) is a 'next' row (SURVEY 8(f) rank 2)")
+            return self.forward_from_inputs(dwi, dce, masks)
+        if mode == "tta":
+            return self.predict_tta(dwi, dce, masks)
+        if mode == "mc":
+            return self.predict_mc_dropout(dwi, dce, passes=mc_passes)
+        if mode == "tta_mc":
+            return self.predict_tta_mc(dwi, dce, masks, passes=mc_passes)
+        raise ValueError(f"Unknown predict mode: {mode}")
 
 
 # ------------------------------------------------------------------ helpers
 PARALLEL_ENCODERS = O.PARALLEL_BRANCHES
+
+
+def _draws_dropout(model):
+    return model.training or any(isinstance(m, nn.Dropout) and m.training and m.p > 0 for m in model.modules())
 
 
 def compute_recon_list_loss(recon_list, input_img):

@@ -113,7 +113,8 @@ class TransformerBlock(nn.Module):
 
     def forward(self, x):
         rng = None
-        if self.training:
+        # dropout follows the nn.Dropout modules (MC dropout turns only them on)
+        if self.attn.attn_drop.training or self.attn.proj_drop.training or self.mlp.drop.training:
             cur = O.RNG_CURRENT[0]
             rng = cur if cur is not None else O.RNG.snapshot(x.device)
         return D.transformer_block(x.float(), self, rng, self._sites)
