@@ -351,6 +351,28 @@ int dmf_weight_quant_fp8(const float* w, int E, int C, int P, void* q, float* co
 int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const float* a_scale, const void* B, int ldb,
                  const float* b_scale, const float* bias, void* C, int ldc, void* stream);
 
+/* ------------------------------------------------------------ data path
+ *  fp32 NCHW-contiguous planes [N*C][HW].
+ * dmf_dwi_normalize: DWINormalize (dataset.py:9-41), ADC slot zero if adc.
+ * dmf_adc_map: compute_adc_map (preprocess_helpers.py:133-167) -> [N][HW];
+ *   preprocess != 0 fuses preprocess_adc (:39-49).
+ * dmf_plane_select: the ranks[T] (ascending, T <= 64) order statistics of
+ *   every plane -> vals [planes][T] (exact; multi-target radix select).
+ * dmf_plane_percentiles: numpy 'linear' percentiles from them: perc
+ *   [planes][L] (float64) = _lerp(vals[lo_idx[l]], vals[hi_idx[l]], gamma[l]).
+ * dmf_nyul_apply: NyulStandardizer.transform (preprocess_helpers.py:94-120):
+ *   y = interp(interp(x, perc[plane], avg[c]), avg[c], scale), np.interp
+ *   semantics, float64 arithmetic, L <= 32. */
+int dmf_dwi_normalize(const float* x, int N, int C, long long HW, int adc, float z_lo, float z_hi, float* y,
+                      void* stream);
+int dmf_adc_map(const float* dwi, int N, int C, long long HW, const float* bvals, float eps, int preprocess,
+                float* adc, void* stream);
+int dmf_plane_select(const float* x, int planes, long long HW, const int* ranks, int T, float* vals, void* stream);
+int dmf_plane_percentiles(const float* vals, int T, const int* lo_idx, const int* hi_idx, const double* gamma, int L,
+                          int planes, double* perc, void* stream);
+int dmf_nyul_apply(const float* x, int planes, int C, long long HW, const double* perc, const double* avg,
+                   const double* scale, int L, float* y, void* stream);
+
 /* ------------------------------------------------------------ optimizer
  * torch.optim.AdamW as built by LightningFusionOptimizerFactory
  * (selector_helpers.py:632-685, :617-629) -- multi-tensor, one launch. */
