@@ -326,7 +326,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int BUF_FLAGS = 0x00020000;
 
-template <typename T, bool PADCHK, bool DUAL, int BM, int BN>
+// INA >= 0 (plain 1x1 only, PADCHK = DUAL = false): the producer's BN apply
+// + activation x <- act(x*scale + shift) runs on each A chunk between its
+// load and its LDS write (ConvArgs::in_ss = [scale C][shift C]); the
+// activated tensor is never written to HBM.
+template <typename T, bool PADCHK, bool DUAL, int BM, int BN, int INA = -1>
 __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN <= 64 * 128) ? 3 : 2)) k_conv_fwd_buf(ConvArgs a) {
   constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per K-step
   constexpr int SB = (BM + BN) * 128;        // LDS stage bytes
@@ -375,6 +379,15 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
     vb[i] = n < a.Nout ? (unsigned)((n * a.Ktot + q * EPC) * ES) : BUF_OOB;
   }
   const int nk = a.Ktot / BK;
+  // input affine: the whole [scale C][shift C] vector staged once in LDS past
+  // the stage ring + epilogue scratch, so the per-K-step reads are ds_read_b128
+  float* ss_lds = (float*)(smem + conv_lds_main(ES, BM, BN) + CONV_LDS_EXTRA);
+  if constexpr (INA >= 0) {
+    for (int i = tid * 4; i < 2 * a.C; i += CTHREADS * 4) *(float4*)(ss_lds + i) = *(const float4*)(a.in_ss + i);
+    __syncthreads();
+  } else {
+    (void)ss_lds;
+  }
 
   // two register sets: tile kt+1 is in flight while tile kt+2 is issued
   uint4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
@@ -416,8 +429,22 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
     for (int i = 0; i < RB; ++i)
       rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, vb[i], k0 * ES, 0));
   };
-  auto lds_store = [&](int stage, const uint4 (&ra)[RA], const uint4 (&rb)[RB]) {
+  auto lds_store = [&](int stage, uint4 (&ra)[RA], const uint4 (&rb)[RB], int tile) {
     char* base = smem + stage * SB;
+    if constexpr (INA >= 0) {
+      // plain 1x1: tile t covers channels t*BK .. t*BK+BK-1; this thread's 16-B chunk q
+      const int c = tile * BK + q * EPC;
+      float sc[EPC], sh[EPC];
+#pragma unroll
+      for (int e = 0; e < EPC; e += 4) {
+        *(float4*)(sc + e) = *(const float4*)(ss_lds + c + e);
+        *(float4*)(sh + e) = *(const float4*)(ss_lds + a.C + c + e);
+      }
+#pragma unroll
+      for (int i = 0; i < RA; ++i) chunk_affine<T, INA>(ra[i], sc, sh);
+    } else {
+      (void)tile;
+    }
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int row = rbase + 32 * i;
@@ -442,8 +469,8 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
   if (nk <= 2) {  // short K (1x1 over <= 128 channels): no pipeline to fill
     gload(0, ra0, rb0);
     if (nk == 2) gload(1, ra1, rb1);
-    lds_store(0, ra0, rb0);
-    if (nk == 2) lds_store(1, ra1, rb1);
+    lds_store(0, ra0, rb0, 0);
+    if (nk == 2) lds_store(1, ra1, rb1, 1);
     __syncthreads();
     conv_mma<T, BM, BN>(smem, acc, wm, wn, lane);
     if (nk == 2) conv_mma<T, BM, BN>(smem + SB, acc, wm, wn, lane);
@@ -453,19 +480,19 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
   }
   gload(0, ra0, rb0);
   gload(1, ra1, rb1);
-  lds_store(0, ra0, rb0);
+  lds_store(0, ra0, rb0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; kt += 2) {
     // even step: LDS stage 0 holds tile kt, ra1/rb1 carry tile kt+1
     gload(min(kt + 2, nk - 1), ra0, rb0);
     conv_mma<T, BM, BN>(smem, acc, wm, wn, lane);
-    lds_store(1, ra1, rb1);
+    lds_store(1, ra1, rb1, min(kt + 1, nk - 1));
     __syncthreads();
     if (kt + 1 >= nk) break;
     // odd step: stage 1 holds tile kt+1, ra0/rb0 carry tile kt+2
     gload(min(kt + 3, nk - 1), ra1, rb1);
     conv_mma<T, BM, BN>(smem + SB, acc, wm, wn, lane);
-    lds_store(0, ra0, rb0);
+    lds_store(0, ra0, rb0, min(kt + 2, nk - 1));
     __syncthreads();
   }
   conv_epilogue<T, BM, BN>(a, acc, smem, tid, mt, nt, m0, n0);
@@ -1125,6 +1152,13 @@ static bool pers_disabled() {
   }();
   return v != 0;
 }
+static bool ina_buf_disabled() {
+  static const int v = [] {
+    const char* e = std::getenv("DMF_CONV_INA_BUF");
+    return e && e[0] == '0' ? 1 : 0;
+  }();
+  return v != 0;
+}
 static bool fast_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_LEGACY");
@@ -1157,7 +1191,10 @@ static bool wide_disabled() {
 }
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   ConvPlan p{false, false, false, CBM, CBN};
-  if (dgrad || a.in_ss != nullptr || fast_disabled()) return p;
+  const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
+  if (dgrad || fast_disabled() || (a.in_ss != nullptr && !(plain && a.x2 == nullptr && !ina_buf_disabled())))
+    return p;
   const int es = dtype == DMF_BF16 ? 2 : 4;
   const int bk = dtype == DMF_BF16 ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
@@ -1166,6 +1203,11 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const long long wbytes = (long long)a.Nout * a.Ktot * es;
   p.buf = fastc && xbytes < (1LL << 31) && x2bytes < (1LL << 31) && wbytes < (1LL << 31);
   if (!p.buf) return p;
+  if (a.in_ss != nullptr) {
+    p.bn = a.Nout <= 64 ? 64 : 128;
+    p.bm = (long long)cdiv(a.M, 128) * cdiv(a.Nout, p.bn) < 512 ? 64 : 128;
+    return p;
+  }
   if (g_force) {
     const bool wide_ok = dtype == DMF_BF16 && a.Nout % WBN == 0 && a.Ktot >= 512;
     const bool sq_ok = dtype == DMF_BF16 && a.Nout % QBN == 0 && a.Ktot >= 512;
@@ -1258,6 +1300,17 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_wide<true, true>), g, bw, lds_total, st, a);
     else if (plain) hipLaunchKernelGGL((k_conv_fwd_wide<false, false>), g, bw, lds_total, st, a);
     else hipLaunchKernelGGL((k_conv_fwd_wide<true, false>), g, bw, lds_total, st, a);
+  } else if (plan.buf && a.in_ss != nullptr) {
+    DMF_CHECK_ARG(((uintptr_t)a.in_ss % 16) == 0, "%s: input scale/shift must be 16-byte aligned", what);
+    DMF_CHECK_ARG(a.C <= 4096, "%s: input-affine conv over %d channels exceeds the LDS staging", what, a.C);
+    const size_t lds_ina = lds_total + (size_t)a.C * 8;
+    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
+#define DMF_INA_BUF(TT, IA)                                                                                         do {                                                                                                                switch (cfg) {                                                                                                      case 3: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 128, 128, IA>), g, b, lds_ina, st, a); break;       case 2: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 128, 64, IA>), g, b, lds_ina, st, a); break;        case 1: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 64, 128, IA>), g, b, lds_ina, st, a); break;        default: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 64, 64, IA>), g, b, lds_ina, st, a);             }                                                                                                               } while (0)
+#define DMF_INA_ACT(TT)                                                                        do {                                                                                           switch (a.act_in) {                                                                            case DMF_ACT_NONE: DMF_INA_BUF(TT, DMF_ACT_NONE); break;                                     case DMF_ACT_RELU: DMF_INA_BUF(TT, DMF_ACT_RELU); break;                                     case DMF_ACT_GELU: DMF_INA_BUF(TT, DMF_ACT_GELU); break;                                     default: DMF_CHECK_ARG(false, "%s: unsupported input activation %d", what, a.act_in);     }                                                                                          } while (0)
+    if (dtype == DMF_BF16) DMF_INA_ACT(bf16_t);
+    else DMF_INA_ACT(float);
+#undef DMF_INA_ACT
+#undef DMF_INA_BUF
   } else if (plan.buf) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const bool dual = a.x2 != nullptr;
@@ -1379,13 +1432,28 @@ extern "C" int dmf_conv_tune(int key, int value) {
 
 // rows of the BN partial-statistics slab a forward launch of this shape writes
 extern "C" int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2,
-                                         int Cout, int KH, int KW, int Ho, int Wo, int has_in_affine) {
+                                         int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo,
+                                         int has_in_affine) {
   ConvArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = Cin + Cin2; a.ldx = ldx; a.C1 = Cin; a.ldx2 = ldx2;
+  a.stride = stride; a.pad = pad;
   a.x2 = Cin2 > 0 ? (const void*)16 : nullptr;
   a.in_ss = has_in_affine ? (const float*)16 : nullptr;
   a.Nout = Cout; a.KH = KH; a.KW = KW; a.Ktot = KH * KW * a.C; a.M = N * Ho * Wo;
   return cdiv(a.M, conv_plan(dtype, false, a).bm);
+}
+
+// 1 when a plain 1x1 conv of this shape that takes its producer's BN apply +
+// activation in its operand loads (in_scale_shift) runs on the same
+// buffer-load tile as without it -- i.e. the unfused launch would not pick
+// the 256-wide LDS-DMA tiles, which have no input-affine form
+extern "C" int dmf_conv2d_fwd_input_affine_fusable(int dtype, int N, int H, int W, int Cin, int Cout) {
+  if (ina_buf_disabled()) return 0;
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = Cin; a.C1 = Cin;
+  a.Nout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0; a.Ktot = Cin; a.M = N * H * W;
+  const ConvPlan p = conv_plan(dtype, false, a);
+  return p.buf && !p.wide ? 1 : 0;
 }
 
 static int conv_fwd_common(ConvArgs& a, int dtype, const void* x, int N, int H, int W, int Cin, int ldx,

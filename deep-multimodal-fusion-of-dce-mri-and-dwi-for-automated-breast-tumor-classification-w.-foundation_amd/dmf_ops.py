@@ -230,8 +230,8 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     else:
         wk = caches[0].get(weight, x.dtype, cx + cx2, 0)
         if want_stats:
-            tiles = N.load().dmf_conv2d_fwd_stat_tiles(dtc, n, h, w, cx, ldx, cx2, ldx2, co, kh, kw, ho, wo,
-                                                       1 if in_ss is not None else 0)
+            tiles = N.load().dmf_conv2d_fwd_stat_tiles(dtc, n, h, w, cx, ldx, cx2, ldx2, co, kh, kw, g.stride, g.pad,
+                                                       ho, wo, 1 if in_ss is not None else 0)
             partials = torch.empty((tiles, co, 2), dtype=torch.float32, device=dev)
         _conv_launch("dmf_conv2d_fwd",
                      (dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw, g.stride,
@@ -242,7 +242,29 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
 
 
 DGRAD_AS_FWD = os.environ.get("DMF_DGRAD_FWD", "1") != "0"
-FUSED_BN_MAX_MTILES = 32  # measured: at larger slabs every block's drain-before-ticket costs more than a finalize launch
+# no-grad forwards: a BN apply + activation feeding a 1x1 conv runs in that
+# conv's loads (conv_bn_stats + in_ss) instead of its own pass. Opt-in
+# (DMF_FUSE_INA=1): measured 1-2 % slower on the mode-A step (r01zi: 2470 vs
+# 2500 vol/s) -- the affine on the load path costs the 128x128 buffer-load
+# tile more than the saved BN-apply pass
+FUSE_INPUT_AFFINE = os.environ.get("DMF_FUSE_INA", "0") == "1"
+FUSED_BN_MAX_MTILES = 32
+
+def fuse_input_affine(x, producer, consumer, *params):
+    """True when, with no autograd graph to build, ``producer``'s BN apply +
+    activation should run inside the 1x1 ``consumer``'s operand loads: only
+    where that conv keeps the tile it would use unfused (measured: moving a
+    conv off the 256-wide LDS-DMA tiles costs more than the saved pass)."""
+    if not FUSE_INPUT_AFFINE or needs_grad(x, *params):
+        return False
+    gc = ConvGeom(consumer)
+    if (gc.kh, gc.kw, gc.stride, gc.pad) != (1, 1, 1, 0):
+        return False
+    n, _, h, w, _ = nhwc(x)
+    ho, wo = ConvGeom(producer).out_hw(h, w)
+    return bool(N.load().dmf_conv2d_fwd_input_affine_fusable(dt(x), n, ho, wo, consumer.in_channels,
+                                                              consumer.out_channels))
+  # measured: at larger slabs every block's drain-before-ticket costs more than a finalize launch
 
 
 def _bn_site(bn, dev):
@@ -264,7 +286,7 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
     cx2_, ldx2_ = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
     ho_, wo_ = g.out_hw(h_, w_)
     mtiles = N.load().dmf_conv2d_fwd_stat_tiles(dt(x), n_, h_, w_, cx_, ldx_, cx2_, ldx2_, w.shape[0], w.shape[2],
-                                                w.shape[3], ho_, wo_, 1 if in_ss is not None else 0)
+                                                w.shape[3], g.stride, g.pad, ho_, wo_, 1 if in_ss is not None else 0)
     if not (training and _is_mfma_conv(w, g) and mtiles <= FUSED_BN_MAX_MTILES):
         y, part = _conv_forward_raw(x, w, b, g, caches, training, "none", x2=x2, in_ss=in_ss, in_act=in_act)
         n, c, ho, wo, _ = nhwc(y)

@@ -74,12 +74,19 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         h = O.conv_bn_act(x, self.conv1, _caches(self.conv1), self.bn1, "relu")
-        h = O.conv_bn_act(h, self.conv2, _caches(self.conv2), self.bn2, "relu")
+        kw = {}
+        if O.fuse_input_affine(h, self.conv2, self.conv3, x, *self.parameters()):
+            # no autograd (frozen encoder, mode A): conv2's BN apply + ReLU run
+            # inside conv3's operand loads -- act2's output is never written
+            h, ss2 = O.conv_bn_stats(h, self.conv2, _caches(self.conv2), self.bn2)
+            kw = dict(in_ss=ss2, in_act="relu")
+        else:
+            h = O.conv_bn_act(h, self.conv2, _caches(self.conv2), self.bn2, "relu")
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
             return O.conv_bn_act(h, self.conv3, _caches(self.conv3), self.bn3, "relu",
-                                 skip=(x, ds_conv, _caches(ds_conv), ds_bn))
-        return O.conv_bn_act(h, self.conv3, _caches(self.conv3), self.bn3, "relu", res=x)
+                                 skip=(x, ds_conv, _caches(ds_conv), ds_bn), **kw)
+        return O.conv_bn_act(h, self.conv3, _caches(self.conv3), self.bn3, "relu", res=x, **kw)
 
 
 class ResNet50OS8(nn.Module):

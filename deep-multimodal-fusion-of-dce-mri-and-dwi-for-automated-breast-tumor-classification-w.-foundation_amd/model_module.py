@@ -203,12 +203,18 @@ class ResNetLiteBlock_withRecon(nn.Module):
             site_a, site_b = self._sites[i]
             p = self.p if b[3].training else 0.0
             h = O.conv_bn_act(h, b[0], _caches(b[0]), b[1], "gelu", dropout_p=p, rng=rng, site=site_a)
-            h = O.conv_bn_act(h, b[4], _caches(b[4]), b[5], "gelu")
+            kin = {}
+            if O.fuse_input_affine(h, b[4], b[7], x, *b.parameters()):
+                # no autograd: the 3x3's BN apply + GELU run inside the 1x1's loads
+                h, ss = O.conv_bn_stats(h, b[4], _caches(b[4]), b[5])
+                kin = dict(in_ss=ss, in_act="gelu")
+            else:
+                h = O.conv_bn_act(h, b[4], _caches(b[4]), b[5], "gelu")
             if i < last:
-                h = O.conv_bn_act(h, b[7], _caches(b[7]), b[8], "none")
+                h = O.conv_bn_act(h, b[7], _caches(b[7]), b[8], "none", **kin)
             else:
                 # act(bn(conv(h)) + identity) -> dropout, fused in one pass
-                kw = dict(dropout_p=p_out, rng=rng, site=site_b)
+                kw = dict(dropout_p=p_out, rng=rng, site=site_b, **kin)
                 if self.skip is not None:
                     kw["skip"] = (x, self.skip[0], _caches(self.skip[0]), self.skip[1])
                 else:

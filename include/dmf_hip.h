@@ -61,7 +61,12 @@ int dmf_conv_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */
 int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin, int ldx, int Cin2, int ldx2, int Cout, int KH,
-                              int KW, int Ho, int Wo, int has_in_affine);
+                              int KW, int stride, int pad, int Ho, int Wo, int has_in_affine);
+/* 1 when a plain 1x1 conv (Cin -> Cout over N x H x W) fed by
+ * in_scale_shift runs on the same tile family as the unfused conv, so fusing
+ * the producer's BN apply + activation into it saves that pass (the 256-wide
+ * LDS-DMA tiles have no input-affine form); 0 -> apply the BN separately */
+int dmf_conv2d_fwd_input_affine_fusable(int dtype, int N, int H, int W, int Cin, int Cout);
 /* x2 (nullable): second input concatenated along channels after the Cin
  * channels of x (BackboneAdapter chain [C4, C5], model_module.py:471) */
 /* in_scale_shift (nullable, single source only): the producer's batch-norm

@@ -485,3 +485,39 @@ def test_mask_attention_backward_sliced(dtype):
     assert close(md.grad, mr.grad, 5 * tol)
     for p_dev, p_ref in zip(dev_m.parameters(), ref_m.parameters()):
         assert close(p_dev.grad, p_ref.grad, 5 * tol), (p_dev.grad, p_ref.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(64, 128, 16, 16, 256, "relu"), (8, 64, 32, 32, 64, "gelu"),
+                                   (4, 48, 8, 8, 32, "relu")])
+def test_conv_fused_input_affine(dtype, shape):
+    """Forward-only chain of the frozen encoder (foundation_model.py Bottleneck,
+    model_module.py ResNetLite): conv -> BN(batch stats) -> act -> 1x1 conv ->
+    BN -> act, with the first BN apply + act run inside the 1x1 conv's operand
+    loads (conv_bn_stats + in_ss). Channel counts that are multiples of the
+    K-step take the buffer-load kernel; 48 takes the im2col fallback."""
+    n, c, h, w, co, act = shape
+    torch.manual_seed(5)
+    x = torch.randn(n, c, h, w)
+    c1, c2 = nn.Conv2d(c, c, 3, padding=1, bias=False), nn.Conv2d(c, co, 1, bias=False)
+    b1, b2 = nn.BatchNorm2d(c), nn.BatchNorm2d(co)
+    for m in (b1, b2):
+        m.weight.data.uniform_(0.5, 1.5)
+        m.bias.data.uniform_(-0.5, 0.5)
+    f = F.relu if act == "relu" else F.gelu
+    with torch.no_grad():
+        ref = f(b2(c2(f(b1(c1(x))))))
+    mods = [copy.deepcopy(m).to(DEV) for m in (c1, c2)]
+    bns = [copy.deepcopy(m).to(DEV) for m in (b1, b2)]
+    for m in bns:
+        m.running_mean.zero_()
+        m.running_var.fill_(1.0)
+    with torch.no_grad():
+        xd = _to_dev(x, dtype)
+        y1, ss = O.conv_bn_stats(xd, mods[0], (O.WeightCache(), O.WeightCache()), bns[0])
+        y = O.conv_bn_act(y1, mods[1], (O.WeightCache(), O.WeightCache()), bns[1], act, in_ss=ss, in_act=act)
+    rtol, atol = _tol(dtype)
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= atol * 4 + rtol * ref.abs().max().item(), err
+    assert torch.allclose(bns[1].running_mean.cpu(), b2.running_mean, rtol=1e-3,
+                          atol=1e-4 if dtype == torch.float32 else 2e-2)
