@@ -1708,6 +1708,27 @@ def mimic(s_feat, t_feat):
     return _MimicFn.apply(s, t, 1, 0, 0, h * w, c, c)
 
 
+def mimic_items(s_feat, t_feat):
+    """mimic_feat_loss (train.py:1033-1038) on whole batches [B, ...]: rows are
+    batch items (flatten(1)), as in the single-model step (train.py:453-455).
+    Each item is one contiguous block in either dense layout (the cosine does
+    not depend on the element order within an item), so the kernel runs B
+    "pairs" of one row of numel/B elements each; one launch."""
+    if s_feat.shape != t_feat.shape:
+        raise RuntimeError(f"mimic_items: shapes differ {tuple(s_feat.shape)} vs {tuple(t_feat.shape)}")
+    s = s_feat
+    if not (s.is_contiguous() or (s.dim() == 4 and s.is_contiguous(memory_format=torch.channels_last))):
+        s = s.contiguous()
+    t = t_feat.detach().to(s.dtype)
+    if t.stride() != s.stride():
+        t = torch.empty_like(s).copy_(t)
+    b = s.shape[0]
+    k = s[0].numel()
+    if k >= 1 << 31:
+        raise RuntimeError("mimic_items: item too large")
+    return _MimicFn.apply(s, t, b, k, k, k, 1, 1)
+
+
 def mimic_pairs(feats, npairs=2):
     """train_fusion.py:291-294: mean over pairs (items 2i, 2i+1) of
     mimic_feat_loss(feats[2i], feats[2i+1]) -- one launch."""

@@ -2,10 +2,10 @@
 ``code/train.py`` that the fusion step uses (train.py:287-288 encoder
 wrapper forward, :916-923 TTA flips, :991-1048 loss helpers).
 
-The Lightning single-model loop itself is outside the hot-path scope
-(SURVEY.md 8(f) rank 4); ``LightningSingleModel`` here is the thin wrapper the
-fusion step calls (``self.dwi_model(x)`` -> ``self.model(x, masks)``) and keeps
-the ``model.`` state_dict prefix of the reference's checkpoints.
+``LightningSingleModel`` carries the single-modality training step
+(train.py:294-466) and is also the encoder wrapper
+the fusion step calls (``self.dwi_model(x)`` -> ``self.model(x, masks)``),
+keeping the ``model.`` state_dict prefix of the reference's checkpoints.
 """
 from __future__ import annotations
 
@@ -13,19 +13,167 @@ import torch
 import torch.nn as nn
 
 import dmf_ops as O
+from loss import LabelSmoothing
 
 
 class LightningSingleModel(nn.Module):
-    """Encoder wrapper (train.py:19-288 subset): forward(x, masks=None) -> model(x, masks)."""
+    """Single-modality training module (train.py:19-466) without the Lightning
+    runtime: same constructor, ``forward(x, masks)`` and
+    ``_shared_step(batch, batch_idx, phase, return_preds)`` contract; a driver
+    calls ``training_step`` -> backward -> optimizer step. Also the encoder
+    wrapper the fusion step calls (``self.dwi_model(x)`` -> ``self.model(x,
+    masks)``), keeping the ``model.`` state_dict prefix of the reference's
+    checkpoints. Loss terms run in the fused criterion kernels
+    (csrc/losses.hip): focal + smoothing, Dice, the recon terms of one step
+    in one launch, and the item-row mimic in one launch per pair."""
 
-    def __init__(self, model, parameters_dict=None, method="dwi", **kwargs):
+    def __init__(self, model, method="dwi", criterion_clf=None, optimizer_fn=None, scheduler_fn=None,
+                 parameters_dict=None, paths=None):
         super().__init__()
         self.model = model
-        self.parameters_dict = parameters_dict
         self.method = method
+        self.criterion_clf = criterion_clf
+        self.optimizer_fn = optimizer_fn
+        self.scheduler_fn = scheduler_fn
+        self.parameters_dict = parameters_dict
+        self.paths = paths
+        self.current_epoch = 0
+        self.global_step = 0
+        self.optimizer = None
+        self.scheduler = None
+        self.last_metrics = {}
+        self.transforms_list = [tta_id, tta_flip_lr, tta_flip_ud, tta_flip_lrud]
+        if parameters_dict is None:
+            return
+        mp = parameters_dict[f"{method}_model_parameters"]
+        self.model_params = mp
+        self.recon_enabled = mp["recon_enabled"]
+        self.lambda_recon = mp["lambda_recon"]
+        self.mimic_enabled = mp["mimic_enabled"]
+        self.lambda_mimic = mp["lambda_mimic"]
+        self.class_num = parameters_dict["class_num"]
+        self.attn_reg_enabled = mp["attn_reg_enabled"]
+        self.lambda_attn_energy = mp["lambda_attn_energy"]
+        self.lambda_feature_consistency = mp["lambda_feature_consistency"]
+        self.feat_norm_reg_enabled = mp["feat_norm_reg_enabled"]
+        self.lambda_feat_norm = mp["lambda_feat_norm"]
+        mk = mp["mask_parameters"]
+        self.mask_enabled = mk["mask"]
+        self.lambda_mask = mk["lambda_mask"]
+        self.label_smoother = (LabelSmoothing(self.class_num, mp["label_smoothing_alpha"])
+                               if mp["label_smoothing_enabled"] else None)
+        from selector_helpers import mask_criterion_selector
+        self.mask_criterion = mask_criterion_selector(parameters_dict, method)
+        self.use_aux_loss_sched = parameters_dict["use_simple_aux_loss_scheduling"]
+        self.aux_loss_limit = parameters_dict["aux_loss_weight_epoch_limit"]
+
+    @property
+    def device(self):
+        return next(self.model.parameters()).device
 
     def forward(self, x, masks=None):
         return self.model(x, masks)
+
+    def configure_optimizers(self):
+        """train.py:190-224 (the grad_clip keys are returned but never
+        honoured, quirk Q10)."""
+        self.optimizer = self.optimizer_fn(self.model.parameters())
+        if self.scheduler_fn is None:
+            return self.optimizer
+        sched = self.scheduler_fn(self.optimizer)
+        self.scheduler = sched["scheduler"] if isinstance(sched, dict) and "scheduler" in sched else sched
+        return {"optimizer": self.optimizer, "lr_scheduler": sched}
+
+    def _shared_step(self, batch, batch_idx=0, phase="train", return_preds=False):
+        """train.py:294-418 with compute_aux_losses (:423-466)."""
+        is_train = phase == "train"
+        if self.mask_enabled:
+            inputs, masks, labels = batch
+        else:
+            inputs, labels = batch
+            masks = None
+        dev = self.device
+        inputs = inputs.to(dev, non_blocking=True)
+        labels = labels.to(dev, non_blocking=True).long()
+        if masks is not None:
+            masks = masks.to(dev, non_blocking=True)
+        aux_w = max(0.0, 1 - self.current_epoch / self.aux_loss_limit) if self.use_aux_loss_sched else 1.0
+
+        outputs, aux, mask_output = self(inputs, masks)
+
+        if self.label_smoother is not None:
+            smoothed = self.label_smoother(outputs, labels)
+        # Q7: `smoothed` is undefined in training without label smoothing, as in the reference
+        clf_loss = self.criterion_clf(outputs, smoothed) if is_train else self.criterion_clf(outputs, labels)
+        batch_loss = clf_loss
+
+        if self.attn_reg_enabled and is_train:
+            batch_loss = batch_loss + compute_attn_energy_loss(aux, dev) * self.lambda_attn_energy \
+                + compute_feature_consistency_loss(aux, dev) * self.lambda_feature_consistency
+        feat_norm = torch.zeros((), device=dev)
+        if self.feat_norm_reg_enabled:
+            feat_norm = compute_feat_norm_loss(aux, dev)
+            if is_train:
+                batch_loss = batch_loss + feat_norm * self.lambda_feat_norm
+
+        mask_out_resized = None
+        mask_loss = torch.zeros((), device=dev)
+        if self.mask_enabled:
+            if mask_output.shape[-2:] != masks.shape[-2:]:
+                mask_out_resized = O.bilinear(mask_output, *masks.shape[-2:])
+            else:
+                mask_out_resized = mask_output
+            mask_loss = self.mask_criterion(mask_output, masks)
+            if is_train:
+                batch_loss = batch_loss + self.lambda_mask * mask_loss
+
+        recon_loss_val = torch.zeros((), device=dev)
+        mimic_loss_val = torch.zeros((), device=dev)
+        if self.recon_enabled and aux_w > 0.0:
+            recon_loss_val, mimic_loss_val = self.compute_aux_losses(aux, inputs, aux_w, is_train)
+            if is_train:
+                # the values are already lambda * aux_w weighted (train.py:458-460): weighted twice, as there
+                batch_loss = batch_loss + (self.lambda_recon * recon_loss_val * aux_w
+                                           + self.lambda_mimic * mimic_loss_val * aux_w)
+
+        preds = outputs.argmax(dim=1)
+        acc = (preds == labels).float().mean()
+        self.last_metrics = {"loss": batch_loss.detach(), "acc": acc.detach(), "cls": clf_loss.detach(),
+                             "mask": mask_loss.detach(), "recon": recon_loss_val.detach(),
+                             "mimic": mimic_loss_val.detach(), "feat_norm": feat_norm.detach()}
+        if return_preds:
+            return batch_loss.detach(), outputs.detach(), aux, mask_out_resized
+        return batch_loss
+
+    def compute_aux_losses(self, aux, inputs, aux_w, is_train):
+        """train.py:423-466: recon terms SUMMED over recon_feats (bilinear up to
+        the input size vs the input's channel mean), mimic over (p1, p1_r) and
+        (p2, p2_r) with rows = batch items; lambda * aux_w applied in training."""
+        dev = inputs.device
+        recon = torch.zeros((), device=dev)
+        mimic = torch.zeros((), device=dev)
+        if aux_w <= 0.0:
+            return recon, mimic
+        maps = [r for r in (aux.get("recon_feats", []) if aux is not None else []) if r is not None]
+        if maps:
+            if any(r.shape[1] != 1 for r in maps):
+                raise NotImplementedError("multi-channel reconstructions are not on the reference path")
+            tgt = O.channel_mean_map(inputs.detach())
+            recon = O.recon_terms(maps, [0] * len(maps), tgt).sum()
+        pp = aux.get("proj_pairs", None) if aux is not None else None
+        if self.mimic_enabled and pp is not None and len(pp) >= 4:
+            mimic = O.mimic_items(pp[0], pp[1]) + O.mimic_items(pp[2], pp[3])
+        if is_train:
+            recon = recon * self.lambda_recon * aux_w
+            mimic = mimic * self.lambda_mimic * aux_w
+        return recon, mimic
+
+    def training_step(self, batch, batch_idx=0):
+        return self._shared_step(batch, batch_idx, "train")
+
+    def validation_step(self, batch, batch_idx=0):
+        loss, _, _, _ = self._shared_step(batch, batch_idx, phase="val", return_preds=True)
+        return loss
 
 
 # ------------------------------------------------------------------ TTA flips (train.py:916-923)

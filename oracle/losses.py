@@ -140,3 +140,51 @@ def fusion_shared_step(dwi_model, dce_model, fusion_model, batch, P, class_weigh
             total = total + fp["lambda_mimic"] * mimic * aux_w
     out.update(cls=cls, mask=mask, recon=recon, mimic=mimic, total=total)
     return out
+
+
+def single_shared_step(model, batch, P, class_weights, method="dwi", epoch=0, phase="train"):
+    """train.py:294-466 (LightningSingleModel._shared_step + compute_aux_losses)
+    -> dict of the loss terms and ``total``.
+
+    Restated quirks: the recon/mimic values that compute_aux_losses returns in
+    training are already multiplied by lambda * aux_w (train.py:458-460) and
+    _shared_step multiplies them by lambda * aux_w again (:400-403); recon terms
+    are SUMMED over recon_feats (:444-450), not averaged as in the fusion step;
+    mimic pairs (p1, p1_r), (p2, p2_r) with rows = batch items (:453-455)."""
+    mp = P[f"{method}_model_parameters"]
+    inputs, masks, labels = batch
+    labels = labels.long()
+    is_train = phase == "train"
+    aux_w = max(0.0, 1 - epoch / P["aux_loss_weight_epoch_limit"]) if P["use_simple_aux_loss_scheduling"] else 1.0
+    logits, aux, mask_out = model(inputs, masks)
+    K = P["class_num"]
+    gamma = mp["classification_loss_parameters"]["gamma"]
+    tgt = label_smoothing(logits, labels, K, mp["label_smoothing_alpha"]) if is_train else labels
+    cls = soft_weighted_focal(logits, tgt, gamma, class_weights)
+    total = cls
+    feat_norm = torch.zeros(())
+    if mp["feat_norm_reg_enabled"]:
+        feat_norm = feat_norm_loss(aux)
+        if is_train:
+            total = total + feat_norm * mp["lambda_feat_norm"]
+    mask = soft_dice(mask_out, masks)
+    if is_train:
+        total = total + mp["mask_parameters"]["lambda_mask"] * mask
+    recon = torch.zeros(())
+    mimic = torch.zeros(())
+    if mp["recon_enabled"] and aux_w > 0:
+        for r in aux["recon_feats"]:
+            if r is None:
+                continue
+            up = F.interpolate(r, size=inputs.shape[-2:], mode="bilinear", align_corners=False)
+            tgt_img = inputs.mean(1, keepdim=True) if up.size(1) == 1 and inputs.size(1) > 1 else inputs
+            recon = recon + recon_image_loss(up, tgt_img)
+        pp = aux.get("proj_pairs")
+        if mp["mimic_enabled"] and pp is not None and len(pp) >= 4:
+            mimic = mimic_feat_loss(pp[0], pp[1]) + mimic_feat_loss(pp[2], pp[3])
+        if is_train:
+            recon = recon * mp["lambda_recon"] * aux_w
+            mimic = mimic * mp["lambda_mimic"] * aux_w
+            total = total + mp["lambda_recon"] * recon * aux_w + mp["lambda_mimic"] * mimic * aux_w
+    return {"logits": logits, "aux": aux, "mask_pred": mask_out, "cls": cls, "mask": mask, "recon": recon,
+            "mimic": mimic, "feat_norm": feat_norm, "total": total}
