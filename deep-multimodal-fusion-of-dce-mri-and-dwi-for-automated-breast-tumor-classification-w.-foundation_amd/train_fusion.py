@@ -189,6 +189,12 @@ class LightningFusionModel(nn.Module):
             return total.detach(), logits.detach(), aux, fused_mask_logits
         return total
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", strict=True, **kwargs):
+        """Lightning-layout .ckpt -> module (run_training.py:123-131); see run_training.py."""
+        from run_training import load_from_checkpoint
+        return load_from_checkpoint(cls, checkpoint_path, map_location=map_location, strict=strict, **kwargs)
+
     def training_step(self, batch, batch_idx=0):
         return self._shared_step(batch, "train")
 

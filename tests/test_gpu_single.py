@@ -93,3 +93,32 @@ def test_single_step_parity(phase):
         if e_mine > 3 * e_ref + 5e-3:
             bad[n] = (round(e_mine, 5), round(e_ref, 5))
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
+
+
+def test_checkpoint_reload_reproduces_logits(tmp_path):
+    """run_training.py:123-131 on the device: a Lightning-layout .ckpt written
+    from a GPU module and loaded into a differently initialised one gives the
+    same eval logits (frozen-weight caches re-prepare on the new versions)."""
+    import run_training as RT
+
+    P = PR.small_parameters(dropout=0.0)
+    enc, _, P = build_pair(P, "dce", 6, 71)
+    lm = TR.LightningSingleModel(model=enc, method="dce", parameters_dict=P)
+    for p in lm.parameters():
+        p.requires_grad = False
+    lm.eval()
+    _, dce, _, _ = batch(2, 64, 17)
+    with torch.no_grad():
+        want, _, _ = lm(dce.to(DEV))
+    path = RT.save_checkpoint(lm, str(tmp_path / "best.ckpt"))
+    other, _, _ = build_pair(P, "dce", 6, 72)
+    for p in other.parameters():
+        p.requires_grad = False
+    with torch.no_grad():
+        before, _, _ = other.eval()(dce.to(DEV))  # warms the weight caches on the old weights
+    got_m = TR.LightningSingleModel.load_from_checkpoint(path, map_location=DEV, model=other, method="dce",
+                                                         parameters_dict=P).eval()
+    with torch.no_grad():
+        got, _, _ = got_m(dce.to(DEV))
+    assert (before - want).abs().max().item() > 1e-3
+    assert torch.equal(got, want)
