@@ -201,6 +201,9 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     if x2 is not None:
         _, cx2, _, _, ldx2 = nhwc(x2)
     co, ci, kh, kw = weight.shape
+    if cx + cx2 < ci:  # (more is the zero channel padding of the staged input)
+        raise RuntimeError(f"conv2d: weight of size {list(weight.shape)} expected input with {ci} channels, but got "
+                           f"{cx + cx2} channels instead")
     ho, wo = g.out_hw(h, w)
     dtc = dt(x)
     dev = x.device
@@ -763,6 +766,9 @@ def _act_f32(x, out, act):
 
 
 def linear(x, w, b=None, act="none"):
+    if x.shape[-1] != w.shape[1]:
+        raise RuntimeError(f"linear: input features {x.shape[-1]} (shape {tuple(x.shape)}) do not match weight "
+                           f"{tuple(w.shape)}")
     return _LinearFn.apply(x, w, b, act)
 
 

@@ -385,6 +385,7 @@ class ModelMaskHeadBackbone(nn.Module):
         super().__init__()
         P = parameters_dict
         mp = P[f"{method}_model_parameters"]
+        self.method = method
         self.channel_num = P[f"{method}_channel_num"]
         self.num_classes = P["class_num"]
         self.dim = P["dim"]
@@ -477,6 +478,13 @@ class ModelMaskHeadBackbone(nn.Module):
         return proj(O.adaptive_avgpool(_to_compute(f, _dt(self)), self.proj_dim, self.proj_dim))
 
     def _stage_input(self, x):
+        # the messages of torch's conv2d shape checks (SURVEY 8(b) Errors)
+        if x.dim() != 4:
+            raise RuntimeError(f"Expected 4D (batched) input [B,C,H,W] to the {self.method} encoder, but got input "
+                               f"of size: {list(x.shape)}")
+        if x.shape[1] != self.channel_num:
+            raise RuntimeError(f"{self.method} encoder expected input {list(x.shape)} to have {self.channel_num} "
+                               f"channels, but got {x.shape[1]} channels instead")
         dt = _dt(self)
         if self.modality_attention is not None:
             fc = self.modality_attention.fc

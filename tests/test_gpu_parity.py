@@ -91,9 +91,12 @@ def _fusion_pair(P, seed):
     return fm.to(DEV), fr
 
 
-def test_fusion_step_parity_mode_a():
+@pytest.mark.parametrize("B", [4, 2, 5])
+def test_fusion_step_parity_mode_a(B):
     """Reference default at epoch 0: encoders frozen (train mode), backward
-    through FusionModel only; compare every loss term and every fusion grad."""
+    through FusionModel only; compare every loss term and every fusion grad.
+    B=2: fewer than 4 items, so the mimic term is skipped (train_fusion.py:291,
+    quirk Q5); B=5: a ragged batch (odd M for every conv / reduction)."""
     P = PR.small_parameters(dropout=0.0)
     dwi_m, dwi_r, P1 = build_pair(P, "dwi", 14, 21)
     dce_m, dce_r, _ = build_pair(P, "dce", 6, 22)
@@ -107,7 +110,7 @@ def test_fusion_step_parity_mode_a():
         m.train()
     for p in list(dwi_r.parameters()) + list(dce_r.parameters()):
         p.requires_grad = False
-    bt = batch(4, 64, 7)
+    bt = batch(B, 64, 7)
     loss = lm.training_step(tuple(t.to(DEV) for t in bt))
     loss.backward()
     cw = OL.class_weights_from_labels(train_labels)
@@ -260,3 +263,22 @@ def test_fusion_step_config5_hybrid_mode_b():
         if n.startswith("transformer.") and named[n].grad is not None:
             g2 = named[n].grad
             assert (p1.grad.cpu().reshape(g2.shape) - g2).abs().max() <= 5e-2 * max(1e-3, g2.abs().max().item()), n
+
+
+def test_encoder_rejects_bad_input_loudly():
+    """Shape errors surface as Python exceptions (SURVEY 8(b) Errors), not
+    aborts or silent garbage: wrong channel count, and a non-4-D input."""
+    P = PR.small_parameters(dropout=0.0)
+    enc, _, _ = build_pair(P, "dwi", 14, 11)
+    enc.eval()
+    with torch.no_grad():
+        with pytest.raises((RuntimeError, ValueError)):
+            enc(torch.rand(2, 13, 64, 64, device=DEV))
+        with pytest.raises((RuntimeError, ValueError, IndexError)):
+            enc(torch.rand(14, 64, 64, device=DEV))
+        lo, aux, mp = enc(torch.rand(2, 14, 64, 64, device=DEV))  # still usable afterwards
+        fm, _ = _fusion_pair(P, 23)
+        short = [f[:, : f.shape[1] // 2] for f in aux["raw_feats"]]
+        with pytest.raises(RuntimeError):
+            fm(short, aux["raw_feats"], mp, mp)
+    assert torch.isfinite(lo).all()
