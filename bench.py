@@ -40,21 +40,27 @@ F32_MFMA_PEAK_TFLOPS = 157.3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (default 32; 16 for config 2, 4 for config 1)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--mode", choices=["A", "B"], default="A")
     ap.add_argument("--patch-embed", choices=["fp8", "bf16"], default="fp8",
                     help="config 5: PatchEmbed.proj on e4m3 MFMA (default) or the bf16 conv engine")
-    ap.add_argument("--config", type=int, choices=[3, 5], default=3,
-                    help="5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
+    ap.add_argument("--config", type=int, choices=[1, 2, 3, 5], default=3,
+                    help="1: single-modality DWI CNN without backbone (C=16, S=128, train step); "
+                         "2: DCE-only ResNet-50 OS8 feature extractor (5 phases, forward); "
+                         "3: fusion step (default); "
+                         "5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="default run only: skip the mode-B and config-2 sub-measurements")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -212,13 +218,28 @@ def _cpu_params(PR, args):
     return P
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the process's CPU share. On the GPU
+    box os.cpu_count() reports the whole machine while OMP_NUM_THREADS holds
+    this job's share (16), so the share wins when it is set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() and int(env) > 0 else (os.cpu_count() or 1)
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(args, P_fn):
     """fp32 CPU oracle (same eager op sequence as the reference) on a bounded
-    sample: cpu-batch volumes at SxS, mode A step, 1 warm-up + cpu-steps timed."""
+    sample of the benched workload: cpu-batch volumes at SxS (B=32 = the GPU
+    line's per-GPU batch), mode A/B step, 1 warm-up then the median of
+    cpu-steps timed steps (3 timed steps after 1 warm-up)."""
     from oracle import losses as OL
     from oracle import model as OM
 
-    torch.set_num_threads(os.cpu_count() if os.cpu_count() <= 16 else 16)
+    torch.set_num_threads(cpu_threads())
     P = P_fn()
     P["dwi_model_parameters"]["backbone_index_lists"] = [[0], [1], [2, 3]]
     torch.manual_seed(0)
@@ -240,14 +261,217 @@ def cpu_baseline(args, P_fn):
         opt.step()
 
     step()
-    t0 = time.perf_counter()
+    times = []
     for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
         step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(args.cpu_batch / med, 4), "unit": "volumes/s",
+            "cores": torch.get_num_threads(), "host_cpu_count": os.cpu_count(), "kind": "port",
+            "step_s": [round(t, 3) for t in times],
+            "sample": f"oracle fp32 CPU (torch eager, {torch.get_num_threads()} threads = this job's CPU share; "
+                      f"os.cpu_count() {os.cpu_count()}), config {args.config} mode {args.mode}, median of "
+                      f"{args.cpu_steps} timed steps x {args.cpu_batch} volumes at {args.size}x{args.size} "
+                      f"(1 warm-up step)"}
+
+
+def _graph(fn):
+    """Capture fn() (GPU work only, inputs resident) into a hipGraph after
+    two eager runs on a side stream (allocator / weight-cache warm-up)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = fn()
+    return g, out
+
+
+def _median_step_ms(step, n):
+    """Median of n individually event-timed steps (SURVEY 8(d) timing
+    procedure) -- reported beside the pipelined K-step mean."""
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    return ts[len(ts) // 2]
+
+
+def conv_probe(fn, dtype):
+    """Dominant-kernel roofline of one eager run of fn (see roofline_probe)."""
+    import dmf_ops as O
+
+    recs = []
+    O.PROBE["conv_fwd"] = recs
+    torch.cuda.synchronize()
+    fn()
+    torch.cuda.synchronize()
+    O.PROBE["conv_fwd"] = None
+    if not recs:
+        return None
+    flops = sum(r["flops"] for r in recs)
+    byt = sum(r["bytes"] for r in recs)
+    n = len(recs)
+    avg_ms, _ = O.probe_replay(recs)
+    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    achieved = flops / n / (avg_ms * 1e-3) / 1e12
+    recs.clear()
+    return {"kernel": "conv2d forward (k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "launches_per_step": n,
+            "avg_launch_us": round(avg_ms * 1e3, 2), "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
+            "algorithmic_mb_per_launch": round(byt / n / 1e6, 2)}
+
+
+# SURVEY 8(d) config 2: timm ResNet-50 OS8, in_chans=5, S=256: 50.0 GFLOP per volume (2 x MACs of every conv)
+CONFIG2_GFLOP_PER_VOL = 50.0
+
+
+def bench_config2(device, batch, steps, warmup, size=256, probe=True):
+    """Config 2: DCE-only foundation feature extractor (foundation_model.py:
+    build_medical_backbone(..., 'dce', in_channels=5) -> timm resnet50
+    features_only OS8, :260-267), bf16, forward only, inference (eval BN),
+    inputs resident in HBM; one step = one forward over the batch, replayed
+    from a hipGraph."""
+    import foundation_model as FM
+    import parameters as PR
+
+    P = PR.default_parameters()
+    P["dce_channel_num"] = 5
+    P["dwi_model_parameters"]["compute_dtype"] = torch.bfloat16
+    torch.manual_seed(0)
+    bb = FM.build_medical_backbone(P, "cpu", "dce", 5).to(device).eval()
+    for p in bb.parameters():
+        p.requires_grad = False
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand(batch, 5, size, size, generator=g).to(device)
+
+    def fwd():
+        with torch.no_grad():
+            return bb(x)
+
+    graph, feats = _graph(fwd)
+    for _ in range(warmup):
+        graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {"value": round(args.cpu_batch * args.cpu_steps / dt, 4), "unit": "volumes/s",
-            "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle fp32 CPU, mode {args.mode}, {args.cpu_steps} timed steps x {args.cpu_batch} volumes "
-                      f"at {args.size}x{args.size} (1 warm-up step)"}
+    ms = dt * 1e3 / steps
+    med = _median_step_ms(graph.replay, max(5, min(steps, 50)))
+    gflop = CONFIG2_GFLOP_PER_VOL * (size / 256) ** 2
+    tf = gflop * batch / (ms * 1e-3) / 1e3
+    finite = all(bool(torch.isfinite(f).all()) for f in feats)
+    out = {"metric": "DCE volumes/sec (foundation feature extraction, fwd)", "value": round(batch * steps / dt, 2),
+           "unit": "volumes/s", "ms_per_step": round(ms, 3), "ms_per_step_median": round(med, 3),
+           "steps": steps, "warmup": warmup, "dtype": "bf16", "finite": finite,
+           "config": {"workload": "config 2: DCE-only ResNet-50 OS8 feature extractor (5 phases, eval BN, fwd)",
+                      "per_gpu_batch": batch, "size": size, "in_chans": 5, "hipgraph": True},
+           "step_roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(tf / BF16_MFMA_PEAK_TFLOPS, 4),
+                             "algorithmic_gflop_per_volume": gflop}}
+    if probe:
+        out["roofline"] = conv_probe(fwd, torch.bfloat16)
+    del graph
+    return out
+
+
+def bench_config1(device, batch, steps, warmup, size=128, chans=16):
+    """Config 1: the single-modality DWI CNN without backbone
+    (model_module.py:550-552, :663-666), C=16, S=128, one training step =
+    LightningSingleModel.training_step -> backward -> AdamW (train.py:294-428),
+    bf16, replayed from a hipGraph."""
+    import model_module as MM
+    import parameters as PR
+    import train as TR
+    from dmf_optim import FusedAdamW
+    from selector_helpers import get_classification_loss
+
+    P = PR.default_parameters()
+    mp = P["dwi_model_parameters"]
+    mp["use_backbone"] = False
+    mp["input_size"] = size
+    mp["compute_dtype"] = torch.bfloat16
+    P["dwi_channel_num"] = chans
+    torch.manual_seed(0)
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, None), True).to(device)
+    crit = get_classification_loss(P, torch.arange(1024) % P["class_num"], "dwi", device)
+    lm = TR.LightningSingleModel(model=enc, method="dwi", criterion_clf=crit, parameters_dict=P)
+    lm.train()
+    opt = FusedAdamW(lm.parameters(), lr=1e-4, weight_decay=4e-5)
+    g = torch.Generator().manual_seed(0)
+    x = (0.5 + torch.randn(batch, chans, size, size, generator=g) / 6).clamp(0, 1).to(device)
+    masks = (torch.rand(batch, 1, 32, 32, generator=g) > 0.5).float().to(device)
+    labels = (torch.arange(batch) % 4).to(device)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = lm.training_step((x, masks, labels))
+        loss.backward()
+        opt.step()
+        return loss.detach()
+
+    step()  # the optimizer's tables exist before capture
+    graph, loss = _graph(step)
+    for _ in range(warmup):
+        graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "DWI volumes/sec (single-modality CNN training step, fwd+bwd+AdamW)",
+            "value": round(batch * steps / dt, 2), "unit": "volumes/s", "ms_per_step": round(dt * 1e3 / steps, 3),
+            "steps": steps, "warmup": warmup, "dtype": "bf16", "loss": round(float(loss.item()), 5),
+            "config": {"workload": "config 1: DWI CNN, use_backbone=False, all trainable", "per_gpu_batch": batch,
+                       "size": size, "in_chans": chans, "hipgraph": True}}
+
+
+def bench_fusion(P, device, dtype, mode, batch_size, size, steps, warmup, world, rank, use_graph=True):
+    """Config 3/5 fusion training step -> (trainer, batch, seconds for steps)."""
+    from dmf_dp import FusionTrainer
+
+    lm = build(P, device, dtype, mode, seed=0)
+    trainer = FusionTrainer(lm, world=world, use_graph=use_graph)
+    batch = synthetic_batch(batch_size, size, device, seed=2 + rank)
+    if use_graph:
+        trainer.capture(batch)
+    for _ in range(warmup):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    return trainer, batch, dt
+
+
+# SURVEY 8(d): algorithmic work per volume of the fusion step
+GFLOP_PER_VOL = {"A": 155.0, "B": 458.0}
 
 
 def main():
@@ -267,8 +491,22 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", dev_idx)
     import parameters as PR
-    from dmf_dp import FusionTrainer
 
+    if args.config in (1, 2):
+        if world > 1:
+            raise SystemExit("configs 1 and 2 are single-GPU configurations (BASELINE.json)")
+        if args.config == 2:
+            out = bench_config2(device, args.batch or 16, args.steps, args.warmup,
+                                size=args.size, probe=not args.no_roofline)
+        else:
+            out = bench_config1(device, args.batch or 4, args.steps, args.warmup,
+                                size=128 if args.size == 256 else args.size)
+        out.update({"n_gpus": 1, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                    "data": "synthetic volumes, random-init weights"})
+        print(json.dumps(out), flush=True)
+        return
+
+    args.batch = args.batch or 32
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     P = PR.default_parameters()
     if args.config == 5:
@@ -280,40 +518,20 @@ def main():
         if args.size == 256:
             args.size = 384
     P["dwi_model_parameters"]["input_size"] = args.size
-    lm = build(P, device, dtype, args.mode, seed=0)
-    trainer = FusionTrainer(lm, world=world, use_graph=not args.no_graph)
-    batch = synthetic_batch(args.batch, args.size, device, seed=2 + rank)
-
-    roof = None
-    if not args.no_graph:
-        trainer.capture(batch)
-    for _ in range(args.warmup):
-        trainer.step(batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step(batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+    trainer, batch, dt = bench_fusion(P, device, dtype, args.mode, args.batch, args.size, args.steps, args.warmup,
+                                      world, rank, use_graph=not args.no_graph)
     loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
     if loss_val is not None and loss_val != loss_val:
         raise RuntimeError("training loss is NaN: the benchmarked step is numerically broken")
+    med = _median_step_ms(lambda: trainer.step(batch), min(args.steps, 50)) if world == 1 else None
+    roof = None
     if not args.no_roofline:
         # every rank: the probe's eager step contains the gradient all-reduce
         roof = roofline_probe(trainer, batch, dtype)
     enc = encoder_forward_probe(trainer, batch, args) if (rank == 0 and not args.no_roofline) else None
 
     vols = args.batch * world * args.steps
+    ms = dt * 1e3 / args.steps
     out = {
         "metric": "DCE+DWI volumes/sec/node (fwd+bwd)",
         "value": round(vols / dt, 2),
@@ -321,7 +539,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt * 1e3 / args.steps, 3),
+        "ms_per_step": round(ms, 3),
+        "ms_per_step_median": round(med, 3) if med is not None else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -337,8 +556,37 @@ def main():
         "peak_hbm_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
         "roofline": roof,
     }
+    if args.config == 3 and args.size == 256:
+        tf = GFLOP_PER_VOL[args.mode] * args.batch / (ms * 1e-3) / 1e3
+        out["step_roofline"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(tf / BF16_MFMA_PEAK_TFLOPS, 4),
+                                "algorithmic_gflop_per_volume": GFLOP_PER_VOL[args.mode]}
     if enc is not None:
         out["encoder_forward"] = enc
+    extras = (args.config == 3 and args.mode == "A" and args.dtype == "bf16" and args.size == 256
+              and not args.no_extras)
+    del trainer
+    if extras:
+        # mode B (all unfrozen) is the DP-scaling headline; measured on every rank (it is a
+        # second fusion step, same exchange), reported by rank 0
+        torch.cuda.empty_cache()
+        tb, bb_, dtb = bench_fusion(PR.default_parameters(), device, dtype, "B", args.batch, args.size,
+                                    max(10, args.steps // 2), 3, world, rank, use_graph=not args.no_graph)
+        nb = max(10, args.steps // 2)
+        msb = dtb * 1e3 / nb
+        tfb = GFLOP_PER_VOL["B"] * args.batch / (msb * 1e-3) / 1e3
+        out["mode_b"] = {"value": round(args.batch * world * nb / dtb, 2), "unit": "volumes/s",
+                         "ms_per_step": round(msb, 3), "steps": nb, "warmup": 3,
+                         "loss": float(tb.loss.item()) if tb.loss is not None else None,
+                         "workload": "fusion training step, config 3, mode B (all trainable)",
+                         "step_roofline": {"bound": "mfma", "achieved": round(tfb, 1),
+                                           "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                           "frac": round(tfb / BF16_MFMA_PEAK_TFLOPS, 4),
+                                           "algorithmic_gflop_per_volume": GFLOP_PER_VOL["B"]}}
+        del tb, bb_
+        torch.cuda.empty_cache()
+        if world == 1:
+            out["config2"] = bench_config2(device, 16, 20, 5, probe=False)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args, lambda: _cpu_params(PR, args))
