@@ -46,7 +46,14 @@ def allreduce_mean_(bucket, world, group=None):
     """Sum a flat bucket over ranks, in place; the 1/world factor is applied
     by the consumer (AdamW grad_scale) so the bucket is touched once."""
     if world > 1:
-        dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
+        if bucket.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo (CPU rehearsal of the multi-rank path, e.g. two ranks sharing
+            # one GPU): stage through the host
+            host = bucket.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            bucket.copy_(host)
+        else:
+            dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=group)
     return bucket
 
 
@@ -61,7 +68,17 @@ def allgather_rows(t, world):
 
 class FusionTrainer:
     """Owns the LightningFusionModel-equivalent, its FusedAdamW and the
-    captured step. ``step(batch)`` runs one training step."""
+    captured step. ``step(batch)`` runs one training step.
+
+    The captured graphs hold device pointers of the optimizer tables, the
+    hyper-parameter table and the gradient bucket. ``step`` therefore
+    (i) writes the current learning rates / weight decays into the existing
+    hyper table before every replay (a scheduler's changes reach the device),
+    and (ii) drops the graphs and the bucket whenever the trainable set, the
+    param-group layout or the optimizer's tables change (gradual unfreeze,
+    selector_helpers.py:541-613; load_state_dict), re-capturing on that step's
+    batch -- capture restores the training state its warm-up steps touched, so
+    it never advances training."""
 
     def __init__(self, lm, world=1, use_graph=True):
         self.lm = lm
@@ -73,7 +90,18 @@ class FusionTrainer:
         self.graphs = None
         self.static_batch = None
         self._bucket_ready = False
+        self._bucket_sig = None
+        self._graph_sig = None
         self.loss = None
+        self.captures = 0
+
+    # ------------------------------------------------------------ signature
+    def _trainable(self):
+        return [p for g in self.opt.param_groups for p in g["params"] if p.requires_grad]
+
+    def _signature(self):
+        groups = tuple(len(g["params"]) for g in self.opt.param_groups)
+        return groups, tuple(id(p) for p in self._trainable()), self.opt.tables_version
 
     # ---------------------------------------------------------- eager step
     def _fwd_bwd(self, batch):
@@ -89,26 +117,76 @@ class FusionTrainer:
         self.opt.step()
 
     def _setup_bucket(self):
-        params = [p for g in self.opt.param_groups for p in g["params"] if p.grad is not None]
-        if self.world > 1 and params:
-            self.opt.make_bucket(params)
-            self.opt.use_bucket_grads(True, 1.0 / self.world)
+        params = [p for p in self._trainable() if p.grad is not None]
+        if self.world > 1:
+            self.opt.use_bucket_grads(False)
+            if params:
+                self.opt.make_bucket(params)
+                self.opt.use_bucket_grads(True, 1.0 / self.world)
         self._bucket_ready = True
+        self._bucket_sig = self._signature()[:2]
 
     def eager_step(self, batch):
         loss = self._fwd_bwd(batch)
-        if not self._bucket_ready:
+        if not self._bucket_ready or self._bucket_sig != self._signature()[:2]:
             self._setup_bucket()
         self._exchange_and_update()
         self.lm.global_step += 1
         self.loss = loss.detach()
         return loss
 
+    # ------------------------------------------------------------- state
+    def _snapshot(self):
+        """Device copies of everything a training step mutates: trainable
+        parameters, every buffer (BN running stats, num_batches_tracked), the
+        optimizer moments and step counters, the dropout Philox states."""
+        import dmf_ops as O
+
+        o = self.opt
+        return {"params": [(p, p.detach().clone()) for p in self._trainable()],
+                "buffers": [(b, b.clone()) for _, b in self.lm.named_buffers()],
+                "opt": {id(t): (t, t.clone()) for st in o.state.values() for t in st.values()
+                        if torch.is_tensor(t) and t.is_cuda},
+                "steps": o._steps.clone() if o._steps is not None else None,
+                "rng": [(t, t.clone()) for t in O.RNG.states.values()],
+                "global_step": self.lm.global_step}
+
+    def _restore(self, snap):
+        """Undo what the steps since ``snap`` changed, in place (the captured
+        graphs keep pointing at the same storage). Moments created after the
+        snapshot go back to zero, step counters to their snapshot values."""
+        o = self.opt
+        with torch.no_grad():
+            for key in ("params", "buffers", "rng"):
+                for t, v in snap[key]:
+                    t.copy_(v)
+            saved = snap["opt"]
+            for st in o.state.values():
+                for t in st.values():
+                    if torch.is_tensor(t) and t.is_cuda:
+                        if id(t) in saved:
+                            t.copy_(saved[id(t)][1])
+                        else:
+                            t.zero_()
+            if o._steps is not None:
+                want = torch.zeros_like(o._steps)
+                if snap["steps"] is not None:
+                    want[: snap["steps"].numel()] = snap["steps"]
+                o._steps.copy_(want)
+                if o._table_key is not None and o._live_steps is not None:
+                    o._live_steps.copy_(want[o._slot])
+        self.lm.global_step = snap["global_step"]
+
     # ----------------------------------------------------------- graphs
     def capture(self, batch):
         """Capture fwd+bwd(+pack) and the update as hipGraphs; the RCCL
-        all-reduce between them stays eager (one collective per step)."""
+        all-reduce between them stays eager (one collective per step). The
+        two eager warm-up steps (allocator pools, weight caches, optimizer
+        tables) are undone afterwards, so capture leaves the parameters,
+        buffers, optimizer state, RNG and global_step as it found them."""
         self.static_batch = tuple(t.clone() for t in batch)
+        torch.cuda.synchronize()
+        snap = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -125,13 +203,28 @@ class FusionTrainer:
         with torch.cuda.graph(g2):
             self.opt.step()
         self.graphs = (g1, g2)
+        self._restore(snap)
+        torch.cuda.synchronize()
+        self._graph_sig = self._signature()
+        self.captures += 1
 
     def step(self, batch=None):
+        if self.graphs is not None and self._graph_sig != self._signature():
+            # unfreeze / new param group / reloaded optimizer: the captured
+            # pointers are stale -- rebuild the bucket and capture again
+            self.graphs = None
+            self._bucket_ready = False
+            if self.use_graph:
+                self.capture(batch if batch is not None else self.static_batch)
         if self.graphs is None:
-            return self.eager_step(batch)
+            if self.use_graph and self.captures == 0 and batch is not None:
+                self.capture(batch)
+            else:
+                return self.eager_step(batch)
         if batch is not None and batch[0].data_ptr() != self.static_batch[0].data_ptr():
             for dst, src in zip(self.static_batch, batch):
                 dst.copy_(src, non_blocking=True)
+        self.opt.sync_hyper()  # scheduler lr / wd changes -> the captured hyper table (same storage)
         g1, g2 = self.graphs
         g1.replay()
         if self.world > 1:

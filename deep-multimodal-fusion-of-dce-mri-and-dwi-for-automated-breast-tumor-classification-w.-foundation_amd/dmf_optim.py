@@ -22,7 +22,10 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False):
         if amsgrad:
             raise NotImplementedError("amsgrad is not used on the reference path")
-        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False)
+        # torch.optim.AdamW's group keys too, so a saved state_dict loads into either optimizer
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled_weight_decay=True)
         super().__init__(params, defaults)
         self._table_key = None
         self._hyper = None
@@ -31,6 +34,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self._index = {}
         self.grad_source = None  # optional flat bucket (see pack_grads)
         self.grad_scale = 1.0
+        self.tables_version = 0  # bumped whenever the device tables are rebuilt (captured graphs go stale)
 
     # -------------------------------------------------------------- tables
     def _live(self):
@@ -60,19 +64,34 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _build(self, live):
         dev = live[0][1].device
-        # every param ever stepped keeps its slot (and step count) in _index
+        # every param ever stepped keeps its slot (and step count) in _index;
+        # moments loaded by load_state_dict are kept, and their 'step' seeds the slot
+        seed = []
         for gi, p in live:
             if id(p) not in self._index:
                 st = self.state[p]
-                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                self._index[id(p)] = len(self._index)
+                if "exp_avg" in st and "exp_avg_sq" in st:
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        st[k] = st[k].to(device=p.device, dtype=torch.float32).contiguous()
+                else:
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                slot = len(self._index)
+                self._index[id(p)] = slot
+                step0 = st.get("step", 0)
+                step0 = int(step0.item()) if torch.is_tensor(step0) else int(step0)
+                if step0:
+                    seed.append((slot, step0))
         nslots = len(self._index)
         if self._steps is None or self._steps.numel() < nslots:
             old = self._steps
             self._steps = torch.zeros(max(nslots, 1), dtype=torch.int32, device=dev)
             if old is not None:
                 self._steps[: old.numel()].copy_(old)
+        if seed:
+            idx = torch.tensor([a for a, _ in seed], dtype=torch.int64)
+            val = torch.tensor([b for _, b in seed], dtype=torch.int32)
+            self._steps[idx.to(dev)] = val.to(dev)
         rows, chunks = [], []
         slot_ids = []
         for t, (gi, p) in enumerate(live):
@@ -90,6 +109,7 @@ class FusedAdamW(torch.optim.Optimizer):
         # per-live-tensor step counters: gather/scatter via a slot map kept on device
         self._slot = torch.tensor(slot_ids, dtype=torch.int64, device=dev)
         self._live_steps = self._steps[self._slot].clone()
+        self.tables_version += 1
 
     def _grad_ptr(self, p):
         if self.grad_source is not None:
@@ -149,12 +169,46 @@ class FusedAdamW(torch.optim.Optimizer):
         N.call("dmf_multi_copy", self._zero_chunks.shape[0], self._zero_chunks.data_ptr(), self._zero_pairs.data_ptr(),
                0.0, N.stream_ptr())
 
+    def _flush_steps(self):
+        """Device step counters -> self._steps (slot order)."""
+        if self._table_key is not None:
+            self._steps[self._slot] = self._live_steps
+
     def step_counts(self):
         """Per-parameter step counts (host copy; for tests)."""
-        if self._table_key is None:
+        if self._table_key is None and self._steps is None:
             return {}
-        self._steps[self._slot] = self._live_steps
+        self._flush_steps()
         return {i: int(v) for i, v in enumerate(self._steps.tolist())}
+
+    # ---------------------------------------------------------- checkpoints
+    def state_dict(self):
+        """torch.optim.AdamW layout: per-parameter {'step' (float32 scalar
+        tensor), 'exp_avg', 'exp_avg_sq'} -- the device step counters are
+        written back into state[p]['step'] first, so the file loads into
+        torch.optim.AdamW (what the reference's Lightning checkpoints hold)
+        as well as into a FusedAdamW."""
+        if self._steps is not None:
+            self._flush_steps()
+            host = self._steps.tolist()
+            for g in self.param_groups:
+                for p in g["params"]:
+                    slot = self._index.get(id(p))
+                    if slot is not None and p in self.state:
+                        self.state[p]["step"] = torch.tensor(float(host[slot]), dtype=torch.float32)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """Replaces self.state (torch semantics) and drops every device table
+        built over the old moment buffers: the next step rebuilds them over the
+        loaded exp_avg / exp_avg_sq and seeds the step counters from 'step'."""
+        super().load_state_dict(state_dict)
+        self._table_key = None
+        self._index = {}
+        self._steps = None
+        self._tensors = self._chunks = self._slot = self._live_steps = None
+        self._hyper_host = None
+        self.tables_version += 1
 
     # ----------------------------------------------------- flat grad bucket
     def make_bucket(self, params):

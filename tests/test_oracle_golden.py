@@ -151,3 +151,16 @@ def test_oracle_reproduces_step_golden():
     np.testing.assert_allclose(got["terms"], G["terms"], rtol=1e-5)
     np.testing.assert_allclose(got["logits"], G["logits"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(got["fusion_grad_norms"], G["fusion_grad_norms"], rtol=1e-3, atol=1e-7)
+
+
+def test_oracle_reproduces_full_width_resnet_maps():
+    """SURVEY 8(c) fixture (5) pins the oracle's ResNet-50 OS8 (B=1, S=64)."""
+    import make_golden as MG
+
+    G = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "resnet50_os8_maps.npz")))
+    _, ref = MG.seeded_backbone(6, 51)
+    ref.eval()
+    with torch.no_grad():
+        feats = ref(MG.backbone_input(1, 6, 64, 52))
+    for i, f in enumerate(feats):
+        np.testing.assert_allclose(f.numpy(), G[f"C{i + 2}"], rtol=1e-4, atol=1e-5)

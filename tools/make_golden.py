@@ -9,7 +9,7 @@ they do NOT pin the reference ("parity unpinned").
 Weights are not stored: each fixture records the seed recipe the tests
 re-run (product-side seeded construction, state_dict loaded into the oracle).
 
-    python tools/make_golden.py
+    python tools/make_golden.py [small] [full]
 """
 import copy
 import os
@@ -126,12 +126,135 @@ def step_fixture():
                 fusion_grad_norms=gn)
 
 
+# ---------------------------------------------------------------------------
+# SURVEY 8(c) fixtures (2), (4), (5) at the reference's real widths
+# (channels 128/256/512, S=256, ResNet-50 OS8 at full width). Inputs are not
+# stored: they are re-made from the seeded recipes below (volume_batch,
+# backbone_input) with torch's CPU generator.
+def feature_stats(f):
+    """Per-channel mean and mean square (fp64 reductions) of an NCHW map."""
+    f = f.double()
+    return np.concatenate([f.mean((0, 2, 3)).numpy(), f.pow(2).mean((0, 2, 3)).numpy()]).astype(np.float64)
+
+
+def full_encoders(seed_dwi=31, seed_dce=32, seed_fm=33):
+    P = copy.deepcopy(PR.default_parameters())
+    P["dwi_model_parameters"]["dropout"] = 0.0  # train-mode fixtures with p=0 (SURVEY 8(c) (2))
+    _, dwi_r = seeded_encoder(P, "dwi", 14, seed_dwi)
+    _, dce_r = seeded_encoder(P, "dce", 6, seed_dce)
+    _, fr = seeded_fusion(P, seed_fm)
+    return P, dwi_r, dce_r, fr
+
+
+def config3_forward_fixture():
+    """(2) encoder + fusion forward at config-3 shapes, B=2, eval and train (p=0)."""
+    P, dwi_r, dce_r, fr = full_encoders()
+    dwi, dce, _, _ = volume_batch(2, 256, 9)
+    out = {"recipe": np.array("default_parameters(), dropout 0; dwi seed 31, dce seed 32, fusion seed 33 "
+                              "(seeded_encoder / seeded_fusion); batch volume_batch(2,256,9)")}
+    for mode in ("eval", "train"):
+        for m in (dwi_r, dce_r, fr):
+            m.train(mode == "train")
+        with torch.no_grad():
+            lo_d, aux_d, mp_d = dwi_r(dwi)
+            lo_c, aux_c, mp_c = dce_r(dce)
+            logits, fmask, aux = fr(aux_d["raw_feats"], aux_c["raw_feats"], mp_d, mp_c)
+        out.update({
+            f"{mode}_dwi_logits": lo_d.numpy(), f"{mode}_dce_logits": lo_c.numpy(),
+            f"{mode}_dwi_mask": mp_d.numpy(), f"{mode}_dce_mask": mp_c.numpy(),
+            f"{mode}_fusion_logits": logits.numpy(), f"{mode}_fused_mask": fmask.numpy(),
+            f"{mode}_gating": aux["gating_weights"].numpy(), f"{mode}_attn": aux["attn_weights"].numpy(),
+        })
+        for tag, a in (("dwi", aux_d), ("dce", aux_c)):
+            for i, f in enumerate(a["raw_feats"]):
+                out[f"{mode}_{tag}_f{i + 1}_stats"] = feature_stats(f)
+        if mode == "train":
+            rs = [b.double().sum().item() for m in (dwi_r, dce_r, fr) for n, b in m.named_buffers()
+                  if n.endswith("running_mean") or n.endswith("running_var")]
+            out["train_running_stat_sums"] = np.array(rs)
+    return out
+
+
+def config3_adamw_fixture():
+    """(4) one mode-A fusion step at config-3 shapes (B=4 so the mimic term is
+    on) and the AdamW delta of that step (selector_helpers.py:632-685 frozen
+    start: one group, lr 1e-4, wd reg_base 1e-4, eps 1e-8)."""
+    P, dwi_r, dce_r, fr = full_encoders(41, 42, 43)
+    for m in (dwi_r, dce_r, fr):
+        m.train()
+    for p in list(dwi_r.parameters()) + list(dce_r.parameters()):
+        p.requires_grad = False
+    bt = volume_batch(4, 256, 12)
+    train_labels = torch.arange(1024) % 4
+    out = OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, OL.class_weights_from_labels(train_labels), epoch=0)
+    out["total"].backward()
+    op = P["fusion_model_parameters"]["optimizer_parameters"]
+    before = [p.detach().clone() for p in fr.parameters()]
+    opt = torch.optim.AdamW([p for p in fr.parameters()], lr=op["lr"], betas=op["betas"], eps=op["eps"],
+                            weight_decay=op["reg_base"])
+    opt.step()
+    gn = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0 for p in fr.parameters()])
+    dn = np.array([(p.detach() - b).double().norm().item() for p, b in zip(fr.parameters(), before)])
+    return dict(recipe=np.array("default_parameters(), dropout 0; dwi seed 41, dce seed 42, fusion seed 43; train; "
+                                "mode A; batch volume_batch(4,256,12); train_labels arange(1024)%4; AdamW lr 1e-4 "
+                                "wd 1e-4 eps 1e-8"),
+                logits=out["logits"].detach().numpy(),
+                terms=np.array([out[k].item() for k in ("cls", "mask", "recon", "mimic", "total")]),
+                fusion_grad_norms=gn, fusion_delta_norms=dn)
+
+
+def backbone_input(B, C, S, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, C, S, S, generator=g)
+
+
+def seeded_backbone(cin, seed):
+    """Product-side ResNet-50 OS8 with the encoder's BN re-initialisation
+    (initialize_model, model_module.py:1002-1023, quirk Q3) -- timm's
+    zero-initialised last BN of each block would leave every residual
+    branch silent."""
+    P = copy.deepcopy(PR.default_parameters())
+    torch.manual_seed(seed)
+    bb = FM.build_medical_backbone(P, "cpu", "dce", cin)
+    bb.apply(MM.init_parameter)
+    ref = OM.ResNet50OS8(cin)
+    ref.load_state_dict(bb.state_dict())
+    return bb, ref
+
+
+def resnet_maps_fixture():
+    """(5) ResNet-50 OS8 feature maps at B=1, S=64 (full maps), eval, plus the
+    config-2 shape (5 phases, S=256, B=2) as per-channel statistics."""
+    _, ref = seeded_backbone(6, 51)
+    ref.eval()
+    x = backbone_input(1, 6, 64, 52)
+    with torch.no_grad():
+        feats = ref(x)
+    out = {"recipe": np.array("seeded_backbone(6, 51) eval; backbone_input(1,6,64,52); config2: seeded_backbone(5, "
+                              "53) eval, backbone_input(2,5,256,54)")}
+    for i, f in enumerate(feats):
+        out[f"C{i + 2}"] = f.numpy().astype(np.float32)
+    _, ref5 = seeded_backbone(5, 53)
+    ref5.eval()
+    with torch.no_grad():
+        feats5 = ref5(backbone_input(2, 5, 256, 54))
+    for i, f in enumerate(feats5):
+        out[f"config2_C{i + 2}_stats"] = feature_stats(f)
+    return out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    np.savez_compressed(os.path.join(OUT, "losses.npz"), **losses_fixture())
-    np.savez_compressed(os.path.join(OUT, "encoder_small.npz"), **encoder_fixture())
-    np.savez_compressed(os.path.join(OUT, "fusion_step_small.npz"), **step_fixture())
+    which = set(sys.argv[1:]) or {"small", "full"}
+    if "small" in which:
+        np.savez_compressed(os.path.join(OUT, "losses.npz"), **losses_fixture())
+        np.savez_compressed(os.path.join(OUT, "encoder_small.npz"), **encoder_fixture())
+        np.savez_compressed(os.path.join(OUT, "fusion_step_small.npz"), **step_fixture())
+    if "full" in which:
+        np.savez_compressed(os.path.join(OUT, "config3_forward.npz"), **config3_forward_fixture())
+        np.savez_compressed(os.path.join(OUT, "config3_adamw_step.npz"), **config3_adamw_fixture())
+        np.savez_compressed(os.path.join(OUT, "resnet50_os8_maps.npz"), **resnet_maps_fixture())
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
