@@ -59,6 +59,10 @@ struct ConvArgs {
   // finalizes them into `fin`, then re-zeroes its ticket.
   unsigned* tickets;
   BnFin fin;
+  // stat_acc: the BN statistics are ADDED into (double*)partials [Nout][2]
+  // (float64 atomics, zeroed by the caller) instead of one slab row per M
+  // tile; the consumer (dmf_bn_apply) finalizes them
+  int stat_acc;
 };
 
 template <int ACT>
@@ -168,6 +172,25 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16
 
 constexpr int BUF_FLAGS_EP = 0x00020000;  // buffer descriptor word 3 (as BUF_FLAGS below)
 
+// BN statistics of one column of one M tile into the accumulator (stat_acc):
+// stat_acc = 1: float64 atomics into [Nout][2]; stat_acc = R > 1: into
+// replica (mt % R) of [R][Nout][2] (spreads the same-address contention of
+// the M tiles over R addresses; the consumer sums the replicas);
+// stat_acc < 0: benchmarking variants (-1 f32 atomics, -2 plain slab store)
+__device__ __forceinline__ void acc_stats(const ConvArgs& a, int mt, int col, float2 v) {
+  if (a.stat_acc >= 1) {
+    const int rep = a.stat_acc > 1 ? mt % a.stat_acc : 0;
+    double* d = (double*)a.partials + ((size_t)rep * a.Nout + col) * 2;
+    unsafeAtomicAdd(d, (double)v.x);
+    unsafeAtomicAdd(d + 1, (double)v.y);
+  } else if (a.stat_acc == -1) {
+    unsafeAtomicAdd(a.partials + (size_t)col * 2, v.x);
+    unsafeAtomicAdd(a.partials + (size_t)col * 2 + 1, v.y);
+  } else {
+    *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+  }
+}
+
 // bias / activation or BN partial statistics, LDS-staged 16-B stores
 template <typename T, int BM = CBM, int BN = CBN, int WMW = 2, int WNW = 2>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[BM / (16 * WMW)][BN / (16 * WNW)],
@@ -219,7 +242,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
           v.y += red[(q * BN + tid) * 2 + 1];
         }
         float2* dst = (float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2);
-        if (a.tickets) {
+        if (a.stat_acc) {
+          acc_stats(a, mt, col, v);
+        } else if (a.tickets) {
           // write-through (sc1) slab store: visible to the reducer on any XCD without a release fence
           __hip_atomic_store((unsigned long long*)dst, *(unsigned long long*)&v, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -837,7 +862,11 @@ __device__ __forceinline__ void conv_epilogue_stage(const ConvArgs& a, f32x4_t (
         float2 v;
         v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
         v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
-        *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+        if (a.stat_acc) {
+          acc_stats(a, mt, col, v);
+        } else {
+          *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+        }
       }
     }
   }
@@ -1182,6 +1211,8 @@ static int g_sq_enable = 1, g_sq_var = 1;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
 // 3 buf 128x64, 4 buf 64x64, 5 wide 256x128, 6 square 256x256 (only where legal)
 static int g_force = 0;
+// 3 = dmf_conv2d_fwd_acc accumulation mode (benchmarking; see acc_stats): 0 default
+static int g_stat_mode = 0;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1426,6 +1457,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 0: g_sq_enable = value != 0; return 0;
     case 1: DMF_CHECK_ARG(value >= 0 && value < 4, "dmf_conv_tune: square-tile variant %d", value); g_sq_var = value; return 0;
     case 2: DMF_CHECK_ARG(value >= 0 && value <= 6, "dmf_conv_tune: forced tile %d", value); g_force = value; return 0;
+    case 3: DMF_CHECK_ARG(value >= -2 && value <= 64, "dmf_conv_tune: stat mode %d", value); g_stat_mode = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1491,6 +1523,21 @@ extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int
   if (rc) return rc;
   a.partials = bn_partials;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd");
+}
+
+extern "C" int dmf_conv2d_fwd_acc(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                                  int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad,
+                                  int dil, const float* bias, void* y, int Ho, int Wo, int ldy, double* bn_acc,
+                                  int replicas, const float* in_scale_shift, int in_act, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, x2, Cin2, ldx2, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                           Ho, Wo, ldy, DMF_ACT_NONE, in_scale_shift, in_act, "dmf_conv2d_fwd_acc");
+  if (rc) return rc;
+  DMF_CHECK_ARG(bn_acc != nullptr && ((uintptr_t)bn_acc % 8) == 0, "dmf_conv2d_fwd_acc: bn_acc must be 8-byte aligned");
+  DMF_CHECK_ARG(replicas >= 1 && replicas <= 64, "dmf_conv2d_fwd_acc: replicas %d out of [1, 64]", replicas);
+  a.partials = (float*)bn_acc;
+  a.stat_acc = g_stat_mode != 0 ? g_stat_mode : replicas;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_acc");
 }
 
 extern "C" int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,

@@ -202,6 +202,123 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
   }
 }
 
+// ------------------------------------------- BN apply with the finalize folded in
+// One affine source: batch statistics accumulated by the producing conv
+// (dmf_conv2d_fwd_acc, [C][2] sums) finalized here, or a precomputed
+// scale/shift, or none.
+struct BnApplySrc {
+  const double* acc;  // [replicas][C][2]
+  const float* ss;
+  BnFin fin;
+  int replicas;
+};
+
+// (scale, shift) of channel c; `write`: this block also publishes
+// scale_shift / save_mean_invstd and updates the running statistics
+// (exactly what dmf_bn_finalize does for a slab)
+__device__ __forceinline__ void bn_src_affine(const BnApplySrc& s, int c, int C, bool write, float& sc, float& sh) {
+  if (s.acc) {
+    double sum = 0.0, sq = 0.0;
+    for (int r = 0; r < s.replicas; ++r) {  // fixed order
+      sum += s.acc[((size_t)r * C + c) * 2];
+      sq += s.acc[((size_t)r * C + c) * 2 + 1];
+    }
+    if (write) {
+      bn_fin_channel(s.fin, c, C, sum, sq);
+    }
+    const double m = sum / s.fin.count;
+    double v = sq / s.fin.count - m * m;
+    if (v < 0.0) v = 0.0;
+    const float inv = rsqrtf((float)v + s.fin.eps);
+    const float g = s.fin.gamma ? s.fin.gamma[c] : 1.f, b = s.fin.beta ? s.fin.beta[c] : 0.f;
+    sc = g * inv;
+    sh = b - (float)m * g * inv;
+  } else if (s.ss) {
+    sc = s.ss[c];
+    sh = s.ss[C + c];
+  } else {
+    sc = 1.f;
+    sh = 0.f;
+  }
+}
+
+// y = drop(act(x*sa + ba [+ res*sr + br | + res])). Block = 64 channels
+// (blockIdx.y) x rows_per_blk pixels (blockIdx.x); 256 threads = 8 16-B
+// channel chunks x 32 rows; the block's 64 (scale, shift) pairs are
+// finalized once into LDS. Dropout elements are indexed m*C + c exactly as
+// k_affine_act8 / k_act_bwd, so backward regenerates the same masks.
+template <typename T, int ACT, int RES>
+__global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int ldx, BnApplySrc A,
+                                                   const T* __restrict__ res, int ldr, BnApplySrc R, float p,
+                                                   const unsigned long long* rng, int site, T* __restrict__ y, int ldy,
+                                                   int M, int C, int rows_per_blk) {
+  __shared__ float sa[2][64], sr[2][64];
+  const int tid = threadIdx.x;
+  const int cg = blockIdx.y * 64;
+  const bool first = blockIdx.x == 0;
+  if (tid < 64) {
+    const int c = cg + tid;
+    float sc = 1.f, sh = 0.f;
+    if (c < C) bn_src_affine(A, c, C, first, sc, sh);
+    sa[0][tid] = sc;
+    sa[1][tid] = sh;
+  } else if (RES == 2 && tid < 128) {
+    const int c = cg + tid - 64;
+    float sc = 1.f, sh = 0.f;
+    if (c < C) bn_src_affine(R, c, C, first, sc, sh);
+    sr[0][tid - 64] = sc;
+    sr[1][tid - 64] = sh;
+  }
+  if (first && blockIdx.y == 0 && tid == 0) {
+    if (A.acc && A.fin.nbt) *A.fin.nbt += 1;
+    if (RES == 2 && R.acc && R.fin.nbt) *R.fin.nbt += 1;
+  }
+  __syncthreads();
+  const int cl = (tid & 7) * 8, c0 = cg + cl;
+  if (c0 >= C) return;
+  float s8[8], h8[8], rs8[8], rh8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s8[k] = sa[0][cl + k];
+    h8[k] = sa[1][cl + k];
+    if (RES == 2) {
+      rs8[k] = sr[0][cl + k];
+      rh8[k] = sr[1][cl + k];
+    }
+  }
+  const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const int mbeg = blockIdx.x * rows_per_blk;
+  const int mend = min(M, mbeg + rows_per_blk);
+  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
+    float v[8];
+    ld8(x + (size_t)m * ldx + c0, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * s8[k] + h8[k];
+    if (RES != 0) {
+      float r[8];
+      ld8(res + (size_t)m * ldr + c0, r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += RES == 2 ? r[k] * rs8[k] + rh8[k] : r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
+      else if (ACT == DMF_ACT_GELU) v[k] = gelu_f(v[k]);
+      else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+    }
+    if (p > 0.f) {
+      bool keep[4];
+      dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * dsc : 0.f;
+      dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * dsc : 0.f;
+    }
+    st8(y + (size_t)m * ldy + c0, v);
+  }
+}
+
 // dz = dy * drop' * act'(z), z recomputed exactly as in k_affine_act
 template <typename T>
 __global__ void k_act_bwd(const T* __restrict__ dy, int lddy, const T* __restrict__ x, int ldx,
@@ -550,6 +667,73 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
                        scale_shift, (const float*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (float*)y,
                        ldy, M, C);
   DMF_LAUNCH_CHECK("dmf_affine_act");
+  return 0;
+}
+
+static BnApplySrc bn_src(const dmf_bn_desc* d, const float* ss) {
+  BnApplySrc s{};
+  if (d) {
+    s.acc = d->acc;
+    s.fin = BnFin{d->gamma, d->beta, d->running_mean, d->running_var, d->num_batches_tracked, d->momentum, d->eps,
+                  d->count, d->unbias_count, 1, d->scale_shift, d->save_mean_invstd};
+    s.replicas = d->replicas;
+  } else {
+    s.ss = ss;
+  }
+  return s;
+}
+
+extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc* bn, const float* scale_shift,
+                            const void* res, int ldr, const dmf_bn_desc* res_bn, const float* res_scale_shift, int act,
+                            float dropout_p, const unsigned long long* rng, int site, void* y, int ldy, long long M,
+                            int C, void* stream) {
+  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_bn_apply: bad dtype %d", dtype);
+  DMF_CHECK_ARG(C > 0 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!res || ldr % 8 == 0),
+                "dmf_bn_apply: C=%d and strides must be multiples of 8", C);
+  DMF_CHECK_ARG(M < (1LL << 31), "dmf_bn_apply: M=%lld too large", M);
+  DMF_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0),
+                "dmf_bn_apply: pointers must be 16-byte aligned");
+  DMF_CHECK_ARG(!bn || (bn->acc && bn->scale_shift && bn->count > 0 && bn->replicas >= 1 && bn->replicas <= 64),
+                "dmf_bn_apply: bad batch-norm descriptor");
+  DMF_CHECK_ARG(!res_bn || (res && res_bn->acc && res_bn->scale_shift && res_bn->count > 0 && res_bn->replicas >= 1 &&
+                            res_bn->replicas <= 64),
+                "dmf_bn_apply: bad residual batch-norm descriptor");
+  DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_bn_apply: dropout needs rng state");
+  DMF_CHECK_ARG(dropout_p < 1.f, "dmf_bn_apply: dropout p must be < 1");
+  if (M == 0) return 0;
+  const BnApplySrc A = bn_src(bn, scale_shift);
+  const BnApplySrc R = bn_src(res_bn, res_scale_shift);
+  const int gy = cdiv(C, 64);
+  // ~8 row iterations per thread, but at least ~1024 blocks in flight
+  int rows = 256;
+  while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
+  const dim3 g((unsigned)cdiv(M, rows), (unsigned)gy);
+  const int resk = res == nullptr ? 0 : ((res_bn || res_scale_shift) ? 2 : 1);
+  hipStream_t s = (hipStream_t)stream;
+#define DMF_BA(TT, AC, RK)                                                                                     \
+  hipLaunchKernelGGL((k_bn_apply<TT, AC, RK>), g, dim3(256), 0, s, (const TT*)x, ldx, A, (const TT*)res, ldr, R, \
+                     dropout_p, rng, site, (TT*)y, ldy, (int)M, C, rows)
+#define DMF_BA_R(TT, AC)                 \
+  do {                                   \
+    if (resk == 0) DMF_BA(TT, AC, 0);     \
+    else if (resk == 1) DMF_BA(TT, AC, 1); \
+    else DMF_BA(TT, AC, 2);               \
+  } while (0)
+#define DMF_BA_A(TT)                                      \
+  do {                                                    \
+    switch (act) {                                        \
+      case DMF_ACT_RELU: DMF_BA_R(TT, DMF_ACT_RELU); break; \
+      case DMF_ACT_GELU: DMF_BA_R(TT, DMF_ACT_GELU); break; \
+      case DMF_ACT_SIGMOID: DMF_BA_R(TT, DMF_ACT_SIGMOID); break; \
+      default: DMF_BA_R(TT, DMF_ACT_NONE);                \
+    }                                                     \
+  } while (0)
+  if (dtype == DMF_BF16) DMF_BA_A(bf16_t);
+  else DMF_BA_A(float);
+#undef DMF_BA_A
+#undef DMF_BA_R
+#undef DMF_BA
+  DMF_LAUNCH_CHECK("dmf_bn_apply");
   return 0;
 }
 

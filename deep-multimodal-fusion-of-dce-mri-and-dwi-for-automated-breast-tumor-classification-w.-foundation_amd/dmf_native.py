@@ -116,6 +116,17 @@ def call(name, *args):
     return rc
 
 
+class BnDesc(ctypes.Structure):
+    """dmf_bn_desc of include/dmf_hip.h (a training-mode BatchNorm2d whose
+    statistics a dmf_conv2d_fwd_acc launch accumulated)."""
+
+    _fields_ = [("acc", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("num_batches_tracked", ctypes.c_void_p), ("scale_shift", ctypes.c_void_p),
+                ("save_mean_invstd", ctypes.c_void_p), ("count", ctypes.c_double), ("unbias_count", ctypes.c_double),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("replicas", ctypes.c_int)]
+
+
 def stream_ptr(device=None):
     """hipStream_t of torch's current stream (graph-capture aware)."""
     return torch.cuda.current_stream(device).cuda_stream

@@ -11,6 +11,7 @@ Every op here runs on the device through the C-ABI; there is no CPU path.
 """
 from __future__ import annotations
 
+import ctypes
 import itertools
 import math
 import os
@@ -270,6 +271,123 @@ def fuse_input_affine(x, producer, consumer, *params):
   # measured: at larger slabs every block's drain-before-ticket costs more than a finalize launch
 
 
+# ------------------------------------------------- BN statistics arena
+class BnArena:
+    """Zeroed float64 storage that the training-mode BatchNorm statistics of one
+    top-level forward accumulate into (dmf_conv2d_fwd_acc): every BN use takes
+    the next [C][2] slice, the consuming dmf_bn_apply finalizes it. One zero
+    fill per forward, issued at the forward's start on its stream (so side
+    branches forked later see it), replaces a finalize launch per BatchNorm.
+    Slices are handed out in forward order, so a captured hipGraph reuses the
+    same addresses."""
+
+    def __init__(self, device, floats):
+        self.device = device
+        self.chunks = [torch.zeros(max(floats, 1024), dtype=torch.float64, device=device)]
+        self.ci = 0
+        self.off = 0
+
+    def begin(self, zero):
+        self.ci = 0
+        self.off = 0
+        if zero:
+            for c in self.chunks:
+                c.zero_()
+
+    def take(self, n):
+        n = (n + 7) // 8 * 8
+        while True:
+            c = self.chunks[self.ci]
+            if self.off + n <= c.numel():
+                v = c[self.off:self.off + n]
+                self.off += n
+                return v
+            self.ci += 1
+            self.off = 0
+            if self.ci == len(self.chunks):
+                # more BN uses than the module tree suggested (a BN used twice): a fresh zeroed chunk on this
+                # stream; zeroed with the others from the next forward on
+                self.chunks.append(torch.zeros(max(n, 1 << 14), dtype=torch.float64, device=self.device))
+
+
+ARENA = [None]
+
+
+class bn_scope:
+    """Top-level forward scope: the BN statistics of everything below
+    accumulate into ``owner``'s arena (nested scopes reuse the outer one)."""
+
+    def __init__(self, owner, device):
+        self.owner, self.device, self.entered = owner, torch.device(device), False
+
+    def __enter__(self):
+        if ARENA[0] is not None or self.device.type != "cuda":
+            return self
+        key = "_dmf_bn_arena"
+        ar = self.owner.__dict__.get(key)
+        if ar is None or ar.device != self.device:
+            bns = [m for m in self.owner.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
+            ar = BnArena(self.device, sum((2 * m.num_features * BN_ACC_REPLICAS + 7) // 8 * 8 for m in bns))
+            ar.bns = bns
+            self.owner.__dict__[key] = ar
+            ar.begin(zero=False)  # freshly zeroed
+        else:
+            ar.begin(zero=any(m.training for m in ar.bns))
+        ARENA[0] = ar
+        self.entered = True
+        return self
+
+    def __exit__(self, *exc):
+        if self.entered:
+            ARENA[0] = None
+        return False
+
+
+# float64 accumulator replicas per BatchNorm use (dmf_conv2d_fwd_acc): M tile t adds into replica t % 8 --
+# measured (tools/stat_bench.py): one copy serialises 1024 tiles' atomics on one address (22 -> 56 us on a
+# 64-channel 3x3 at 64x64), 8 copies match the slab form
+BN_ACC_REPLICAS = 8
+
+
+def _bn_acc(c, dev):
+    n = 2 * c * BN_ACC_REPLICAS
+    ar = ARENA[0]
+    if ar is not None and ar.device == dev:
+        return ar.take(n)
+    return torch.zeros(n, dtype=torch.float64, device=dev)  # outside any forward scope (unit tests)
+
+
+def _bn_desc(bn, acc, count, unbias_count, ss, save):
+    track = bn.track_running_stats and bn.running_mean is not None
+    d = N.BnDesc()
+    d.acc = acc.data_ptr()
+    d.gamma = _p(bn.weight)
+    d.beta = _p(bn.bias)
+    d.running_mean = _p(bn.running_mean) if track else None
+    d.running_var = _p(bn.running_var) if track else None
+    d.num_batches_tracked = _p(bn.num_batches_tracked) if track else None
+    d.scale_shift = ss.data_ptr()
+    d.save_mean_invstd = save.data_ptr()
+    d.count = float(count)
+    d.unbias_count = float(unbias_count)
+    d.momentum = float(bn.momentum if bn.momentum is not None else 0.1)
+    d.eps = float(bn.eps)
+    d.replicas = BN_ACC_REPLICAS
+    d.keep = (acc, ss, save)
+    return d
+
+
+def _bn_apply_ok(*ts):
+    """dmf_bn_apply's layout contract (8-channel strides, 16-B alignment)."""
+    for t in ts:
+        if t is None:
+            continue
+        _, c, _, _, ld = nhwc(t)
+        if c % 8 or ld % 8 or t.data_ptr() % 16:
+            return False
+    return True
+
+
 def _bn_site(bn, dev):
     """Persistent, self-cleaning per-column-tile tickets of one BatchNorm2d
     for the conv + finalize launch (zero at rest; kept out of the state_dict)."""
@@ -280,11 +398,35 @@ def _bn_site(bn, dev):
     return st
 
 
-def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None, in_act="none"):
-    """conv -> (y_raw, scale_shift, save) of the following BatchNorm2d. In
-    training mode on the MFMA path the statistics and the finalize run inside
-    the conv launch (dmf_conv2d_fwd_bn)."""
+def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None, in_act="none", defer=False):
+    """conv -> (y_raw, scale_shift, save, desc) of the following BatchNorm2d.
+
+    defer=True, training mode, MFMA conv: the conv epilogue accumulates the
+    batch statistics into an arena slice (dmf_conv2d_fwd_acc) and ``desc``
+    (dmf_bn_desc) hands the finalize to the consuming dmf_bn_apply, which
+    fills scale_shift / save; otherwise desc is None and scale_shift / save
+    are final when this returns (in-launch ticket finalize, or a finalize
+    launch)."""
     training = bn.training or bn.running_mean is None
+    if defer and training and in_ss is None and _is_mfma_conv(w, g) and w.shape[0] % 8 == 0:
+        n, cx, h, wd, ldx = nhwc(x)
+        cx2, ldx2 = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
+        co, ci, kh, kw = w.shape
+        ho, wo = g.out_hw(h, wd)
+        dev = x.device
+        y = empty_nhwc(n, co, ho, wo, x.dtype, dev)
+        m = n * ho * wo
+        acc = _bn_acc(co, dev)
+        ss = torch.empty(2 * co, dtype=torch.float32, device=dev)
+        save = torch.empty(2 * co, dtype=torch.float32, device=dev)
+        wk = caches[0].get(w, x.dtype, cx + cx2, 0)
+        _conv_launch("dmf_conv2d_fwd_acc",
+                     (dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, kh, kw, g.stride,
+                      g.pad, g.dil, _p(b), y.data_ptr(), ho, wo, nhwc(y)[4], acc.data_ptr(), BN_ACC_REPLICAS, None,
+                      N.ACT_NONE),
+                     (x, x2, wk, b, y, acc), x, n, h, wd, cx + cx2, co, kh, kw, g, ho, wo)
+        desc = _bn_desc(bn, acc, m, m * unbias_mult if unbias_mult != 1 else 0.0, ss, save)
+        return y, ss, save, desc
     n_, cx_, h_, w_, ldx_ = nhwc(x)
     cx2_, ldx2_ = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
     ho_, wo_ = g.out_hw(h_, w_)
@@ -295,7 +437,7 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
         n, c, ho, wo, _ = nhwc(y)
         m = n * ho * wo
         ss, save = _bn_finalize(part, m, bn, unbias_count=m * unbias_mult if unbias_mult != 1 else 0.0)
-        return y, ss, save
+        return y, ss, save, None
     n, cx, h, wd, ldx = nhwc(x)
     cx2, ldx2 = 0, 0
     if x2 is not None:
@@ -322,7 +464,7 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
                   save.data_ptr()),
                  (x, x2, wk, b, y, in_ss, partials, tickets, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                   bn.num_batches_tracked, ss, save), x, n, h, wd, cx + cx2, co, kh, kw, g, ho, wo)
-    return y, ss, save
+    return y, ss, save, None
 
 
 def _col_stats(y):
@@ -524,21 +666,30 @@ class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, x2, w, b, gamma, beta, res, xr, wr, gamma_r, beta_r, spec):
         (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act) = spec
-        y, ss, save = _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss, in_act=in_act)
+        defer = in_ss is None and (res is None or _bn_apply_ok(res))
+        y, ss, save, desc = _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss, in_act=in_act,
+                                             defer=defer)
         ctx.gate_holder = x.__dict__.get("_dmf_gate")
         n, c, ho, wo, ldy = nhwc(y)
         m = n * ho * wo
-        yr = ss_r = save_r = None
+        yr = ss_r = save_r = desc_r = None
         if xr is not None:
-            yr, ss_r, save_r = _conv_bn_forward(xr, wr, None, gr, caches_r, bn_r)
+            yr, ss_r, save_r, desc_r = _conv_bn_forward(xr, wr, None, gr, caches_r, bn_r, defer=desc is not None)
             res_t, ldr = yr, nhwc(yr)[4]
         elif res is not None:
             res_t, ldr = res, nhwc(res)[4]
         else:
             res_t, ldr = None, 0
         out = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
-        N.call("dmf_affine_act", dt(y), y.data_ptr(), ldy, ss.data_ptr(), _p(res_t), ldr, _p(ss_r), ACT[act],
-               float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
+        if desc is not None or desc_r is not None:
+            # finalize(s) folded into the apply: one launch
+            N.call("dmf_bn_apply", dt(y), y.data_ptr(), ldy, ctypes.byref(desc) if desc is not None else None,
+                   _p(ss) if desc is None else None, _p(res_t), ldr,
+                   ctypes.byref(desc_r) if desc_r is not None else None, _p(ss_r) if desc_r is None else None,
+                   ACT[act], float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
+        else:
+            N.call("dmf_affine_act", dt(y), y.data_ptr(), ldy, ss.data_ptr(), _p(res_t), ldr, _p(ss_r), ACT[act],
+                   float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
         ctx.save_for_backward(x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng)
         ctx.spec = spec
         return out
@@ -645,8 +796,8 @@ def conv_bn_stats(x, conv, caches, bn, in_ss=None, in_act="none", x2=None, unbia
         raise RuntimeError("conv_bn_stats is forward-only (no autograd graph)")
     g = ConvGeom(conv)
     with torch.no_grad():
-        y, ss, _ = _conv_bn_forward(x, conv.weight, conv.bias, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss,
-                                    in_act=in_act)
+        y, ss, _, _ = _conv_bn_forward(x, conv.weight, conv.bias, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss,
+                                       in_act=in_act)
     return y, ss
 
 

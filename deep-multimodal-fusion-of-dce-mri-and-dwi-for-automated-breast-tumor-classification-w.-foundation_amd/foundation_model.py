@@ -155,6 +155,10 @@ class ResNet50OS8(nn.Module):
     def forward(self, x, on_feature=None):
         """on_feature(i, feats): called as soon as out_indices map i is
         produced (lets a consumer start on C2 while layer2..4 still run)."""
+        with O.bn_scope(self, x.device):
+            return self._forward(x, on_feature)
+
+    def _forward(self, x, on_feature):
         if x.shape[1] == self.in_chans or x.dtype != self.compute_dtype:
             x = self.stage_input(x)
         x = O.conv_bn_act(x, self.conv1, _caches(self.conv1), self.bn1, "relu")

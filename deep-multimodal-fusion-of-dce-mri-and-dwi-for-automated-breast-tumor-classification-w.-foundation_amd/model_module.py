@@ -499,7 +499,7 @@ class ModelMaskHeadBackbone(nn.Module):
     def forward(self, x, masks=None):
         mask_pred = None
         mask_attn_map = None
-        with _rng_scope(self, x.device):
+        with _rng_scope(self, x.device), O.bn_scope(self, x.device):
             x_in, mod_attn_map = self._stage_input(x)
             if self.use_backbone:
                 f1_b, f2_b, f3_b = self.backbone_adapter(x_in)
@@ -641,7 +641,7 @@ class FusionModel(nn.Module):
         return O.to_tokens(_to_compute(feat, _dt(self)), hp, wp)
 
     def forward(self, raw_feats_dwi, raw_feats_dce, dwi_mask_pred=None, dce_mask_pred=None):
-        with _rng_scope(self, raw_feats_dwi[-1].device):
+        with _rng_scope(self, raw_feats_dwi[-1].device), O.bn_scope(self, raw_feats_dwi[-1].device):
             p_dwi = self._proj(self.proj_in_dwi, raw_feats_dwi[-1])
             p_dce = self._proj(self.proj_in_dce, raw_feats_dce[-1])
             # Q4: reduce + refine are computed (BN running stats move in train

@@ -90,6 +90,18 @@ int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, int Cin, in
                       float* bn_partials, unsigned* bn_tickets, double count, double unbias_count, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, long long* num_batches_tracked,
                       float momentum, float eps, float* scale_shift, float* save_mean_invstd, void* stream);
+/* dmf_conv2d_fwd whose epilogue ADDS each block's per-channel (sum, sum^2)
+ * into bn_acc [replicas][Cout][2] -- replica (M tile % replicas), float64
+ * atomics: arrival order does not show at fp32, and the replicas keep the
+ * same-address contention of many M tiles off the epilogue; bn_acc zeroed by
+ * the caller, one slice per BatchNorm use. No slab and no finalize launch:
+ * the consumer dmf_bn_apply finalizes the statistics (training-mode
+ * BatchNorm2d after every conv of timm Bottleneck, the necks, ResNetLite,
+ * projectors). */
+int dmf_conv2d_fwd_acc(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
+                       int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                       const float* bias, void* y, int Ho, int Wo, int ldy, double* bn_acc, int replicas,
+                       const float* in_scale_shift, int in_act, void* stream);
 int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
@@ -139,6 +151,35 @@ int dmf_bn_finalize(const float* partials, int ntiles, int C, double count, doub
                     const float* gamma, const float* beta, float* running_mean, float* running_var,
                     long long* num_batches_tracked, float momentum, float eps, int training, float* scale_shift,
                     float* save_mean_invstd, double* workspace, void* stream);
+/* a training-mode BatchNorm2d whose batch statistics a dmf_conv2d_fwd_acc
+ * launch accumulated: finalized inside dmf_bn_apply (torch semantics as
+ * dmf_bn_finalize: biased batch variance, running stats with momentum and
+ * the unbiased variance over unbias_count (0 -> count) rows) */
+typedef struct dmf_bn_desc {
+  const double* acc;            /* [replicas][C][2] (sum, sum^2) */
+  const float* gamma;           /* nullable (affine=False) */
+  const float* beta;
+  float* running_mean;          /* nullable (no running statistics) */
+  float* running_var;
+  long long* num_batches_tracked; /* nullable */
+  float* scale_shift;           /* out [2][C] */
+  float* save_mean_invstd;      /* out [2][C], nullable */
+  double count;
+  double unbias_count;
+  float momentum;
+  float eps;
+  int replicas;                 /* of acc (dmf_conv2d_fwd_acc) */
+} dmf_bn_desc;
+/* y = drop(act(x*a + [res*r | res])) with a = finalize(bn) when bn is given
+ * (else scale_shift, else identity) and r likewise from res_bn /
+ * res_scale_shift (residual optional). One launch replaces
+ * dmf_bn_finalize (x2 for a projection shortcut) + dmf_affine_act; the
+ * finalized scale_shift / save_mean_invstd are written for the backward.
+ * C and the strides multiples of 8, 16-byte aligned tensors. */
+int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc* bn, const float* scale_shift,
+                 const void* res, int ldr, const dmf_bn_desc* res_bn, const float* res_scale_shift, int act,
+                 float dropout_p, const unsigned long long* rng, int site, void* y, int ldy, long long M, int C,
+                 void* stream);
 int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
                    const float* res_scale_shift, int act, float dropout_p, const unsigned long long* rng, int site,
                    void* y, int ldy, long long M, int C, void* stream);
