@@ -809,6 +809,285 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
   conv_epilogue<bf16_t, QBM, QBN, QWM, QWN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
+// ------------------------------- forward, persistent LDS-DMA square form (bf16)
+// The 256x256 / BK=64 LDS-DMA tile of k_conv_fwd_sq as a PERSISTENT kernel:
+// gridDim = min(tiles, CUs), each block walks its tiles (xcd-remapped
+// linear order, stride gridDim) as ONE flat stream of K-steps, so the next
+// tile's first K-step is already in flight while the current tile's
+// epilogue runs -- the per-tile fill and drain that dominate short-K convs
+// (1x1 over 256..1024 channels: 4..16 K-steps per tile) overlap.
+// The epilogue needs no LDS: the MFMA operands are swapped (weights are the
+// row operand, pixels the column operand) and the weight rows of each
+// wave's 64-channel slab are loaded in a permuted order, so after the K loop
+// lane (g = lane>>4, p = lane&15) holds 16 CONSECUTIVE output channels of
+// pixel p of every pixel fragment: two 16-B bf16 stores per pixel row,
+// straight from the accumulators (no C staging, the stage ring stays free
+// for the next tile's DMA). BN statistics: per-lane sums over the lane's
+// pixels, a 16-lane shuffle reduction, then the 2 pixel-half waves combine
+// in a 4 KiB LDS slot (slab mode) or each add (stat_acc mode).
+constexpr int PS_LDS = 2 * QSTAGE + 2 * 256 * 2 * 4;  // ring + [2 halves][256 cols][2] stats (+ bias: Nout floats)
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+
+// local W-tile row -> channel offset within the 256-column tile: inside each
+// 64-row wave slab, row 16j + 4g + r holds channel 16g + 4j + r (digits j, g
+// swapped; an involution)
+__device__ __forceinline__ int ps_perm(int row) {
+  const int slab = row & ~63, x = row & 63;
+  return slab | ((x & 3) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2));
+}
+
+// PV: DMA piece schedule of the next K-step -- 0: spread over both k-halves
+// (pieces 0-3 in the first, 4-7 in the second), 1: all 8 in the first half (one
+// per pixel fragment), 2: all 8 right after the barrier
+template <bool PADCHK, bool DUAL, int PV>
+__global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
+  constexpr int ES = 2, BK = 64;
+  constexpr int NW = QTHREADS / 64;
+  constexpr int NA = QBM / 8 / NW;  // pixel row-groups (8 rows) per wave: 4
+  constexpr int NB = QBN / 8 / NW;  // weight row-groups per wave: 4
+  constexpr int FM = QBM / (16 * QWM), FN = QBN / (16 * QWN);  // 8 pixel x 4 channel fragments
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / QWN, wn = wid % QWN;
+  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;  // source-side swizzle (see k_conv_fwd_wide)
+  const int fr = lane & 15, fg = lane >> 4;
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  float* sred = (float*)(smem + 2 * QSTAGE);
+
+  const v4i_t rx = buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * ES);
+  const v4i_t rx2 = buf_rsrc(DUAL ? a.x2 : a.x, (long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES);
+  const v4i_t rw = buf_rsrc(a.w, (long long)a.Nout * a.Ktot * ES);
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)((long long)a.M * a.ldy * ES), BUF_FLAGS);
+  const int nk = a.Ktot / BK;
+  const int ntile = a.mtiles * a.ntiles;
+  const int hw = a.Ho * a.Wo;
+  // bias (heads / projections with bias) staged once: the epilogue must issue no vmem load
+  // (a compiler-visible load would be waited for behind the in-flight DMA)
+  float* sbias = sred + 2 * 256 * 2;
+  if (a.bias) {
+    for (int i = tid; i < a.Nout; i += QTHREADS) sbias[i] = a.bias[i];
+    __syncthreads();
+  }
+
+  // DMA row state of the tile being STAGED (may run one tile ahead of the tile being computed)
+  int h0[NA], w0[NA], b1[NA], b2[NA];
+  bool mok[NA];
+  unsigned vb[NB];
+  auto rows_for = [&](int lin) {
+    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+    const int m0 = mt * QBM, n0 = nt * QBN;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + wid * (NA * 8) + i * 8 + lr;
+      mok[i] = m < a.M;
+      const int mm = mok[i] ? m : 0;
+      const int n = mm / hw, rem = mm - (mm / hw) * hw;
+      const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+      h0[i] = ho * a.stride - a.pad;
+      w0[i] = wo * a.stride - a.pad;
+      const int pix = (n * a.H + h0[i]) * a.W + w0[i];
+      b1[i] = pix * a.ldx + lc * 8;
+      b2[i] = DUAL ? pix * a.ldx2 + lc * 8 : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = n0 + ps_perm(wid * (NB * 8) + i * 8 + lr);  // Nout % 256 == 0: in range
+      vb[i] = (unsigned)((n * a.Ktot + lc * 8) * ES);
+    }
+  };
+
+  // K cursor of the staged stream: channel chunk outer, tap inner
+  int cr = 0, cs = 0, cc = 0;
+  bool p_hi = false;
+  int p_toff = 0, p_rd = 0, p_sd = 0;
+  unsigned p_koff = 0, p_As = 0, p_Bs = 0;
+  auto prep = [&](int stage) {
+    const int c0 = cc, rd = cr * a.dil, sd = cs * a.dil;
+    p_koff = (unsigned)(((cr * a.KW + cs) * a.C + c0) * ES);
+    if (++cs == a.KW) {
+      cs = 0;
+      if (++cr == a.KH) { cr = 0; cc += BK; }
+    }
+    p_hi = DUAL && c0 >= a.C1;
+    p_toff = p_hi ? (rd * a.W + sd) * a.ldx2 + (c0 - a.C1) : (rd * a.W + sd) * a.ldx + c0;
+    p_rd = rd;
+    p_sd = sd;
+    p_As = lds0 + stage * QSTAGE;
+    p_Bs = p_As + QBM * 128;
+  };
+  auto piece = [&](int p) {
+    if (p < NA) {
+      bool ok = mok[p];
+      if (PADCHK) ok = ok && (unsigned)(h0[p] + p_rd) < (unsigned)a.H && (unsigned)(w0[p] + p_sd) < (unsigned)a.W;
+      const unsigned vo = ok ? (unsigned)(((p_hi ? b2[p] : b1[p]) + p_toff) * ES) : BUF_OOB;
+      dma16(p_hi ? rx2 : rx, vo, 0, p_As + (wid * (NA * 8) + p * 8) * 128);
+    } else {
+      const int i = p - NA;
+      dma16(rw, vb[i], p_koff, p_Bs + (wid * (NB * 8) + i * 8) * 128);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  int t = blockIdx.x;  // position in this block's tile sequence (stride gridDim)
+  if (t >= ntile) return;
+  int lin = xcd_remap(t, ntile);
+  rows_for(lin);
+  prep(0);
+#pragma unroll
+  for (int p = 0; p < NA + NB; ++p) piece(p);
+  int kt = 0, st = 0;
+  bool epi = false;  // the previous iteration ran an epilogue (its stores may stay in flight)
+  for (;;) {
+    // retire the staged step's DMA (the oldest vmem ops of this wave); the barrier publishes every
+    // wave's part and orders the refill of the other stage after every wave's reads of the previous
+    // step. After an epilogue its 16 stores (+2 atomics) are younger: leave them in flight.
+    if (epi) {
+      if (a.stat_acc > 0 || a.stat_acc == -1)
+        asm volatile("s_waitcnt vmcnt(18)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      epi = false;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const bool last = kt + 1 == nk;
+    const int tnext = t + (int)gridDim.x;
+    bool more = true;
+    if (!last) {
+      prep(st ^ 1);
+    } else if (tnext < ntile) {
+      // first K-step of this block's next tile goes in flight under this step and the epilogue
+      rows_for(xcd_remap(tnext, ntile));
+      cr = 0; cs = 0; cc = 0;
+      prep(st ^ 1);
+    } else {
+      more = false;
+    }
+    const char* Ps = smem + st * QSTAGE;  // pixel rows
+    const char* Ws = Ps + QBM * 128;      // weight rows (permuted)
+    if (PV == 2 && more) {
+#pragma unroll
+      for (int p = 0; p < NA + NB; ++p) piece(p);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fg;
+      uint4 pv[FM], wv[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * (QBN / QWN) + j * 16 + fr;
+        wv[j] = *(const uint4*)(Ws + row * 128 + ((ch ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * (QBM / QWM) + i * 16 + fr;
+        pv[i] = *(const uint4*)(Ps + row * 128 + ((ch ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (PV == 0 && more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
+        if (PV == 1 && more && kk == 0) piece(i);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&wv[j], *(bf16x8_t*)&pv[i], acc[i][j], 0,
+                                                              0, 0);
+      }
+    }
+    st ^= 1;
+    if (!last) {
+      ++kt;
+      continue;
+    }
+    // ---------------- epilogue of tile `lin` (the next tile's step 0 is in flight)
+    // Every global access here is issued unconditionally (buffer stores with an
+    // out-of-range offset for rows past M) so the wave's vmem count is static:
+    // PS_EPI_OPS stores (+2 atomics in stat_acc mode), all YOUNGER than the
+    // in-flight DMA, which the loop head then retires with a counted vmcnt.
+    {
+      const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+      const int m0 = mt * QBM, n0 = nt * QBN;
+      const int cl = wn * 64 + fg * 16;  // this lane's 16 channels: n0 + cl .. +15
+      const bool stats = a.partials != nullptr;
+      float bsv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + cl + e] : 0.f;
+      float s[16], q[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * (QBM / QWM) + i * 16 + fr;
+        const bool ok = m < a.M;
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bsv[j * 4 + r];
+        if (stats) {
+          const float w = ok ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) v[e] = apply_act_rt(a.act, v[e]);
+        }
+        uint32_t w8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+        const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 16 : BUF_OOB, 0, 0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+      if (stats) {
+        // butterfly over the 16 pixel lanes of this lane group: every lane gets the totals
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s[e] += __shfl_xor(s[e], o, 64);
+            q[e] += __shfl_xor(q[e], o, 64);
+          }
+        }
+        float S = s[0], Q = q[0];  // lane fr keeps channel cl + fr (select chain: no scratch)
+#pragma unroll
+        for (int e = 1; e < 16; ++e) {
+          S = fr == e ? s[e] : S;
+          Q = fr == e ? q[e] : Q;
+        }
+        if (a.stat_acc) {
+          acc_stats(a, mt, n0 + cl + fr, make_float2(S, Q));
+        } else {
+          // combine the two pixel-half waves through LDS, then one slab row per M tile
+          sred[(wm * 256 + cl + fr) * 2] = S;
+          sred[(wm * 256 + cl + fr) * 2 + 1] = Q;
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (tid < 256) {
+            const float2 v = make_float2(sred[tid * 2] + sred[(256 + tid) * 2],
+                                         sred[tid * 2 + 1] + sred[(256 + tid) * 2 + 1]);
+            *(float2*)(a.partials + ((size_t)mt * a.Nout + n0 + tid) * 2) = v;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+      }
+    }
+    epi = true;
+    if (!more) break;
+    t = tnext;
+    lin = xcd_remap(t, ntile);
+    kt = 0;
+  }
+}
+
 // ---------------------------------------- forward, persistent buffer-load form
 // 128x128 tiles, gridDim = resident blocks; each block walks its tiles as ONE
 // flat stream of K-steps, so the two-tile register pipeline runs across tile
@@ -1205,6 +1484,7 @@ struct ConvPlan {
   bool wide;  // k_conv_fwd_wide (LDS-DMA, 256x128)
   bool sq;    // k_conv_fwd_sq (LDS-DMA, 256x256)
   int bm, bn;
+  bool ps;    // k_conv_fwd_ps (persistent LDS-DMA 256x256, register epilogue)
 };
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
@@ -1213,6 +1493,13 @@ static int g_sq_enable = 1, g_sq_var = 1;
 static int g_force = 0;
 // 3 = dmf_conv2d_fwd_acc accumulation mode (benchmarking; see acc_stats): 0 default
 static int g_stat_mode = 0;
+// 4 = persistent square form (k_conv_fwd_ps) on (1, default) / off
+static int g_ps_enable = [] {
+  const char* e = std::getenv("DMF_PS");
+  return e && e[0] == '0' ? 0 : 1;
+}();
+// 5 = its DMA piece schedule (k_conv_fwd_ps PV)
+static int g_ps_var = 0;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1220,8 +1507,19 @@ static bool wide_disabled() {
   }();
   return v != 0;
 }
+static int cu_count() {
+  static int cached = 0;
+  if (!cached) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cached <= 0) cached = 256;
+  }
+  return cached;
+}
+
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, false, false, CBM, CBN};
+  ConvPlan p{false, false, false, CBM, CBN, false};
   const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
   // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
   if (dgrad || fast_disabled() || (a.in_ss != nullptr && !(plain && a.x2 == nullptr && !ina_buf_disabled())))
@@ -1249,6 +1547,15 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
       p.bn = (g_force == 1 || g_force == 2) ? 128 : 64;
       return p;
     }
+  }
+  // persistent square LDS-DMA tile: whole 256-column tiles, >= one tile per CU, no fused-finalize
+  // tickets, output addressable by a 32-bit buffer offset
+  if (dtype == DMF_BF16 && !wide_disabled() && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
+      a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= 256 && (long long)a.M * a.ldy * 2 < (1LL << 31)) {
+    p.wide = p.sq = p.ps = true;
+    p.bm = QBM;
+    p.bn = QBN;
+    return p;
   }
   // square LDS-DMA tile: whole 256-column tiles and >= one block per CU
   // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
@@ -1290,8 +1597,9 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = dtype == DMF_BF16 ? 2 : 4;
-  const size_t lds_total = plan.sq ? (size_t)QLDS : plan.wide ? (size_t)WLDS
-                                                            : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
+  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
+                          : plan.sq ? (size_t)QLDS
+                          : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
   const int bk = dtype == DMF_BF16 ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
@@ -1309,6 +1617,22 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
+  } else if (plan.ps) {
+    DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
+#define DMF_PS(V)                                                                                     \
+  do {                                                                                                \
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, V>), gp, bq, lds_total, st, a);  \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, V>), gp, bq, lds_total, st, a);    \
+    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, V>), gp, bq, lds_total, st, a);                \
+  } while (0)
+    switch (g_ps_var) {
+      case 1: DMF_PS(1); break;
+      case 2: DMF_PS(2); break;
+      default: DMF_PS(0);
+    }
+#undef DMF_PS
   } else if (plan.sq) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 bq(QTHREADS);
@@ -1458,6 +1782,8 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 1: DMF_CHECK_ARG(value >= 0 && value < 4, "dmf_conv_tune: square-tile variant %d", value); g_sq_var = value; return 0;
     case 2: DMF_CHECK_ARG(value >= 0 && value <= 6, "dmf_conv_tune: forced tile %d", value); g_force = value; return 0;
     case 3: DMF_CHECK_ARG(value >= -2 && value <= 64, "dmf_conv_tune: stat mode %d", value); g_stat_mode = value; return 0;
+    case 4: g_ps_enable = value != 0; return 0;
+    case 5: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ps variant %d", value); g_ps_var = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
