@@ -6,7 +6,9 @@
 //     gamma/beta column reductions;
 //   * the LayerScale/dropout branch backward of x + drop(y) * gamma (:79-80,
 //     proj_drop :115, MLP drop :133): dy, dgamma and the linear's dbias in one pass;
-//   * bf16 column sums (qkv bias grad) and the f32 -> bf16 weight cast.
+//   * column sums (qkv bias grad) and the f32 -> bf16 weight cast.
+// The branch backward also comes in f32 (the parity mode; the f32 column
+// sums are dense.hip's dmf_colsum_f32).
 // Token rows are R = B * N, channels E contiguous (E % 256 == 0, E <= 1024).
 #include "dmf_common.h"
 #include "../../include/dmf_hip.h"
@@ -138,10 +140,11 @@ __global__ void __launch_bounds__(256) k_ln_bwd(const float* __restrict__ dy, co
 // Branch backward of out = res + drop(y) * gamma, given gout = d out (f32):
 //   dy = keep/(1-p) * gamma * gout (bf16, the linear's output grad),
 //   dgamma += sum gout * drop(y), dbias += sum dy. Dropout element index r*E + c at `site`.
-__global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ gout, const bf16_t* __restrict__ yaux,
+template <typename T>
+__global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ gout, const T* __restrict__ yaux,
                                                     long long R, int E, const float* __restrict__ gamma, float p,
                                                     const unsigned long long* rng, int site,
-                                                    bf16_t* __restrict__ dy, float* __restrict__ dgamma,
+                                                    T* __restrict__ dy, float* __restrict__ dgamma,
                                                     float* __restrict__ dbias) {
   extern __shared__ float red[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -160,9 +163,8 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
         const int c = j * 256 + lane * 4;
         const float4 go = *(const float4*)(gout + r * E + c);
         const float4 gg = *(const float4*)(gamma + c);
-        const uint2 u = *(const uint2*)(yaux + r * E + c);
-        float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-                       __uint_as_float(u.y & 0xffff0000u)};
+        const float4 y4 = tk_ld4(yaux + r * E + c);
+        const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
         float m[4] = {ks, ks, ks, ks};
         if (p > 0.f) {
           bool keep[4];
@@ -175,10 +177,7 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
         ag[j].x += go.x * m[0] * yv[0]; ag[j].y += go.y * m[1] * yv[1];
         ag[j].z += go.z * m[2] * yv[2]; ag[j].w += go.w * m[3] * yv[3];
         ab[j].x += d0; ab[j].y += d1; ab[j].z += d2; ab[j].w += d3;
-        uint2 o;
-        o.x = (uint32_t)f2bf(d0) | ((uint32_t)f2bf(d1) << 16);
-        o.y = (uint32_t)f2bf(d2) | ((uint32_t)f2bf(d3) << 16);
-        *(uint2*)(dy + r * E + c) = o;
+        tk_st4(dy + r * E + c, make_float4(d0, d1, d2, d3));
       }
   }
   if (dgamma) tk_col_flush(red, ag, nj, dgamma);
@@ -186,8 +185,14 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
 }
 
 // out[c] += sum_r X[r][c] (bf16 X, C % 8 == 0); block = 256 column chunks of 8 x 64 rows
-__global__ void __launch_bounds__(256) k_colsum_bf16(const bf16_t* __restrict__ X, int ldx, long long R, int C,
-                                                     float* __restrict__ out) {
+__device__ __forceinline__ void tk_ld8(const bf16_t* p, float* v) { ld8(p, v); }
+__device__ __forceinline__ void tk_ld8(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <typename T>
+__global__ void __launch_bounds__(256) k_tok_colsum(const T* __restrict__ X, int ldx, long long R, int C,
+                                                float* __restrict__ out) {
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= C) return;
   const long long r0 = (long long)blockIdx.y * 64;
@@ -195,7 +200,7 @@ __global__ void __launch_bounds__(256) k_colsum_bf16(const bf16_t* __restrict__ 
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (long long r = r0; r < r1; ++r) {
     float v[8];
-    ld8(X + r * ldx + c, v);
+    tk_ld8(X + r * ldx + c, v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] += v[e];
   }
@@ -273,30 +278,49 @@ extern "C" int dmf_tok_layernorm_bwd(const float* dy, int x_dtype, const void* x
   return 0;
 }
 
+template <typename T>
+static int lsdrop_launch(const char* name, const float* gout, const void* yaux, long long R, int E,
+                         const float* gamma, float dropout_p, const unsigned long long* rng, int site, void* dy,
+                         float* dgamma, float* dbias, void* stream) {
+  DMF_CHECK_ARG(gout && yaux && gamma && dy && R >= 0, "%s: bad args", name);
+  DMF_CHECK_ARG(tk_width_ok(E), "%s: E (%d) must be a multiple of 256, <= %d", name, E, 256 * TK_JMAX);
+  DMF_CHECK_ARG(dropout_p <= 0.f || (rng && dropout_p < 1.f), "%s: dropout needs rng, p < 1", name);
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(k_lsdrop_bwd<T>, dim3((unsigned)((R + TK_ROWS - 1) / TK_ROWS)), dim3(256),
+                     4 * E * sizeof(float), (hipStream_t)stream, gout, (const T*)yaux, R, E, gamma, dropout_p, rng,
+                     site, (T*)dy, dgamma, dbias);
+  DMF_LAUNCH_CHECK(name);
+  return 0;
+}
+
 extern "C" int dmf_tok_scale_dropout_bwd(const float* gout, const void* yaux, long long R, int E, const float* gamma,
                                          float dropout_p, const unsigned long long* rng, int site, void* dy,
                                          float* dgamma, float* dbias, void* stream) {
-  DMF_CHECK_ARG(gout && yaux && gamma && dy && R >= 0, "dmf_tok_scale_dropout_bwd: bad args");
-  DMF_CHECK_ARG(tk_width_ok(E), "dmf_tok_scale_dropout_bwd: E (%d) must be a multiple of 256, <= %d", E,
-                256 * TK_JMAX);
-  DMF_CHECK_ARG(dropout_p <= 0.f || (rng && dropout_p < 1.f), "dmf_tok_scale_dropout_bwd: dropout needs rng, p < 1");
-  if (R == 0) return 0;
-  hipLaunchKernelGGL(k_lsdrop_bwd, dim3((unsigned)((R + TK_ROWS - 1) / TK_ROWS)), dim3(256), 4 * E * sizeof(float),
-                     (hipStream_t)stream, gout, (const bf16_t*)yaux, R, E, gamma, dropout_p, rng, site, (bf16_t*)dy,
-                     dgamma, dbias);
-  DMF_LAUNCH_CHECK("dmf_tok_scale_dropout_bwd");
+  return lsdrop_launch<bf16_t>("dmf_tok_scale_dropout_bwd", gout, yaux, R, E, gamma, dropout_p, rng, site, dy, dgamma,
+                               dbias, stream);
+}
+
+extern "C" int dmf_tok_scale_dropout_bwd_f32(const float* gout, const float* yaux, long long R, int E,
+                                             const float* gamma, float dropout_p, const unsigned long long* rng,
+                                             int site, float* dy, float* dgamma, float* dbias, void* stream) {
+  return lsdrop_launch<float>("dmf_tok_scale_dropout_bwd_f32", gout, yaux, R, E, gamma, dropout_p, rng, site, dy,
+                              dgamma, dbias, stream);
+}
+
+template <typename T>
+static int colsum_launch(const char* name, const void* X, int ldx, long long R, int C, float* out, void* stream) {
+  DMF_CHECK_ARG(X && out && R >= 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X % 16) == 0,
+                "%s: bad args (C=%d ldx=%d)", name, C, ldx);
+  if (R == 0 || C == 0) return 0;
+  DMF_CHECK_ARG((R + 63) / 64 < 65536, "%s: too many rows", name);
+  hipLaunchKernelGGL(k_tok_colsum<T>, dim3((unsigned)cdiv(C / 8, 256), (unsigned)((R + 63) / 64)), dim3(256), 0,
+                     (hipStream_t)stream, (const T*)X, ldx, R, C, out);
+  DMF_LAUNCH_CHECK(name);
   return 0;
 }
 
 extern "C" int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, void* stream) {
-  DMF_CHECK_ARG(X && out && R >= 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X % 16) == 0,
-                "dmf_colsum_bf16: bad args (C=%d ldx=%d)", C, ldx);
-  if (R == 0 || C == 0) return 0;
-  DMF_CHECK_ARG((R + 63) / 64 < 65536, "dmf_colsum_bf16: too many rows");
-  hipLaunchKernelGGL(k_colsum_bf16, dim3((unsigned)cdiv(C / 8, 256), (unsigned)((R + 63) / 64)), dim3(256), 0,
-                     (hipStream_t)stream, (const bf16_t*)X, ldx, R, C, out);
-  DMF_LAUNCH_CHECK("dmf_colsum_bf16");
-  return 0;
+  return colsum_launch<bf16_t>("dmf_colsum_bf16", X, ldx, R, C, out, stream);
 }
 
 extern "C" int dmf_cast_bf16(const float* x, long long n, void* y, void* stream) {

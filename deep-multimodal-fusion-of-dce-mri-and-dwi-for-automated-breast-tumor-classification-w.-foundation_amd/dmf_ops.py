@@ -1813,14 +1813,6 @@ def branch(owner, name, fn, *inputs):
 RNG_CURRENT = [None]
 
 
-def self_attention(qkv, heads, e):
-    """softmax(q k^T / sqrt(d)) v with q|k|v packed along the last dim of qkv."""
-    if qkv.shape[1] > 64:
-        raise NotImplementedError("long-sequence attention kernel (config 5, >64 tokens) is not built yet")
-    o, _ = _CrossAttnFn.apply(qkv, qkv, heads, e)
-    return o
-
-
 def layerscale_residual(x, y, gamma):
     """x + y * gamma (LayerScale, transformer_model.py:79-80)."""
     return x + y * gamma

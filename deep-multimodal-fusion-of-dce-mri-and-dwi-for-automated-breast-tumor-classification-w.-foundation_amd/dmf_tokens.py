@@ -1,5 +1,5 @@
 """Token-stream ops of the hybrid TransformerStage (configuration 5) on the
-bf16 MFMA GEMM (csrc/gemm.hip) and the token kernels (csrc/tokens.hip).
+MFMA GEMM (csrc/gemm.hip) and the token kernels (csrc/tokens.hip).
 
 Reference: ``code/transformer_model.py`` -- PatchEmbed :7-32 (conv k=s=patch,
 then LayerNorm over tokens), TransformerBlock :68-81 (pre-LN, LayerScale
@@ -11,8 +11,11 @@ A whole TransformerBlock is ONE autograd node (`_BlockFn`): the forward is 6
 GEMM launches + softmax/dropout + 2 LayerNorms with every bias / GELU /
 dropout / LayerScale / residual fused into a GEMM epilogue, and the backward
 is written out by hand (13 GEMMs, the dropout masks re-drawn from the Philox
-snapshot instead of stored). Residual stream: f32 [B*N, E]; GEMM operands:
-bf16; accumulation and weight grads: f32.
+snapshot instead of stored). Residual stream: f32 [B*N, E]; accumulation
+and weight grads: f32; GEMM operands and saved activations in the compute
+dtype -- bf16 (throughput: 16x16x32 bf16 MFMA) or f32 (the parity mode,
+``set_compute_dtype(float32)``: 16x16x4 f32 MFMA, f32 probabilities and
+pre-activations, so the block matches the fp32 oracle to rounding).
 """
 from __future__ import annotations
 
@@ -31,14 +34,23 @@ def _s():
 def gemm(out, a, b, M, Nn, K, ta=0, tb=0, lda=None, ldb=None, ldc=None, batch=(1, 1), sa=(0, 0), sb=(0, 0),
          sc=(0, 0), a_off=0, b_off=0, c_off=0, bias=None, act="none", colscale=None, res=None, aux=None, pre=None,
          dropout_p=0.0, rng=None, site=0, dbias=None, alpha=1.0):
-    """out[z] = epilogue(alpha * op(A[z]) op(B[z])) -- see include/dmf_hip.h dmf_gemm_bf16.
-    Offsets are in elements of the operand's dtype."""
+    """out[z] = epilogue(alpha * op(A[z]) op(B[z])) -- see include/dmf_hip.h
+    dmf_gemm_bf16 / dmf_gemm_f32 (picked by the operand dtype; aux and pre are
+    in the operand dtype). Offsets are in elements of the operand's dtype."""
     N.require_cuda(out, a, b)
-    assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+    if a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16:
+        fn, esz = "dmf_gemm_bf16", 2
+    elif a.dtype == torch.float32 and b.dtype == torch.float32:
+        fn, esz = "dmf_gemm_f32", 4
+    else:
+        raise TypeError(f"gemm: operands must both be bf16 or both f32, got {a.dtype} / {b.dtype}")
+    for t in (aux, pre):
+        if t is not None and t.dtype != a.dtype:
+            raise TypeError("gemm: aux / pre must have the operand dtype")
     esz_c = out.element_size()
-    N.call("dmf_gemm_bf16", F32 if out.dtype == torch.float32 else BF16, int(ta), int(tb), int(M), int(Nn), int(K),
-           float(alpha), a.data_ptr() + 2 * a_off, int(lda), int(sa[0]), int(sa[1]),
-           b.data_ptr() + 2 * b_off, int(ldb), int(sb[0]), int(sb[1]),
+    N.call(fn, F32 if out.dtype == torch.float32 else BF16, int(ta), int(tb), int(M), int(Nn), int(K),
+           float(alpha), a.data_ptr() + esz * a_off, int(lda), int(sa[0]), int(sa[1]),
+           b.data_ptr() + esz * b_off, int(ldb), int(sb[0]), int(sb[1]),
            out.data_ptr() + esz_c * c_off, int(ldc), int(sc[0]), int(sc[1]), int(batch[0]), int(batch[1]),
            O._p(bias), O.ACT[act], O._p(colscale), O._p(res), int(res.stride(0)) if res is not None else 0,
            O._p(aux), int(aux.stride(0)) if aux is not None else 0,
@@ -182,126 +194,285 @@ def tokens_to_map(t, h, w, dtype):
 
 
 # ------------------------------------------------------- transformer block
+# The two residual branches as forward / backward helpers, shared by the
+# fused TransformerBlock node and the standalone MultiHeadSelfAttention / MLP
+# modules. Rows r = B*N, width e; `a` is the branch input in the compute
+# dtype, the branch output f32:
+#   attention: out = res + drop(proj(drop(softmax(q k^T * scale)) v)) * gamma
+#   MLP:       out = res + drop(fc2(drop(gelu(fc1(a))))) * gamma
+# (res / gamma absent for the standalone modules: out = the branch itself).
+def _wcast(cdt, *ws):
+    if cdt == torch.bfloat16:
+        return tuple(cast_bf16(w) for w in ws)
+    return tuple(w.contiguous() for w in ws)
+
+
+def _sfx(cdt):
+    return "" if cdt == torch.bfloat16 else "_f32"
+
+
+def _attn_fwd(a, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, gamma=None, res=None):
+    r, e = a.shape
+    d = e // heads
+    cdt, dev = a.dtype, a.device
+    bf = dict(dtype=cdt, device=dev)
+    f32 = dict(dtype=torch.float32, device=dev)
+    qkv = gemm(torch.empty((r, 3 * e), **bf), a, wq, r, 3 * e, e, lda=e, ldb=e, ldc=3 * e, bias=qkvb)
+    S = torch.empty((b, heads, n, n), **f32)
+    gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * 3 * e, d),
+         sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
+    P = torch.empty((b, heads, n, n), **bf)
+    Pd = torch.empty((b, heads, n, n), **bf) if p_attn > 0 else P
+    N.call("dmf_softmax_dropout" + _sfx(cdt), S.data_ptr(), n, b * heads * n, n, float(d ** -0.5), float(p_attn),
+           O._p(rng), int(s_attn), P.data_ptr(), Pd.data_ptr(), n, _s())
+    del S
+    o = gemm(torch.empty((r, e), **bf), Pd, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads),
+             sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
+    y = torch.empty((r, e), **bf)
+    out = gemm(torch.empty((r, e), **f32), o, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=projb, colscale=gamma, res=res,
+               aux=y, dropout_p=p_proj, rng=rng, site=s_proj)
+    return out, (qkv, P, Pd, o, y)
+
+
+def _attn_bwd(dout, a, saved, wq, wp, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, gamma, grads):
+    """dout (f32 [r, e]) -> d a (f32); grads: dqkvw, dqkvb, dprojw, dprojb, dgamma (nullable)."""
+    qkv, P, Pd, o, y = saved
+    r, e = a.shape
+    d = e // heads
+    cdt, dev = a.dtype, a.device
+    bf = dict(dtype=cdt, device=dev)
+    f32 = dict(dtype=torch.float32, device=dev)
+    dqkvw, dqkvb, dprojw, dprojb, dgamma = grads
+    dy = torch.empty((r, e), **bf)
+    N.call("dmf_tok_scale_dropout_bwd" + _sfx(cdt), dout.data_ptr(), y.data_ptr(), r, e, gamma.data_ptr(),
+           float(p_proj), O._p(rng), int(s_proj), dy.data_ptr(), O._p(dgamma), dprojb.data_ptr(), _s())
+    gemm(dprojw, dy, o, e, e, r, ta=1, tb=1, lda=e, ldb=e, ldc=e)
+    do = gemm(torch.empty((r, e), **bf), dy, wp, r, e, e, tb=1, lda=e, ldb=e, ldc=e)
+    del dy
+    dPd = torch.empty((b, heads, n, n), **f32)
+    gemm(dPd, do, qkv, n, n, d, lda=e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * e, d), sb=(n * 3 * e, d),
+         sc=(heads * n * n, n * n), b_off=2 * e)
+    dqkv = torch.empty((r, 3 * e), **bf)
+    # dV = Pd^T dO
+    gemm(dqkv, Pd, do, n, d, n, ta=1, tb=1, lda=n, ldb=e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
+         sb=(n * e, d), sc=(n * 3 * e, d), c_off=2 * e)
+    dS = torch.empty((b, heads, n, n), **bf)
+    N.call("dmf_softmax_dropout_bwd" + _sfx(cdt), P.data_ptr(), n, dPd.data_ptr(), n, b * heads * n, n,
+           float(d ** -0.5), float(p_attn), O._p(rng), int(s_attn), dS.data_ptr(), n, _s())
+    del dPd
+    # dQ = dS K, dK = dS^T Q
+    gemm(dqkv, dS, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
+         sb=(n * 3 * e, d), sc=(n * 3 * e, d), b_off=e)
+    gemm(dqkv, dS, qkv, n, d, n, ta=1, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads),
+         sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * 3 * e, d), c_off=e)
+    del dS
+    gemm(dqkvw, dqkv, a, 3 * e, e, r, ta=1, tb=1, lda=3 * e, ldb=e, ldc=e)
+    if dqkvb is not None:
+        if cdt == torch.bfloat16:
+            N.call("dmf_colsum_bf16", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), _s())
+        else:
+            N.call("dmf_colsum_f32", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), 1, _s())
+    return gemm(torch.empty((r, e), **f32), dqkv, wq, r, e, 3 * e, tb=1, lda=3 * e, ldb=e, ldc=e)
+
+
+def _mlp_fwd(a, w1, b1, w2, b2, p, rng, s1, s2, gamma=None, res=None):
+    r, e = a.shape
+    hid = w1.shape[0]
+    cdt, dev = a.dtype, a.device
+    bf = dict(dtype=cdt, device=dev)
+    hpre = torch.empty((r, hid), **bf)
+    h = gemm(torch.empty((r, hid), **bf), a, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=b1, act="gelu", aux=hpre,
+             dropout_p=p, rng=rng, site=s1)
+    y = torch.empty((r, e), **bf)
+    out = gemm(torch.empty((r, e), dtype=torch.float32, device=dev), h, w2, r, e, hid, lda=hid, ldb=hid, ldc=e,
+               bias=b2, colscale=gamma, res=res, aux=y, dropout_p=p, rng=rng, site=s2)
+    return out, (hpre, h, y)
+
+
+def _mlp_bwd(dout, a, saved, w1, w2, p, rng, s1, s2, gamma, grads):
+    """dout (f32 [r, e]) -> d a (f32); grads: dfc1w, dfc1b, dfc2w, dfc2b, dgamma (nullable)."""
+    hpre, h, y = saved
+    r, e = a.shape
+    hid = w1.shape[0]
+    cdt, dev = a.dtype, a.device
+    bf = dict(dtype=cdt, device=dev)
+    dfc1w, dfc1b, dfc2w, dfc2b, dgamma = grads
+    dy = torch.empty((r, e), **bf)
+    N.call("dmf_tok_scale_dropout_bwd" + _sfx(cdt), dout.data_ptr(), y.data_ptr(), r, e, gamma.data_ptr(), float(p),
+           O._p(rng), int(s2), dy.data_ptr(), O._p(dgamma), dfc2b.data_ptr(), _s())
+    gemm(dfc2w, dy, h, e, hid, r, ta=1, tb=1, lda=e, ldb=hid, ldc=hid)
+    dpre = gemm(torch.empty((r, hid), **bf), dy, w2, r, hid, e, tb=1, lda=e, ldb=hid, ldc=hid, act="gelu",
+                pre=hpre, dropout_p=p, rng=rng, site=s1, dbias=dfc1b)
+    del dy
+    gemm(dfc1w, dpre, a, hid, e, r, ta=1, tb=1, lda=hid, ldb=e, ldc=e)
+    return gemm(torch.empty((r, e), dtype=torch.float32, device=dev), dpre, w1, r, e, hid, tb=1, lda=hid, ldb=e,
+                ldc=e)
+
+
+def _zeros(dev, *shapes):
+    return [torch.zeros(s, dtype=torch.float32, device=dev) for s in shapes]
+
+
 class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cfg, rng, ln1w, ln1b, qkvw, qkvb, projw, projb, ln2w, ln2b, fc1w, fc1b, fc2w, fc2b, g1, g2):
-        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites = cfg
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt = cfg
         s_attn, s_proj, s_m1, s_m2 = sites
         b, n, e = x.shape
-        r, d, hid = b * n, e // heads, fc1w.shape[0]
-        dev = x.device
-        x = x.contiguous().view(r, e)
-        wq, wp, w1, w2 = cast_bf16(qkvw), cast_bf16(projw), cast_bf16(fc1w), cast_bf16(fc2w)
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        f32 = dict(dtype=torch.float32, device=dev)
+        x = x.contiguous().view(b * n, e)
+        wq, wp, w1, w2 = _wcast(cdt, qkvw, projw, fc1w, fc2w)
         # attention branch: x1 = x + drop(proj(attn(ln1(x)))) * g1
-        ln1, save1 = ln_fwd(x, ln1w, ln1b, eps1, torch.bfloat16)
-        qkv = gemm(torch.empty((r, 3 * e), **bf), ln1, wq, r, 3 * e, e, lda=e, ldb=e, ldc=3 * e, bias=qkvb)
-        S = torch.empty((b, heads, n, n), **f32)
-        gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * 3 * e, d),
-             sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
-        P = torch.empty((b, heads, n, n), **bf)
-        Pd = torch.empty((b, heads, n, n), **bf) if p_attn > 0 else P
-        N.call("dmf_softmax_dropout", S.data_ptr(), n, b * heads * n, n, float(d ** -0.5), float(p_attn), O._p(rng),
-               int(s_attn), P.data_ptr(), Pd.data_ptr(), n, _s())
-        del S
-        o = gemm(torch.empty((r, e), **bf), Pd, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads),
-                 sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
-        y1 = torch.empty((r, e), **bf)
-        x1 = gemm(torch.empty((r, e), **f32), o, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=projb, colscale=g1, res=x,
-                  aux=y1, dropout_p=p_proj, rng=rng, site=s_proj)
+        ln1, save1 = ln_fwd(x, ln1w, ln1b, eps1, cdt)
+        x1, sa = _attn_fwd(ln1, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, g1, x)
         # MLP branch: x2 = x1 + drop(fc2(drop(gelu(fc1(ln2(x1)))))) * g2
-        ln2, save2 = ln_fwd(x1, ln2w, ln2b, eps2, torch.bfloat16)
-        hpre = torch.empty((r, hid), **bf)
-        h = gemm(torch.empty((r, hid), **bf), ln2, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=fc1b, act="gelu",
-                 aux=hpre, dropout_p=p_mlp, rng=rng, site=s_m1)
-        y2 = torch.empty((r, e), **bf)
-        x2 = gemm(torch.empty((r, e), **f32), h, w2, r, e, hid, lda=hid, ldb=hid, ldc=e, bias=fc2b, colscale=g2,
-                  res=x1, aux=y2, dropout_p=p_mlp, rng=rng, site=s_m2)
-        ctx.save_for_backward(x, ln1, save1, qkv, P, Pd, o, y1, x1, ln2, save2, hpre, h, y2, wq, wp, w1, w2,
-                              ln1w, ln2w, g1, g2, rng)
+        ln2, save2 = ln_fwd(x1, ln2w, ln2b, eps2, cdt)
+        x2, sm = _mlp_fwd(ln2, w1, fc1b, w2, fc2b, p_mlp, rng, s_m1, s_m2, g2, x1)
+        ctx.save_for_backward(x, ln1, save1, *sa, x1, ln2, save2, *sm, wq, wp, w1, w2, ln1w, ln2w, g1, g2, rng)
         ctx.cfg = cfg
-        ctx.dims = (b, n, e, heads, d, hid)
+        ctx.dims = (b, n, e)
         return x2.view(b, n, e)
 
     @staticmethod
     def backward(ctx, dx2):
-        (x, ln1, save1, qkv, P, Pd, o, y1, x1, ln2, save2, hpre, h, y2, wq, wp, w1, w2,
-         ln1w, ln2w, g1, g2, rng) = ctx.saved_tensors
-        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites = ctx.cfg
+        t = ctx.saved_tensors
+        x, ln1, save1, sa, x1, ln2, save2, sm = t[0], t[1], t[2], t[3:8], t[8], t[9], t[10], t[11:14]
+        wq, wp, w1, w2, ln1w, ln2w, g1, g2, rng = t[14:]
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt = ctx.cfg
         s_attn, s_proj, s_m1, s_m2 = sites
-        b, n, e, heads, d, hid = ctx.dims
-        r = b * n
+        b, n, e = ctx.dims
+        hid = w1.shape[0]
         dev = x.device
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        f32 = dict(dtype=torch.float32, device=dev)
-
-        def z(*s):
-            return torch.zeros(s, **f32)
-
-        dln1w, dln1b, dqkvw, dqkvb, dprojw, dprojb = z(e), z(e), z(3 * e, e), z(3 * e), z(e, e), z(e)
-        dln2w, dln2b, dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2 = z(e), z(e), z(hid, e), z(hid), z(e, hid), z(e), z(e), z(e)
-        dx2 = dx2.contiguous().view(r, e).float()
-        # ---- MLP branch
-        dy2 = torch.empty((r, e), **bf)
-        N.call("dmf_tok_scale_dropout_bwd", dx2.data_ptr(), y2.data_ptr(), r, e, g2.data_ptr(), float(p_mlp),
-               O._p(rng), int(s_m2), dy2.data_ptr(), dg2.data_ptr(), dfc2b.data_ptr(), _s())
-        gemm(dfc2w, dy2, h, e, hid, r, ta=1, tb=1, lda=e, ldb=hid, ldc=hid)
-        dpre = gemm(torch.empty((r, hid), **bf), dy2, w2, r, hid, e, tb=1, lda=e, ldb=hid, ldc=hid, act="gelu",
-                    pre=hpre, dropout_p=p_mlp, rng=rng, site=s_m1, dbias=dfc1b)
-        gemm(dfc1w, dpre, ln2, hid, e, r, ta=1, tb=1, lda=hid, ldb=e, ldc=e)
-        dln2 = gemm(torch.empty((r, e), **f32), dpre, w1, r, e, hid, tb=1, lda=hid, ldb=e, ldc=e)
-        del dpre
+        dln1w, dln1b, dqkvw, dqkvb, dprojw, dprojb = _zeros(dev, e, e, (3 * e, e), 3 * e, (e, e), e)
+        dln2w, dln2b, dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2 = _zeros(dev, e, e, (hid, e), hid, (e, hid), e, e, e)
+        dx2 = dx2.contiguous().view(b * n, e).float()
+        dln2 = _mlp_bwd(dx2, ln2, sm, w1, w2, p_mlp, rng, s_m1, s_m2, g2, (dfc1w, dfc1b, dfc2w, dfc2b, dg2))
         dx1 = ln_bwd(dln2, x1, save2, ln2w, dx2.clone(), dln2w, dln2b)
-        # ---- attention branch
-        dy1 = torch.empty((r, e), **bf)
-        N.call("dmf_tok_scale_dropout_bwd", dx1.data_ptr(), y1.data_ptr(), r, e, g1.data_ptr(), float(p_proj),
-               O._p(rng), int(s_proj), dy1.data_ptr(), dg1.data_ptr(), dprojb.data_ptr(), _s())
-        gemm(dprojw, dy1, o, e, e, r, ta=1, tb=1, lda=e, ldb=e, ldc=e)
-        do = gemm(torch.empty((r, e), **bf), dy1, wp, r, e, e, tb=1, lda=e, ldb=e, ldc=e)
-        dPd = torch.empty((b, heads, n, n), **f32)
-        gemm(dPd, do, qkv, n, n, d, lda=e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * e, d), sb=(n * 3 * e, d),
-             sc=(heads * n * n, n * n), b_off=2 * e)
-        dqkv = torch.empty((r, 3 * e), **bf)
-        # dV = Pd^T dO
-        gemm(dqkv, Pd, do, n, d, n, ta=1, tb=1, lda=n, ldb=e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
-             sb=(n * e, d), sc=(n * 3 * e, d), c_off=2 * e)
-        dS = torch.empty((b, heads, n, n), **bf)
-        N.call("dmf_softmax_dropout_bwd", P.data_ptr(), n, dPd.data_ptr(), n, b * heads * n, n, float(d ** -0.5),
-               float(p_attn), O._p(rng), int(s_attn), dS.data_ptr(), n, _s())
-        del dPd
-        # dQ = dS K, dK = dS^T Q
-        gemm(dqkv, dS, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads), sa=(heads * n * n, n * n),
-             sb=(n * 3 * e, d), sc=(n * 3 * e, d), b_off=e)
-        gemm(dqkv, dS, qkv, n, d, n, ta=1, tb=1, lda=n, ldb=3 * e, ldc=3 * e, batch=(b, heads),
-             sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * 3 * e, d), c_off=e)
-        del dS
-        gemm(dqkvw, dqkv, ln1, 3 * e, e, r, ta=1, tb=1, lda=3 * e, ldb=e, ldc=e)
-        N.call("dmf_colsum_bf16", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), _s())
-        dln1 = gemm(torch.empty((r, e), **f32), dqkv, wq, r, e, 3 * e, tb=1, lda=3 * e, ldb=e, ldc=e)
+        dln1 = _attn_bwd(dx1, ln1, sa, wq, wp, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, g1,
+                         (dqkvw, dqkvb, dprojw, dprojb, dg1))
         dx = ln_bwd(dln1, x, save1, ln1w, dx1, dln1w, dln1b)
         return (dx.view(b, n, e), None, None, dln1w, dln1b, dqkvw, dqkvb, dprojw, dprojb, dln2w, dln2b,
                 dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2)
 
 
-def transformer_block(x, blk, rng, sites):
-    """TransformerBlock.forward (transformer_model.py:78-81) as one node."""
-    at, mlp = blk.attn, blk.mlp
+def _branch_input(x, cdt):
+    b, n, e = x.shape
+    x2d = x.reshape(b * n, e)
+    if cdt == torch.bfloat16:
+        return cast_bf16(x2d.float()) if x2d.dtype != torch.bfloat16 else x2d.contiguous()
+    return x2d.float().contiguous()
+
+
+class _MHSAFn(torch.autograd.Function):
+    """Standalone MultiHeadSelfAttention.forward (transformer_model.py:100-116)."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, rng, qkvw, qkvb, projw, projb):
+        heads, p_attn, p_proj, sites, cdt = cfg
+        b, n, e = x.shape
+        a = _branch_input(x, cdt)
+        wq, wp = _wcast(cdt, qkvw, projw)
+        out, sa = _attn_fwd(a, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, sites[0], sites[1])
+        ones = torch.ones(e, dtype=torch.float32, device=x.device)
+        ctx.save_for_backward(a, *sa, wq, wp, ones, rng)
+        ctx.cfg, ctx.dims, ctx.xdtype = cfg, (b, n, e), x.dtype
+        return out.view(b, n, e)
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, *rest = ctx.saved_tensors
+        sa, (wq, wp, ones, rng) = rest[:5], rest[5:]
+        heads, p_attn, p_proj, sites, cdt = ctx.cfg
+        b, n, e = ctx.dims
+        need = ctx.needs_input_grad
+        dqkvw, dqkvb, dprojw, dprojb = _zeros(a.device, (3 * e, e), 3 * e, (e, e), e)
+        da = _attn_bwd(dout.contiguous().view(b * n, e).float(), a, sa, wq, wp, b, n, heads, p_attn, p_proj, rng,
+                       sites[0], sites[1], ones, (dqkvw, dqkvb if need[4] else None, dprojw, dprojb, None))
+        return (da.view(b, n, e).to(ctx.xdtype), None, None, dqkvw, dqkvb if need[4] else None, dprojw, dprojb)
+
+
+class _MLPFn(torch.autograd.Function):
+    """Standalone MLP.forward (transformer_model.py:128-134)."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, rng, fc1w, fc1b, fc2w, fc2b):
+        p, sites, cdt = cfg
+        b, n, e = x.shape
+        a = _branch_input(x, cdt)
+        w1, w2 = _wcast(cdt, fc1w, fc2w)
+        out, sm = _mlp_fwd(a, w1, fc1b, w2, fc2b, p, rng, sites[0], sites[1])
+        ones = torch.ones(e, dtype=torch.float32, device=x.device)
+        ctx.save_for_backward(a, *sm, w1, w2, ones, rng)
+        ctx.cfg, ctx.dims, ctx.xdtype = cfg, (b, n, e), x.dtype
+        return out.view(b, n, e)
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, hpre, h, y, w1, w2, ones, rng = ctx.saved_tensors
+        p, sites, cdt = ctx.cfg
+        b, n, e = ctx.dims
+        hid = w1.shape[0]
+        dfc1w, dfc1b, dfc2w, dfc2b = _zeros(a.device, (hid, e), hid, (e, hid), e)
+        da = _mlp_bwd(dout.contiguous().view(b * n, e).float(), a, (hpre, h, y), w1, w2, p, rng, sites[0], sites[1],
+                      ones, (dfc1w, dfc1b, dfc2w, dfc2b, None))
+        return da.view(b, n, e).to(ctx.xdtype), None, None, dfc1w, dfc1b, dfc2w, dfc2b
+
+
+def _check_tokens(what, x, e, head_dim=8):
+    if e % 256 or e > 1024 or head_dim % 8:
+        raise ValueError(f"{what}: embed_dim {e} must be a multiple of 256 (<= 1024), head_dim % 8 == 0")
+    if x.dim() != 3 or x.shape[-1] != e:
+        raise ValueError(f"{what}: expected tokens [B, N, {e}], got {tuple(x.shape)}")
+    if x.shape[1] % 8:
+        raise ValueError(f"{what}: token count {x.shape[1]} must be a multiple of 8")
+
+
+def _check_dtype(what, dtype):
+    if dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError(f"{what}: compute dtype must be bf16 or f32, got {dtype}")
+
+
+def _need_rng(what, rng, *ps):
+    if rng is None and any(p > 0 for p in ps):
+        raise RuntimeError(f"{what}: dropout requested without an rng snapshot")
+
+
+def multihead_self_attention(x, at, rng, dtype=torch.bfloat16):
+    """MultiHeadSelfAttention.forward (transformer_model.py:100-116) as one node."""
+    p_attn = float(at.attn_drop.p) if at.attn_drop.training else 0.0
+    p_proj = float(at.proj_drop.p) if at.proj_drop.training else 0.0
+    _need_rng("MultiHeadSelfAttention", rng, p_attn, p_proj)
+    _check_tokens("MultiHeadSelfAttention", x, at.embed_dim, at.head_dim)
+    _check_dtype("MultiHeadSelfAttention", dtype)
+    if at.qkv.bias is None:
+        raise ValueError("MultiHeadSelfAttention: qkv_bias=False is not supported by the fused path")
+    cfg = (at.num_heads, p_attn, p_proj, tuple(at._sites), dtype)
+    return _MHSAFn.apply(x, cfg, rng, at.qkv.weight, at.qkv.bias, at.proj.weight, at.proj.bias)
+
+
+def mlp(x, m, rng, dtype=torch.bfloat16):
+    """MLP.forward (transformer_model.py:128-134) as one node."""
+    p = float(m.drop.p) if m.drop.training else 0.0
+    _need_rng("MLP", rng, p)
+    _check_tokens("MLP", x, m.fc1.in_features)
+    _check_dtype("MLP", dtype)
+    return _MLPFn.apply(x, (p, tuple(m._sites), dtype), rng, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)
+
+
+def transformer_block(x, blk, rng, sites, dtype=torch.bfloat16):
+    """TransformerBlock.forward (transformer_model.py:78-81) as one node;
+    ``dtype`` is the compute dtype (bf16, or f32 for the parity mode)."""
+    at, ml = blk.attn, blk.mlp
     # the nn.Dropout modules' own flags (train() / eval() set them with the
     # block's; MC dropout turns on only these, train_fusion.py:445-449)
     p_attn = float(at.attn_drop.p) if at.attn_drop.training else 0.0
     p_proj = float(at.proj_drop.p) if at.proj_drop.training else 0.0
-    p_mlp = float(mlp.drop.p) if mlp.drop.training else 0.0
-    if rng is None and (p_attn > 0 or p_proj > 0 or p_mlp > 0):
-        raise RuntimeError("transformer dropout requested without an rng snapshot")
-    e = x.shape[-1]
-    if e % 256 or e > 1024 or at.head_dim % 8:
-        raise ValueError(f"TransformerBlock: embed_dim {e} must be a multiple of 256 (<= 1024), head_dim % 8 == 0")
-    if x.shape[1] % 8:
-        raise ValueError(f"TransformerBlock: token count {x.shape[1]} must be a multiple of 8")
+    p_mlp = float(ml.drop.p) if ml.drop.training else 0.0
+    _need_rng("TransformerBlock", rng, p_attn, p_proj, p_mlp)
+    _check_tokens("TransformerBlock", x, at.embed_dim, at.head_dim)
+    _check_dtype("TransformerBlock", dtype)
     if at.qkv.bias is None:
         raise ValueError("TransformerBlock: qkv_bias=False is not supported by the fused path")
-    cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites))
+    cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites), dtype)
     return _BlockFn.apply(x, cfg, rng, blk.norm1.weight, blk.norm1.bias, at.qkv.weight, at.qkv.bias, at.proj.weight,
-                          at.proj.bias, blk.norm2.weight, blk.norm2.bias, mlp.fc1.weight, mlp.fc1.bias,
-                          mlp.fc2.weight, mlp.fc2.bias, blk.gamma1, blk.gamma2)
+                          at.proj.bias, blk.norm2.weight, blk.norm2.bias, ml.fc1.weight, ml.fc1.bias,
+                          ml.fc2.weight, ml.fc2.bias, blk.gamma1, blk.gamma2)

@@ -6,7 +6,8 @@ Module and parameter names match the reference (PatchEmbed :7-32,
 TokensToFeatureMap :34-52, TransformerEncoder :54-66, TransformerBlock
 :68-81, MultiHeadSelfAttention :83-116, MLP :118-134, TransformerStage
 :137-175). Patch embedding runs on the conv engine; LayerNorm, the linear
-layers and attention on the fp32 token kernels.
+layers and attention on the MFMA GEMM + token kernels (dmf_tokens), in the
+module's compute dtype (bf16, or f32 for the parity mode).
 """
 from __future__ import annotations
 
@@ -23,6 +24,16 @@ def _caches(conv):
         c = (O.WeightCache(), O.WeightCache())
         conv._dmf_caches = c
     return c
+
+
+def _rng_if(x, *drops):
+    """The Philox snapshot when any of the nn.Dropout modules draws (their own
+    train flags: MC dropout turns on only them) -- the enclosing encoder's
+    snapshot if there is one, else a fresh one."""
+    if not any(d.training and d.p > 0 for d in drops):
+        return None
+    cur = O.RNG_CURRENT[0]
+    return cur if cur is not None else O.RNG.snapshot(x.device)
 
 
 class PatchEmbed(nn.Module):
@@ -72,14 +83,11 @@ class MultiHeadSelfAttention(nn.Module):
         self.attn_drop = nn.Dropout(attn_drop)
         self.proj = nn.Linear(embed_dim, embed_dim)
         self.proj_drop = nn.Dropout(proj_drop)
+        self._sites = (O.RNG.new_site(), O.RNG.new_site())   # Philox: attn_drop, proj_drop
 
     def forward(self, x):
-        if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
-            raise NotImplementedError("attention/projection dropout in train mode is not built yet (config 5)")
-        b, n, c = x.shape
-        qkv = O.linear(x.reshape(b * n, c), self.qkv.weight, self.qkv.bias).view(b, n, 3 * c)
-        o = O.self_attention(qkv, self.num_heads, c)
-        return O.linear(o.reshape(b * n, c), self.proj.weight, self.proj.bias).view(b, n, c)
+        rng = _rng_if(x, self.attn_drop, self.proj_drop)
+        return D.multihead_self_attention(x, self, rng, getattr(self, "compute_dtype", torch.bfloat16))
 
 
 class MLP(nn.Module):
@@ -90,13 +98,11 @@ class MLP(nn.Module):
         self.act = nn.GELU()
         self.fc2 = nn.Linear(hidden_dim, embed_dim)
         self.drop = nn.Dropout(drop)
+        self._sites = (O.RNG.new_site(), O.RNG.new_site())   # Philox: drop after GELU, drop after fc2
 
     def forward(self, x):
-        if self.training and self.drop.p > 0:
-            raise NotImplementedError("MLP dropout in train mode is not built yet (config 5)")
-        b, n, c = x.shape
-        h = O.linear(x.reshape(b * n, c), self.fc1.weight, self.fc1.bias, act="gelu")
-        return O.linear(h, self.fc2.weight, self.fc2.bias).view(b, n, c)
+        rng = _rng_if(x, self.drop)
+        return D.mlp(x, self, rng, getattr(self, "compute_dtype", torch.bfloat16))
 
 
 class TransformerBlock(nn.Module):
@@ -109,15 +115,11 @@ class TransformerBlock(nn.Module):
         self.gamma1 = nn.Parameter(init_scale * torch.ones(embed_dim))
         self.gamma2 = nn.Parameter(init_scale * torch.ones(embed_dim))
         # Philox sites: attn_drop, proj_drop, MLP drop after GELU, MLP drop after fc2
-        self._sites = tuple(O.RNG.new_site() for _ in range(4))
+        self._sites = self.attn._sites + self.mlp._sites
 
     def forward(self, x):
-        rng = None
-        # dropout follows the nn.Dropout modules (MC dropout turns only them on)
-        if self.attn.attn_drop.training or self.attn.proj_drop.training or self.mlp.drop.training:
-            cur = O.RNG_CURRENT[0]
-            rng = cur if cur is not None else O.RNG.snapshot(x.device)
-        return D.transformer_block(x.float(), self, rng, self._sites)
+        rng = _rng_if(x, self.attn.attn_drop, self.attn.proj_drop, self.mlp.drop)
+        return D.transformer_block(x.float(), self, rng, self._sites, getattr(self, "compute_dtype", torch.bfloat16))
 
 
 class TransformerEncoder(nn.Module):

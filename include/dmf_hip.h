@@ -349,6 +349,14 @@ int dmf_gemm_bf16(int out_dtype, int ta, int tb, int M, int N, int K, float alph
                   int ldc, long long sC1, long long sC2, int batch1, int batch2, const float* bias, int act,
                   const float* colscale, const float* res, int ldr, void* aux, int ldaux, const void* pre, int ldpre,
                   float dropout_p, const unsigned long long* rng, int site, float* dbias, void* stream);
+/* the same GEMM with f32 A, B, aux and pre on the 16x16x4 f32 MFMA (exact
+ * f32 products): the fp32 parity mode of the transformer stage
+ * (set_compute_dtype(float32)); K, lda, ldb multiples of 4. */
+int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda,
+                 long long sA1, long long sA2, const float* B, int ldb, long long sB1, long long sB2, void* C,
+                 int ldc, long long sC1, long long sC2, int batch1, int batch2, const float* bias, int act,
+                 const float* colscale, const float* res, int ldr, float* aux, int ldaux, const float* pre, int ldpre,
+                 float dropout_p, const unsigned long long* rng, int site, float* dbias, void* stream);
 /* attention probabilities (transformer_model.py:104-110): per row of L f32
  * scores, probs = softmax(scale * s) (bf16, kept for backward) and
  * probs_dropped = dropout(probs, p) (bf16, the P operand of P v); Philox
@@ -360,6 +368,13 @@ int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, float sc
 int dmf_softmax_dropout_bwd(const void* probs, int ldp, const float* dprobs_dropped, int ldg, long long rows, int L,
                             float scale, float dropout_p, const unsigned long long* rng, int site, void* dscores,
                             int lds, void* stream);
+/* f32 probs / dscores (parity mode) */
+int dmf_softmax_dropout_f32(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
+                            const unsigned long long* rng, int site, float* probs, float* probs_dropped, int ldp,
+                            void* stream);
+int dmf_softmax_dropout_bwd_f32(const float* probs, int ldp, const float* dprobs_dropped, int ldg, long long rows,
+                                int L, float scale, float dropout_p, const unsigned long long* rng, int site,
+                                float* dscores, int lds, void* stream);
 
 /* token-stream kernels (transformer_model.py:29, :71-80, :115, :133); rows R = B*N,
  * E % 256 == 0 and E <= 1024. LayerNorm: y bf16, save = (mean, rstd) per row. */
@@ -374,6 +389,10 @@ int dmf_tok_layernorm_bwd(const float* dy, int x_dtype, const void* x, int ldx, 
 int dmf_tok_scale_dropout_bwd(const float* gout, const void* yaux, long long R, int E, const float* gamma,
                               float dropout_p, const unsigned long long* rng, int site, void* dy, float* dgamma,
                               float* dbias, void* stream);
+/* f32 yaux / dy (parity mode) */
+int dmf_tok_scale_dropout_bwd_f32(const float* gout, const float* yaux, long long R, int E, const float* gamma,
+                                  float dropout_p, const unsigned long long* rng, int site, float* dy, float* dgamma,
+                                  float* dbias, void* stream);
 int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, void* stream);
 int dmf_cast_bf16(const float* x, long long n, void* y, void* stream);
 int dmf_cast_f32(const void* x, long long n, float* y, void* stream);

@@ -227,9 +227,11 @@ def test_fusion_step_config5_hybrid_mode_b():
     """Config 5 (hybrid TransformerStage, model_module.py:564-579 / :701-703) at a
     reduced size that keeps its shape regime: S=192 -> f2 24x24 -> 144 tokens,
     f3 12x12, proj_pool 24 -> 64 (non-integer ratio), fused recon map 12x12
-    beside 24x24 encoder maps. Everything trainable (mode B). Convs in the f32
-    parity mode; the transformer GEMMs are bf16, so the tolerance is the bf16
-    one (3e-2 relative on the loss, 5e-2 of the max on grads)."""
+    beside 24x24 encoder maps. Everything trainable (mode B), everything in
+    the f32 parity mode -- the transformer GEMMs on the 16x16x4 f32 MFMA
+    (dmf_gemm_f32) -- so the north-star tolerances hold: logits within 1e-3,
+    the loss within 1e-4 relative; transformer grads within 1e-3 of their
+    max (they sit above the ill-conditioned backbone in the backward)."""
     P = PR.small_parameters(channels=(16, 32, 64), input_size=192, dropout=0.0)
     mp = P["dwi_model_parameters"]
     mp["use_hybrid_transformer"] = True
@@ -252,17 +254,27 @@ def test_fusion_step_config5_hybrid_mode_b():
     for m in (dwi_r, dce_r, fr):
         m.train()
     bt = batch(4, 192, 17)
-    loss = lm.training_step(tuple(t.to(DEV) for t in bt))
+    bd = tuple(t.to(DEV) for t in bt)
+    with torch.no_grad():
+        _, logits, _, _ = lm._shared_step(bd, "train", return_preds=True)
+    loss = lm.training_step(bd)
     loss.backward()
     cw = OL.class_weights_from_labels(train_labels)
     ref = OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, cw, epoch=0)
     ref["total"].backward()
-    assert abs(loss.item() - ref["total"].item()) < 3e-2 * max(1, abs(ref["total"].item()))
+    lerr = (logits.cpu() - ref["logits"].detach()).abs().max().item()
+    print(f"config 5 f32: logits max err {lerr:.2e}, loss {loss.item():.6f} vs {ref['total'].item():.6f}")
+    assert lerr <= 1e-3, lerr
+    assert abs(loss.item() - ref["total"].item()) <= 1e-4 * max(1, abs(ref["total"].item()))
     named = dict(dwi_r.named_parameters())
+    worst = 0.0
     for n, p1 in dwi_m.named_parameters():
         if n.startswith("transformer.") and named[n].grad is not None:
             g2 = named[n].grad
-            assert (p1.grad.cpu().reshape(g2.shape) - g2).abs().max() <= 5e-2 * max(1e-3, g2.abs().max().item()), n
+            e = (p1.grad.cpu().reshape(g2.shape) - g2).abs().max().item() / max(1e-6, g2.abs().max().item())
+            worst = max(worst, e)
+            assert e <= 1e-3, (n, e)
+    print(f"config 5 f32: worst transformer grad error {worst:.2e} of the tensor max")
 
 
 def test_encoder_rejects_bad_input_loudly():
