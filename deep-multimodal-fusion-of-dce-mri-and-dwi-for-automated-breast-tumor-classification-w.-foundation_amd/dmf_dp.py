@@ -4,12 +4,21 @@ Replaces the Lightning Trainer that ``run_training.run_fusion_model``
 (run_training.py:181-333) builds, for the hot path only:
   * rank-strided sampling of volumes (each rank its own local batch; BN stays
     LOCAL, as the reference uses plain BatchNorm2d -- SURVEY.md 8(e));
-  * ONE gradient exchange per step: the gradients of every trainable
-    parameter are packed into a single fp32 bucket (one kernel), summed with
-    one ``all_reduce`` (backend "nccl" == RCCL), and the AdamW kernel reads the
-    reduced bucket directly with scale 1/world (no unpack pass);
-  * the step (forward + backward + pack [+ all-reduce] + AdamW) is captured
-    into hipGraphs after warm-up, so the Python launch overhead is paid once;
+  * the gradients of every trainable parameter go to ONE flat fp32 bucket
+    that the AdamW kernel reads directly with scale 1/world (no unpack pass);
+  * with RCCL (backend "nccl") the exchange OVERLAPS the backward: the bucket
+    is laid out in gradient-ready order and cut into ~DMF_DP_BUCKET_MB
+    segments; a post-accumulate-grad hook launches pack + ``all_reduce`` of a
+    segment on a communication stream the moment its last gradient lands,
+    while autograd keeps computing the earlier layers' gradients (fusion
+    model first, then the encoders' heads, layer4 ... stem). The collectives
+    run on a bare RCCL communicator (dmf_rccl) and are captured into the
+    step's hipGraph with everything else (RCCL supports stream capture;
+    probed in tools/capture_fork_probe.py);
+  * with gloo (the CPU / shared-GPU rehearsal) the bucket is packed after
+    backward and all-reduced once, eagerly, between the two captured graphs;
+  * the step (forward + backward [+ exchange] + AdamW) is captured into
+    hipGraphs after warm-up, so the Python launch overhead is paid once;
   * epoch-end AUROC over the all-gathered probabilities (metrics.py).
 """
 from __future__ import annotations
@@ -24,6 +33,13 @@ def dist_env():
     """(rank, local_rank, world) from the torchrun environment (1-process defaults)."""
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
             int(os.environ.get("WORLD_SIZE", 1)))
+
+
+# a comm stream forked from the concurrent DCE encoder stream during capture
+# (a fork of a fork): torch 2.10 + HIP 7 crash at capture end on such a
+# topology with aten kernels on the nested stream (tools/capture_fork_probe.py),
+# so by default those segments are launched after backward instead
+NESTED_FORK_OK = os.environ.get("DMF_DP_NESTED_FORK", "0") == "1"
 
 
 def rank_strided_indices(n_items, rank, world, epoch=0, shuffle=False, seed=0):
@@ -80,10 +96,22 @@ class FusionTrainer:
     batch -- capture restores the training state its warm-up steps touched, so
     it never advances training."""
 
-    def __init__(self, lm, world=1, use_graph=True):
+    def __init__(self, lm, world=1, use_graph=True, overlap=None, bucket_mb=None):
         self.lm = lm
         self.world = world
         self.use_graph = use_graph
+        if overlap is None:
+            overlap = world > 1 and dist.is_initialized() and dist.get_backend() == "nccl"
+        # overlap=True with world=1 runs the same hooks / segments / captured
+        # collectives over a 1-rank communicator (the single-GPU test of the path)
+        self.overlap = bool(overlap)
+        mb = bucket_mb if bucket_mb is not None else float(os.environ.get("DMF_DP_BUCKET_MB", "32"))
+        self.segment_bytes = int(mb * (1 << 20))
+        self._hooks = []
+        self._ready_order = []
+        self._armed = False
+        self._comm = None
+        self._rccl = None
         cfg = lm.configure_optimizers()
         self.opt = cfg["optimizer"] if isinstance(cfg, dict) else cfg
         self.lm.optimizer = self.opt
@@ -103,30 +131,120 @@ class FusionTrainer:
         groups = tuple(len(g["params"]) for g in self.opt.param_groups)
         return groups, tuple(id(p) for p in self._trainable()), self.opt.tables_version
 
+    # ------------------------------------------------- overlapped exchange
+    def _install_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self._trainable()]
+
+    def _on_grad(self, p):
+        if not self._armed:
+            return
+        if not self._bucket_ready:
+            # first step: learn the gradient-ready order and the stream each
+            # gradient is produced on (DWI / fusion: the step's stream; DCE:
+            # its concurrent encoder stream)
+            self._ready_order.append((p, torch.cuda.current_stream().cuda_stream))
+            return
+        k = self._seg_of.get(p)
+        if k is None:
+            return
+        self._pending[k] -= 1
+        if self._pending[k] == 0:
+            self._launch_segment(k)
+
+    def _launch_segment(self, k):
+        """pack + all_reduce segment k on the comm stream, forked from the
+        stream its last gradient was produced on. A gradient made on a side
+        stream (the concurrent DCE encoder) is deferred to the end of
+        backward while a graph is being captured: a fork from a forked stream
+        breaks capture end on this stack."""
+        cur = torch.cuda.current_stream()
+        if torch.cuda.is_current_stream_capturing() and cur != self._origin and not NESTED_FORK_OK:
+            self._deferred.append(k)
+            return
+        self._launched.add(k)
+        self._comm.wait_stream(cur)
+        with torch.cuda.stream(self._comm):
+            self.opt.pack_segment(k)
+            a, b = self.opt.segment_range(k)
+            self._rccl.all_reduce_sum_(self.opt.bucket[a:b])
+
+    def _begin_backward(self):
+        self._origin = torch.cuda.current_stream()
+        if self._comm is None:
+            from dmf_rccl import RcclComm
+            self._comm = torch.cuda.Stream(self._origin.device)
+            rank = dist.get_rank() if dist.is_initialized() else 0
+            self._rccl = RcclComm(rank, self.world, self._origin.device)
+        if self._bucket_ready:
+            self._pending = [len(s) for s in self.opt.segments]
+        self._launched, self._deferred = set(), []
+        self._armed = True
+
+    def _end_backward(self):
+        self._armed = False
+        if not self._bucket_ready or self._bucket_sig != self._signature()[:2]:
+            self._setup_bucket()
+        # segments whose params got no gradient this step, and deferred ones
+        for k in range(len(self.opt.segments)):
+            if k not in self._launched:
+                self._launch_segment(k)
+        self._origin.wait_stream(self._comm)
+
     # ---------------------------------------------------------- eager step
     def _fwd_bwd(self, batch):
         self.opt.zero_grad(set_to_none=False)
         loss = self.lm.training_step(batch)
-        loss.backward()
+        if self.overlap:
+            self._begin_backward()
+            loss.backward()
+            self._end_backward()
+        else:
+            loss.backward()
         return loss
 
     def _exchange_and_update(self):
-        if self.world > 1:
+        if self.world > 1 and not self.overlap:
             self.opt.pack_grads()
             allreduce_mean_(self.opt.bucket, self.world)
         self.opt.step()
 
     def _setup_bucket(self):
         params = [p for p in self._trainable() if p.grad is not None]
-        if self.world > 1:
+        if self.overlap and self._ready_order:
+            # gradient-ready order (what backward produced first is reduced
+            # first), one run per producing stream: a segment never mixes
+            # gradients of two concurrent streams, so it is launched from the
+            # stream that made all of its gradients; anything not seen last
+            runs = {}
+            for p, sid in self._ready_order:
+                if p.grad is not None and p.requires_grad:
+                    runs.setdefault(sid, []).append(p)
+            seen = {id(p) for p, _ in self._ready_order}
+            params = [p for run in runs.values() for p in run] + [p for p in params if id(p) not in seen]
+            cuts = []
+            n = 0
+            for run in runs.values():
+                n += len(run)
+                cuts.append(n)
+        if self.world > 1 or self.overlap:
             self.opt.use_bucket_grads(False)
             if params:
-                self.opt.make_bucket(params)
+                self.opt.make_bucket(params, self.segment_bytes if self.overlap else None,
+                                     cuts if self.overlap and self._ready_order else None)
                 self.opt.use_bucket_grads(True, 1.0 / self.world)
+                if self.overlap:
+                    self._seg_of = {p: k for k, seg in enumerate(self.opt.segments)
+                                    for i in seg for p in (self.opt._bucket_params[i],)}
         self._bucket_ready = True
         self._bucket_sig = self._signature()[:2]
 
     def eager_step(self, batch):
+        if self.overlap and (not self._hooks or self._bucket_sig != self._signature()[:2]):
+            self._install_hooks()
+            self._bucket_ready = False
+            self._ready_order = []
         loss = self._fwd_bwd(batch)
         if not self._bucket_ready or self._bucket_sig != self._signature()[:2]:
             self._setup_bucket()
@@ -179,11 +297,13 @@ class FusionTrainer:
 
     # ----------------------------------------------------------- graphs
     def capture(self, batch):
-        """Capture fwd+bwd(+pack) and the update as hipGraphs; the RCCL
-        all-reduce between them stays eager (one collective per step). The
-        two eager warm-up steps (allocator pools, weight caches, optimizer
-        tables) are undone afterwards, so capture leaves the parameters,
-        buffers, optimizer state, RNG and global_step as it found them."""
+        """Capture fwd+bwd(+pack) and the update as hipGraphs. With overlap
+        the segment all-reduces are inside the first graph; otherwise (gloo)
+        the one all-reduce stays eager between the two. The two eager
+        warm-up steps (allocator pools, weight caches, optimizer and pack
+        tables, the gradient-ready order) are undone afterwards, so capture
+        leaves the parameters, buffers, optimizer state, RNG and global_step
+        as it found them."""
         self.static_batch = tuple(t.clone() for t in batch)
         torch.cuda.synchronize()
         snap = self._snapshot()
@@ -197,7 +317,7 @@ class FusionTrainer:
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             self.loss = self._fwd_bwd(self.static_batch)
-            if self.world > 1:
+            if self.world > 1 and not self.overlap:
                 self.opt.pack_grads()
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
@@ -227,7 +347,7 @@ class FusionTrainer:
         self.opt.sync_hyper()  # scheduler lr / wd changes -> the captured hyper table (same storage)
         g1, g2 = self.graphs
         g1.replay()
-        if self.world > 1:
+        if self.world > 1 and not self.overlap:
             allreduce_mean_(self.opt.bucket, self.world)
         g2.replay()
         self.lm.global_step += 1

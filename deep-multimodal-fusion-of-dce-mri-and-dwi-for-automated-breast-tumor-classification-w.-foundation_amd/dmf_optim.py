@@ -211,9 +211,15 @@ class FusedAdamW(torch.optim.Optimizer):
         self.tables_version += 1
 
     # ----------------------------------------------------- flat grad bucket
-    def make_bucket(self, params):
+    def make_bucket(self, params, segment_bytes=None, cuts=None):
         """Allocate ONE fp32 bucket laid out over ``params`` (the ones that
-        receive gradients); returns it. Use ``pack_grads`` after backward."""
+        receive gradients, in the order given); returns it. With
+        ``segment_bytes`` the bucket is also cut into contiguous segments of
+        about that size (``segments``: lists of param indices) that
+        ``pack_segment`` fills one at a time -- the data-parallel driver
+        all-reduces each as soon as its gradients are complete; ``cuts``
+        (param counts) force segment boundaries. Use ``pack_grads`` (all of
+        it) or ``pack_segment`` after backward."""
         self._bucket_params = list(params)
         self._bucket_offsets = {}
         off = 0
@@ -222,20 +228,42 @@ class FusedAdamW(torch.optim.Optimizer):
             off += p.numel()
         dev = self._bucket_params[0].device
         self.bucket = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.segments, cur, size = [], [], 0
+        limit = segment_bytes if segment_bytes else float("inf")
+        cuts = set(cuts or ())
+        for i, p in enumerate(self._bucket_params):
+            cur.append(i)
+            size += 4 * p.numel()
+            if size >= limit or (i + 1) in cuts:
+                self.segments.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.segments.append(cur)
         self._pack_key = None
+        self._seg_tables = {}
         return self.bucket
 
-    @torch.no_grad()
-    def pack_grads(self):
-        """bucket <- concat(p.grad) in one launch."""
+    def segment_range(self, k):
+        """(start, end) element range of segment k inside the bucket."""
+        idx = self.segments[k]
+        first, last = self._bucket_params[idx[0]], self._bucket_params[idx[-1]]
+        return self._bucket_offsets[first], self._bucket_offsets[last] + last.numel()
+
+    def _pack_tables(self, idx):
         pairs, chunks = [], []
-        for t, p in enumerate(self._bucket_params):
+        for t, i in enumerate(idx):
+            p = self._bucket_params[i]
             if p.grad is None:
                 raise RuntimeError("pack_grads: a bucket parameter has no gradient")
             pairs.append([p.grad.data_ptr(), self.bucket.data_ptr() + 4 * self._bucket_offsets[p]])
             for b in range(0, p.numel(), CHUNK):
                 chunks.append([t, b, min(p.numel(), b + CHUNK)])
-        key = tuple(x[0] for x in pairs)
+        return tuple(x[0] for x in pairs), pairs, chunks
+
+    @torch.no_grad()
+    def pack_grads(self):
+        """bucket <- concat(p.grad) in one launch."""
+        key, pairs, chunks = self._pack_tables(range(len(self._bucket_params)))
         if key != self._pack_key:
             dev = self.bucket.device
             self._pk_pairs = torch.tensor(pairs, dtype=torch.int64, device=dev)
@@ -243,6 +271,20 @@ class FusedAdamW(torch.optim.Optimizer):
             self._pack_key = key
         N.call("dmf_multi_copy", self._pk_chunks.shape[0], self._pk_chunks.data_ptr(), self._pk_pairs.data_ptr(), 1.0,
                N.stream_ptr())
+
+    @torch.no_grad()
+    def pack_segment(self, k):
+        """bucket[segment k] <- concat(p.grad of its params), one launch on
+        the current stream (the device tables are built once per grad layout,
+        outside any capture: call it eagerly once before capturing)."""
+        key, pairs, chunks = self._pack_tables(self.segments[k])
+        tab = self._seg_tables.get(k)
+        if tab is None or tab[0] != key:
+            dev = self.bucket.device
+            tab = (key, torch.tensor(pairs, dtype=torch.int64, device=dev),
+                   torch.tensor(chunks, dtype=torch.int64, device=dev))
+            self._seg_tables[k] = tab
+        N.call("dmf_multi_copy", tab[2].shape[0], tab[2].data_ptr(), tab[1].data_ptr(), 1.0, N.stream_ptr())
 
     def use_bucket_grads(self, enabled=True, scale=1.0):
         self.grad_source = self.bucket if enabled else None
