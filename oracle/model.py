@@ -121,6 +121,20 @@ class MaskHeadResize(nn.Module):
         return _conv(x, self.out)
 
 
+# Test hook: when a list, ResNetLiteBlock_withRecon's dropouts take their
+# (1/(1-p)-scaled) masks from it in call order instead of drawing -- the MC
+# "shared-mask" parity check feeds the build's Philox masks through here.
+DROPOUT_MASKS = None
+
+
+def _dropout(x, p, on):
+    if not on or p <= 0:
+        return x
+    if DROPOUT_MASKS is not None:
+        return x * DROPOUT_MASKS.pop(0).to(x.dtype)
+    return F.dropout(x, p, True)
+
+
 class ResNetLiteBlock_withRecon(nn.Module):
     """model_module.py:220-316 (2-D)."""
 
@@ -154,10 +168,12 @@ class ResNetLiteBlock_withRecon(nn.Module):
         ident = x if self.skip is None else _bn(_conv(x, self.skip[0]), self.skip[1])
         h = x
         for b in self.bottlenecks:
-            h = F.dropout(F.gelu(_bn(_conv(h, b[0]), b[1])), self.p, self.training)
+            # the nn.Dropout modules' own flags, as the reference's
+            # nn.Sequential / self.dropout calls (MC dropout turns on only them)
+            h = _dropout(F.gelu(_bn(_conv(h, b[0]), b[1])), self.p, b[3].training)
             h = F.gelu(_bn(_conv(h, b[4]), b[5]))
             h = _bn(_conv(h, b[7]), b[8])
-        h = F.dropout(F.gelu(h + ident), self.p, self.training)
+        h = _dropout(F.gelu(h + ident), self.p, self.dropout.training)
         if self.se is not None:
             h, _ = self.se(h)
         r = self.reconstruct(h) if self.reconstruct is not None else None
