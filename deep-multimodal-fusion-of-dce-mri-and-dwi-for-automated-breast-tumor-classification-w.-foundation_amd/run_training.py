@@ -62,13 +62,51 @@ def read_checkpoint(path, map_location="cpu"):
         raise RuntimeError(f"{path}: not loadable with weights_only=True ({e})") from e
 
 
+# The reference's encoders are Lightning-wrapped twice (quirk Q2:
+# prepare_single_model.py:198-206 returns a LightningSingleModel that
+# run_training.py:66-74 wraps again; the fusion run then holds that
+# double-wrapped module as dwi_model / dce_model). Its checkpoints therefore
+# key an encoder as ``model.model.<encoder>`` (single run) or
+# ``dwi_model.model.model.<encoder>`` (fusion run); the build holds the
+# encoder directly (``model.<encoder>`` / ``dwi_model.<encoder>``). A module
+# compiled as a whole (parameters["compile"], run_training.py:90-91, :239-241)
+# adds a leading ``_orig_mod.``.
+REFERENCE_KEY_PREFIXES = (
+    ("dwi_model.model.model.", "dwi_model."), ("dce_model.model.model.", "dce_model."),
+    ("dwi_model.model.", "dwi_model."), ("dce_model.model.", "dce_model."),
+    ("model.model.", "model."),
+)
+
+
+def to_build_keys(state_dict, build_keys):
+    """Map a reference-layout state_dict onto the build's key names (keys the
+    build already has are kept as they are); returns a new dict."""
+    build_keys = set(build_keys)
+    out = {}
+    for k, v in state_dict.items():
+        if k.startswith("_orig_mod.") and k not in build_keys:
+            k = k[len("_orig_mod."):]
+        if k not in build_keys:
+            for src, dst in REFERENCE_KEY_PREFIXES:
+                if k.startswith(src) and dst + k[len(src):] in build_keys:
+                    k = dst + k[len(src):]
+                    break
+        if k in out:
+            raise RuntimeError(f"checkpoint maps two entries onto {k!r}")
+        out[k] = v
+    return out
+
+
 def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", strict=True, **kwargs):
     """``cls.load_from_checkpoint(path, **init_kwargs)`` (run_training.py:123-131):
     build ``cls(**kwargs)``, load the checkpoint's state_dict, restore epoch /
-    global_step. Raises RuntimeError on missing / unexpected keys when strict."""
+    global_step. Checkpoints written by the reference (doubly wrapped
+    encoders, see REFERENCE_KEY_PREFIXES) load as well as the build's own.
+    Raises RuntimeError on missing / unexpected keys when strict."""
     ckpt = read_checkpoint(checkpoint_path, map_location)
     sd = ckpt["state_dict"] if isinstance(ckpt, dict) and "state_dict" in ckpt else ckpt
     module = cls(**kwargs)
+    sd = to_build_keys(sd, module.state_dict().keys())
     res = module.load_state_dict(sd, strict=strict)
     module.current_epoch = int(ckpt.get("epoch", 0)) if isinstance(ckpt, dict) else 0
     module.global_step = int(ckpt.get("global_step", 0)) if isinstance(ckpt, dict) else 0

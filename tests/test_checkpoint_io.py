@@ -6,6 +6,7 @@ modules, the reference's state_dict key layout (including the duplicate
 the legacy model-dict file and the metrics JSON schema."""
 import copy
 import json
+import os
 
 import numpy as np
 import pytest
@@ -93,6 +94,52 @@ def test_fusion_ckpt_and_model_dict(tmp_path):
     assert sorted(loaded) == ["dce_0", "dce_1", "dwi_0", "dwi_1", "fusion_0", "fusion_1"]
     for k, v in fm.state_dict().items():
         assert torch.equal(loaded["fusion_0"][k], v)
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _ref_layout_modules():
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0, use_backbone=False))
+    dwi = MM.ModelMaskHeadBackbone("dwi", P, None)
+    dce = MM.ModelMaskHeadBackbone("dce", P, None)
+    fm = MM.FusionModel(P)
+    crit = get_classification_loss(P, torch.arange(64) % 4, "fusion", "cpu")
+    return P, dict(dwi_model=dwi, dce_model=dce, fusion_model=fm, parameters_dict=P, criterion_clf=crit)
+
+
+def test_reference_layout_fusion_ckpt_loads_strictly(tmp_path):
+    """tests/golden/fusion_reference_layout.ckpt is keyed the way the
+    REFERENCE's fusion run writes it (doubly wrapped encoders,
+    dwi_model.model.model.*; quirk Q2, run_training.py:66-74, :123-131;
+    made by tools/make_golden.py from the oracle). It must load strictly --
+    every key mapped, none left over -- with epoch / global_step restored."""
+    path = os.path.join(GOLDEN, "fusion_reference_layout.ckpt")
+    ck = RT.read_checkpoint(path)
+    assert any(k.startswith("dwi_model.model.model.") for k in ck["state_dict"])
+    _, kw = _ref_layout_modules()
+    got = TF.LightningFusionModel.load_from_checkpoint(path, **kw)
+    assert got.current_epoch == 17 and got.global_step == 544
+    own = got.state_dict()
+    for k, v in ck["state_dict"].items():
+        kk = k.replace("_model.model.model.", "_model.")
+        assert torch.equal(own[kk], v), k
+    # a single-model ckpt in the reference's doubly wrapped layout (model.model.*)
+    P, _ = _ref_layout_modules()
+    enc = MM.ModelMaskHeadBackbone("dwi", P, None)
+    sd = {"model.model." + k: v for k, v in got.dwi_model.state_dict().items()}
+    p1 = str(tmp_path / "ref_layout_single.ckpt")
+    torch.save({"state_dict": sd, "epoch": 2, "global_step": 5}, p1)
+    lm = TR.LightningSingleModel.load_from_checkpoint(p1, model=enc, method="dwi", parameters_dict=P)
+    for k, v in got.dwi_model.state_dict().items():
+        assert torch.equal(lm.model.state_dict()[k], v), k
+    # keys that match nothing still fail loudly
+    bad = dict(sd)
+    bad["model.model.not_a_layer.weight"] = torch.zeros(1)
+    torch.save({"state_dict": bad}, p1)
+    with pytest.raises(RuntimeError):
+        TR.LightningSingleModel.load_from_checkpoint(p1, model=MM.ModelMaskHeadBackbone("dwi", P, None),
+                                                     method="dwi", parameters_dict=P)
 
 
 def test_metrics_json_schema(tmp_path):

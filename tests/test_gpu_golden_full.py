@@ -245,3 +245,32 @@ def test_mode_b_bf16_full_width_step_vs_oracle():
     assert lrel < 3e-2
     for k in g_amp:
         assert g_hip[k] <= 1.25 * g_amp[k] + 0.01, (k, g_hip[k], g_amp[k])
+
+
+def test_reference_layout_ckpt_forward_matches_fixture():
+    """The fusion .ckpt in the reference's doubly wrapped key layout
+    (tests/golden/fusion_reference_layout.ckpt, quirk Q2) loaded strictly into
+    the build, f32 parity mode, eval: logits and fused mask equal the
+    oracle's outputs stored beside it (fusion_reference_layout.npz)."""
+    import copy
+
+    import make_golden as MG
+    import model_module as MM
+    import parameters as PR
+    import train_fusion as TF
+    from selector_helpers import get_classification_loss
+
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0, use_backbone=False))
+    kw = dict(dwi_model=MM.ModelMaskHeadBackbone("dwi", P, None), dce_model=MM.ModelMaskHeadBackbone("dce", P, None),
+              fusion_model=MM.FusionModel(P), parameters_dict=P,
+              criterion_clf=get_classification_loss(P, torch.arange(64) % 4, "fusion", "cpu"))
+    lm = TF.LightningFusionModel.load_from_checkpoint(os.path.join(GOLD, "fusion_reference_layout.ckpt"), **kw)
+    for m in (lm.dwi_model, lm.dce_model, lm.fusion_model):
+        MM.set_compute_dtype(m, torch.float32)
+    lm = lm.to(DEV).eval()
+    want = np.load(os.path.join(GOLD, "fusion_reference_layout.npz"))
+    dwi, dce, _, _ = MG.volume_batch(2, 64, 91)
+    with torch.no_grad():
+        logits, fmask, _ = lm.forward_from_inputs(dwi.to(DEV), dce.to(DEV))
+    assert np.abs(logits.float().cpu().numpy() - want["logits"]).max() <= 1e-4
+    assert np.abs(fmask.float().cpu().numpy() - want["fused_mask"]).max() <= 1e-4 * max(1, np.abs(want["fused_mask"]).max())

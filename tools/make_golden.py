@@ -9,7 +9,7 @@ they do NOT pin the reference ("parity unpinned").
 Weights are not stored: each fixture records the seed recipe the tests
 re-run (product-side seeded construction, state_dict loaded into the oracle).
 
-    python tools/make_golden.py [small] [full]
+    python tools/make_golden.py [small] [full] [ckpt]
 """
 import copy
 import os
@@ -243,6 +243,44 @@ def resnet_maps_fixture():
     return out
 
 
+def reference_layout_ckpt_fixture():
+    """A fusion .ckpt in the layout the REFERENCE writes (quirk Q2,
+    run_training.py:66-74 / :123-131 / :175, ModelCheckpoint :93-99): the
+    encoders are doubly Lightning-wrapped, so their keys read
+    ``dwi_model.model.model.<encoder>``; fusion keys ``fusion_model.<...>``;
+    Lightning 2.x top-level entries. No-backbone encoders (config 1 widths
+    16/32/64) keep the file small. Returns (ckpt dict, expected-output npz
+    dict): the oracle's eval-mode logits / fused mask on volume_batch(2,64,91)."""
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0, use_backbone=False))
+    encs = {}
+    for name, cin, seed in (("dwi", 14, 61), ("dce", 6, 62)):
+        torch.manual_seed(seed)
+        enc = MM.initialize_model(MM.ModelMaskHeadBackbone(name, P, None), True)
+        ref = OM.ModelMaskHeadBackbone(name, P, None)
+        ref.load_state_dict(enc.state_dict())
+        encs[name] = ref
+    _, fr = seeded_fusion(P, 63)
+    sd = {}
+    for name in ("dwi", "dce"):
+        for k, v in encs[name].state_dict().items():
+            sd[f"{name}_model.model.model.{k}"] = v.clone()
+    for k, v in fr.state_dict().items():
+        sd[f"fusion_model.{k}"] = v.clone()
+    ckpt = {"epoch": 17, "global_step": 544, "pytorch-lightning_version": "2.5.1", "state_dict": sd,
+            "loops": {}, "callbacks": {}, "optimizer_states": [], "lr_schedulers": []}
+    dwi, dce, _, _ = volume_batch(2, 64, 91)
+    for m in (encs["dwi"], encs["dce"], fr):
+        m.eval()
+    with torch.no_grad():
+        _, aux_d, mp_d = encs["dwi"](dwi)
+        _, aux_c, mp_c = encs["dce"](dce)
+        logits, fmask, _ = fr(aux_d["raw_feats"], aux_c["raw_feats"], mp_d, mp_c)
+    out = {"recipe": np.array("small_parameters(dropout=0, use_backbone=False); dwi seed 61, dce seed 62 "
+                              "(initialize_model), fusion seed 63; eval; batch volume_batch(2,64,91)"),
+           "logits": logits.numpy(), "fused_mask": fmask.numpy()}
+    return ckpt, out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -251,6 +289,10 @@ def main():
         np.savez_compressed(os.path.join(OUT, "losses.npz"), **losses_fixture())
         np.savez_compressed(os.path.join(OUT, "encoder_small.npz"), **encoder_fixture())
         np.savez_compressed(os.path.join(OUT, "fusion_step_small.npz"), **step_fixture())
+    if "ckpt" in which or "small" in which:
+        ckpt, out = reference_layout_ckpt_fixture()
+        torch.save(ckpt, os.path.join(OUT, "fusion_reference_layout.ckpt"))
+        np.savez_compressed(os.path.join(OUT, "fusion_reference_layout.npz"), **out)
     if "full" in which:
         np.savez_compressed(os.path.join(OUT, "config3_forward.npz"), **config3_forward_fixture())
         np.savez_compressed(os.path.join(OUT, "config3_adamw_step.npz"), **config3_adamw_fixture())
