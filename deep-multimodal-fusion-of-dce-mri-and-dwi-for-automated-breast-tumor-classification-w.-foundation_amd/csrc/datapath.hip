@@ -8,6 +8,12 @@
 //   preprocess_adc          preprocess_helpers.py:39-49    log1p(max(adc, 0)) -> clip [0, 3e-3] / 3e-3
 //   NyulStandardizer        preprocess_helpers.py:52-120   per-image percentiles (numpy 'linear')
 //                                               at the landmarks, then np.interp twice
+//   train augmentation      prepare_single_model.py:107-113  torchvision RandomAffine(90, (0.1, 0.1),
+//                                               (0.1, 0.1)) -> RandomHorizontalFlip -> RandomVerticalFlip
+//                                               as ONE nearest-neighbour gather per output pixel (the
+//                                               per-volume parameters drawn on the host in torchvision's
+//                                               order), then Resize (bilinear, antialias) as two
+//                                               separable passes (W then H, as aten's upsample_*_aa)
 // Percentiles are exact order statistics: a multi-target radix select over
 // the order-preserving uint32 image of the float keys (4 passes of 8-bit
 // digits, one 256-bin LDS histogram per target rank), one block per
@@ -208,6 +214,83 @@ __global__ void __launch_bounds__(256) k_nyul_apply(const float* __restrict__ x,
   }
 }
 
+// ------------------------------------------------------------ augmentation
+// torchvision F.affine on a tensor (inverse matrix m[6] in centred pixel
+// coordinates, _get_inverse_affine_matrix) = grid_sample(nearest, zeros,
+// align_corners=False) of the grid that _gen_affine_grid builds; then the
+// flips (applied AFTER the affine: out(i, j) = affine(i', j') with i' / j'
+// mirrored). The float32 operation order follows torch's: base grid
+// (j - W/2 + 0.5, i - H/2 + 0.5, 1) times theta^T / (W/2, H/2) (bmm, k = 0..2),
+// unnormalise ((g + 1) * W - 1) / 2, round half to even (nearbyint).
+// params[n] = {m0..m5, hflip, vflip}. One thread per output pixel, all
+// channels (NCHW planes).
+__global__ void __launch_bounds__(256) k_affine_flip(const float* __restrict__ x, int C, int H, int W,
+                                                     const float* __restrict__ params, float* __restrict__ y) {
+  const int n = blockIdx.y;
+  const long long HW = (long long)H * W;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= HW) return;
+  const float* pm = params + n * 8;
+  int i = (int)(pix / W), j = (int)(pix - (long long)i * W);
+  if (pm[7] != 0.f) i = H - 1 - i;
+  if (pm[6] != 0.f) j = W - 1 - j;
+  const float hw = __fmul_rn(0.5f, (float)W), hh = __fmul_rn(0.5f, (float)H);
+  const float bx = __fadd_rn(__fadd_rn((float)j, -__fmul_rn((float)W, 0.5f)), 0.5f);
+  const float by = __fadd_rn(__fadd_rn((float)i, -__fmul_rn((float)H, 0.5f)), 0.5f);
+  const float t00 = __fdiv_rn(pm[0], hw), t10 = __fdiv_rn(pm[1], hw), t20 = __fdiv_rn(pm[2], hw);
+  const float t01 = __fdiv_rn(pm[3], hh), t11 = __fdiv_rn(pm[4], hh), t21 = __fdiv_rn(pm[5], hh);
+  const float gx = __fadd_rn(__fadd_rn(__fmul_rn(bx, t00), __fmul_rn(by, t10)), t20);
+  const float gy = __fadd_rn(__fadd_rn(__fmul_rn(bx, t01), __fmul_rn(by, t11)), t21);
+  const float ix = __fdiv_rn(__fadd_rn(__fmul_rn(__fadd_rn(gx, 1.f), (float)W), -1.f), 2.f);
+  const float iy = __fdiv_rn(__fadd_rn(__fmul_rn(__fadd_rn(gy, 1.f), (float)H), -1.f), 2.f);
+  const float rx = rintf(ix), ry = rintf(iy);
+  const bool in = rx >= 0.f && rx < (float)W && ry >= 0.f && ry < (float)H;
+  const long long src = in ? (long long)ry * W + (long long)rx : 0;
+  const float* xp = x + (long long)n * C * HW;
+  float* yp = y + (long long)n * C * HW + pix;
+  for (int c = 0; c < C; ++c) yp[c * HW] = in ? xp[c * HW + src] : 0.f;
+}
+
+// Resize, bilinear with antialias (aten _upsample_bilinear2d_aa, the kernel
+// torchvision's tensor Resize runs): per output index o along one axis,
+// scale = in/out, support = scale >= 1 ? scale : 1, centre = scale * (o + 0.5),
+// window [max(int(centre - support + 0.5), 0), min(int(centre + support + 0.5), in)),
+// triangle weights on (k + xmin - centre + 0.5) / max(scale, 1), normalised.
+// axis 0: along W (rows of length Win -> Wout), axis 1: along H.
+__device__ __forceinline__ float aa_tri(float v) {
+  v = fabsf(v);
+  return v < 1.f ? 1.f - v : 0.f;
+}
+
+__global__ void __launch_bounds__(256) k_resize_aa(const float* __restrict__ x, long long planes, int Hin, int Win,
+                                                   int Hout, int Wout, int axis, float* __restrict__ y) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long per = (long long)Hout * Wout;
+  if (idx >= planes * per) return;
+  const long long pl = idx / per;
+  const int r = (int)(idx - pl * per);
+  const int oi = r / Wout, oj = r - (r / Wout) * Wout;
+  const int in_size = axis == 0 ? Win : Hin, out_size = axis == 0 ? Wout : Hout, o = axis == 0 ? oj : oi;
+  const float scale = (float)in_size / (float)out_size;
+  const float support = scale >= 1.f ? scale : 1.f;
+  const float invscale = scale >= 1.f ? 1.f / scale : 1.f;
+  const float centre = scale * ((float)o + 0.5f);
+  int xmin = (int)(centre - support + 0.5f);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(centre + support + 0.5f);
+  if (xmax > in_size) xmax = in_size;
+  float tot = 0.f;
+  for (int k = xmin; k < xmax; ++k) tot += aa_tri(((float)(k - xmin) + (float)xmin - centre + 0.5f) * invscale);
+  const float* xp = x + pl * (long long)Hin * Win;
+  float acc = 0.f;
+  for (int k = xmin; k < xmax; ++k) {
+    float w = aa_tri(((float)(k - xmin) + (float)xmin - centre + 0.5f) * invscale);
+    if (tot != 0.f) w /= tot;
+    acc += w * (axis == 0 ? xp[(long long)oi * Win + k] : xp[(long long)k * Win + oj]);
+  }
+  y[idx] = acc;
+}
+
 }  // namespace dmf
 
 using namespace dmf;
@@ -260,5 +343,44 @@ extern "C" int dmf_nyul_apply(const float* x, int planes, int C, long long HW, c
   hipLaunchKernelGGL(k_nyul_apply, dim3((unsigned)gx, planes), dim3(256), 0, (hipStream_t)stream, x, HW, C, perc, avg,
                      scale, L, y);
   DMF_LAUNCH_CHECK("dmf_nyul_apply");
+  return 0;
+}
+
+extern "C" int dmf_affine_flip(const float* x, int N, int C, int H, int W, const float* params, float* y,
+                               void* stream) {
+  DMF_CHECK_ARG(x && params && y && N > 0 && C > 0 && H > 0 && W > 0 && N < 65536, "dmf_affine_flip: bad args");
+  DMF_CHECK_ARG(x != y, "dmf_affine_flip: in-place is not supported (the gather reads arbitrary source pixels)");
+  const long long HW = (long long)H * W;
+  hipLaunchKernelGGL(k_affine_flip, dim3((unsigned)((HW + 255) / 256), (unsigned)N), dim3(256), 0,
+                     (hipStream_t)stream, x, C, H, W, params, y);
+  DMF_LAUNCH_CHECK("dmf_affine_flip");
+  return 0;
+}
+
+extern "C" int dmf_resize_aa(const float* x, long long planes, int Hin, int Win, int Hout, int Wout, float* tmp,
+                             float* y, void* stream) {
+  DMF_CHECK_ARG(x && y && planes > 0 && Hin > 0 && Win > 0 && Hout > 0 && Wout > 0, "dmf_resize_aa: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const float* cur = x;
+  int h = Hin, w = Win;
+  if (Wout != Win) {  // horizontal pass first (aten order), into tmp unless it is the only pass
+    float* dst = Hout != Hin ? tmp : y;
+    DMF_CHECK_ARG(dst, "dmf_resize_aa: a two-pass resize needs tmp [planes][Hin][Wout]");
+    const long long tot = planes * (long long)Hin * Wout;
+    hipLaunchKernelGGL(k_resize_aa, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, cur, planes, Hin, Win, Hin,
+                       Wout, 0, dst);
+    cur = dst;
+    w = Wout;
+  }
+  if (Hout != Hin) {
+    const long long tot = planes * (long long)Hout * w;
+    hipLaunchKernelGGL(k_resize_aa, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, cur, planes, h, w, Hout,
+                       w, 1, y);
+  } else if (Wout == Win) {
+    DMF_CHECK_ARG(hipMemcpyAsync(y, x, planes * (long long)Hin * Win * sizeof(float), hipMemcpyDeviceToDevice, st) ==
+                      hipSuccess,
+                  "dmf_resize_aa: copy failed");
+  }
+  DMF_LAUNCH_CHECK("dmf_resize_aa");
   return 0;
 }

@@ -437,6 +437,17 @@ int dmf_plane_percentiles(const float* vals, int T, const int* lo_idx, const int
                           int planes, double* perc, void* stream);
 int dmf_nyul_apply(const float* x, int planes, int C, long long HW, const double* perc, const double* avg,
                    const double* scale, int L, float* y, void* stream);
+/* training augmentation (prepare_single_model.py:107-113), NCHW f32:
+ * dmf_affine_flip: torchvision RandomAffine (nearest, fill 0) then the
+ *   horizontal / vertical flips, one gather; params [N][8] per volume =
+ *   the inverse affine matrix m0..m5 (_get_inverse_affine_matrix, centred
+ *   pixel coordinates), hflip, vflip (0 / 1). y must not alias x.
+ * dmf_resize_aa: Resize (bilinear, antialias; aten _upsample_bilinear2d_aa)
+ *   of [planes][Hin][Win] -> [planes][Hout][Wout], W pass then H pass; tmp
+ *   [planes][Hin][Wout] when both axes change. */
+int dmf_affine_flip(const float* x, int N, int C, int H, int W, const float* params, float* y, void* stream);
+int dmf_resize_aa(const float* x, long long planes, int Hin, int Win, int Hout, int Wout, float* tmp, float* y,
+                  void* stream);
 
 /* ------------------------------------------------------------ optimizer
  * torch.optim.AdamW as built by LightningFusionOptimizerFactory
