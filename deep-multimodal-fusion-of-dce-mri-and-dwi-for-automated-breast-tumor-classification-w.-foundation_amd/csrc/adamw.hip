@@ -3,6 +3,11 @@
 // 632-685 / _get_base_optimizer :617-629) in ONE launch over a chunk table,
 // plus a multi-tensor copy used to pack/unpack gradient buckets for the
 // RCCL all-reduce. Step counts live on the device (graph-replay safe).
+// Dynamic loss scaling ("16-mixed": torch.amp.GradScaler, as Lightning runs
+// it): amp = {scale, found_inf} on the device; a non-finite check over the
+// gradients sets found_inf, the update then skips every tensor (and the
+// step counters) and unscales by 1/scale inside the same pass, and
+// k_amp_update applies _amp_update_scale_'s growth / backoff rule.
 //   p <- p * (1 - lr*wd); m <- m + (1-b1)(g-m); v <- b2 v + (1-b2) g^2
 //   p <- p - lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
 #include "dmf_common.h"
@@ -12,7 +17,12 @@ namespace dmf {
 
 // tensors: [T][6] int64 = p, g, m, v, group, numel ; chunks: [n][3] = tensor, begin, end
 __global__ void k_adamw(const long long* __restrict__ chunks, const long long* __restrict__ tensors,
-                        const float* __restrict__ hyper, const int* __restrict__ steps, float gscale) {
+                        const float* __restrict__ hyper, const int* __restrict__ steps, float gscale,
+                        const float* __restrict__ amp) {
+  if (amp) {
+    if (amp[1] != 0.f) return;  // found_inf: the whole step is skipped
+    gscale = gscale / amp[0];
+  }
   const long long* ch = chunks + 3 * blockIdx.x;
   const int t = (int)ch[0];
   const long long b = ch[1], e = ch[2];
@@ -43,9 +53,43 @@ __global__ void k_adamw(const long long* __restrict__ chunks, const long long* _
   }
 }
 
-__global__ void k_steps_inc(int* steps, int n) {
+__global__ void k_steps_inc(int* steps, int n, const float* __restrict__ amp) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (amp && amp[1] != 0.f) return;
   if (i < n) steps[i] += 1;
+}
+
+// found_inf (amp[1]) <- 1 if any gradient element of the table is inf / nan
+// (torch._amp_foreach_non_finite_check_and_unscale_'s test; the unscale
+// itself is folded into k_adamw). Benign race: every writer stores 1.
+__global__ void k_amp_nonfinite(const long long* __restrict__ chunks, const long long* __restrict__ tensors,
+                                float* __restrict__ amp) {
+  const long long* ch = chunks + 3 * blockIdx.x;
+  const float* g = (const float*)tensors[6 * ch[0] + 1];
+  bool bad = false;
+  for (long long i = ch[1] + threadIdx.x; i < ch[2]; i += blockDim.x) bad |= !isfinite(g[i]);
+  const bool wave_bad = __any(bad);
+  if (wave_bad && (threadIdx.x & 63) == 0) amp[1] = 1.f;
+}
+
+// torch._amp_update_scale_: found_inf -> scale *= backoff, tracker = 0;
+// else tracker += 1 and, at growth_interval, scale *= growth (if finite), tracker = 0.
+__global__ void k_amp_update(float* amp, int* tracker, float growth, float backoff, int interval) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (amp[1] != 0.f) {
+    amp[0] *= backoff;
+    tracker[0] = 0;
+  } else {
+    const int t = tracker[0] + 1;
+    if (t == interval) {
+      const float ns = amp[0] * growth;
+      if (isfinite(ns)) amp[0] = ns;
+      tracker[0] = 0;
+    } else {
+      tracker[0] = t;
+    }
+  }
+  amp[1] = 0.f;  // ready for the next step's check
 }
 
 // pairs: [T][2] int64 = src, dst ; dst[i] = src[i] * scale
@@ -70,15 +114,44 @@ extern "C" int dmf_adamw_multi(int nchunks, const long long* chunks, const long 
   DMF_CHECK_ARG(nchunks >= 0 && chunks && tensors && hyper && steps, "dmf_adamw_multi: bad args");
   if (nchunks == 0) return 0;
   hipLaunchKernelGGL(k_adamw, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, chunks, tensors, hyper, steps,
-                     grad_scale);
+                     grad_scale, (const float*)nullptr);
   DMF_LAUNCH_CHECK("dmf_adamw_multi");
+  return 0;
+}
+
+extern "C" int dmf_adamw_multi_amp(int nchunks, const long long* chunks, const long long* tensors, const float* hyper,
+                                   int* steps, int nsteps, float grad_scale, const float* amp, void* stream) {
+  DMF_CHECK_ARG(nchunks >= 0 && chunks && tensors && hyper && steps && amp && nsteps >= 0,
+                "dmf_adamw_multi_amp: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (nsteps > 0) hipLaunchKernelGGL(k_steps_inc, dim3(cdiv(nsteps, 256)), dim3(256), 0, st, steps, nsteps, amp);
+  if (nchunks > 0)
+    hipLaunchKernelGGL(k_adamw, dim3(nchunks), dim3(256), 0, st, chunks, tensors, hyper, steps, grad_scale, amp);
+  DMF_LAUNCH_CHECK("dmf_adamw_multi_amp");
+  return 0;
+}
+
+extern "C" int dmf_amp_nonfinite(int nchunks, const long long* chunks, const long long* tensors, float* amp,
+                                 void* stream) {
+  DMF_CHECK_ARG(nchunks >= 0 && chunks && tensors && amp, "dmf_amp_nonfinite: bad args");
+  if (nchunks == 0) return 0;
+  hipLaunchKernelGGL(k_amp_nonfinite, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, chunks, tensors, amp);
+  DMF_LAUNCH_CHECK("dmf_amp_nonfinite");
+  return 0;
+}
+
+extern "C" int dmf_amp_update(float* amp, int* tracker, float growth, float backoff, int interval, void* stream) {
+  DMF_CHECK_ARG(amp && tracker && interval > 0, "dmf_amp_update: bad args");
+  hipLaunchKernelGGL(k_amp_update, dim3(1), dim3(64), 0, (hipStream_t)stream, amp, tracker, growth, backoff, interval);
+  DMF_LAUNCH_CHECK("dmf_amp_update");
   return 0;
 }
 
 extern "C" int dmf_steps_inc(int* steps, int n, void* stream) {
   DMF_CHECK_ARG(steps && n >= 0, "dmf_steps_inc: bad args");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_steps_inc, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, steps, n);
+  hipLaunchKernelGGL(k_steps_inc, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, steps, n,
+                     (const float*)nullptr);
   DMF_LAUNCH_CHECK("dmf_steps_inc");
   return 0;
 }

@@ -112,6 +112,12 @@ class FusionTrainer:
         self._armed = False
         self._comm = None
         self._rccl = None
+        # Lightning precision "16-mixed" (the reference's default,
+        # parameters_generate.py:211): dynamic loss scaling on the device
+        self.scaler = None
+        if lm.parameters_dict.get("precision") in ("16-mixed", "16"):
+            from dmf_optim import DeviceGradScaler
+            self.scaler = DeviceGradScaler(lm.device)
         cfg = lm.configure_optimizers()
         self.opt = cfg["optimizer"] if isinstance(cfg, dict) else cfg
         self.lm.optimizer = self.opt
@@ -196,19 +202,20 @@ class FusionTrainer:
     def _fwd_bwd(self, batch):
         self.opt.zero_grad(set_to_none=False)
         loss = self.lm.training_step(batch)
+        bwd = self.scaler.backward if self.scaler is not None else (lambda t: t.backward())
         if self.overlap:
             self._begin_backward()
-            loss.backward()
+            bwd(loss)
             self._end_backward()
         else:
-            loss.backward()
+            bwd(loss)
         return loss
 
     def _exchange_and_update(self):
         if self.world > 1 and not self.overlap:
             self.opt.pack_grads()
             allreduce_mean_(self.opt.bucket, self.world)
-        self.opt.step()
+        self.opt.step(scaler=self.scaler)
 
     def _setup_bucket(self):
         params = [p for p in self._trainable() if p.grad is not None]
@@ -266,7 +273,9 @@ class FusionTrainer:
                 "opt": {id(t): (t, t.clone()) for st in o.state.values() for t in st.values()
                         if torch.is_tensor(t) and t.is_cuda},
                 "steps": o._steps.clone() if o._steps is not None else None,
-                "rng": [(t, t.clone()) for t in O.RNG.states.values()],
+                "rng": [(t, t.clone()) for t in O.RNG.states.values()]
+                + ([(self.scaler.amp, self.scaler.amp.clone()), (self.scaler.tracker, self.scaler.tracker.clone())]
+                   if self.scaler is not None else []),
                 "global_step": self.lm.global_step}
 
     def _restore(self, snap):
@@ -321,7 +330,7 @@ class FusionTrainer:
                 self.opt.pack_grads()
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
-            self.opt.step()
+            self.opt.step(scaler=self.scaler)
         self.graphs = (g1, g2)
         self._restore(snap)
         torch.cuda.synchronize()

@@ -124,7 +124,12 @@ class FusedAdamW(torch.optim.Optimizer):
 
     # ---------------------------------------------------------------- step
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, scaler=None):
+        """One AdamW update of every live tensor. With ``scaler`` (a
+        DeviceGradScaler) the gradients are the scaled ones: a device-side
+        inf / nan check runs first and, on overflow, the update and the step
+        counters are skipped on the device; otherwise the update unscales by
+        1/scale; then the scale is updated (GradScaler.step + update)."""
         loss = closure() if closure is not None else None
         live = self._live()
         if not live:
@@ -141,6 +146,14 @@ class FusedAdamW(torch.optim.Optimizer):
         elif self._table_key is None:
             raise RuntimeError("run one eager optimizer step before capturing it in a graph")
         s = N.stream_ptr()
+        if scaler is not None and scaler.enabled:
+            N.call("dmf_amp_nonfinite", self._nchunks, self._chunks.data_ptr(), self._tensors.data_ptr(),
+                   scaler.amp.data_ptr(), s)
+            N.call("dmf_adamw_multi_amp", self._nchunks, self._chunks.data_ptr(), self._tensors.data_ptr(),
+                   self._hyper.data_ptr(), self._live_steps.data_ptr(), self._live_steps.numel(),
+                   float(self.grad_scale), scaler.amp.data_ptr(), s)
+            scaler.update()
+            return loss
         N.call("dmf_steps_inc", self._live_steps.data_ptr(), self._live_steps.numel(), s)
         N.call("dmf_adamw_multi", self._nchunks, self._chunks.data_ptr(), self._tensors.data_ptr(),
                self._hyper.data_ptr(), self._live_steps.data_ptr(), float(self.grad_scale), s)
@@ -290,3 +303,51 @@ class FusedAdamW(torch.optim.Optimizer):
         self.grad_source = self.bucket if enabled else None
         self.grad_scale = scale
         self._table_key = None if not enabled else self._table_key
+
+
+class DeviceGradScaler:
+    """torch.amp.GradScaler semantics for the captured step -- the reference
+    trains with Lightning precision "16-mixed" (parameters_generate.py:211),
+    i.e. autocast + GradScaler: the loss is scaled before backward, a step
+    whose gradients overflow is skipped and the scale backs off (x0.5), and
+    after ``growth_interval`` clean steps it grows (x2). Scale, growth tracker
+    and the found-inf flag live on the device (no host sync, graph-replay
+    safe): ``backward(loss)`` seeds autograd with the device scale,
+    FusedAdamW.step(scaler=...) checks, unscales inside the update and
+    updates the scale. The 16-bit MFMA type here is bf16 (fp32 range, so
+    overflow skips are rare); the protocol is the reference's."""
+
+    def __init__(self, device, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 enabled=True):
+        self.enabled = enabled
+        self.growth_factor, self.backoff_factor, self.growth_interval = growth_factor, backoff_factor, growth_interval
+        self.amp = torch.tensor([init_scale, 0.0], dtype=torch.float32, device=device)
+        self.tracker = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def backward(self, loss):
+        if not self.enabled:
+            return loss.backward()
+        if loss.dtype != torch.float32 or loss.dim() != 0:
+            raise ValueError("DeviceGradScaler.backward: needs a scalar float32 loss")
+        loss.backward(gradient=self.amp[0])
+
+    def update(self):
+        N.call("dmf_amp_update", self.amp.data_ptr(), self.tracker.data_ptr(), float(self.growth_factor),
+               float(self.backoff_factor), int(self.growth_interval), N.stream_ptr())
+
+    def get_scale(self):
+        return float(self.amp[0].item())
+
+    def state_dict(self):
+        """torch.amp.GradScaler.state_dict layout."""
+        return {"scale": self.get_scale(), "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
+                "growth_interval": self.growth_interval, "_growth_tracker": int(self.tracker.item())}
+
+    def load_state_dict(self, sd):
+        with torch.no_grad():
+            self.amp[0] = float(sd["scale"])
+            self.amp[1] = 0.0
+            self.tracker[0] = int(sd["_growth_tracker"])
+        self.growth_factor = sd.get("growth_factor", self.growth_factor)
+        self.backoff_factor = sd.get("backoff_factor", self.backoff_factor)
+        self.growth_interval = sd.get("growth_interval", self.growth_interval)

@@ -86,7 +86,10 @@ def default_parameters():
         "fusion_channels": 128, "dwi_out_channels": mp["channels"][-1], "dce_out_channels": mp["channels"][-1],
         "fusion_recon_ch": 1}
     P["early_stopping_parameters"] = {"metric": "val_roc_auc", "mode": "max", "patience": 90, "min_delta": 1e-4}
-    P["precision"] = "bf16-mixed"                       # :211 ("16-mixed"); bf16 is the MI355X mixed mode
+    # :211 is "16-mixed" (autocast + GradScaler). The 16-bit MFMA type here is
+    # bf16; "16-mixed" is honoured too -- the same bf16 compute plus the
+    # GradScaler protocol (dmf_optim.DeviceGradScaler, FusionTrainer).
+    P["precision"] = "bf16-mixed"
     P["test_mode"] = "tta_mc"                           # :215
     P["mc_passes"] = 10                                 # :216
     P["backbone_freeze_on_start"] = True                # :221

@@ -455,6 +455,17 @@ int dmf_resize_aa(const float* x, long long planes, int Hin, int Win, int Hout, 
 int dmf_adamw_multi(int nchunks, const long long* chunks, const long long* tensors, const float* hyper,
                     const int* steps, float grad_scale, void* stream);
 int dmf_steps_inc(int* steps, int n, void* stream);
+/* dynamic loss scaling ("16-mixed", torch.amp.GradScaler under Lightning;
+ * parameters_generate.py:211): amp = {scale, found_inf} (device f32[2]).
+ * dmf_amp_nonfinite: found_inf = 1 if any gradient of the AdamW table is
+ *   inf / nan; dmf_adamw_multi_amp: steps += 1 and the AdamW update with
+ *   g * grad_scale / scale, both skipped entirely when found_inf;
+ * dmf_amp_update: torch._amp_update_scale_ (backoff on found_inf, growth
+ *   every `interval` clean steps), then found_inf = 0. */
+int dmf_adamw_multi_amp(int nchunks, const long long* chunks, const long long* tensors, const float* hyper, int* steps,
+                        int nsteps, float grad_scale, const float* amp, void* stream);
+int dmf_amp_nonfinite(int nchunks, const long long* chunks, const long long* tensors, float* amp, void* stream);
+int dmf_amp_update(float* amp, int* tracker, float growth, float backoff, int interval, void* stream);
 int dmf_multi_copy(int nchunks, const long long* chunks, const long long* pairs, float scale, void* stream);
 
 #ifdef __cplusplus

@@ -1,0 +1,106 @@
+""""16-mixed" dynamic loss scaling (the reference's default precision,
+parameters_generate.py:211: Lightning autocast + torch.amp.GradScaler) as
+the device-side DeviceGradScaler + FusedAdamW: against torch.optim.AdamW
+driven by torch's own GradScaler rule on the same gradients --
+
+* a clean step: the scaled gradients are unscaled inside the update
+  (power-of-two scale: the update equals the unscaled one to rounding);
+* an overflowing step (an inf in one gradient): every parameter, moment and
+  step counter untouched, the scale backs off x0.5;
+* growth x2 after growth_interval clean steps; GradScaler.state_dict layout;
+* the captured FusionTrainer step with precision "16-mixed" matches the
+  unscaled trainer."""
+import copy
+
+import pytest
+import torch
+
+from dmf_optim import DeviceGradScaler, FusedAdamW
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _params(seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(s, generator=g).to(DEV).requires_grad_(True) for s in ((64, 32), (300,), (7, 5, 3))]
+
+
+def test_scaler_step_skip_backoff_growth():
+    ps = _params(0)
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt = FusedAdamW(ps, lr=1e-2, weight_decay=1e-2)
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    sc = DeviceGradScaler(DEV, init_scale=1024.0, growth_interval=2)
+    g = torch.Generator().manual_seed(1)
+    for it in range(5):
+        grads = [torch.randn(p.shape, generator=g).to(DEV) for p in ps]
+        overflow = it == 2
+        for p, gr in zip(ps, grads):
+            p.grad = gr * sc.get_scale()
+        if overflow:
+            ps[1].grad[17] = float("inf")
+        before = [p.detach().clone() for p in ps]
+        scale_before = sc.get_scale()
+        opt.step(scaler=sc)
+        torch.cuda.synchronize()
+        if overflow:
+            for p, b in zip(ps, before):
+                assert torch.equal(p.detach(), b)
+            assert sc.get_scale() == scale_before * 0.5
+            continue
+        for r, gr in zip(ref, grads):
+            r.grad = gr.clone()
+        ropt.step()
+        for p, r in zip(ps, ref):
+            assert torch.allclose(p.detach(), r.detach(), rtol=1e-6, atol=1e-7)
+    # scales: 1024 -> (2 clean) 2048 -> overflow 1024 -> (2 clean) 2048
+    assert sc.get_scale() == 2048.0
+    st = opt.step_counts()
+    assert all(v == 4 for v in st.values()), st  # the skipped step did not count
+    sd = sc.state_dict()
+    assert set(sd) == {"scale", "growth_factor", "backoff_factor", "growth_interval", "_growth_tracker"}
+    sc2 = DeviceGradScaler(DEV)
+    sc2.load_state_dict(sd)
+    assert sc2.get_scale() == 2048.0
+
+
+@pytest.mark.parametrize("mode", ["A", "B"])
+def test_trainer_16_mixed_matches_unscaled(mode):
+    import make_golden as MG
+    import foundation_model as FM
+    import model_module as MM
+    import parameters as PR
+    import train_fusion as TF
+    from dmf_dp import FusionTrainer
+    from selector_helpers import get_classification_loss
+
+    out = {}
+    for prec in ("32", "16-mixed"):
+        P = copy.deepcopy(PR.small_parameters(channels=(16, 32, 64), input_size=64, dropout=0.0))
+        P["backbone_freeze_on_start"] = mode == "A"
+        P["precision"] = prec
+        P["dwi_model_parameters"]["optimizer_parameters"]["eps"] = 0.1  # linear updates (see test_gpu_dp)
+        torch.manual_seed(0)
+        dwi = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, FM.build_medical_backbone(P, "cpu", "dwi", 14)),
+                                  True)
+        dce = MM.initialize_model(MM.ModelMaskHeadBackbone("dce", P, FM.build_medical_backbone(P, "cpu", "dce", 6)),
+                                  True)
+        fm = MM.FusionModel(P)
+        for m in (dwi, dce, fm):
+            MM.set_compute_dtype(m, torch.float32)
+        crit = get_classification_loss(P, torch.arange(64) % 4, "fusion", DEV)
+        lm = TF.LightningFusionModel(dwi.to(DEV), dce.to(DEV), fm.to(DEV), P, crit)
+        lm.train()
+        tr = FusionTrainer(lm, world=1, use_graph=True)
+        assert (tr.scaler is not None) == (prec == "16-mixed")
+        losses = [float(tr.step(tuple(t.to(DEV) for t in MG.volume_batch(4, 64, 70 + i))).item()) for i in range(3)]
+        out[prec] = ({n: p.detach().cpu() for n, p in lm.named_parameters()}, losses)
+        if tr.scaler is not None:
+            assert tr.scaler.get_scale() == 2.0 ** 16
+    (p32, l32), (p16, l16) = out["32"], out["16-mixed"]
+    for a, b in zip(l32, l16):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (l32, l16)
+    num = sum((p16[n] - p32[n]).pow(2).sum().item() for n in p32)
+    den = sum((p32[n]).pow(2).sum().item() for n in p32)
+    assert (num / den) ** 0.5 < 1e-5, (num / den) ** 0.5
