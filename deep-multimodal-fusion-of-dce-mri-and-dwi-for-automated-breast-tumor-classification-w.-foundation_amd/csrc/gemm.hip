@@ -323,7 +323,8 @@ __global__ void __launch_bounds__(GTHREADS, 2) k_gemm(GemmArgs g) {
 // One wave per row of length L (fp32 scores S): p = softmax(scale * s);
 // Ps (PT: bf16, or f32 in the parity mode) = p (kept for backward);
 // Pd = dropout(p) / (1 - dp) (the operand of P v). Dropout element index =
-// row * L + col (site `site`).
+// row * L + col (site `site`). Columns >= Lv are key padding (a token count
+// rounded up to the GEMM granule): excluded from the max / sum, p = 0 there.
 __device__ __forceinline__ float4 g_ld4(const bf16_t* p) {
   const uint2 u = *(const uint2*)p;
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
@@ -333,22 +334,32 @@ __device__ __forceinline__ float4 g_ld4(const float* p) { return *(const float4*
 
 template <typename PT>
 __global__ void __launch_bounds__(256) k_softmax_drop(const float* __restrict__ S, int lds_, long long rows, int L,
-                                                      float scale, float dp, const unsigned long long* rng, int site,
-                                                      PT* __restrict__ Ps, PT* __restrict__ Pd, int ldp) {
+                                                      int Lv, float scale, float dp, const unsigned long long* rng,
+                                                      int site, PT* __restrict__ Ps, PT* __restrict__ Pd, int ldp) {
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* s = S + row * lds_;
+  auto ld = [&](int c) {  // 4 scores, key padding at -inf
+    float4 v = *(const float4*)(s + c);
+    if (c + 3 >= Lv) {
+      if (c >= Lv) v.x = -INFINITY;
+      if (c + 1 >= Lv) v.y = -INFINITY;
+      if (c + 2 >= Lv) v.z = -INFINITY;
+      v.w = -INFINITY;
+    }
+    return v;
+  };
   float mx = -INFINITY;
   for (int c = lane * 4; c < L; c += 256) {
-    const float4 v = *(const float4*)(s + c);
+    const float4 v = ld(c);
     mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   float sum = 0.f;
   for (int c = lane * 4; c < L; c += 256) {
-    const float4 v = *(const float4*)(s + c);
+    const float4 v = ld(c);
     sum += __expf((v.x - mx) * scale) + __expf((v.y - mx) * scale) + __expf((v.z - mx) * scale) +
            __expf((v.w - mx) * scale);
   }
@@ -357,7 +368,7 @@ __global__ void __launch_bounds__(256) k_softmax_drop(const float* __restrict__ 
   const float inv = 1.f / sum;
   const float ks = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   for (int c = lane * 4; c < L; c += 256) {
-    const float4 v = *(const float4*)(s + c);
+    const float4 v = ld(c);
     float p[4] = {__expf((v.x - mx) * scale) * inv, __expf((v.y - mx) * scale) * inv,
                   __expf((v.z - mx) * scale) * inv, __expf((v.w - mx) * scale) * inv};
     g_store_aux(Ps + row * ldp + c, p);
@@ -490,15 +501,16 @@ extern "C" int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, 
 }
 
 template <typename PT>
-static int softmax_launch(const char* name, const float* S, int lds, long long rows, int L, float scale,
+static int softmax_launch(const char* name, const float* S, int lds, long long rows, int L, int Lv, float scale,
                           float dropout_p, const unsigned long long* rng, int site, void* probs, void* probs_dropped,
                           int ldp, void* stream) {
   DMF_CHECK_ARG(L % 4 == 0 && lds % 4 == 0 && ldp % 4 == 0, "%s: L and strides must be multiples of 4", name);
+  DMF_CHECK_ARG(Lv > 0 && Lv <= L, "%s: valid length %d must be in [1, L=%d]", name, Lv, L);
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "%s: dropout needs rng state", name);
   DMF_CHECK_ARG(dropout_p < 1.f, "%s: p must be < 1", name);
   if (rows == 0) return 0;
   hipLaunchKernelGGL(k_softmax_drop<PT>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, S, lds,
-                     rows, L, scale, dropout_p, rng, site, (PT*)probs, (PT*)probs_dropped, ldp);
+                     rows, L, Lv, scale, dropout_p, rng, site, (PT*)probs, (PT*)probs_dropped, ldp);
   DMF_LAUNCH_CHECK(name);
   return 0;
 }
@@ -518,17 +530,17 @@ static int softmax_bwd_launch(const char* name, const void* probs, int ldp, cons
   return 0;
 }
 
-extern "C" int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
-                                   const unsigned long long* rng, int site, void* probs, void* probs_dropped, int ldp,
-                                   void* stream) {
-  return softmax_launch<bf16_t>("dmf_softmax_dropout", S, lds, rows, L, scale, dropout_p, rng, site, probs,
+extern "C" int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, int Lv, float scale,
+                                   float dropout_p, const unsigned long long* rng, int site, void* probs,
+                                   void* probs_dropped, int ldp, void* stream) {
+  return softmax_launch<bf16_t>("dmf_softmax_dropout", S, lds, rows, L, Lv, scale, dropout_p, rng, site, probs,
                                 probs_dropped, ldp, stream);
 }
 
-extern "C" int dmf_softmax_dropout_f32(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
-                                       const unsigned long long* rng, int site, float* probs, float* probs_dropped,
-                                       int ldp, void* stream) {
-  return softmax_launch<float>("dmf_softmax_dropout_f32", S, lds, rows, L, scale, dropout_p, rng, site, probs,
+extern "C" int dmf_softmax_dropout_f32(const float* S, int lds, long long rows, int L, int Lv, float scale,
+                                       float dropout_p, const unsigned long long* rng, int site, float* probs,
+                                       float* probs_dropped, int ldp, void* stream) {
+  return softmax_launch<float>("dmf_softmax_dropout_f32", S, lds, rows, L, Lv, scale, dropout_p, rng, site, probs,
                                probs_dropped, ldp, stream);
 }
 

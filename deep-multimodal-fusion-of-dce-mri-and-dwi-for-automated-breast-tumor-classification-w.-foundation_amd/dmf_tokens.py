@@ -211,7 +211,7 @@ def _sfx(cdt):
     return "" if cdt == torch.bfloat16 else "_f32"
 
 
-def _attn_fwd(a, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, gamma=None, res=None):
+def _attn_fwd(a, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, gamma=None, res=None, nv=None):
     r, e = a.shape
     d = e // heads
     cdt, dev = a.dtype, a.device
@@ -223,8 +223,8 @@ def _attn_fwd(a, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, 
          sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
     P = torch.empty((b, heads, n, n), **bf)
     Pd = torch.empty((b, heads, n, n), **bf) if p_attn > 0 else P
-    N.call("dmf_softmax_dropout" + _sfx(cdt), S.data_ptr(), n, b * heads * n, n, float(d ** -0.5), float(p_attn),
-           O._p(rng), int(s_attn), P.data_ptr(), Pd.data_ptr(), n, _s())
+    N.call("dmf_softmax_dropout" + _sfx(cdt), S.data_ptr(), n, b * heads * n, n, int(nv or n), float(d ** -0.5),
+           float(p_attn), O._p(rng), int(s_attn), P.data_ptr(), Pd.data_ptr(), n, _s())
     del S
     o = gemm(torch.empty((r, e), **bf), Pd, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads),
              sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
@@ -316,14 +316,14 @@ def _zeros(dev, *shapes):
 class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cfg, rng, ln1w, ln1b, qkvw, qkvb, projw, projb, ln2w, ln2b, fc1w, fc1b, fc2w, fc2b, g1, g2):
-        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt = cfg
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt, nv = cfg
         s_attn, s_proj, s_m1, s_m2 = sites
         b, n, e = x.shape
         x = x.contiguous().view(b * n, e)
         wq, wp, w1, w2 = _wcast(cdt, qkvw, projw, fc1w, fc2w)
         # attention branch: x1 = x + drop(proj(attn(ln1(x)))) * g1
         ln1, save1 = ln_fwd(x, ln1w, ln1b, eps1, cdt)
-        x1, sa = _attn_fwd(ln1, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, g1, x)
+        x1, sa = _attn_fwd(ln1, wq, qkvb, wp, projb, b, n, heads, p_attn, p_proj, rng, s_attn, s_proj, g1, x, nv)
         # MLP branch: x2 = x1 + drop(fc2(drop(gelu(fc1(ln2(x1)))))) * g2
         ln2, save2 = ln_fwd(x1, ln2w, ln2b, eps2, cdt)
         x2, sm = _mlp_fwd(ln2, w1, fc1b, w2, fc2b, p_mlp, rng, s_m1, s_m2, g2, x1)
@@ -337,7 +337,7 @@ class _BlockFn(torch.autograd.Function):
         t = ctx.saved_tensors
         x, ln1, save1, sa, x1, ln2, save2, sm = t[0], t[1], t[2], t[3:8], t[8], t[9], t[10], t[11:14]
         wq, wp, w1, w2, ln1w, ln2w, g1, g2, rng = t[14:]
-        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt = ctx.cfg
+        heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt, _ = ctx.cfg
         s_attn, s_proj, s_m1, s_m2 = sites
         b, n, e = ctx.dims
         hid = w1.shape[0]
@@ -458,9 +458,12 @@ def mlp(x, m, rng, dtype=torch.bfloat16):
     return _MLPFn.apply(x, (p, tuple(m._sites), dtype), rng, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)
 
 
-def transformer_block(x, blk, rng, sites, dtype=torch.bfloat16):
+def transformer_block(x, blk, rng, sites, dtype=torch.bfloat16, n_valid=None, gammas=None):
     """TransformerBlock.forward (transformer_model.py:78-81) as one node;
-    ``dtype`` is the compute dtype (bf16, or f32 for the parity mode)."""
+    ``dtype`` is the compute dtype (bf16, or f32 for the parity mode).
+    ``n_valid``: tokens beyond it are key padding (masked out of every
+    softmax row); ``gammas``: LayerScale vectors for a block without them
+    (ones: timm's ViT Block, init_values=None)."""
     at, ml = blk.attn, blk.mlp
     # the nn.Dropout modules' own flags (train() / eval() set them with the
     # block's; MC dropout turns on only these, train_fusion.py:445-449)
@@ -472,7 +475,9 @@ def transformer_block(x, blk, rng, sites, dtype=torch.bfloat16):
     _check_dtype("TransformerBlock", dtype)
     if at.qkv.bias is None:
         raise ValueError("TransformerBlock: qkv_bias=False is not supported by the fused path")
-    cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites), dtype)
+    cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites), dtype, n_valid)
+    g1 = blk.gamma1 if gammas is None else gammas[0]
+    g2 = blk.gamma2 if gammas is None else gammas[1]
     return _BlockFn.apply(x, cfg, rng, blk.norm1.weight, blk.norm1.bias, at.qkv.weight, at.qkv.bias, at.proj.weight,
                           at.proj.bias, blk.norm2.weight, blk.norm2.bias, ml.fc1.weight, ml.fc1.bias,
-                          ml.fc2.weight, ml.fc2.bias, blk.gamma1, blk.gamma2)
+                          ml.fc2.weight, ml.fc2.bias, g1, g2)

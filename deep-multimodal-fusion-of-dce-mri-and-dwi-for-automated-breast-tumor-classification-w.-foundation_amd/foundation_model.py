@@ -199,6 +199,136 @@ class _DisabledWrapper(nn.Module):
         return self._orig_mod(x, **kw)
 
 
+# ------------------------------------------------------------- ViT-B/16
+# The reference's alternate backbone (foundation_model.py:371-431, dispatch
+# :526-545): timm ``vit_base_patch16_224(features_only=True,
+# out_indices=range(12), img_size=input_size)`` -- a FeatureGetterNet whose
+# ``model`` is the VisionTransformer with norm / head pruned, returning every
+# block's output tokens without the class token, reshaped to NCHW maps
+# (forward_intermediates, norm=False). Restated with timm's module and
+# parameter names (state_dict ``model.blocks.{i}.attn.qkv.weight`` ...); each
+# block runs as ONE fused node of the transformer engine (dmf_tokens: pre-LN
+# attention + MLP with bias / GELU / residual in the GEMM epilogues;
+# LayerScale = ones as timm's init_values=None). The token count 1 + (S/16)^2
+# is padded to the GEMM granule of 8 and the padded keys are masked out of
+# every softmax row.
+class _ViTAttention(nn.Module):
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.embed_dim = dim
+        self.scale = self.head_dim ** -0.5
+        self.qkv = nn.Linear(dim, dim * 3, bias=True)
+        self.attn_drop = nn.Dropout(0.0)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(0.0)
+        self._sites = (O.RNG.new_site(), O.RNG.new_site())
+
+
+class _ViTMlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.act = nn.GELU()
+        self.drop = nn.Dropout(0.0)
+        self.fc2 = nn.Linear(hidden, dim)
+        self._sites = (O.RNG.new_site(), O.RNG.new_site())
+
+
+class ViTBlock(nn.Module):
+    """timm Block (pre-LN, no LayerScale, drop_path 0), LayerNorm eps 1e-6."""
+
+    def __init__(self, dim=768, num_heads=12, mlp_ratio=4.0):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = _ViTAttention(dim, num_heads)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = _ViTMlp(dim, int(dim * mlp_ratio))
+        self._sites = self.attn._sites + self.mlp._sites
+
+
+class _ViTPatchEmbed(nn.Module):
+    def __init__(self, in_chans, dim, patch):
+        super().__init__()
+        self.proj = nn.Conv2d(in_chans, dim, kernel_size=patch, stride=patch)
+
+
+class _VisionTransformer(nn.Module):
+    def __init__(self, in_chans, img_size, patch, dim, depth, num_heads):
+        super().__init__()
+        self.patch = patch
+        self.grid = img_size // patch
+        self.patch_embed = _ViTPatchEmbed(in_chans, dim, patch)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, self.grid * self.grid + 1, dim))
+        self.blocks = nn.ModuleList([ViTBlock(dim, num_heads) for _ in range(depth)])
+        # timm init: pos_embed trunc_normal(0.02), cls_token normal(1e-6), Linear trunc_normal(0.02) / bias 0
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.normal_(self.cls_token, std=1e-6)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+
+
+class VisionTransformerFeatures(nn.Module):
+    """timm FeatureGetterNet(vit_base_patch16_224, out_indices=0..11): forward(x)
+    -> 12 maps [B, 768, S/16, S/16] (NCHW logical, NHWC storage, compute dtype)."""
+
+    def __init__(self, in_chans=6, img_size=256, patch=16, dim=768, depth=12, num_heads=12):
+        super().__init__()
+        self.model = _VisionTransformer(in_chans, img_size, patch, dim, depth, num_heads)
+        self.feature_info = _FeatureInfo([dim] * depth, [patch] * depth)
+        self.register_buffer("_ones", torch.ones(dim), persistent=False)
+
+    def forward(self, x, on_feature=None):
+        import dmf_tokens as D
+
+        m = self.model
+        dt = getattr(self, "compute_dtype", torch.bfloat16)
+        b, c, h, w = x.shape
+        if h % m.patch or w % m.patch or (h // m.patch) * (w // m.patch) + 1 != m.pos_embed.shape[1]:
+            raise ValueError(f"ViT-B/16: input {h}x{w} does not match the {m.grid}x{m.grid} patch grid of pos_embed")
+        cin = m.patch_embed.proj.in_channels
+        if x.dtype != dt or c != O.channel_pad(cin, dt):  # a raw NCHW stack (the encoder stages it already)
+            x, _ = O.input_stage(x, dt, None)
+        y = O.conv2d(O.as_nhwc(x), m.patch_embed.proj, _caches(m.patch_embed.proj))  # [B, E, h', w'] NHWC
+        gh, gw = y.shape[-2:]
+        e = y.shape[1]
+        tok = y.permute(0, 2, 3, 1).reshape(b, gh * gw, e).float()       # NHWC storage == token order
+        n = gh * gw + 1
+        t = torch.cat([m.cls_token.expand(b, 1, e), tok], 1) + m.pos_embed   # _pos_embed (class token first)
+        npad = (n + 7) // 8 * 8
+        if npad != n:
+            t = torch.nn.functional.pad(t, (0, 0, 0, npad - n))
+        feats = []
+        for i, blk in enumerate(m.blocks):
+            t = D.transformer_block(t, blk, None, blk._sites, dt, n_valid=n, gammas=(self._ones, self._ones))
+            f = t[:, 1:n].reshape(b, gh, gw, e).to(dt)                        # prefix token dropped
+            feats.append(O.as_nhwc(f.permute(0, 3, 1, 2)))
+            if on_feature is not None:
+                on_feature(i, feats)
+        return feats
+
+
+def build_vit_dino_backbone(name="vit_base_patch16_224", pretrained=True, device="cuda", in_channels=6,
+                            out_indices=None, img_size=256, use_advanced_adapt=False, compute_dtype=torch.bfloat16):
+    """foundation_model.py:371-431. No hub access here: pretrained weights
+    are unavailable and the backbone keeps timm's random init (documented)."""
+    if out_indices is not None and list(out_indices) != list(range(12)):
+        raise NotImplementedError("ViT-B/16 features: out_indices must be all 12 blocks (the reference's call)")
+    if pretrained:
+        warnings.warn("ViT-B/16 pretrained weights unavailable offline: backbone keeps timm random init")
+    vit = VisionTransformerFeatures(in_chans=in_channels, img_size=img_size)
+    vit.compute_dtype = compute_dtype
+    vit = vit.to(device)  # ModelMaskHeadBackbone adds the _orig_mod wrapper (model_module.py:539)
+    vit.output_dims = vit.feature_info.channels()
+    vit.expected_input = "B, C, H, W"
+    vit.is_3d = False
+    return vit
+
+
 # --------------------------------------------------------- weight plumbing
 def adapt_first_conv(state_dict, in_channels):
     """foundation_model.py:99-124: RGB conv1 -> mean over input channels,
@@ -334,5 +464,12 @@ def build_medical_backbone(parameters, device, method, in_channels):
         mp["downsample_each_repeat"] = False
         return bb
     if name in ("vit_base_patch16_224", "dino_vitbase16_pretrain"):
-        raise NotImplementedError("ViT-B/16 backbone (config 5 alternate) is not built yet on MI355X")
+        # :526-545: all 12 block maps at stride 16, chains 3 / 4 / 5 blocks
+        mp["backbone_index_lists"] = [[0, 1, 2], [3, 4, 5, 6], [7, 8, 9, 10, 11]]
+        mp["downsample"] = (False, False, False)
+        mp["channels"] = (768, 768, 768)
+        mp["transformer_backbone"] = True
+        return build_vit_dino_backbone(in_channels=in_channels, device=device, out_indices=list(range(12)),
+                                       img_size=mp["input_size"], use_advanced_adapt=mp["use_advanced_adapt"],
+                                       compute_dtype=dtype)
     raise ValueError(f"Unknown backbone_str {name!r}")

@@ -328,7 +328,10 @@ class BackboneAdapter(nn.Module):
         elif len(parts) == 2:
             h = O.conv_bn_act(parts[0], nk[0], _caches(nk[0]), nk[1], "gelu", x2=parts[1])
         else:
-            raise NotImplementedError("neck chains of more than two feature maps are not built yet")
+            # ViT chains (3-5 block maps of 768 channels at stride 16): the
+            # concat is small at that resolution -- materialise it (NHWC)
+            cat = torch.cat([p.permute(0, 2, 3, 1) for p in parts], -1)
+            h = O.conv_bn_act(O.as_nhwc(cat.permute(0, 3, 1, 2)), nk[0], _caches(nk[0]), nk[1], "gelu")
         return O.conv_bn_act(h, nk[3], _caches(nk[3]), nk[4], "gelu")
 
     def forward(self, x):

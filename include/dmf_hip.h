@@ -360,8 +360,9 @@ int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha
 /* attention probabilities (transformer_model.py:104-110): per row of L f32
  * scores, probs = softmax(scale * s) (bf16, kept for backward) and
  * probs_dropped = dropout(probs, p) (bf16, the P operand of P v); Philox
- * element index row*L + col at dropout site `site`. */
-int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
+ * element index row*L + col at dropout site `site`. Columns >= Lv are key
+ * padding (token counts rounded up to the GEMM granule): probability 0. */
+int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, int Lv, float scale, float dropout_p,
                         const unsigned long long* rng, int site, void* probs, void* probs_dropped, int ldp,
                         void* stream);
 /* dscores = scale * P * (g - sum(P g)), g = dropout_mask(dprobs_dropped) (bf16 out) */
@@ -369,7 +370,7 @@ int dmf_softmax_dropout_bwd(const void* probs, int ldp, const float* dprobs_drop
                             float scale, float dropout_p, const unsigned long long* rng, int site, void* dscores,
                             int lds, void* stream);
 /* f32 probs / dscores (parity mode) */
-int dmf_softmax_dropout_f32(const float* S, int lds, long long rows, int L, float scale, float dropout_p,
+int dmf_softmax_dropout_f32(const float* S, int lds, long long rows, int L, int Lv, float scale, float dropout_p,
                             const unsigned long long* rng, int site, float* probs, float* probs_dropped, int ldp,
                             void* stream);
 int dmf_softmax_dropout_bwd_f32(const float* probs, int ldp, const float* dprobs_dropped, int ldg, long long rows,

@@ -360,6 +360,88 @@ class BackboneAdapter(nn.Module):
         return outs[0], outs[1], outs[2]
 
 
+# ------------------------------------------------------------- ViT-B/16
+class _VitAttention(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.num_heads, self.head_dim = heads, dim // heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        b, n, c = x.shape
+        q, k, v = self.qkv(x).reshape(b, n, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4)
+        a = torch.softmax((q @ k.transpose(-2, -1)) * self.head_dim ** -0.5, dim=-1)
+        return self.proj((a @ v).transpose(1, 2).reshape(b, n, c))
+
+
+class _VitMlp(nn.Module):
+    def __init__(self, dim, hid):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hid)
+        self.fc2 = nn.Linear(hid, dim)
+
+    def forward(self, x):
+        return self.fc2(F.gelu(self.fc1(x)))
+
+
+class _VitBlock(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = _VitAttention(dim, heads)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = _VitMlp(dim, 4 * dim)
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        return x + self.mlp(self.norm2(x))
+
+
+class _PatchProj(nn.Module):
+    def __init__(self, cin, dim, p):
+        super().__init__()
+        self.proj = nn.Conv2d(cin, dim, p, stride=p)
+
+
+class _Vit(nn.Module):
+    def __init__(self, cin, img, p, dim, depth, heads):
+        super().__init__()
+        self.patch = p
+        self.patch_embed = _PatchProj(cin, dim, p)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, (img // p) ** 2 + 1, dim))
+        self.blocks = nn.ModuleList([_VitBlock(dim, heads) for _ in range(depth)])
+
+
+class VisionTransformerFeatures(nn.Module):
+    """timm vit_base_patch16_224(features_only=True, out_indices=range(12),
+    img_size=S) as foundation_model.py:371-431 builds it: FeatureGetterNet
+    ('model' = the VisionTransformer, norm / head pruned) ->
+    forward_intermediates(norm=False, output_fmt='NCHW'): patch_embed (conv
+    k = s = 16, flatten), class token prepended, + pos_embed, then every
+    block's output with the class token dropped, reshaped [B, 768, S/16, S/16]."""
+
+    def __init__(self, in_chans=6, img_size=256, patch=16, dim=768, depth=12, heads=12):
+        super().__init__()
+        self.model = _Vit(in_chans, img_size, patch, dim, depth, heads)
+        self.feature_info = _FeatInfo([dim] * depth, [patch] * depth)
+        self.output_dims = self.feature_info.channels()
+
+    def forward(self, x):
+        m = self.model
+        b = x.shape[0]
+        y = _conv(x, m.patch_embed.proj)
+        gh, gw = y.shape[-2:]
+        t = y.flatten(2).transpose(1, 2)
+        t = torch.cat([m.cls_token.expand(b, -1, -1), t], 1) + m.pos_embed
+        feats = []
+        for blk in m.blocks:
+            t = blk(t)
+            feats.append(t[:, 1:].reshape(b, gh, gw, -1).permute(0, 3, 1, 2).contiguous())
+        return feats
+
+
 # ------------------------------------------------- hybrid transformer stage
 class PatchEmbed(nn.Module):
     """transformer_model.py:7-32."""

@@ -196,7 +196,7 @@ def test_softmax_dropout_fwd_bwd():
     Sd = S.to(DEV)
     P = torch.empty((rows, L), dtype=torch.bfloat16, device=DEV)
     Pd = torch.empty_like(P)
-    N.call("dmf_softmax_dropout", Sd.data_ptr(), L, rows, L, scale, p, rng.data_ptr(), site, P.data_ptr(),
+    N.call("dmf_softmax_dropout", Sd.data_ptr(), L, rows, L, L, scale, p, rng.data_ptr(), site, P.data_ptr(),
            Pd.data_ptr(), L, N.stream_ptr())
     keep = torch.empty(rows * L, dtype=torch.uint8, device=DEV)
     N.call("dmf_dropout_keep_mask", rng.data_ptr(), site, rows * L, p, keep.data_ptr(), N.stream_ptr())
