@@ -202,7 +202,9 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     if x2 is not None:
         _, cx2, _, _, ldx2 = nhwc(x2)
     co, ci, kh, kw = weight.shape
-    if cx + cx2 < ci:  # (more is the zero channel padding of the staged input)
+    # exactly ci channels -- or, for a single staged input, ci zero-padded to
+    # the 16-byte K granule (input_stage's layout)
+    if cx + cx2 != ci and not (x2 is None and cx == channel_pad(ci, x.dtype)):
         raise RuntimeError(f"conv2d: weight of size {list(weight.shape)} expected input with {ci} channels, but got "
                            f"{cx + cx2} channels instead")
     ho, wo = g.out_hw(h, w)
@@ -1545,7 +1547,9 @@ class _FocalFn(torch.autograd.Function):
     def forward(ctx, logits, labels, soft, cw, gamma, smoothing, use_smoothing, reduction):
         z = logits.contiguous().float()
         b, k = z.shape
-        red = {"mean": 0, "sum": 1, "none": 2}[reduction]
+        # loss.py:151-155: anything but 'mean' / 'sum' returns the per-row losses
+        # (the 'fl' selector's argument mix-up passes gamma here, quirk Q8)
+        red = {"mean": 0, "sum": 1}.get(reduction, 2) if isinstance(reduction, str) else 2
         loss = torch.empty((), dtype=torch.float32, device=z.device)
         per_row = torch.empty(b, dtype=torch.float32, device=z.device) if red == 2 else None
         dl = torch.empty_like(z) if z.requires_grad or logits.requires_grad else None

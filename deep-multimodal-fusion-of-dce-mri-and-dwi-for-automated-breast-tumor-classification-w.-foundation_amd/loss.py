@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+import dmf_native as N
 import dmf_ops as O
 
 
@@ -99,10 +100,30 @@ class WeightedFocalLoss(nn.Module):
 
     def forward(self, inputs, targets):
         if targets.ndim > 1:
-            targets = targets.argmax(dim=1)
+            return self._soft(inputs, targets)
         a = self.alpha
         if a is None:
             return O.focal_ce(inputs, targets, self.gamma, 1.0, None, self.reduction)
         if isinstance(a, (int, float)):
             return O.focal_ce(inputs, targets, self.gamma, float(a), None, self.reduction)
         return O.focal_ce(inputs, targets, self.gamma, 1.0, a.to(inputs.device).float().contiguous(), self.reduction)
+
+    def _soft(self, inputs, targets):
+        """loss.py:96-128 with soft / smoothed targets: ce = F.cross_entropy on
+        the probabilities (-sum t log p), pt = exp(-ce), focal = alpha *
+        (1 - pt)^gamma * ce, per-class alpha looked up at argmax(t). Off the
+        default path (get_classification_loss builds SoftWeightedFocalLoss):
+        device tensor ops."""
+        N.require_cuda(inputs, targets)
+        ce = -(targets.float() * torch.log_softmax(inputs.float(), dim=1)).sum(1)
+        fl = (1 - torch.exp(-ce)) ** self.gamma * ce
+        a = self.alpha
+        if isinstance(a, (int, float)):
+            fl = a * fl
+        elif a is not None:
+            fl = a.to(inputs.device).float().gather(0, targets.argmax(dim=1).long()) * fl
+        if self.reduction == "mean":
+            return fl.mean()
+        if self.reduction == "sum":
+            return fl.sum()
+        return fl
