@@ -81,6 +81,44 @@ __device__ __forceinline__ float apply_act_rt(int act, float v) {
   }
 }
 
+// the activation over a whole register group with ONE uniform branch: a
+// per-element apply_act_rt unrolls into a compare-and-branch chain per value
+// and drags every activation's code through the instruction cache (the
+// persistent conv's epilogue was ~40 % of its time that way)
+template <int N>
+__device__ __forceinline__ void apply_act_arr(int act, float (&v)[N]) {
+  switch (act) {
+    case DMF_ACT_RELU:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = fmaxf(v[e], 0.f);
+      break;
+    case DMF_ACT_GELU:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = gelu_f(v[e]);
+      break;
+    case DMF_ACT_SIGMOID:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = sigmoid_f(v[e]);
+      break;
+    default:
+      break;
+  }
+}
+template <int FM, int FN>
+__device__ __forceinline__ void apply_act_col(int act, f32x4_t (&acc)[FM][FN], int j) {
+  if (act == DMF_ACT_NONE) return;
+  float v[FM * 4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[i * 4 + r] = acc[i][j][r];
+  apply_act_arr(act, v);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[i][j][r] = v[i * 4 + r];
+}
+
 constexpr int CBM = 128, CBN = 128, CTHREADS = 256;
 constexpr int STAGE_BYTES = (CBM + CBN) * 128;  // A + B, 128-byte rows
 // main LDS: two A/B stages, reused for the C staging tile [BM][BN + 16 B pad]
@@ -216,10 +254,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         const int row = m0 + wm * (BM / WMW) + i * 16 + fg * 4 + r;
         float v = acc[i][j][r] + bsv;
         if (stats && row < a.M) { s += v; ss += v * v; }
-        if (!stats) v = apply_act_rt(a.act, v);
         acc[i][j][r] = v;
       }
     }
+    if (!stats) apply_act_col(a.act, acc, j);
     if (stats) {
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
@@ -836,10 +874,13 @@ __device__ __forceinline__ int ps_perm(int row) {
   return slab | ((x & 3) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2));
 }
 
-// PV: DMA piece schedule of the next K-step -- 0: spread over both k-halves
-// (pieces 0-3 in the first, 4-7 in the second), 1: all 8 in the first half (one
-// per pixel fragment), 2: all 8 right after the barrier
-template <bool PADCHK, bool DUAL, int PV>
+// EPI: the epilogue, fixed at compile time so only its path is in the code
+// (a runtime switch per tile inflated the kernel to ~13 k instructions of
+// activation variants): 0 = BN partial statistics (no activation), 1 + act =
+// bias + DMF_ACT_* activation. The next K-step's DMA pieces are spread over
+// both k-halves (pieces 0-3 in the first, 4-7 in the second; "all 8 in one
+// half" or "all 8 after the barrier" measured no better).
+template <bool PADCHK, bool DUAL, int EPI>
 __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
   constexpr int ES = 2, BK = 64;
   constexpr int NW = QTHREADS / 64;
@@ -973,10 +1014,6 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     }
     const char* Ps = smem + st * QSTAGE;  // pixel rows
     const char* Ws = Ps + QBM * 128;      // weight rows (permuted)
-    if (PV == 2 && more) {
-#pragma unroll
-      for (int p = 0; p < NA + NB; ++p) piece(p);
-    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + fg;
@@ -993,8 +1030,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if (PV == 0 && more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
-        if (PV == 1 && more && kk == 0) piece(i);
+        if (more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&wv[j], *(bf16x8_t*)&pv[i], acc[i][j], 0,
@@ -1015,7 +1051,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
       const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
       const int m0 = mt * QBM, n0 = nt * QBN;
       const int cl = wn * 64 + fg * 16;  // this lane's 16 channels: n0 + cl .. +15
-      const bool stats = a.partials != nullptr;
+      constexpr bool stats = EPI == 0;
       float bsv[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + cl + e] : 0.f;
@@ -1035,9 +1071,9 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
           const float w = ok ? 1.f : 0.f;
 #pragma unroll
           for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
-        } else {
+        } else if constexpr (EPI > 1) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] = apply_act_rt(a.act, v[e]);
+          for (int e = 0; e < 16; ++e) v[e] = apply_act<EPI - 1>(v[e]);
         }
         uint32_t w8[8];
 #pragma unroll
@@ -1119,10 +1155,10 @@ __device__ __forceinline__ void conv_epilogue_stage(const ConvArgs& a, f32x4_t (
         const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
         float v = acc[i][j][r] + bsv;
         if (stats && row < a.M) { s += v; ss += v * v; }
-        if (!stats) v = apply_act_rt(a.act, v);
         acc[i][j][r] = v;
       }
     }
+    if (!stats) apply_act_col(a.act, acc, j);
     if (stats) {
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
@@ -1498,8 +1534,6 @@ static int g_ps_enable = [] {
   const char* e = std::getenv("DMF_PS");
   return e && e[0] == '0' ? 0 : 1;
 }();
-// 5 = its DMA piece schedule (k_conv_fwd_ps PV)
-static int g_ps_var = 0;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1621,16 +1655,20 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
-#define DMF_PS(V)                                                                                     \
-  do {                                                                                                \
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, V>), gp, bq, lds_total, st, a);  \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, V>), gp, bq, lds_total, st, a);    \
-    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, V>), gp, bq, lds_total, st, a);                \
+    const int epi = a.partials != nullptr ? 0 : 1 + a.act;
+    DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
+#define DMF_PS(E)                                                                                      \
+  do {                                                                                                 \
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E>), gp, bq, lds_total, st, a);  \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E>), gp, bq, lds_total, st, a);    \
+    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E>), gp, bq, lds_total, st, a);                \
   } while (0)
-    switch (g_ps_var) {
+    switch (epi) {
+      case 0: DMF_PS(0); break;
       case 1: DMF_PS(1); break;
       case 2: DMF_PS(2); break;
-      default: DMF_PS(0);
+      case 3: DMF_PS(3); break;
+      default: DMF_PS(4); break;
     }
 #undef DMF_PS
   } else if (plan.sq) {
@@ -1783,7 +1821,6 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 2: DMF_CHECK_ARG(value >= 0 && value <= 6, "dmf_conv_tune: forced tile %d", value); g_force = value; return 0;
     case 3: DMF_CHECK_ARG(value >= -2 && value <= 64, "dmf_conv_tune: stat mode %d", value); g_stat_mode = value; return 0;
     case 4: g_ps_enable = value != 0; return 0;
-    case 5: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ps variant %d", value); g_ps_var = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
