@@ -10,9 +10,11 @@ ROOT=$(pwd)
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $OUT/tests.log; exit 1; }
   tail -3 $OUT/tests.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail -30 $OUT/smoke.log; exit 1; }
+  tail -2 $OUT/smoke.log
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
-  DMF_CONV_DUMP=$OUT/conv.jsonl timeout -k 10 600 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?"; tail -30 $OUT/bench.err; exit 1; }
+  DMF_CONV_DUMP=$OUT/conv.jsonl timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?"; tail -30 $OUT/bench.err; exit 1; }
   cat $OUT/bench.json
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
