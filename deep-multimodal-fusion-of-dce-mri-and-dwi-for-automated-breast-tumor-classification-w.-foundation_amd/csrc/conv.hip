@@ -857,8 +857,11 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
 // The epilogue needs no LDS: the MFMA operands are swapped (weights are the
 // row operand, pixels the column operand) and the weight rows of each
 // wave's 64-channel slab are loaded in a permuted order, so after the K loop
-// lane (g = lane>>4, p = lane&15) holds 16 CONSECUTIVE output channels of
-// pixel p of every pixel fragment: two 16-B bf16 stores per pixel row,
+// lane (g = lane>>4, p = lane&15) holds output channels 8g..8g+7 and
+// 32+8g..32+8g+7 (of the wave's 64) of pixel p of every pixel fragment: two
+// 16-B bf16 stores per pixel row, in each of which the 4 lanes of a pixel
+// write one contiguous 64-B run (whole half-lines, not interleaved 16-B
+// pieces of two stores),
 // straight from the accumulators (no C staging, the stage ring stays free
 // for the next tile's DMA). BN statistics: per-lane sums over the lane's
 // pixels, a 16-lane shuffle reduction, then the 2 pixel-half waves combine
@@ -867,12 +870,15 @@ constexpr int PS_LDS = 2 * QSTAGE + 2 * 256 * 2 * 4;  // ring + [2 halves][256 c
 typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
 
 // local W-tile row -> channel offset within the 256-column tile: inside each
-// 64-row wave slab, row 16j + 4g + r holds channel 16g + 4j + r (digits j, g
-// swapped; an involution)
+// 64-row wave slab, row 16j + 4g + r (bits j1 j0 g1 g0 r1 r0) holds channel
+// 32*j1 + 8g + 4*j0 + r (bits j1 g1 g0 j0 r1 r0): a lane's accumulators of
+// fragments j = 0,1 are channels 8g..8g+7, of j = 2,3 channels 32+8g..+7
 __device__ __forceinline__ int ps_perm(int row) {
   const int slab = row & ~63, x = row & 63;
-  return slab | ((x & 3) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2));
+  return slab | (x & 0x23) | (((x >> 2) & 3) << 3) | (((x >> 4) & 1) << 2);
 }
+// channel offset (within the 256-column tile) of accumulator value e = 4j + r of lane group g in wave column wn
+__device__ __forceinline__ int ps_chan(int wn, int g, int e) { return wn * 64 + g * 8 + (e & 7) + ((e >> 3) << 5); }
 
 // EPI: the epilogue, fixed at compile time so only its path is in the code
 // (a runtime switch per tile inflated the kernel to ~13 k instructions of
@@ -1050,11 +1056,11 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     {
       const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
       const int m0 = mt * QBM, n0 = nt * QBN;
-      const int cl = wn * 64 + fg * 16;  // this lane's 16 channels: n0 + cl .. +15
+      const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
       constexpr bool stats = EPI == 0;
       float bsv[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + cl + e] : 0.f;
+      for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
       float s[16], q[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
@@ -1080,7 +1086,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
         for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
         const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
         __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 16 : BUF_OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 0);
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       }
@@ -1094,18 +1100,19 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
             q[e] += __shfl_xor(q[e], o, 64);
           }
         }
-        float S = s[0], Q = q[0];  // lane fr keeps channel cl + fr (select chain: no scratch)
+        float S = s[0], Q = q[0];  // lane fr keeps value fr's channel (select chain: no scratch)
 #pragma unroll
         for (int e = 1; e < 16; ++e) {
           S = fr == e ? s[e] : S;
           Q = fr == e ? q[e] : Q;
         }
+        const int ch = ps_chan(wn, fg, fr);
         if (a.stat_acc) {
-          acc_stats(a, mt, n0 + cl + fr, make_float2(S, Q));
+          acc_stats(a, mt, n0 + ch, make_float2(S, Q));
         } else {
           // combine the two pixel-half waves through LDS, then one slab row per M tile
-          sred[(wm * 256 + cl + fr) * 2] = S;
-          sred[(wm * 256 + cl + fr) * 2 + 1] = Q;
+          sred[(wm * 256 + ch) * 2] = S;
+          sred[(wm * 256 + ch) * 2 + 1] = Q;
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
           if (tid < 256) {
             const float2 v = make_float2(sred[tid * 2] + sred[(256 + tid) * 2],
