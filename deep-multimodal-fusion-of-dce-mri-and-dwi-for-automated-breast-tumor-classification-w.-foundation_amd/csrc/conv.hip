@@ -63,6 +63,10 @@ struct ConvArgs {
   // (float64 atomics, zeroed by the caller) instead of one slab row per M
   // tile; the consumer (dmf_bn_apply) finalizes them
   int stat_acc;
+  // benchmarking only (dmf_conv_tune key 6), k_conv_fwd_ps: bit 1 skips the
+  // DMA (the loop then computes on stale LDS), bit 2 the epilogue, bit 3 its
+  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal
+  int dbg;
 };
 
 template <int ACT>
@@ -880,6 +884,116 @@ __device__ __forceinline__ int ps_perm(int row) {
 // channel offset (within the 256-column tile) of accumulator value e = 4j + r of lane group g in wave column wn
 __device__ __forceinline__ int ps_chan(int wn, int g, int e) { return wn * 64 + g * 8 + (e & 7) + ((e >> 3) << 5); }
 
+// Register epilogue of one 256x256 tile of the persistent forms (see
+// k_conv_fwd_ps): bias (+ activation) or BN partial statistics, two 16-B
+// buffer stores per pixel row straight from the accumulators. Every global
+// access is issued unconditionally (out-of-range rows get BUF_OOB offsets) so
+// a wave's vmem count is static: 16 stores (+2 float64 atomics in stat_acc
+// mode, pixel-half wm == 0 only), all YOUNGER than the in-flight DMA, which
+// the caller retires with a counted vmcnt.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+// reduce-scatter over the 16 lanes of a DPP row: returns the row's sum of
+// v[lane & 15]. Four halving rounds (partners lane ^ 15 by row_mirror,
+// (lane & 8) | (7 - lane & 7) by row_half_mirror, then quad xor 2 and xor 1):
+// 15 exchanged values per lane instead of 64 shuffles of a full butterfly.
+__device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int fr) {
+  const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float keep = b3 ? v[k + 8] : v[k], send = b3 ? v[k] : v[k + 8];
+    v[k] = keep + dpp_f<0x140>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float keep = b2 ? v[k + 4] : v[k], send = b2 ? v[k] : v[k + 4];
+    v[k] = keep + dpp_f<0x141>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float keep = b1 ? v[k + 2] : v[k], send = b1 ? v[k] : v[k + 2];
+    v[k] = keep + dpp_f<0x4E>(send);
+  }
+  const float keep = b0 ? v[1] : v[0], send = b0 ? v[0] : v[1];
+  return keep + dpp_f<0xB1>(send);
+}
+
+template <int EPI, int TBN = QBN>
+__device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[8][4], int lin,
+                                            __amdgpu_buffer_rsrc_t ry, float* sred, const float* sbias, int tid,
+                                            int wm, int wn, int fr, int fg) {
+  constexpr int FM = 8, FN = 4;
+  const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+  const int m0 = mt * QBM, n0 = nt * TBN;
+  const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
+  constexpr bool stats = EPI == 0;
+  float bsv[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
+  float s[16], q[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * (QBM / QWM) + i * 16 + fr;
+    const bool ok = m < a.M;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bsv[j * 4 + r];
+    if (stats) {
+      const float w = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
+    } else if constexpr (EPI > 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = apply_act<EPI - 1>(v[e]);
+    }
+    uint32_t w8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+    const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
+    if (a.dbg & 32) {
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 2);
+    } else if (!(a.dbg & 8)) {
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  if (stats && !(a.dbg & 16)) {
+    // lane fr of lane group fg ends with the 16 pixel lanes' totals of value fr's channel
+    const float S = row_reduce_scatter16(s, fr), Q = row_reduce_scatter16(q, fr);
+    const int ch = ps_chan(wn, fg, fr);
+    if (a.stat_acc) {
+      // the two pixel-half waves of each channel slab meet in LDS: half the atomics
+      // (the K-step barriers order this slot's reuse by the next tile's epilogue)
+      if (wm == 1) {
+        sred[ch * 2] = S;
+        sred[ch * 2 + 1] = Q;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (wm == 0) acc_stats(a, mt, n0 + ch, make_float2(S + sred[ch * 2], Q + sred[ch * 2 + 1]));
+    } else {
+      // combine the two pixel-half waves through LDS, then one slab row per M tile
+      sred[(wm * TBN + ch) * 2] = S;
+      sred[(wm * TBN + ch) * 2 + 1] = Q;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid < TBN) {
+        const float2 v = make_float2(sred[tid * 2] + sred[(TBN + tid) * 2],
+                                     sred[tid * 2 + 1] + sred[(TBN + tid) * 2 + 1]);
+        *(float2*)(a.partials + ((size_t)mt * a.Nout + n0 + tid) * 2) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+}
+
 // EPI: the epilogue, fixed at compile time so only its path is in the code
 // (a runtime switch per tile inflated the kernel to ~13 k instructions of
 // activation variants): 0 = BN partial statistics (no activation), 1 + act =
@@ -998,7 +1112,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     // wave's part and orders the refill of the other stage after every wave's reads of the previous
     // step. After an epilogue its 16 stores (+2 atomics) are younger: leave them in flight.
     if (epi) {
-      if (a.stat_acc > 0 || a.stat_acc == -1)
+      if ((a.stat_acc > 0 || a.stat_acc == -1) && wm == 0)
         asm volatile("s_waitcnt vmcnt(18)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       epi = false;
@@ -1036,7 +1150,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if (more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
+        if (more && (i & 1) == 0 && !(a.dbg & 2)) piece(kk * 4 + (i >> 1));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&wv[j], *(bf16x8_t*)&pv[i], acc[i][j], 0,
@@ -1049,81 +1163,8 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
       continue;
     }
     // ---------------- epilogue of tile `lin` (the next tile's step 0 is in flight)
-    // Every global access here is issued unconditionally (buffer stores with an
-    // out-of-range offset for rows past M) so the wave's vmem count is static:
-    // PS_EPI_OPS stores (+2 atomics in stat_acc mode), all YOUNGER than the
-    // in-flight DMA, which the loop head then retires with a counted vmcnt.
-    {
-      const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-      const int m0 = mt * QBM, n0 = nt * QBN;
-      const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
-      constexpr bool stats = EPI == 0;
-      float bsv[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
-      float s[16], q[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * (QBM / QWM) + i * 16 + fr;
-        const bool ok = m < a.M;
-        float v[16];
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bsv[j * 4 + r];
-        if (stats) {
-          const float w = ok ? 1.f : 0.f;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
-        } else if constexpr (EPI > 1) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] = apply_act<EPI - 1>(v[e]);
-        }
-        uint32_t w8[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
-        const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 0);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-      if (stats) {
-        // butterfly over the 16 pixel lanes of this lane group: every lane gets the totals
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s[e] += __shfl_xor(s[e], o, 64);
-            q[e] += __shfl_xor(q[e], o, 64);
-          }
-        }
-        float S = s[0], Q = q[0];  // lane fr keeps value fr's channel (select chain: no scratch)
-#pragma unroll
-        for (int e = 1; e < 16; ++e) {
-          S = fr == e ? s[e] : S;
-          Q = fr == e ? q[e] : Q;
-        }
-        const int ch = ps_chan(wn, fg, fr);
-        if (a.stat_acc) {
-          acc_stats(a, mt, n0 + ch, make_float2(S, Q));
-        } else {
-          // combine the two pixel-half waves through LDS, then one slab row per M tile
-          sred[(wm * 256 + ch) * 2] = S;
-          sred[(wm * 256 + ch) * 2 + 1] = Q;
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          if (tid < 256) {
-            const float2 v = make_float2(sred[tid * 2] + sred[(256 + tid) * 2],
-                                         sred[tid * 2 + 1] + sred[(256 + tid) * 2 + 1]);
-            *(float2*)(a.partials + ((size_t)mt * a.Nout + n0 + tid) * 2) = v;
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-      }
-    }
-    epi = true;
+    if (!(a.dbg & 4)) ps_epilogue<EPI>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
+    epi = !(a.dbg & 4);
     if (!more) break;
     t = tnext;
     lin = xcd_remap(t, ntile);
@@ -1541,6 +1582,7 @@ static int g_ps_enable = [] {
   const char* e = std::getenv("DMF_PS");
   return e && e[0] == '0' ? 0 : 1;
 }();
+static int g_ps_dbg = 0;
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1663,6 +1705,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
     const int epi = a.partials != nullptr ? 0 : 1 + a.act;
+    a.dbg = g_ps_dbg;
     DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
 #define DMF_PS(E)                                                                                      \
   do {                                                                                                 \
@@ -1828,6 +1871,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 2: DMF_CHECK_ARG(value >= 0 && value <= 6, "dmf_conv_tune: forced tile %d", value); g_force = value; return 0;
     case 3: DMF_CHECK_ARG(value >= -2 && value <= 64, "dmf_conv_tune: stat mode %d", value); g_stat_mode = value; return 0;
     case 4: g_ps_enable = value != 0; return 0;
+    case 6: g_ps_dbg = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

@@ -36,6 +36,22 @@ SHAPES = [
 ]
 
 
+ACC = [False]  # --acc: BN statistics into a float64 arena (dmf_conv2d_fwd_acc), as the training forward does
+
+
+def _fwd_acc(x, weight, g, caches, acc):
+    import dmf_native as N
+    n, cx, h, w, ldx = O.nhwc(x)
+    co, ci, kh, kw = weight.shape
+    ho, wo = g.out_hw(h, w)
+    y = O.empty_nhwc(n, co, ho, wo, x.dtype, x.device)
+    wk = caches[0].get(weight, x.dtype, cx, 0)
+    N.call("dmf_conv2d_fwd_acc", O.dt(x), x.data_ptr(), n, h, w, cx, ldx, None, 0, 0, wk.data_ptr(), co, kh, kw,
+           g.stride, g.pad, g.dil, None, y.data_ptr(), ho, wo, O.nhwc(y)[4], acc.data_ptr(), O.BN_ACC_REPLICAS, None,
+           N.ACT_NONE, O._stream())
+    return y
+
+
 def run_shape(shape, reps, stats, dtype=torch.bfloat16):
     n, h, w, ci, co, k, st, dl = shape
     conv = torch.nn.Conv2d(ci, co, k, stride=st, padding=(k // 2) * dl, dilation=dl, bias=False).cuda()
@@ -43,15 +59,23 @@ def run_shape(shape, reps, stats, dtype=torch.bfloat16):
     x = torch.randn(n, ci, h, w, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
     g = O.ConvGeom(conv)
     caches = (O.WeightCache(), O.WeightCache())
+    acc = torch.zeros(2 * co * O.BN_ACC_REPLICAS, dtype=torch.float64, device="cuda")
+
+    def launch():
+        if ACC[0] and stats and O._is_mfma_conv(conv.weight, g):
+            _fwd_acc(x, conv.weight, g, caches, acc)
+        else:
+            O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
+
     with torch.no_grad():
         for _ in range(3):
-            O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
+            launch()
         torch.cuda.synchronize()
         # replay R launches from a hipGraph: GPU time only (no Python launch overhead)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for _ in range(reps):
-                O._conv_forward_raw(x, conv.weight, None, g, caches, stats, "none")
+                launch()
         graph.replay()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -110,7 +134,9 @@ def main():
     ap.add_argument("--tunes", default="", help="A/B variants, e.g. '0:0;0:1,1:0;0:1,1:1' (dmf_conv_tune key:value "
                                                 "lists), timed interleaved in this process")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--acc", action="store_true", help="BN statistics into the float64 arena (the training forward's mode)")
     a = ap.parse_args()
+    ACC[0] = a.acc
     if a.tunes:
         return ab(a)
     shapes = SHAPES
