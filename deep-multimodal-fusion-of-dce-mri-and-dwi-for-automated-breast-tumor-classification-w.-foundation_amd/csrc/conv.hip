@@ -1829,32 +1829,95 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
 //   mode 1: [CinP][KH][KW][Cout]   (dgrad B operand)
 //   mode 2: [CinP][KH][KW][Cout] with the taps flipped (r -> KH-1-r, s -> KW-1-s):
 //           a stride-1 dgrad is then a forward conv of dY (pad' = dil*(K-1) - pad)
+// element i of the re-laid-out weight (see k_weight_prep's modes)
+__device__ __forceinline__ float weight_prep_elem(const float* __restrict__ w, long long i, int Cout, int Cin,
+                                                  int CinP, int KH, int KW, int mode) {
+  int co, ci, r, s;
+  if (mode == 0) {
+    ci = (int)(i % CinP);
+    long long t = i / CinP;
+    s = (int)(t % KW); t /= KW;
+    r = (int)(t % KH);
+    co = (int)(t / KH);
+  } else {
+    co = (int)(i % Cout);
+    long long t = i / Cout;
+    s = (int)(t % KW); t /= KW;
+    r = (int)(t % KH);
+    ci = (int)(t / KH);
+  }
+  if (mode == 2) {
+    r = KH - 1 - r;
+    s = KW - 1 - s;
+  }
+  return ci < Cin ? w[(((long long)co * Cin + ci) * KH + r) * KW + s] : 0.f;
+}
+
+// Every re-layout of a training step in ONE launch (dmf_conv_weight_prep_multi).
+// Block code = (job << 40) | unit. Mode 0 ([Cout][KH][KW][CinP], rows of CinP
+// channels): unit = first output element of a WPM_SPAN run, 32-bit index math,
+// stores coalesced, the reads a KH*KW-strided walk over one torch row (L1/L2
+// hits). Modes 1/2 ([CinP][KH][KW][Cout]) are a transpose of the torch
+// [Cout][Cin*KH*KW] matrix (taps flipped for mode 2): unit = one 64x64 tile
+// staged through LDS, both the reads (along K) and the writes (along Cout)
+// coalesced -- a per-element gather there strides Cin*KH*KW floats per lane.
+constexpr int WPM_SPAN = 4096;
+__device__ __forceinline__ void wprep_store(const dmf_wprep_job& J, long long i, float v) {
+  if (J.dtype == DMF_BF16) ((bf16_t*)J.out)[i] = f2bf(v);
+  else ((float*)J.out)[i] = v;
+}
+__global__ void __launch_bounds__(256) k_weight_prep_multi(const dmf_wprep_job* __restrict__ jobs,
+                                                           const long long* __restrict__ blk) {
+  __shared__ float tile[64][65];
+  const long long code = blk[blockIdx.x];
+  const dmf_wprep_job J = jobs[(int)(code >> 40)];
+  const int unit = (int)(code & ((1LL << 40) - 1));
+  const int taps = J.KH * J.KW;
+  const int tid = threadIdx.x;
+  if (J.mode == 0) {
+    const int total = J.Cout * taps * J.CinP;
+    const int end = min(total, unit + WPM_SPAN);
+    for (int i = unit + tid; i < end; i += 256) {
+      const int row = i / J.CinP, ci = i - row * J.CinP;  // row = co * taps + (r, s)
+      const int co = row / taps, rs = row - co * taps;
+      const float v = ci < J.Cin ? J.w[((size_t)co * J.Cin + ci) * taps + rs] : 0.f;
+      wprep_store(J, i, v);
+    }
+    return;
+  }
+  const int K = J.CinP * taps;  // output rows
+  const int ctiles = (J.Cout + 63) / 64;
+  const int k0 = (unit / ctiles) * 64, co0 = (unit % ctiles) * 64;
+  const int tx = tid & 63, ty = tid >> 6;
+  // load: tile[kk][c] = W[co0 + c][src(k0 + kk)], lanes along kk (source columns nearly consecutive)
+  {
+    const int kk = k0 + tx;
+    int src = -1;
+    if (kk < K) {
+      const int ci = kk / taps, rs = kk - ci * taps;
+      const int r = rs / J.KW, s = rs - r * J.KW;
+      const int rr = J.mode == 2 ? J.KH - 1 - r : r, ss = J.mode == 2 ? J.KW - 1 - s : s;
+      if (ci < J.Cin) src = (ci * J.KH + rr) * J.KW + ss;
+    }
+    for (int c = ty; c < 64; c += 4) {
+      const int co = co0 + c;
+      tile[tx][c] = (src >= 0 && co < J.Cout) ? J.w[(size_t)co * J.Cin * taps + src] : 0.f;
+    }
+  }
+  __syncthreads();
+  for (int kk = ty; kk < 64; kk += 4) {
+    const int k = k0 + kk, co = co0 + tx;
+    if (k < K && co < J.Cout) wprep_store(J, (size_t)k * J.Cout + co, tile[kk][tx]);
+  }
+}
+
 template <typename T>
 __global__ void k_weight_prep(const float* __restrict__ w, T* __restrict__ out, int Cout, int Cin, int CinP, int KH,
                               int KW, int mode) {
   const long long total = (long long)Cout * CinP * KH * KW;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    int co, ci, r, s;
-    if (mode == 0) {
-      ci = (int)(i % CinP);
-      long long t = i / CinP;
-      s = (int)(t % KW); t /= KW;
-      r = (int)(t % KH);
-      co = (int)(t / KH);
-    } else {
-      co = (int)(i % Cout);
-      long long t = i / Cout;
-      s = (int)(t % KW); t /= KW;
-      r = (int)(t % KH);
-      ci = (int)(t / KH);
-    }
-    if (mode == 2) {
-      r = KH - 1 - r;
-      s = KW - 1 - s;
-    }
-    const float v = ci < Cin ? w[(((long long)co * Cin + ci) * KH + r) * KW + s] : 0.f;
-    out[i] = Cvt<T>::store(v);
+    out[i] = Cvt<T>::store(weight_prep_elem(w, i, Cout, Cin, CinP, KH, KW, mode));
   }
 }
 
@@ -1990,6 +2053,14 @@ extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo
   a.M = N * H * W;
   a.act = DMF_ACT_NONE;
   return launch_conv(dtype, true, a, (hipStream_t)stream, "dmf_conv2d_dgrad");
+}
+
+extern "C" int dmf_conv_weight_prep_multi(const dmf_wprep_job* jobs, const long long* blk, long long nblocks,
+                                          void* stream) {
+  DMF_CHECK_ARG(jobs && blk && nblocks > 0 && nblocks < (1LL << 31), "dmf_conv_weight_prep_multi: bad tables");
+  hipLaunchKernelGGL(k_weight_prep_multi, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, jobs, blk);
+  DMF_LAUNCH_CHECK("dmf_conv_weight_prep_multi");
+  return 0;
 }
 
 extern "C" int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW,

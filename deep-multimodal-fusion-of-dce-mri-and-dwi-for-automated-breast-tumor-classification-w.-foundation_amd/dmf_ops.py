@@ -15,6 +15,7 @@ import ctypes
 import itertools
 import math
 import os
+import weakref
 
 import torch
 
@@ -107,10 +108,104 @@ RNG = _Rng()
 
 
 # ------------------------------------------------------------ weight cache
+class _WPrepJob(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("dtype", ctypes.c_int), ("Cout", ctypes.c_int),
+                ("Cin", ctypes.c_int), ("CinP", ctypes.c_int), ("KH", ctypes.c_int), ("KW", ctypes.c_int),
+                ("mode", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
+WPREP_SPAN = 4096  # output elements per mode-0 block of dmf_conv_weight_prep_multi (modes 1/2: 64x64 tiles)
+
+
+class PrepPlan:
+    """Every trainable conv weight's re-layouts of a training step in ONE
+    launch (dmf_conv_weight_prep_multi) instead of one dmf_conv_weight_prep
+    per conv and layout (mode B: ~330 launches of ~6 us per step).
+
+    ``prep_step(module)`` -- called by the training steps before their forward
+    -- re-lays-out every (weight, dtype, CinP, mode) of the module's trainable
+    parameters the plan has seen into its persistent buffer; until
+    ``invalidate()`` (the optimizers call it after updating the weights)
+    ``WeightCache.get`` returns those buffers. A layout first asked for during
+    a step is prepared on its own (as without a plan) into a new persistent
+    buffer and joins the plan for the next step. A weight whose ``_version``
+    moved since the batched launch (an in-place update by torch) is
+    re-prepared individually."""
+
+    def __init__(self):
+        self.entries = {}  # (data_ptr, dtype, cinp, mode) -> Entry
+        self.gen = 0
+        self.fresh = False
+        self.tables = {}  # (device, signature) -> (jobs tensor, blk tensor, nblocks)
+        self.enabled = os.environ.get("DMF_PREP_PLAN", "1") != "0"
+
+    class Entry:
+        __slots__ = ("ref", "out", "version", "gen", "serial")
+        serials = itertools.count()
+
+        def __init__(self, weight, out):
+            self.serial = next(PrepPlan.Entry.serials)
+            self.ref = weakref.ref(weight)
+            self.out = out
+            self.version = None
+            self.gen = -1
+
+    def lookup(self, weight, key):
+        e = self.entries.get(key)
+        if e is not None and e.ref() is not weight:  # storage reused by another tensor
+            del self.entries[key]
+            e = None
+        return e
+
+    def prep_step(self, module):
+        """One batched re-layout of ``module``'s planned weights (no-op before
+        the plan has seen a step, or on the first use inside a capture)."""
+        if not self.enabled or not self.entries:
+            return
+        ptrs = {p.data_ptr(): p for p in module.parameters() if p.requires_grad and p.is_cuda}
+        live = [(k, e) for k, e in self.entries.items() if k[0] in ptrs and e.ref() is ptrs[k[0]]]
+        if not live:
+            return
+        dev = live[0][1].out.device
+        sig = (dev.index or 0, tuple((k, e.serial) for k, e in live))
+        t = self.tables.get(sig)
+        if t is None:
+            if torch.cuda.is_current_stream_capturing():
+                return  # a table needs a host->device copy: stay on the per-conv path
+            jobs = (_WPrepJob * len(live))()
+            blk = []
+            for j, ((_, dtype, cinp, mode), e) in enumerate(live):
+                w = e.ref()
+                co, ci, kh, kw = w.shape
+                jobs[j] = _WPrepJob(w.data_ptr(), e.out.data_ptr(), N.dtype_code(dtype), co, ci, cinp, kh, kw, mode,
+                                    0)
+                if mode == 0:
+                    blk.extend((j << 40) | s for s in range(0, co * cinp * kh * kw, WPREP_SPAN))
+                else:  # 64x64 transpose tiles
+                    blk.extend((j << 40) | t for t in range(-(-cinp * kh * kw // 64) * -(-co // 64)))
+            t = (torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(dev),
+                 torch.tensor(blk, dtype=torch.int64).to(dev), len(blk))
+            self.tables[sig] = t
+        N.call("dmf_conv_weight_prep_multi", t[0].data_ptr(), t[1].data_ptr(), t[2], _stream())
+        self.gen += 1
+        for _, e in live:
+            e.version = e.ref()._version
+            e.gen = self.gen
+        self.fresh = True
+
+    def invalidate(self):
+        self.fresh = False
+
+
+PREP = PrepPlan()
+
+
 class WeightCache:
     """Device re-layout of a conv weight ([Cout][KH][KW][CinP] / transposed)
     in the compute dtype. Frozen weights are prepared once per version;
-    trainable ones every call (so a captured graph re-reads updated params)."""
+    trainable ones every step -- by the step's batched PrepPlan launch, or
+    per call outside a planned training step (so a captured graph re-reads
+    updated params either way)."""
 
     def __init__(self):
         self.key = None
@@ -122,10 +217,19 @@ class WeightCache:
         if not weight.requires_grad and self.key == key:
             return self.val
         shape = (co, kh, kw, cinp) if mode == 0 else (cinp, kh, kw, co)
-        out = torch.empty(shape, dtype=dtype, device=weight.device)
         w = weight.detach()
         if not w.is_contiguous():
             w = w.contiguous()
+        entry = None
+        if weight.requires_grad and PREP.enabled and w.data_ptr() == weight.data_ptr():
+            pk = (weight.data_ptr(), dtype, cinp, mode)
+            entry = PREP.lookup(weight, pk)
+            if entry is not None and PREP.fresh and entry.gen == PREP.gen and entry.version == weight._version:
+                return entry.out
+            if entry is None:
+                entry = PrepPlan.Entry(weight, torch.empty(shape, dtype=dtype, device=weight.device))
+                PREP.entries[pk] = entry
+        out = entry.out if entry is not None else torch.empty(shape, dtype=dtype, device=weight.device)
         N.call("dmf_conv_weight_prep", N.dtype_code(dtype), w.data_ptr(), out.data_ptr(), co, ci, cinp, kh, kw, mode,
                _stream())
         if not weight.requires_grad:

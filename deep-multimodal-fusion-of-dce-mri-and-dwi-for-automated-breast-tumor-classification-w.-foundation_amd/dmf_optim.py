@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 
 import dmf_native as N
+import dmf_ops as O
 
 CHUNK = 8192
 
@@ -134,6 +135,7 @@ class FusedAdamW(torch.optim.Optimizer):
         live = self._live()
         if not live:
             return loss
+        O.PREP.invalidate()  # the weights change: the step's batched conv re-layouts go stale
         capturing = torch.cuda.is_current_stream_capturing()
         if not capturing:
             self.sync_hyper()

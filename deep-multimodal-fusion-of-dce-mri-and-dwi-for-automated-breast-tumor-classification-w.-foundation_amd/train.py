@@ -175,6 +175,8 @@ class LightningSingleModel(nn.Module):
         return load_from_checkpoint(cls, checkpoint_path, map_location=map_location, strict=strict, **kwargs)
 
     def training_step(self, batch, batch_idx=0):
+        # every trainable conv weight's re-layouts for this step in one launch (dmf_ops.PrepPlan)
+        O.PREP.prep_step(self)
         return self._shared_step(batch, batch_idx, "train")
 
     def validation_step(self, batch, batch_idx=0):

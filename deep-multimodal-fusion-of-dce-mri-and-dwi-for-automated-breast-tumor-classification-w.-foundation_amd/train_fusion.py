@@ -196,6 +196,8 @@ class LightningFusionModel(nn.Module):
         return load_from_checkpoint(cls, checkpoint_path, map_location=map_location, strict=strict, **kwargs)
 
     def training_step(self, batch, batch_idx=0):
+        # every trainable conv weight's re-layouts for this step in one launch (dmf_ops.PrepPlan)
+        O.PREP.prep_step(self)
         return self._shared_step(batch, "train")
 
     def validation_step(self, batch, batch_idx=0):

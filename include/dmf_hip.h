@@ -106,6 +106,18 @@ int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
                          void* stream);
+/* Batched re-layout: every conv weight a training step uses, in one launch
+ * (replaces one dmf_conv_weight_prep per conv per step). jobs: device array of
+ * dmf_wprep_job; blk: device array of nblocks block codes (job index << 40) |
+ * unit, unit = first element of a 4096-element run (mode 0) or index of a
+ * 64x64 output tile, K-tile major (modes 1/2). No reference
+ * counterpart: the reference lets cuDNN read the torch-layout weights. */
+typedef struct {
+  const float* w; /* torch layout [Cout][Cin][KH][KW], fp32 */
+  void* out;      /* re-laid-out copy, DMF_BF16 or DMF_F32 */
+  int dtype, Cout, Cin, CinP, KH, KW, mode, pad_;
+} dmf_wprep_job;
+int dmf_conv_weight_prep_multi(const dmf_wprep_job* jobs, const long long* blk, long long nblocks, void* stream);
 int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M);
 int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
                      int ldx2, const void* dy, int Ho, int Wo, int Cout, int lddy, int KH, int KW, int stride, int pad,
