@@ -390,8 +390,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 // range check -- no branches, no 64-bit address math. The K-step's tap and
 // channel offsets are block-uniform (SGPR soffset). PADCHK = false for 1x1,
 // stride-1, pad-0 convs (no per-row bounds at all).
-constexpr unsigned BUF_OOB = 0x80000000u;
-constexpr int BUF_FLAGS = 0x00020000;
 
 // INA >= 0 (plain 1x1 only, PADCHK = DUAL = false): the producer's BN apply
 // + activation x <- act(x*scale + shift) runs on each A chunk between its
@@ -580,23 +578,6 @@ __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN
 constexpr int WBM = 256, WBN = 128, WSTAGE = (WBM + WBN) * 128, WNSTAGE = 3;
 constexpr int WWM = 4, WWN = 2, WTHREADS = 64 * WWM * WWN;  // 8 waves of 64x64: two per SIMD
 constexpr int WLDS = WNSTAGE * WSTAGE;  // 147456 B: also holds the C staging tile
-
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ v4i_t buf_rsrc(const void* p, long long bytes) {
-  const unsigned long long u = (unsigned long long)p;
-  return v4i_t{(int)(unsigned)u, (int)(unsigned)(u >> 32), (int)bytes, BUF_FLAGS};
-}
-// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff(+soff) to LDS
-// [lds, lds + 1 KiB). Inline asm so the compiler neither tracks it (it would
-// drain vmcnt(0) before every ds_read it cannot disambiguate) nor reorders it
-// across LDS accesses; m0 is saved and restored.
-__device__ __forceinline__ void dma16(v4i_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
-               : "memory");
-}
 
 template <bool PADCHK, bool DUAL>
 __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {

@@ -11,6 +11,8 @@
 // model_module.py:117, :187) and the 1-input-channel 1x1 convs
 // (MaskGuidedSpatialAttention.mask_processor[0], Projector on r1/r2,
 // model_module.py:68, :639-640).
+#include <algorithm>
+
 #include "dmf_common.h"
 #include "../../include/dmf_hip.h"
 
@@ -348,6 +350,144 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
       }
 }
 
+// k_conv_wgrad_tr<2, 2> with both operands staged by LDS-DMA (buffer_load ...
+// lds) instead of global -> VGPR -> ds_write_b128: the register-staged form
+// spends 8 ds_write_b128 per thread per K-step (13 LDS-transfer cycles each,
+// ~830 cycles per 64-pixel step at two workgroups per CU against ~1024 MFMA
+// cycles), which the DMA path does not pay. Same 128x128 tile, 64-pixel
+// K-steps, sub-image layout (wtr_off) and transposed fragment reads; the XOR
+// swizzle is applied on the source side: DMA piece p of wave w lands rows
+// 16w + 4p .. +3 (lane -> row 16w + 4p + lane/16, slot lane%16), so the lane
+// loads chunk slot ^ (((lane/16) << 2) | p). Zero padding, pixel tails and
+// channel tails read zeros from the buffer range check. Two stages, the next
+// step's 8 pieces per wave issued right after the barrier that frees them.
+// DUAL (channel-concat input): each 128-column tile must lie in one tap of
+// one source (Cin % 128 == 0, C1 % 128 == 0), so the source is wave-uniform.
+template <bool DUAL>
+__global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 64, SUB = BK * 256, STAGE = 2 * SUB, NP = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x % a.ntiles;
+  const int co0 = mt * BM, k0 = nt * BN;
+  const int p_begin = blockIdx.y * a.pix_per_split;
+  const int p_end = min(a.M, p_begin + a.pix_per_split);
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  const v4i_t rdy = buf_rsrc(a.dy, (long long)a.M * a.lddy * 2);
+  // B source of this tile (one tap, one source when DUAL)
+  const int tap0 = k0 / a.Cin;
+  const bool hi_src = DUAL && (k0 - tap0 * a.Cin) >= a.C1;
+  const v4i_t rx = hi_src ? buf_rsrc(a.x2, (long long)a.N * a.H * a.W * a.ldx2 * 2)
+                          : buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * 2);
+  const int ldxs = hi_src ? a.ldx2 : a.ldx;
+
+  // per piece: this lane's chunk, A channel, B (tap offsets, channel) and gather-row cursor
+  int ach[NP], bci[NP], roff[NP], soff[NP], cn[NP], cho[NP], cwo[NP];
+  bool aok[NP], bok[NP];
+  const int hw = a.Ho * a.Wo;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int ch = (lane & 15) ^ (((lane >> 4) << 2) | p);
+    ach[p] = co0 + ch * 8;
+    aok[p] = ach[p] < a.Cout;
+    const int kcol = k0 + ch * 8;
+    bok[p] = kcol < a.Ktot;
+    const int tap = bok[p] ? kcol / a.Cin : 0;
+    int ci = kcol - tap * a.Cin;
+    if (hi_src) ci -= a.C1;
+    bci[p] = ci;
+    roff[p] = (tap / a.KW) * a.dil - a.pad;
+    soff[p] = (tap % a.KW) * a.dil - a.pad;
+    const int pix = p_begin + wid * 16 + p * 4 + (lane >> 4);
+    cn[p] = pix / hw;
+    const int rem = pix - cn[p] * hw;
+    cho[p] = rem / a.Wo;
+    cwo[p] = rem - cho[p] * a.Wo;
+  }
+  const int dho = BK / a.Wo, dwo = BK % a.Wo;
+  auto issue = [&](int stage, int kb) {
+    const unsigned As = lds0 + stage * STAGE, Bs = As + SUB;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int row = wid * 16 + p * 4;
+      const int pix = kb + row + (lane >> 4);
+      const bool pin = pix < p_end;
+      const unsigned ao = (pin && aok[p]) ? (unsigned)(((long long)pix * a.lddy + ach[p]) * 2) : BUF_OOB;
+      dma16(rdy, ao, 0, As + row * 256);
+      const int hi = cho[p] * a.stride + roff[p], wi = cwo[p] * a.stride + soff[p];
+      const bool ok = pin && bok[p] && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const unsigned bo = ok ? (unsigned)((((long long)(cn[p] * a.H + hi) * a.W + wi) * ldxs + bci[p]) * 2) : BUF_OOB;
+      dma16(rx, bo, 0, Bs + row * 256);
+      int wo = cwo[p] + dwo, ho = cho[p] + dho, n = cn[p];
+      if (wo >= a.Wo) { wo -= a.Wo; ++ho; }
+      while (ho >= a.Ho) { ho -= a.Ho; ++n; }
+      cwo[p] = wo; cho[p] = ho; cn[p] = n;
+    }
+  };
+
+  f32x4_w acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p_end - p_begin + BK - 1) / BK;
+  if (nk > 0) issue(0, p_begin);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt is the only DMA in flight: retire it; the barrier publishes every wave's
+    // pieces and orders the refill of the other stage after every wave's reads of step kt-1
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 1 < nk) issue((kt + 1) & 1, p_begin + (kt + 1) * BK);
+    const char* SA = smem + (kt & 1) * STAGE;
+    const char* SB = SA + SUB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_w af[4], bfr[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int cl = wm * 64 + i * 16;
+          const char* pa = SA + wtr_off(row, (cl >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pa);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cl = wn * 64 + j * 16;
+          const char* pb = SB + wtr_off(row, (cl >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* slab = a.ws + (size_t)blockIdx.y * a.Cout * a.Ktot;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * 64 + i * 16 + fg * 4 + e;
+        const int k = k0 + wn * 64 + j * 16 + fr;
+        if (co < a.Cout && k < a.Ktot) slab[(size_t)co * a.Ktot + k] = acc[i][j][e];
+      }
+}
+
 // Gate gradient of a channel-gated conv input y = x * gate[n][c] (the SE
 // block in front of the backbone stem, model_module.py:584-591) from the
 // per-sample weight-gradient slabs G_n = sum_{pixels of n} dY (x) im2col(y):
@@ -615,13 +755,33 @@ static int wgrad_tr_enabled() {
   return v;
 }
 
+// LDS-DMA staging for the bf16 transposed-read weight gradient (k_conv_wgrad_dma);
+// DMF_WGRAD_DMA=0 keeps the register-staged k_conv_wgrad_tr, dmf_conv_wgrad_tune(0, v) switches at run time
+static int g_wgrad_dma = [] {
+  const char* e = std::getenv("DMF_WGRAD_DMA");
+  return e && e[0] == '0' ? 0 : 1;
+}();
+static int wgrad_dma_enabled() { return g_wgrad_dma; }
+
+extern "C" int dmf_conv_wgrad_tune(int key, int value) {
+  DMF_CHECK_ARG(key == 0, "dmf_conv_wgrad_tune: unknown key %d", key);
+  g_wgrad_dma = value != 0;
+  return 0;
+}
+
 extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M) {
   const long long tiles = (long long)cdiv(Cout, 128) * cdiv((long long)KH * KW * Cin, 128);
   // transposed-read kernel: ~2 resident blocks per CU, and every split costs
   // a Cout x K fp32 slab round trip, so aim for one wave of 512 blocks
   const long long target = (dtype == DMF_BF16 && wgrad_tr_enabled()) ? 512 : 1024;
   long long want = (target + tiles - 1) / tiles;
-  long long maxs = (M + 1023) / 1024;              // >= 1024 pixels per split
+  // >= 256 pixels (4 K-steps) per split, and at most 64 MiB of fp32 slabs: a small
+  // weight (64x64 1x1: one tile) then runs 128 splits of 4 K-steps instead of 32
+  // latency-bound splits of 16 (~20 us -> a few us), a large one keeps its split count
+  long long maxs = (M + 255) / 256;
+  const long long slab = (long long)Cout * KH * KW * Cin;
+  const long long maxb = std::max(1LL, (16LL << 20) / std::max(1LL, slab));
+  if (maxs > maxb) maxs = maxb;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
   if (want > 512) want = 512;
@@ -665,6 +825,11 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
     a.ntiles = cdiv(a.Ktot, 256);
     grid = dim3(a.mtiles * a.ntiles, splits);
     hipLaunchKernelGGL((k_conv_wgrad_tr<2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+  } else if (dtype == DMF_BF16 && wgrad_tr_enabled() && wgrad_dma_enabled() &&
+             (long long)a.N * a.H * a.W * std::max(a.ldx, x2 ? a.ldx2 : 0) * 2 < (1LL << 31) &&
+             (long long)a.M * a.lddy * 2 < (1LL << 31) && (!x2 || (a.Cin % 128 == 0 && a.C1 % 128 == 0))) {
+    if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((k_conv_wgrad_dma<false>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
   } else if (dtype == DMF_BF16 && wgrad_tr_enabled())
     hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
   else if (dtype == DMF_BF16)

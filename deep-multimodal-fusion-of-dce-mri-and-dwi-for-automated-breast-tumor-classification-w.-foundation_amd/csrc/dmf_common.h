@@ -199,4 +199,27 @@ __device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// ------------------------------------------------ raw buffer loads / LDS-DMA
+// Out-of-range lanes (tile edges, zero padding) get an offset past the buffer
+// and read zeros from the range check: no branches, no 64-bit address math.
+constexpr unsigned BUF_OOB = 0x80000000u;
+constexpr int BUF_FLAGS = 0x00020000;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i_t buf_rsrc(const void* p, long long bytes) {
+  const unsigned long long u = (unsigned long long)p;
+  return v4i_t{(int)(unsigned)u, (int)(unsigned)(u >> 32), (int)bytes, BUF_FLAGS};
+}
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff(+soff) to LDS
+// [lds, lds + 1 KiB). Inline asm so the compiler neither tracks it (it would
+// drain vmcnt(0) before every ds_read it cannot disambiguate) nor reorders it
+// across LDS accesses; m0 is saved and restored.
+__device__ __forceinline__ void dma16(v4i_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+               : "memory");
+}
+
+
 }  // namespace dmf

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Weight-gradient microbench on the hot path's conv shapes (bf16, B=32): the
+split-K slab kernel (dmf_conv2d_wgrad) per shape, HIP events over a hipGraph
+of R launches, for each engine variant (dmf_conv_wgrad_tune key 0: LDS-DMA
+staging on / off), interleaved; the reduced gradients of the variants are
+compared (they share the MFMA order, so they must agree bit for bit).
+
+    python tools/wgrad_bench.py [--from profiles/r02o_conv_launches.jsonl] [--reps 10] [--rounds 3]
+"""
+import argparse
+import collections
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "deep-multimodal-fusion-of-dce-mri-and-dwi-for-automated-breast-tumor-classification-w.-foundation_amd")
+sys.path[:0] = [ROOT, PKG]
+
+import torch  # noqa: E402
+
+import dmf_native as N  # noqa: E402
+import dmf_ops as O  # noqa: E402
+
+
+def setup(shape):
+    n, h, w, ci, co, k, st, dl = shape
+    pad = (k // 2) * dl
+    ho, wo = (h + 2 * pad - dl * (k - 1) - 1) // st + 1, (w + 2 * pad - dl * (k - 1) - 1) // st + 1
+    x = torch.randn(n, ci, h, w, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, co, ho, wo, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    m = n * ho * wo
+    splits = N.load().dmf_conv2d_wgrad_splits(N.BF16, co, ci, k, k, m)
+    ws = torch.empty(splits * co * k * k * ci, dtype=torch.float32, device="cuda")
+    dw = torch.empty(co, ci, k, k, dtype=torch.float32, device="cuda")
+
+    def launch():
+        N.call("dmf_conv2d_wgrad", N.BF16, x.data_ptr(), n, h, w, ci, ci, None, 0, 0, dy.data_ptr(), ho, wo, co, co, k,
+               k, st, pad, dl, splits, ws.data_ptr(), O._stream())
+
+    def reduce():
+        N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), splits, co, ci, ci, k, k, dw.data_ptr(), 0, O._stream())
+        return dw.clone()
+
+    flops = 2.0 * m * co * ci * k * k
+    return launch, reduce, flops
+
+
+def timed(launch, reps):
+    launch()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            launch()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--from", dest="src", default=os.path.join(ROOT, "profiles", "r02o_conv_launches.jsonl"))
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    cnt = collections.Counter(tuple(json.loads(l)["shape"]) for l in open(a.src))
+    shapes = [s for s in sorted(cnt, key=lambda s: -cnt[s] * s[0] * s[1] * s[2] * s[3] * s[4] * s[5] ** 2 / s[6] ** 2)
+              if s[3] >= 8 and s[4] >= 8]
+    sel = [int(i) for i in a.only.split(",")] if a.only else range(len(shapes))
+    variants = (0, 1)
+    tot = [0.0, 0.0]
+    torch.manual_seed(0)
+    for i in sel:
+        shape = shapes[i]
+        launch, reduce, flops = setup(shape)
+        times = [[], []]
+        outs = []
+        for vi, v in enumerate(variants):
+            N.call("dmf_conv_wgrad_tune", 0, v)
+            launch()
+            outs.append(reduce())
+        same = torch.equal(outs[0], outs[1])
+        for _ in range(a.rounds):
+            for vi, v in enumerate(variants):
+                N.call("dmf_conv_wgrad_tune", 0, v)
+                times[vi].append(timed(launch, a.reps))
+        med = [statistics.median(t) for t in times]
+        for vi in range(2):
+            tot[vi] += med[vi] * cnt[shape]
+        print(f"{i:2d} {str(shape):38s} x{cnt[shape]:2d} reg {med[0] * 1e3:7.1f} us  dma {med[1] * 1e3:7.1f} us "
+              f"({flops / med[1] / 1e9:6.1f} TF/s)  identical={same}", flush=True)
+        if not same:
+            print("   max diff", (outs[0] - outs[1]).abs().max().item(), flush=True)
+    N.call("dmf_conv_wgrad_tune", 0, 1)
+    print(f"weighted totals (ms per step, one encoder pair's forward shapes): reg {tot[0]:.3f}  dma {tot[1]:.3f}")
+
+
+if __name__ == "__main__":
+    main()
