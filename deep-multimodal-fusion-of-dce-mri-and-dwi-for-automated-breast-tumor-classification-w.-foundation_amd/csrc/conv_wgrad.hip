@@ -508,22 +508,33 @@ __global__ void k_gate_grad_wslab(const float* __restrict__ ws, int Cout, int C,
   if (threadIdx.x == 0) dgate[(size_t)n * C + c] = acc / gate[(size_t)n * C + c];
 }
 
-// sum slabs, reorder [Cout][KH][KW][CinP] -> torch [Cout][Cin][KH][KW], accumulate
-__global__ void k_wgrad_reduce(const float* __restrict__ ws, int splits, int Cout, int Cin, int CinP, int KH, int KW,
-                               float* __restrict__ dw, int accumulate) {
-  const long long total = (long long)Cout * Cin * KH * KW;
-  const long long slab = (long long)Cout * KH * KW * CinP;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int s = (int)(i % KW);
-    long long t = i / KW;
-    const int r = (int)(t % KH); t /= KH;
-    const int ci = (int)(t % Cin);
-    const int co = (int)(t / Cin);
-    const long long src = (((long long)co * KH + r) * KW + s) * CinP + ci;
-    float v = 0.f;
-    for (int sp = 0; sp < splits; ++sp) v += ws[sp * slab + src];
-    dw[i] = accumulate ? dw[i] + v : v;
+// sum slabs, reorder [Cout][KH][KW][CinP] -> torch [Cout][Cin][KH][KW], accumulate.
+// Threads walk the SLAB order (ci fastest: every split's read is coalesced),
+// 32-bit index math, four splits' loads in flight; the torch-layout store is
+// KH*KW-strided for 3x3 (1/splits of the traffic). The split sum keeps its
+// fixed order (deterministic).
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ ws, int splits, int Cout, int Cin,
+                                                      int CinP, int KH, int KW, float* __restrict__ dw,
+                                                      int accumulate) {
+  const int KK = KH * KW;
+  const int total = Cout * KK * Cin;  // slab elements that map to a torch element
+  const long long slab = (long long)Cout * KK * CinP;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int ci = i % Cin, t = i / Cin;  // t = co * KK + rs
+    const int co = t / KK, rs = t - co * KK;
+    const float* src = ws + (long long)t * CinP + ci;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4) {
+      v0 += src[(sp + 0) * slab];
+      v1 += src[(sp + 1) * slab];
+      v2 += src[(sp + 2) * slab];
+      v3 += src[(sp + 3) * slab];
+    }
+    for (; sp < splits; ++sp) v0 += src[sp * slab];
+    const float v = (v0 + v1) + (v2 + v3);
+    float* d = dw + ((long long)co * Cin + ci) * KK + rs;
+    *d = accumulate ? *d + v : v;
   }
 }
 
@@ -844,6 +855,8 @@ extern "C" int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int C
                                        float* dw, int accumulate, void* stream) {
   DMF_CHECK_ARG(workspace && dw && splits >= 1 && CinP >= Cin, "dmf_conv2d_wgrad_reduce: bad args");
   const long long total = (long long)Cout * Cin * KH * KW;
+  DMF_CHECK_ARG(total < (1LL << 31) && (long long)Cout * KH * KW * CinP < (1LL << 31),
+                "dmf_conv2d_wgrad_reduce: %lld weights exceed the 32-bit walk", total);
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, workspace, splits, Cout, Cin,
                      CinP, KH, KW, dw, accumulate);
   DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");

@@ -638,6 +638,82 @@ __global__ void k_up_nearest8(const T* __restrict__ x, int ldx, T* __restrict__ 
   }
 }
 
+// Max pool forward that also records, per output element, the window
+// position (r*k + q, one byte) of its maximum -- the first one in scan order,
+// first NaN wins, exactly the element k_maxpool_bwd8 re-derives -- so the
+// backward needs no window re-scan (k_maxpool_bwd_idx8).
+template <typename T>
+__global__ void k_maxpool_idx8(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y,
+                               int Ho, int Wo, int ldy, unsigned char* __restrict__ idx, int k, int s, int p) {
+  const int CV = C >> 3;
+  const int total = N * Ho * Wo * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV, pix = i / CV;
+    const int n = pix / (Ho * Wo), rem = pix - n * Ho * Wo;
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    float m[8];
+    unsigned am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { m[j] = -INFINITY; am[j] = 255u; }
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * s - p + r;
+      if (hi < 0 || hi >= H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int wi = wo * s - p + q;
+        if (wi < 0 || wi >= W) continue;
+        float v[8];
+        ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > m[j] || (isnan(v[j]) && !isnan(m[j]))) { m[j] = v[j]; am[j] = (unsigned)(r * k + q); }
+      }
+    }
+    st8(y + (size_t)pix * ldy + cv * 8, m);
+    uint2 packed;
+    packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+    packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+    *(uint2*)(idx + (size_t)i * 8) = packed;
+  }
+}
+
+// dx from the recorded window positions: each input element sums dy over the
+// windows (ho outer, wo inner, as k_maxpool_bwd8) whose recorded maximum is it
+template <typename T>
+__global__ void k_maxpool_bwd_idx8(const T* __restrict__ dy, int N, int H, int W, int C, int Ho, int Wo, int lddy,
+                                   const unsigned char* __restrict__ idx, T* __restrict__ dx, int lddx, int k, int s,
+                                   int p) {
+  const int CV = C >> 3;
+  const int total = N * H * W * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV, pix = i / CV;
+    const int n = pix / (H * W), rem = pix - n * H * W;
+    const int h = rem / W, w = rem - h * W;
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
+    const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const unsigned code = (unsigned)((h + p - ho * s) * k + (w + p - wo * s));
+        const int op = (n * Ho + ho) * Wo + wo;
+        const uint2 pk = *(const uint2*)(idx + ((size_t)op * CV + cv) * 8);
+        unsigned hit = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned b = ((e < 4 ? pk.x : pk.y) >> (8 * (e & 3))) & 255u;
+          hit |= (b == code ? 1u : 0u) << e;
+        }
+        if (hit) {
+          float d[8];
+          ld8(dy + (size_t)op * lddy + cv * 8, d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (hit & (1u << e)) g[e] += d[e];
+        }
+      }
+    st8(dx + (size_t)pix * lddx + cv * 8, g);
+  }
+}
+
 template <typename T>
 __global__ void k_maxpool8(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y, int Ho,
                            int Wo, int ldy, int k, int s, int p) {
@@ -916,6 +992,41 @@ extern "C" int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int 
     hipLaunchKernelGGL(k_maxpool<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
                        C, ldx, (float*)y, Ho, Wo, ldy, k, s, p);
   DMF_LAUNCH_CHECK("dmf_maxpool2d");
+  return 0;
+}
+
+extern "C" int dmf_maxpool2d_idx(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo,
+                                 int ldy, void* idx, int k, int s, int p, void* stream) {
+  DMF_CHECK_ARG(x && y && idx && k >= 1 && k * k <= 255, "dmf_maxpool2d_idx: bad args");
+  DMF_CHECK_ARG(v8ok(C, ldx, ldy, x, y) && ((uintptr_t)idx % 8) == 0, "dmf_maxpool2d_idx: needs C, strides % 8 == 0");
+  const long long total = (long long)N * Ho * Wo * C;
+  DMF_CHECK_ARG(total < (1LL << 31) && (long long)N * H * W * C < (1LL << 31), "dmf_maxpool2d_idx: too large");
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_maxpool_idx8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, N, H, W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, (unsigned char*)idx, k, s, p);
+  else
+    hipLaunchKernelGGL(k_maxpool_idx8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)x, N, H, W, C, ldx, (float*)y, Ho, Wo, ldy, (unsigned char*)idx, k, s, p);
+  DMF_LAUNCH_CHECK("dmf_maxpool2d_idx");
+  return 0;
+}
+
+extern "C" int dmf_maxpool2d_bwd_idx(int dtype, const void* dy, int N, int H, int W, int C, int Ho, int Wo, int lddy,
+                                     const void* idx, void* dx, int lddx, int k, int s, int p, void* stream) {
+  DMF_CHECK_ARG(dy && idx && dx && k >= 1 && k * k <= 255, "dmf_maxpool2d_bwd_idx: bad args");
+  DMF_CHECK_ARG(v8ok(C, lddy, lddx, dy, dx) && ((uintptr_t)idx % 8) == 0, "dmf_maxpool2d_bwd_idx: needs C, strides % 8 == 0");
+  const long long total = (long long)N * H * W * C;
+  DMF_CHECK_ARG(total < (1LL << 31), "dmf_maxpool2d_bwd_idx: too large");
+  if (total == 0) return 0;
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_maxpool_bwd_idx8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)dy, N, H, W, C, Ho, Wo, lddy, (const unsigned char*)idx, (bf16_t*)dx, lddx, k, s,
+                       p);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd_idx8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)dy, N, H, W, C, Ho, Wo, lddy, (const unsigned char*)idx, (float*)dx, lddx, k, s, p);
+  DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd_idx");
   return 0;
 }
 

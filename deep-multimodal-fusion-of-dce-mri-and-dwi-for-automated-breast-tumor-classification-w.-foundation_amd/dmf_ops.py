@@ -1169,17 +1169,34 @@ class _MaxPoolFn(torch.autograd.Function):
         ho = (h + 2 * p - k) // s + 1
         wo = (w + 2 * p - k) // s + 1
         y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
-        N.call("dmf_maxpool2d", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4], k, s, p,
-               _stream())
-        ctx.save_for_backward(x)
+        if ctx.needs_input_grad[0] and c % 8 == 0 and ld % 8 == 0 and k * k <= 255:
+            # record each maximum's window position: the backward then needs no re-scan
+            idx = torch.empty(n * ho * wo * c, dtype=torch.uint8, device=x.device)
+            N.call("dmf_maxpool2d_idx", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4],
+                   idx.data_ptr(), k, s, p, _stream())
+            ctx.save_for_backward(idx)
+            ctx.xshape = (n, c, h, w, x.dtype)
+        else:
+            N.call("dmf_maxpool2d", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4], k, s, p,
+                   _stream())
+            ctx.save_for_backward(x)
+            ctx.xshape = None
         ctx.cfg = (k, s, p, ho, wo)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
         k, s, p, ho, wo = ctx.cfg
         dy = as_nhwc(dy)
+        if ctx.xshape is not None:
+            (idx,) = ctx.saved_tensors
+            n, c, h, w, dtype = ctx.xshape
+            dy = dy if nhwc(dy)[4] % 8 == 0 else dy.contiguous(memory_format=torch.channels_last)
+            dx = empty_nhwc(n, c, h, w, dtype, dy.device)
+            N.call("dmf_maxpool2d_bwd_idx", N.dtype_code(dtype), dy.data_ptr(), n, h, w, c, ho, wo, nhwc(dy)[4],
+                   idx.data_ptr(), dx.data_ptr(), nhwc(dx)[4], k, s, p, _stream())
+            return dx, None, None, None
+        (x,) = ctx.saved_tensors
         n, c, h, w, ld = nhwc(x)
         dx = empty_nhwc(n, c, h, w, x.dtype, x.device)
         N.call("dmf_maxpool2d_bwd", dt(x), x.data_ptr(), n, h, w, c, ld, dy.data_ptr(), ho, wo, nhwc(dy)[4],

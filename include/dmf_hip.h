@@ -247,6 +247,15 @@ int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx,
                   int k, int s, int p, void* stream);
 int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* dy, int Ho, int Wo,
                       int lddy, void* dx, int lddx, int k, int s, int p, void* stream);
+/* Max pool forward that also records each output element's window position
+ * of its maximum (one byte per element, [N*Ho*Wo][C]; first in scan order,
+ * first NaN wins), and the backward from those positions (no window re-scan).
+ * Same results as dmf_maxpool2d / dmf_maxpool2d_bwd (nn.MaxPool2d, timm stem
+ * foundation_model.py:260-267). C and strides multiples of 8, idx 8-B aligned. */
+int dmf_maxpool2d_idx(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo, int ldy,
+                      void* idx, int k, int s, int p, void* stream);
+int dmf_maxpool2d_bwd_idx(int dtype, const void* dy, int N, int H, int W, int C, int Ho, int Wo, int lddy,
+                          const void* idx, void* dx, int lddx, int k, int s, int p, void* stream);
 int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, int N, int H, int W, int C, int r,
                          void* stream);
 /* nn.AdaptiveAvgPool2d((Ho, Wo)) on NHWC, any ratio (proj_pool, model_module.py:534) */

@@ -254,6 +254,35 @@ def test_gn_mix_and_grads():
     assert torch.allclose(gnd.bias.grad.cpu(), gn.bias.grad, atol=1e-4, rtol=1e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool_recorded_positions_match_rescan(dtype):
+    """dmf_maxpool2d_idx + dmf_maxpool2d_bwd_idx (the autograd path for C % 8 == 0)
+    against the window re-scan of dmf_maxpool2d / dmf_maxpool2d_bwd: bit-exact,
+    with heavy ties (integer-valued input), a NaN, and odd spatial sizes."""
+    import dmf_native as N
+    torch.manual_seed(6)
+    x = torch.randint(-3, 4, (3, 64, 33, 30)).float()
+    x[0, 5, 3, 4] = float("nan")
+    xd = _to_dev(x, dtype).requires_grad_(True)
+    y = O.maxpool2d(xd, 3, 2, 1)
+    g = torch.randn(y.shape)
+    gd = _to_dev(g, dtype)
+    y.backward(gd)
+    n, c, h, w = x.shape
+    ho, wo = y.shape[2], y.shape[3]
+    xs = xd.detach()
+    y2 = O.empty_nhwc(n, c, ho, wo, dtype, xs.device)
+    N.call("dmf_maxpool2d", O.dt(xs), xs.data_ptr(), n, h, w, c, c, y2.data_ptr(), ho, wo, c, 3, 2, 1, O._stream())
+    dx2 = O.empty_nhwc(n, c, h, w, dtype, xs.device)
+    N.call("dmf_maxpool2d_bwd", O.dt(xs), xs.data_ptr(), n, h, w, c, c, gd.data_ptr(), ho, wo, c, dx2.data_ptr(), c,
+           3, 2, 1, O._stream())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(y.detach(), nan=1234.0), torch.nan_to_num(y2, nan=1234.0))
+    assert torch.equal(xd.grad, dx2)
+    ref = F.max_pool2d(x.to(dtype).float().requires_grad_(True), 3, 2, 1)
+    assert torch.equal(torch.nan_to_num(y.detach().float().cpu(), nan=9.0), torch.nan_to_num(ref.detach(), nan=9.0))
+
+
 def test_maxpool_and_bilinear_and_tokens():
     torch.manual_seed(5)
     x = torch.randn(2, 16, 17, 15)
