@@ -363,13 +363,17 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
 // step's 8 pieces per wave issued right after the barrier that frees them.
 // DUAL (channel-concat input): each 128-column tile must lie in one tap of
 // one source (Cin % 128 == 0, C1 % 128 == 0), so the source is wave-uniform.
-template <bool DUAL>
-__global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
-  constexpr int BM = 128, BN = 128, BK = 64, SUB = BK * 256, STAGE = 2 * SUB, NP = 4;
+template <bool DUAL, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_wgrad_dma(WgArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = 64 * WM, BN = 64 * WN, BK = 64, SUB = BK * 256;
+  constexpr int SA_N = BM / 128, SB_N = BN / 128, STAGE = (SA_N + SB_N) * SUB;
+  constexpr int PA = SA_N * 16 / NW, PB = SB_N * 16 / NW;  // 1 KiB DMA pieces per wave per operand
+  static_assert(PA >= 1 && PB >= 1 && PA * NW == SA_N * 16 && PB * NW == SB_N * 16, "piece split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x % a.ntiles;
   const int co0 = mt * BM, k0 = nt * BN;
   const int p_begin = blockIdx.y * a.pix_per_split;
@@ -384,47 +388,64 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
                           : buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * 2);
   const int ldxs = hi_src ? a.ldx2 : a.ldx;
 
-  // per piece: this lane's chunk, A channel, B (tap offsets, channel) and gather-row cursor
-  int ach[NP], bci[NP], roff[NP], soff[NP], cn[NP], cho[NP], cwo[NP];
-  bool aok[NP], bok[NP];
+  // A piece i of this wave: global piece P = wid*PA + i -> sub-image P/16, rows 4*(P%16) .. +3
+  // (lane row 4*(P%16) + lane/16); the lane stages chunk (lane%16) ^ ((lane/16 << 2) | (P & 3))
+  int ach[PA], arow[PA];
+  unsigned alds[PA];
+  bool aok[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int P = wid * PA + i;
+    const int ch = (lane & 15) ^ (((lane >> 4) << 2) | (P & 3));
+    ach[i] = co0 + (P >> 4) * 128 + ch * 8;
+    aok[i] = ach[i] < a.Cout;
+    arow[i] = (P & 15) * 4;
+    alds[i] = (unsigned)((P >> 4) * SUB + (P & 15) * 4 * 256);
+  }
+  int bci[PB], roff[PB], soff[PB], cn[PB], cho[PB], cwo[PB], brow[PB];
+  unsigned blds[PB];
+  bool bok[PB];
   const int hw = a.Ho * a.Wo;
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int ch = (lane & 15) ^ (((lane >> 4) << 2) | p);
-    ach[p] = co0 + ch * 8;
-    aok[p] = ach[p] < a.Cout;
-    const int kcol = k0 + ch * 8;
-    bok[p] = kcol < a.Ktot;
-    const int tap = bok[p] ? kcol / a.Cin : 0;
+  for (int i = 0; i < PB; ++i) {
+    const int P = wid * PB + i;
+    const int ch = (lane & 15) ^ (((lane >> 4) << 2) | (P & 3));
+    const int kcol = k0 + (P >> 4) * 128 + ch * 8;
+    bok[i] = kcol < a.Ktot;
+    const int tap = bok[i] ? kcol / a.Cin : 0;
     int ci = kcol - tap * a.Cin;
     if (hi_src) ci -= a.C1;
-    bci[p] = ci;
-    roff[p] = (tap / a.KW) * a.dil - a.pad;
-    soff[p] = (tap % a.KW) * a.dil - a.pad;
-    const int pix = p_begin + wid * 16 + p * 4 + (lane >> 4);
-    cn[p] = pix / hw;
-    const int rem = pix - cn[p] * hw;
-    cho[p] = rem / a.Wo;
-    cwo[p] = rem - cho[p] * a.Wo;
+    bci[i] = ci;
+    roff[i] = (tap / a.KW) * a.dil - a.pad;
+    soff[i] = (tap % a.KW) * a.dil - a.pad;
+    brow[i] = (P & 15) * 4;
+    blds[i] = (unsigned)(SA_N * SUB + (P >> 4) * SUB + (P & 15) * 4 * 256);
+    const int pix = p_begin + brow[i] + (lane >> 4);
+    cn[i] = pix / hw;
+    const int rem = pix - cn[i] * hw;
+    cho[i] = rem / a.Wo;
+    cwo[i] = rem - cho[i] * a.Wo;
   }
   const int dho = BK / a.Wo, dwo = BK % a.Wo;
   auto issue = [&](int stage, int kb) {
-    const unsigned As = lds0 + stage * STAGE, Bs = As + SUB;
+    const unsigned S = lds0 + stage * STAGE;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int row = wid * 16 + p * 4;
-      const int pix = kb + row + (lane >> 4);
-      const bool pin = pix < p_end;
-      const unsigned ao = (pin && aok[p]) ? (unsigned)(((long long)pix * a.lddy + ach[p]) * 2) : BUF_OOB;
-      dma16(rdy, ao, 0, As + row * 256);
-      const int hi = cho[p] * a.stride + roff[p], wi = cwo[p] * a.stride + soff[p];
-      const bool ok = pin && bok[p] && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-      const unsigned bo = ok ? (unsigned)((((long long)(cn[p] * a.H + hi) * a.W + wi) * ldxs + bci[p]) * 2) : BUF_OOB;
-      dma16(rx, bo, 0, Bs + row * 256);
-      int wo = cwo[p] + dwo, ho = cho[p] + dho, n = cn[p];
+    for (int i = 0; i < PA; ++i) {
+      const int pix = kb + arow[i] + (lane >> 4);
+      const unsigned ao = (pix < p_end && aok[i]) ? (unsigned)(((long long)pix * a.lddy + ach[i]) * 2) : BUF_OOB;
+      dma16(rdy, ao, 0, S + alds[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int pix = kb + brow[i] + (lane >> 4);
+      const int hi = cho[i] * a.stride + roff[i], wi = cwo[i] * a.stride + soff[i];
+      const bool ok = pix < p_end && bok[i] && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const unsigned bo = ok ? (unsigned)((((long long)(cn[i] * a.H + hi) * a.W + wi) * ldxs + bci[i]) * 2) : BUF_OOB;
+      dma16(rx, bo, 0, S + blds[i]);
+      int wo = cwo[i] + dwo, ho = cho[i] + dho, n = cn[i];
       if (wo >= a.Wo) { wo -= a.Wo; ++ho; }
       while (ho >= a.Ho) { ho -= a.Ho; ++n; }
-      cwo[p] = wo; cho[p] = ho; cn[p] = n;
+      cwo[i] = wo; cho[i] = ho; cn[i] = n;
     }
   };
 
@@ -443,7 +464,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kt + 1 < nk) issue((kt + 1) & 1, p_begin + (kt + 1) * BK);
     const char* SA = smem + (kt & 1) * STAGE;
-    const char* SB = SA + SUB;
+    const char* SB = SA + SA_N * SUB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8_w af[4], bfr[4];
@@ -453,7 +474,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int cl = wm * 64 + i * 16;
-          const char* pa = SA + wtr_off(row, (cl >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const char* pa = SA + (cl >> 7) * SUB + wtr_off(row, ((cl & 127) >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
           const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pa);
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
@@ -461,7 +482,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad_dma(WgArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int cl = wn * 64 + j * 16;
-          const char* pb = SB + wtr_off(row, (cl >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
+          const char* pb = SB + (cl >> 7) * SUB + wtr_off(row, ((cl & 127) >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
           const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pb);
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[j][4 * h + e] = v[e];
@@ -773,10 +794,15 @@ static int g_wgrad_dma = [] {
   return e && e[0] == '0' ? 0 : 1;
 }();
 static int wgrad_dma_enabled() { return g_wgrad_dma; }
+static int g_wgrad_wide = [] {
+  const char* e = std::getenv("DMF_WGRAD_WIDE");
+  return e && e[0] == '0' ? 0 : 1;
+}();
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
-  DMF_CHECK_ARG(key == 0, "dmf_conv_wgrad_tune: unknown key %d", key);
-  g_wgrad_dma = value != 0;
+  DMF_CHECK_ARG(key == 0 || key == 1, "dmf_conv_wgrad_tune: unknown key %d", key);
+  if (key == 0) g_wgrad_dma = value != 0;
+  else g_wgrad_wide = value != 0;
   return 0;
 }
 
@@ -839,8 +865,21 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
   } else if (dtype == DMF_BF16 && wgrad_tr_enabled() && wgrad_dma_enabled() &&
              (long long)a.N * a.H * a.W * std::max(a.ldx, x2 ? a.ldx2 : 0) * 2 < (1LL << 31) &&
              (long long)a.M * a.lddy * 2 < (1LL << 31) && (!x2 || (a.Cin % 128 == 0 && a.C1 % 128 == 0))) {
-    if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
-    else hipLaunchKernelGGL((k_conv_wgrad_dma<false>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+    // 128x256 tiles (8 waves, one workgroup per CU, 96 KiB): a third less operand staging per
+    // flop than 128x128 at two workgroups per CU. Measured (tools/wgrad_bench.py): faster on the
+    // 1x1 convs up to K = 1024 (512->2048: 96.9 -> 87.0 us), slower on the 3x3s and K = 2048
+    const bool wide = g_wgrad_wide && a.KH * a.KW == 1 && a.Ktot >= 256 && a.Ktot <= 1024 && a.Cout >= 128 &&
+                      (!x2 || (a.Cin % 256 == 0 && a.C1 % 256 == 0));
+    if (wide) {
+      a.ntiles = cdiv(a.Ktot, 256);
+      grid = dim3(a.mtiles * a.ntiles, splits);
+      if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+      else hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+    } else if (x2) {
+      hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+    } else {
+      hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+    }
   } else if (dtype == DMF_BF16 && wgrad_tr_enabled())
     hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
   else if (dtype == DMF_BF16)

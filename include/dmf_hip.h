@@ -58,8 +58,9 @@ int dmf_conv_m_tile(void);
 /* forward-conv tuning knobs (benchmarks / A-B runs): key 0 = 256x256 LDS-DMA
  * tile on (1, default) / off; key 1 = its scheduling variant 0..3 */
 int dmf_conv_tune(int key, int value);
-/* Benchmark knob of the weight-gradient engine: key 0 = LDS-DMA staging of the
- * bf16 transposed-read kernel on (1, default) / off. */
+/* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
+ * bf16 transposed-read kernel on (1, default) / off; key 1 = its 128x256 tile
+ * (one workgroup per CU) where K >= 256 on (1, default) / off. */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */

@@ -2,8 +2,9 @@
 """Weight-gradient microbench on the hot path's conv shapes (bf16, B=32): the
 split-K slab kernel (dmf_conv2d_wgrad) per shape, HIP events over a hipGraph
 of R launches, for each engine variant (dmf_conv_wgrad_tune key 0: LDS-DMA
-staging on / off), interleaved; the reduced gradients of the variants are
-compared (they share the MFMA order, so they must agree bit for bit).
+staging on / off; key 1: its 128x256 tile on / off), interleaved; the reduced
+gradients of the variants are compared (every variant sums each weight's
+pixels in the same order, so they must agree bit for bit).
 
     python tools/wgrad_bench.py [--from profiles/r02o_conv_launches.jsonl] [--reps 10] [--rounds 3]
 """
@@ -75,32 +76,36 @@ def main():
     shapes = [s for s in sorted(cnt, key=lambda s: -cnt[s] * s[0] * s[1] * s[2] * s[3] * s[4] * s[5] ** 2 / s[6] ** 2)
               if s[3] >= 8 and s[4] >= 8]
     sel = [int(i) for i in a.only.split(",")] if a.only else range(len(shapes))
-    variants = (0, 1)
-    tot = [0.0, 0.0]
+    variants = ((0, 0), (1, 0), (1, 1))  # (LDS-DMA, 128x256 tile)
+    tot = [0.0] * len(variants)
     torch.manual_seed(0)
     for i in sel:
         shape = shapes[i]
         launch, reduce, flops = setup(shape)
-        times = [[], []]
+        times = [[] for _ in variants]
         outs = []
-        for vi, v in enumerate(variants):
-            N.call("dmf_conv_wgrad_tune", 0, v)
+        for vi, (d, wd) in enumerate(variants):
+            N.call("dmf_conv_wgrad_tune", 0, d)
+            N.call("dmf_conv_wgrad_tune", 1, wd)
             launch()
             outs.append(reduce())
-        same = torch.equal(outs[0], outs[1])
+        same = all(torch.equal(outs[0], o) for o in outs[1:])
         for _ in range(a.rounds):
-            for vi, v in enumerate(variants):
-                N.call("dmf_conv_wgrad_tune", 0, v)
+            for vi, (d, wd) in enumerate(variants):
+                N.call("dmf_conv_wgrad_tune", 0, d)
+                N.call("dmf_conv_wgrad_tune", 1, wd)
                 times[vi].append(timed(launch, a.reps))
         med = [statistics.median(t) for t in times]
-        for vi in range(2):
+        for vi in range(len(variants)):
             tot[vi] += med[vi] * cnt[shape]
-        print(f"{i:2d} {str(shape):38s} x{cnt[shape]:2d} reg {med[0] * 1e3:7.1f} us  dma {med[1] * 1e3:7.1f} us "
-              f"({flops / med[1] / 1e9:6.1f} TF/s)  identical={same}", flush=True)
+        best = min(med)
+        print(f"{i:2d} {str(shape):38s} x{cnt[shape]:2d} reg {med[0] * 1e3:7.1f}  dma {med[1] * 1e3:7.1f}  "
+              f"dma-wide {med[2] * 1e3:7.1f} us ({flops / best / 1e9:6.1f} TF/s best)  identical={same}", flush=True)
         if not same:
-            print("   max diff", (outs[0] - outs[1]).abs().max().item(), flush=True)
+            print("   max diff", max((outs[0] - o).abs().max().item() for o in outs[1:]), flush=True)
     N.call("dmf_conv_wgrad_tune", 0, 1)
-    print(f"weighted totals (ms per step, one encoder pair's forward shapes): reg {tot[0]:.3f}  dma {tot[1]:.3f}")
+    N.call("dmf_conv_wgrad_tune", 1, 1)
+    print("weighted totals (ms per step, one encoder pair's forward shapes): reg %.3f  dma %.3f  dma-wide %.3f" % tuple(tot))
 
 
 if __name__ == "__main__":
