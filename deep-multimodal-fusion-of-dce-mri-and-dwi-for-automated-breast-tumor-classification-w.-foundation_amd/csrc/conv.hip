@@ -1564,6 +1564,12 @@ static int g_ps_enable = [] {
   return e && e[0] == '0' ? 0 : 1;
 }();
 static int g_ps_dbg = 0;
+// 256x256 tiles a launch needs before the square forms take it (default: one per CU; with two
+// encoder streams in flight a half-filling launch leaves the other CUs to the other stream)
+static long long g_min_tiles = [] {
+  const char* e = std::getenv("DMF_SQ_MIN_TILES");
+  return e ? std::atoll(e) : 256LL;
+}();
 static bool wide_disabled() {
   static const int v = [] {
     const char* e = std::getenv("DMF_CONV_WIDE");
@@ -1615,7 +1621,8 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   // persistent square LDS-DMA tile: whole 256-column tiles, >= one tile per CU, no fused-finalize
   // tickets, output addressable by a 32-bit buffer offset
   if (dtype == DMF_BF16 && !wide_disabled() && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
-      a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= 256 && (long long)a.M * a.ldy * 2 < (1LL << 31)) {
+      a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
+      (long long)a.M * a.ldy * 2 < (1LL << 31)) {
     p.wide = p.sq = p.ps = true;
     p.bm = QBM;
     p.bn = QBN;
@@ -1625,7 +1632,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
   // bound at one 256x256 block per CU and stays on the 256x128 form)
   if (dtype == DMF_BF16 && !wide_disabled() && g_sq_enable && a.Nout % QBN == 0 &&
-      (a.KH * a.KW > 1 ? a.Ktot >= 512 : a.Ktot >= 2048) && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= 256) {
+      (a.KH * a.KW > 1 ? a.Ktot >= 512 : a.Ktot >= 2048) && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles) {
     p.wide = p.sq = true;
     p.bm = QBM;
     p.bn = QBN;
