@@ -1566,6 +1566,10 @@ static int g_ps_enable = [] {
 static int g_ps_dbg = 0;
 // 256x256 tiles a launch needs before the square forms take it (default: one per CU; with two
 // encoder streams in flight a half-filling launch leaves the other CUs to the other stream)
+static long long g_wide_min_tiles = [] {
+  const char* e = std::getenv("DMF_WIDE_MIN_TILES");
+  return e ? std::atoll(e) : 256LL;
+}();
 static long long g_min_tiles = [] {
   const char* e = std::getenv("DMF_SQ_MIN_TILES");
   return e ? std::atoll(e) : 256LL;
@@ -1640,7 +1644,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   }
   // wide LDS-DMA tile: bf16, whole 128-column tiles, long enough K, >= one block per CU
   if (dtype == DMF_BF16 && !wide_disabled() && a.Nout % WBN == 0 && a.Ktot >= 512 &&
-      (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= 256) {
+      (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= g_wide_min_tiles) {
     p.wide = true;
     p.bm = WBM;
     p.bn = WBN;
