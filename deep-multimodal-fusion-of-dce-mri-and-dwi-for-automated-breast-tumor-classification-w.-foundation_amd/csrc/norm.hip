@@ -447,7 +447,8 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
                                                         const float* __restrict__ ssr, float p,
                                                         const unsigned long long* rng, int site,
                                                         const float* __restrict__ save, T* __restrict__ dz, int lddz,
-                                                        long long M, int C, float* __restrict__ part) {
+                                                        long long M, int C, float* __restrict__ part,
+                                                        double* __restrict__ acc, int replicas) {
   __shared__ float red[32][65 * 2];
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.y * 64 + cl * 8;
@@ -515,7 +516,10 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
 #pragma unroll 8
     for (int r = 0; r < 32; ++r) t += red[r][c * 2 + w];
     const int cg = blockIdx.y * 64 + c;
-    if (cg < C) part[((size_t)blockIdx.x * C + cg) * 2 + w] = t;
+    if (cg < C) {
+      if (acc) unsafeAtomicAdd(acc + ((size_t)(blockIdx.x % (unsigned)replicas) * C + cg) * 2 + w, (double)t);
+      else part[((size_t)blockIdx.x * C + cg) * 2 + w] = t;
+    }
   }
 }
 
@@ -533,6 +537,69 @@ __global__ void k_bn_bwd_apply8(const T* __restrict__ dz, int lddz, const T* __r
     ld8(x + (size_t)m * ldx + c0, xv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = coef[c0 + e] * g[e] + coef[C + c0 + e] * xv[e] + coef[2 * C + c0 + e];
+    st8(dx + (size_t)m * lddx + c0, g);
+  }
+}
+
+// BN backward apply with the finalize folded in (dmf_bn_bwd_apply_acc): block =
+// 64 channels (blockIdx.y) x rows_per_blk pixels; its 64 (A, Cc, B) come from the
+// column sums accumulated by dmf_act_bwd_bn_reduce_acc into [replicas][C][2]
+// doubles (summed in a fixed order, the arithmetic of k_bn_bwd_finalize_wide);
+// the blockIdx.x == 0 blocks also add dgamma / dbeta. dx = A*dz + Cc*x + B.
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ dz, int lddz, const T* __restrict__ x,
+                                                          int ldx, const double* __restrict__ acc, int replicas,
+                                                          double count, int training, const float* __restrict__ gamma,
+                                                          const float* __restrict__ save, float* dgamma, float* dbeta,
+                                                          T* __restrict__ dx, int lddx, int M, int C,
+                                                          int rows_per_blk) {
+  __shared__ float sco[3][64];
+  const int tid = threadIdx.x;
+  const int cg = blockIdx.y * 64;
+  if (tid < 64) {
+    const int c = cg + tid;
+    float A = 0.f, Cc = 0.f, B = 0.f;
+    if (c < C) {
+      double s = 0.0, q = 0.0;
+      for (int r = 0; r < replicas; ++r) {  // fixed order
+        s += acc[((size_t)r * C + c) * 2];
+        q += acc[((size_t)r * C + c) * 2 + 1];
+      }
+      if (blockIdx.x == 0) {
+        if (dbeta) dbeta[c] += (float)s;
+        if (dgamma) dgamma[c] += (float)q;
+      }
+      const double g = gamma ? gamma[c] : 1.0;
+      const double mean = save[c], inv = save[C + c];
+      const double a = g * inv;
+      const double cc = training ? -g * inv * inv * q / count : 0.0;
+      const double b = training ? -g * inv * s / count - cc * mean : 0.0;
+      A = (float)a;
+      Cc = (float)cc;
+      B = (float)b;
+    }
+    sco[0][tid] = A;
+    sco[1][tid] = Cc;
+    sco[2][tid] = B;
+  }
+  __syncthreads();
+  const int cl = (tid & 7) * 8, c0 = cg + cl;
+  if (c0 >= C) return;
+  float a8[8], c8[8], b8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a8[k] = sco[0][cl + k];
+    c8[k] = sco[1][cl + k];
+    b8[k] = sco[2][cl + k];
+  }
+  const int mbeg = blockIdx.x * rows_per_blk;
+  const int mend = min(M, mbeg + rows_per_blk);
+  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
+    float g[8], xv[8];
+    ld8(dz + (size_t)m * lddz + c0, g);
+    ld8(x + (size_t)m * ldx + c0, xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
     st8(dx + (size_t)m * lddx + c0, g);
   }
 }
@@ -819,12 +886,69 @@ extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void*
   return 0;
 }
 
+static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* x, int ldx,
+                                  const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
+                                  int act, float dropout_p, const unsigned long long* rng, int site,
+                                  const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
+                                  float* partials, double* acc, int replicas, void* stream);
+
 extern "C" int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, int ldx,
                                      const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
                                      int act, float dropout_p, const unsigned long long* rng, int site,
                                      const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
                                      float* partials, void* stream) {
-  DMF_CHECK_ARG(dy && x && scale_shift && save_mean_invstd && dz && partials && M > 0 && C > 0,
+  DMF_CHECK_ARG(partials, "dmf_act_bwd_bn_reduce: bad args");
+  return act_bwd_bn_reduce_impl(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng,
+                                site, save_mean_invstd, dz, lddz, M, C, partials, nullptr, 0, stream);
+}
+
+extern "C" int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* x, int ldx,
+                                         const float* scale_shift, const void* res, int ldr,
+                                         const float* res_scale_shift, int act, float dropout_p,
+                                         const unsigned long long* rng, int site, const float* save_mean_invstd,
+                                         void* dz, int lddz, long long M, int C, double* acc, int replicas,
+                                         void* stream) {
+  DMF_CHECK_ARG(acc && ((uintptr_t)acc % 8) == 0 && replicas >= 1 && replicas <= 64,
+                "dmf_act_bwd_bn_reduce_acc: bad statistics arena");
+  DMF_CHECK_ARG(C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
+                    ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz)) % 16 == 0,
+                "dmf_act_bwd_bn_reduce_acc: needs 8-channel vectors (C=%d)", C);
+  return act_bwd_bn_reduce_impl(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng,
+                                site, save_mean_invstd, dz, lddz, M, C, nullptr, acc, replicas, stream);
+}
+
+extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int ldx, const double* acc,
+                                    int replicas, double count, int training, const float* gamma,
+                                    const float* save_mean_invstd, float* dgamma, float* dbeta, void* dx, int lddx,
+                                    long long M, int C, void* stream) {
+  DMF_CHECK_ARG(dz && x && acc && save_mean_invstd && dx && count > 0 && replicas >= 1 && replicas <= 64,
+                "dmf_bn_bwd_apply_acc: bad args");
+  DMF_CHECK_ARG(C % 8 == 0 && lddz % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && M < (1LL << 31) &&
+                    ((uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx) % 16 == 0,
+                "dmf_bn_bwd_apply_acc: needs 8-channel vectors (C=%d)", C);
+  if (M == 0) return 0;
+  const int gy = cdiv(C, 64);
+  int rows = 256;
+  while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
+  const dim3 g((unsigned)cdiv(M, rows), (unsigned)gy);
+  if (dtype == DMF_BF16)
+    hipLaunchKernelGGL(k_bn_bwd_apply_acc<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
+                       (const bf16_t*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
+                       (bf16_t*)dx, lddx, (int)M, C, rows);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply_acc<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
+                       (const float*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
+                       (float*)dx, lddx, (int)M, C, rows);
+  DMF_LAUNCH_CHECK("dmf_bn_bwd_apply_acc");
+  return 0;
+}
+
+static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* x, int ldx,
+                                  const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
+                                  int act, float dropout_p, const unsigned long long* rng, int site,
+                                  const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
+                                  float* partials, double* acc, int replicas, void* stream) {
+  DMF_CHECK_ARG(dy && x && scale_shift && save_mean_invstd && dz && (partials || acc) && M > 0 && C > 0,
                 "dmf_act_bwd_bn_reduce: bad args");
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_act_bwd_bn_reduce: dropout needs rng state");
   const bool vec8 = C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
@@ -839,7 +963,7 @@ extern "C" int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const 
   DMF_CHECK_ARG(tiles < 65536LL * 32768LL, "dmf_act_bwd_bn_reduce: too many rows");
   dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
   hipStream_t s = (hipStream_t)stream;
-#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials)
+#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
   if (dtype == DMF_BF16) {
     switch (act) {
       case DMF_ACT_RELU: DMF_ABR(bf16_t, DMF_ACT_RELU); break;

@@ -798,6 +798,11 @@ class _ConvBNActFn(torch.autograd.Function):
                    float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
         ctx.save_for_backward(x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng)
         ctx.spec = spec
+        # the backward's BN column sums: a zeroed slice of this forward's statistics arena
+        # (dmf_act_bwd_bn_reduce_acc / dmf_bn_bwd_apply_acc: no finalize launch)
+        # (training-mode BN only: the arena is zeroed at the forward's start when a BN trains)
+        ctx.bwd_acc = (_bn_acc(c, y.device) if BWD_BN_ARENA and ARENA[0] is not None and c % 8 == 0
+                       and spec[2].training and any(ctx.needs_input_grad) else None)
         return out
 
     @staticmethod
@@ -816,13 +821,26 @@ class _ConvBNActFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         dgamma = grad_sink(bn.weight) if need[4] else None
         dbeta = grad_sink(bn.bias) if need[5] else None
-        # act/dropout backward and the BN column partials in one pass
-        tiles = N.load().dmf_bn_bwd_tiles(m)
-        part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
-        N.call("dmf_act_bwd_bn_reduce", dtc, dout.data_ptr(), nhwc(dout)[4], y.data_ptr(), ldy, ss.data_ptr(),
-               _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
-               nhwc(dz)[4], m, c, part.data_ptr(), _stream())
-        dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
+        acc = ctx.bwd_acc
+        lddo, lddz = nhwc(dout)[4], nhwc(dz)[4]
+        if (acc is not None and ldy % 8 == 0 and lddo % 8 == 0 and (res_t is None or ldr % 8 == 0)
+                and (dout.data_ptr() | y.data_ptr() | (res_t.data_ptr() if res_t is not None else 0)) % 16 == 0):
+            # act/dropout backward + column sums into the arena, then the apply finalizes per block
+            N.call("dmf_act_bwd_bn_reduce_acc", dtc, dout.data_ptr(), lddo, y.data_ptr(), ldy, ss.data_ptr(),
+                   _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
+                   lddz, m, c, acc.data_ptr(), BN_ACC_REPLICAS, _stream())
+            dy = empty_nhwc(n, c, ho, wo, y.dtype, y.device)
+            N.call("dmf_bn_bwd_apply_acc", dtc, dz.data_ptr(), lddz, y.data_ptr(), ldy, acc.data_ptr(),
+                   BN_ACC_REPLICAS, float(m), 1 if bn.training else 0, _p(bn.weight), save.data_ptr(), _p(dgamma),
+                   _p(dbeta), dy.data_ptr(), nhwc(dy)[4], m, c, _stream())
+        else:
+            # act/dropout backward and the BN column partials in one pass
+            tiles = N.load().dmf_bn_bwd_tiles(m)
+            part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
+            N.call("dmf_act_bwd_bn_reduce", dtc, dout.data_ptr(), lddo, y.data_ptr(), ldy, ss.data_ptr(),
+                   _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
+                   lddz, m, c, part.data_ptr(), _stream())
+            dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
         need_dx = need[0] or (x2 is not None and need[1])
         dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2,
                                     gate_holder=ctx.gate_holder, dw_sink=True)
@@ -839,6 +857,11 @@ class _ConvBNActFn(torch.autograd.Function):
             dres = dz
         # gamma/beta (and the MFMA conv weights) were accumulated in place (grad_sink)
         return dx, dx2, dw, db, None, None, dres, dxr, dwr, None, None, None
+
+
+# backward BN column sums into the forward's statistics arena (no finalize launch);
+# DMF_BWD_BN_ARENA=0 restores the per-tile slab + finalize form
+BWD_BN_ARENA = os.environ.get("DMF_BWD_BN_ARENA", "1") != "0"
 
 
 def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True, part=None):

@@ -218,6 +218,19 @@ int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, in
                           const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
                           const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz, int lddz,
                           long long M, int C, float* partials, void* stream);
+/* BatchNorm backward without a finalize launch: the column sums (sum dz,
+ * sum dz*xhat) go by float64 atomics into [replicas][C][2] (zeroed; a slice of
+ * the forward's statistics arena), and the apply finalizes them per 64-channel
+ * block (dgamma / dbeta added once) -- the backward of conv -> BatchNorm2d ->
+ * act of timm Bottleneck / BackboneAdapter (foundation_model.py:260-267,
+ * model_module.py:440-447). C and strides multiples of 8. */
+int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+                              const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
+                              const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz,
+                              int lddz, long long M, int C, double* acc, int replicas, void* stream);
+int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int ldx, const double* acc, int replicas,
+                         double count, int training, const float* gamma, const float* save_mean_invstd, float* dgamma,
+                         float* dbeta, void* dx, int lddx, long long M, int C, void* stream);
 int dmf_col_stats_tiles(long long M);
 int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
 
