@@ -186,12 +186,15 @@ def test_encoder_backward_parity_all_trainable():
     (lr_.pow(2).sum() + mpr.mean() + auxr["raw_feats"][2].mean()).backward()
     (l6.pow(2).sum() + m6.mean() + a6["raw_feats"][2].mean()).backward()
     bad = {}
+    # a gradient that is analytically ~0 (a norm's bias feeding another normalisation) has no
+    # meaningful relative error: scale by at least 1e-4 of the largest parameter gradient
+    floor = 1e-4 * max(p3.grad.float().norm().item() for p3 in ref64.parameters() if p3.grad is not None)
     for (n, p1), (_, p2), (_, p3) in zip(enc.named_parameters(), ref.named_parameters(), ref64.named_parameters()):
         if p3.grad is None:
             continue
         assert p1.grad is not None, n
         truth = p3.grad.float()
-        scale = max(1e-12, truth.norm().item())
+        scale = max(1e-12, floor, truth.norm().item())
         e_mine = (p1.grad.float().cpu().reshape(truth.shape) - truth).norm().item() / scale
         e_ref = (p2.grad - truth).norm().item() / scale
         if e_mine > 3 * e_ref + 5e-3:
