@@ -65,7 +65,7 @@ struct ConvArgs {
   int stat_acc;
   // benchmarking only (dmf_conv_tune key 6), k_conv_fwd_ps: bit 1 skips the
   // DMA (the loop then computes on stale LDS), bit 2 the epilogue, bit 3 its
-  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal
+  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal (env DMF_PS_DBG)
   int dbg;
 };
 
@@ -992,7 +992,8 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / QWN, wn = wid % QWN;
-  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  // (no static priority split between the wave halves here: measured -0.4 % encoder forward
+  // without it, interleaved A/B; k_conv_fwd_sq keeps its VAR 1)
   const int lr = lane >> 3;
   const int lc = (lane & 7) ^ lr;  // source-side swizzle (see k_conv_fwd_wide)
   const int fr = lane & 15, fg = lane >> 4;
@@ -1563,7 +1564,10 @@ static int g_ps_enable = [] {
   const char* e = std::getenv("DMF_PS");
   return e && e[0] == '0' ? 0 : 1;
 }();
-static int g_ps_dbg = 0;
+static int g_ps_dbg = [] {
+  const char* e = std::getenv("DMF_PS_DBG");
+  return e ? std::atoi(e) : 0;
+}();
 // 256x256 tiles a launch needs before the square forms take it (default: one per CU; with two
 // encoder streams in flight a half-filling launch leaves the other CUs to the other stream)
 static long long g_wide_min_tiles = [] {
