@@ -1568,15 +1568,17 @@ static int g_ps_dbg = [] {
   const char* e = std::getenv("DMF_PS_DBG");
   return e ? std::atoi(e) : 0;
 }();
-// 256x256 tiles a launch needs before the square forms take it (default: one per CU; with two
-// encoder streams in flight a half-filling launch leaves the other CUs to the other stream)
+// tiles a launch needs before the wide (256x128) / square (256x256) forms take it: half a
+// tile per CU -- with the two encoder streams in flight a half-filling launch leaves the
+// other CUs to the other stream (measured, both at 128 vs 256: mode-A step -1.2 %, mode B
+// +0.4 %, encoder forward within noise; interleaved A/B over four rounds)
 static long long g_wide_min_tiles = [] {
   const char* e = std::getenv("DMF_WIDE_MIN_TILES");
-  return e ? std::atoll(e) : 256LL;
+  return e ? std::atoll(e) : 128LL;
 }();
 static long long g_min_tiles = [] {
   const char* e = std::getenv("DMF_SQ_MIN_TILES");
-  return e ? std::atoll(e) : 256LL;
+  return e ? std::atoll(e) : 128LL;
 }();
 static bool wide_disabled() {
   static const int v = [] {
