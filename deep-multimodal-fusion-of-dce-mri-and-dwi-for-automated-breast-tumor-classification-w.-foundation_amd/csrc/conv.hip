@@ -1568,17 +1568,17 @@ static int g_ps_dbg = [] {
   const char* e = std::getenv("DMF_PS_DBG");
   return e ? std::atoi(e) : 0;
 }();
-// tiles a launch needs before the wide (256x128) / square (256x256) forms take it: half a
-// tile per CU -- with the two encoder streams in flight a half-filling launch leaves the
-// other CUs to the other stream (measured, both at 128 vs 256: mode-A step -1.2 %, mode B
-// +0.4 %, encoder forward within noise; interleaved A/B over four rounds)
+// tiles a launch needs before the wide (256x128) / square (256x256) forms take it: one per
+// CU. At 128 (half a tile per CU, the other encoder stream filling the rest) the two-stream
+// mode-A step measured -1.2 %, but every single-stream launch runs on half the GPU: config 2
+// (one stream) -14 %, conv-forward roofline fraction 0.27 -> 0.23 (profiles/r02s_bench.json)
 static long long g_wide_min_tiles = [] {
   const char* e = std::getenv("DMF_WIDE_MIN_TILES");
-  return e ? std::atoll(e) : 128LL;
+  return e ? std::atoll(e) : 256LL;
 }();
 static long long g_min_tiles = [] {
   const char* e = std::getenv("DMF_SQ_MIN_TILES");
-  return e ? std::atoll(e) : 128LL;
+  return e ? std::atoll(e) : 256LL;
 }();
 static bool wide_disabled() {
   static const int v = [] {
