@@ -65,7 +65,7 @@ struct ConvArgs {
   int stat_acc;
   // benchmarking only (dmf_conv_tune key 6), k_conv_fwd_ps: bit 1 skips the
   // DMA (the loop then computes on stale LDS), bit 2 the epilogue, bit 3 its
-  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal (env DMF_PS_DBG)
+  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal (dmf_conv_tune key 6 only)
   int dbg;
 };
 
@@ -1564,10 +1564,10 @@ static int g_ps_enable = [] {
   const char* e = std::getenv("DMF_PS");
   return e && e[0] == '0' ? 0 : 1;
 }();
-static int g_ps_dbg = [] {
-  const char* e = std::getenv("DMF_PS_DBG");
-  return e ? std::atoi(e) : 0;
-}();
+// benchmarking bits of k_conv_fwd_ps (skip DMA / epilogue / stores / statistics): set only through
+// dmf_conv_tune key 6 by the A/B tools, never from the environment (a stray variable would
+// silently corrupt outputs)
+static int g_ps_dbg = 0;
 // tiles a launch needs before the wide (256x128) / square (256x256) forms take it: one per
 // CU. At 128 (half a tile per CU, the other encoder stream filling the rest) the two-stream
 // mode-A step measured -1.2 %, but every single-stream launch runs on half the GPU: config 2

@@ -288,6 +288,116 @@ __global__ void __launch_bounds__(256) k_recon_band(ReconArgs a) {
   }
 }
 
+// Streaming form (the recon launch of a fusion step at HBM rate): block =
+// (b, band of RECON_RB output rows), thread = output column(s). The band's
+// <= 3 source rows of every map are staged in LDS once; each thread
+// x-interpolates them for its column, then per output row needs one FMA for
+// the bilinear value, the loss term and dL/dv (targets streamed once,
+// coalesced, straight from HBM). The gradient is contracted separably in
+// registers: over the band's rows first (A[k][r][x] = sum_y wy(y, r) g(y,
+// x)), then over x through LDS (each (k, r, j) sums its <= S/w + 2
+// contributing columns), so a band adds <= 3 rows x w values per map with
+// one atomic each and the loss sums with one atomic per map per block.
+constexpr int RECON_NR = 3;   // source rows a band may touch
+constexpr int RECON_XPT = 2;  // output columns per thread (S <= 512)
+template <typename T>
+__global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a) {
+  __shared__ float Rs[5][RECON_NR][64];
+  __shared__ float Acc[5][RECON_NR][RECON_MAXS];
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int y0 = blockIdx.y * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
+  const int tid = threadIdx.x;
+  const float inv_n = 1.f / ((float)a.B * a.S * a.S);
+  int ib0, ie, tmp;
+  float ftmp;
+  lin_r(y0, a.h, a.S, ib0, tmp, ftmp);
+  lin_r(y1 - 1, a.h, a.S, tmp, ie, ftmp);
+  const int nrows = ie - ib0 + 1;  // <= RECON_NR (checked by the launcher)
+  for (int t = tid; t < a.nterms * RECON_NR * 64; t += blockDim.x) {
+    const int k = t / (RECON_NR * 64), rem = t - k * (RECON_NR * 64), r = rem / 64, j = rem - r * 64;
+    float v = 0.f;
+    if (r < nrows && j < a.w) {
+      const T* R = (const T*)a.r[k] + ((size_t)b * a.h * a.w + (size_t)(ib0 + r) * a.w + j) * a.ldr[k];
+      v = ld(R);
+    }
+    Rs[k][r][j] = v;
+  }
+  __syncthreads();
+  float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < RECON_XPT; ++u) {
+    const int x = tid + u * 256;
+    if (x >= a.S) break;
+    int j0, j1;
+    float lx;
+    lin_r(x, a.w, a.S, j0, j1, lx);
+    float rx[5][RECON_NR], A[5][RECON_NR];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int r = 0; r < RECON_NR; ++r) {
+        rx[k][r] = (1.f - lx) * Rs[k][r][j0] + lx * Rs[k][r][j1];
+        A[k][r] = 0.f;
+      }
+    for (int y = y0; y < y1; ++y) {
+      int i0, i1;
+      float ly;
+      lin_r(y, a.h, a.S, i0, i1, ly);
+      const int q0 = i0 - ib0, q1 = i1 - ib0;
+      const size_t tp = ((size_t)b * a.S + y) * a.S + x;
+      const float tAv = a.tA ? a.tA[tp] : 0.f, tBv = a.tB ? a.tB[tp] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        if (k >= a.nterms) break;
+        // the x-interpolated source rows q0 / q1 (<= 3 rows: select without dynamic register indexing)
+        const float r0 = q0 == 0 ? rx[k][0] : (q0 == 1 ? rx[k][1] : rx[k][2]);
+        const float r1 = q1 == 0 ? rx[k][0] : (q1 == 1 ? rx[k][1] : rx[k][2]);
+        const float v = (1.f - ly) * r0 + ly * r1;
+        float tv = a.target[k] == 0 ? tAv : (a.target[k] == 1 ? tBv : a.ca * tAv + a.cb * tBv);
+        tv = fminf(fmaxf(tv, 0.f), 1.f);
+        const float sg = sigmoid_f(v);
+        const float pp = fminf(fmaxf(sg, 0.f), 1.f);
+        const float d = pp - tv;
+        const float q = sqrtf(d * d + 1e-6f);
+        part[k] += q;
+        const float g = d / q * sg * (1.f - sg) * inv_n;  // dL/dv (the clamp is the identity on (0,1))
+        const float g0 = (1.f - ly) * g, g1 = ly * g;
+#pragma unroll
+        for (int r = 0; r < RECON_NR; ++r) A[k][r] += (q0 == r ? g0 : 0.f) + (q1 == r ? g1 : 0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int r = 0; r < RECON_NR; ++r) Acc[k][r][x] = A[k][r];
+  }
+  __syncthreads();
+  // x-contraction: (k, r, j) sums the columns x whose source column j0 or j1 is j
+  for (int t = tid; t < a.nterms * nrows * a.w; t += blockDim.x) {
+    const int k = t / (nrows * a.w), rem = t - k * (nrows * a.w), r = rem / a.w, j = rem - r * a.w;
+    if (!a.grads[k]) continue;
+    int xl = (int)floorf(((float)j - 1.f + 0.5f) * a.S / a.w - 0.5f) - 1;
+    int xh = (int)ceilf(((float)j + 1.f + 0.5f) * a.S / a.w - 0.5f) + 2;
+    xl = max(xl, 0);
+    xh = min(xh, a.S);
+    float h = 0.f;
+    for (int x = xl; x < xh; ++x) {
+      int j0, j1;
+      float lx;
+      lin_r(x, a.w, a.S, j0, j1, lx);
+      const float av = Acc[k][r][x];
+      if (j0 == j) h += (1.f - lx) * av;
+      if (j1 == j) h += lx * av;
+    }
+    if (h != 0.f) atomicAdd(a.grads[k] + ((size_t)b * a.h + ib0 + r) * a.w + j, h);
+  }
+  for (int k = 0; k < a.nterms; ++k) {
+    const float sm = block_sum(part[k], red);
+    if (tid == 0) atomicAdd(a.sums + k, sm);
+  }
+}
+
 // ------------------------------------------------------------ mimic
 // pair i: student S_i = s + i*sstride, teacher T_i = t + i*tstride, each an
 // [HW][C] NHWC map (channel stride ld). mimic_feat_loss flattens [C,H,W] to
@@ -421,7 +531,16 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
   a.tA = tA; a.tB = tB; a.ca = ca; a.cb = cb;
   a.B = B; a.h = h; a.w = w; a.S = S;
   a.sums = sums;
-  if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
+  // source rows a band of RECON_RB output rows touches: at most ceil(RB*h/S) + 1 (+1 clamp slack)
+  const bool stream_ok = S <= RECON_MAXS && S <= 256 * RECON_XPT && h <= S && w <= 64 &&
+                         (RECON_RB * h + S - 1) / S + 2 <= RECON_NR;
+  if (stream_ok) {
+    const dim3 g(B, cdiv(S, RECON_RB));
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), 0, (hipStream_t)stream, a);
+  } else if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
     const dim3 g(B, cdiv(S, RECON_RB));
     if (dtype == DMF_BF16)
       hipLaunchKernelGGL(k_recon_band<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a);

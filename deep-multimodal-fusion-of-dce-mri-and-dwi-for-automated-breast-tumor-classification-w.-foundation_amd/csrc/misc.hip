@@ -274,7 +274,8 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int 
     const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
     for (int ho = ho_lo; ho <= ho_hi; ++ho)
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        // recompute the window argmax (first max in row-major window order)
+        // recompute the window argmax with torch's rule (max_pool2d_with_indices): the index
+        // starts at the window's first valid element and moves on `v > max || isnan(v)`
         float m = -INFINITY;
         int am = -1;
         for (int r = 0; r < k; ++r) {
@@ -284,7 +285,8 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int 
             const int wi = wo * s - p + q;
             if (wi < 0 || wi >= W) continue;
             const float v = ld(x + ((size_t)(n * H + hi) * W + wi) * ldx + c);
-            if (v > m || (isnan(v) && !isnan(m))) { m = v; am = hi * W + wi; }
+            if (am < 0) am = hi * W + wi;
+            if (v > m || isnan(v)) { m = v; am = hi * W + wi; }
           }
         }
         if (am == h * W + w) g += ld(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy + c);
@@ -326,8 +328,10 @@ __global__ void k_maxpool_bwd8(const T* __restrict__ x, int N, int H, int W, int
             ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + c, v);
             const int pos = hi * W + wi;
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (v[e] > m[e] || (isnan(v[e]) && !isnan(m[e]))) { m[e] = v[e]; am[e] = pos; }
+            for (int e = 0; e < 8; ++e) {
+              if (am[e] < 0) am[e] = pos;  // torch: the first valid element until a max / NaN replaces it
+              if (v[e] > m[e] || isnan(v[e])) { m[e] = v[e]; am[e] = pos; }
+            }
           }
         }
         float d[8];
@@ -688,9 +692,11 @@ __global__ void k_up_nearest8(const T* __restrict__ x, int ldx, T* __restrict__ 
 }
 
 // Max pool forward that also records, per output element, the window
-// position (r*k + q, one byte) of its maximum -- the first one in scan order,
-// first NaN wins, exactly the element k_maxpool_bwd8 re-derives -- so the
-// backward needs no window re-scan (k_maxpool_bwd_idx8).
+// position (r*k + q, one byte) of its maximum with torch's rule
+// (max_pool2d_with_indices: start at the window's first valid element, move
+// on `v > max || isnan(v)`, so an all -inf window routes its gradient to the
+// first element and the last NaN wins), exactly the element k_maxpool_bwd8
+// re-derives -- so the backward needs no window re-scan (k_maxpool_bwd_idx8).
 template <typename T>
 __global__ void k_maxpool_idx8(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y,
                                int Ho, int Wo, int ldy, unsigned char* __restrict__ idx, int k, int s, int p) {
@@ -713,8 +719,10 @@ __global__ void k_maxpool_idx8(const T* __restrict__ x, int N, int H, int W, int
         float v[8];
         ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (v[j] > m[j] || (isnan(v[j]) && !isnan(m[j]))) { m[j] = v[j]; am[j] = (unsigned)(r * k + q); }
+        for (int j = 0; j < 8; ++j) {
+          if (am[j] == 255u) am[j] = (unsigned)(r * k + q);
+          if (v[j] > m[j] || isnan(v[j])) { m[j] = v[j]; am[j] = (unsigned)(r * k + q); }
+        }
       }
     }
     st8(y + (size_t)pix * ldy + cv * 8, m);

@@ -135,7 +135,8 @@ class FusionTrainer:
 
     def _signature(self):
         groups = tuple(len(g["params"]) for g in self.opt.param_groups)
-        return groups, tuple(id(p) for p in self._trainable()), self.opt.tables_version
+        step_sig = self.lm.step_signature() if hasattr(self.lm, "step_signature") else ()
+        return groups, tuple(id(p) for p in self._trainable()), self.opt.tables_version, step_sig
 
     # ------------------------------------------------- overlapped exchange
     def _install_hooks(self):
@@ -272,11 +273,31 @@ class FusionTrainer:
                 "buffers": [(b, b.clone()) for _, b in self.lm.named_buffers()],
                 "opt": {id(t): (t, t.clone()) for st in o.state.values() for t in st.values()
                         if torch.is_tensor(t) and t.is_cuda},
-                "steps": o._steps.clone() if o._steps is not None else None,
+                "steps": self._steps_by_param(),
                 "rng": [(t, t.clone()) for t in O.RNG.states.values()]
                 + ([(self.scaler.amp, self.scaler.amp.clone()), (self.scaler.tracker, self.scaler.tracker.clone())]
                    if self.scaler is not None else []),
                 "global_step": self.lm.global_step}
+
+    def _steps_by_param(self):
+        """{id(param): AdamW step count} as the optimizer would continue from:
+        the device counters where a slot exists, else the state's 'step'
+        (e.g. just after load_state_dict)."""
+        o = self.opt
+        dev_steps = None
+        if o._steps is not None:
+            o._flush_steps()
+            dev_steps = o._steps.tolist()
+        out = {}
+        for g in o.param_groups:
+            for p in g["params"]:
+                slot = o._index.get(id(p))
+                if slot is not None and dev_steps is not None:
+                    out[id(p)] = int(dev_steps[slot])
+                elif p in o.state and "step" in o.state[p]:
+                    st = o.state[p]["step"]
+                    out[id(p)] = int(st.item() if torch.is_tensor(st) else st)
+        return out
 
     def _restore(self, snap):
         """Undo what the steps since ``snap`` changed, in place (the captured
@@ -296,9 +317,13 @@ class FusionTrainer:
                         else:
                             t.zero_()
             if o._steps is not None:
-                want = torch.zeros_like(o._steps)
-                if snap["steps"] is not None:
-                    want[: snap["steps"].numel()] = snap["steps"]
+                # every slot back to its parameter's count at the snapshot: a slot seeded from a
+                # loaded checkpoint's 'step' (load_state_dict leaves _steps unset until the warm-up
+                # steps build it) returns to that value, a slot that did not exist to 0
+                want = torch.zeros(o._steps.numel(), dtype=torch.int32)
+                for pid, slot in o._index.items():
+                    want[slot] = snap["steps"].get(pid, 0)
+                want = want.to(o._steps.device)
                 o._steps.copy_(want)
                 if o._table_key is not None and o._live_steps is not None:
                     o._live_steps.copy_(want[o._slot])
@@ -325,7 +350,9 @@ class FusionTrainer:
         torch.cuda.synchronize()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
-            self.loss = self._fwd_bwd(self.static_batch)
+            # detached: keeping the capture pass's autograd graph alive would pin its saved
+            # activations (and trips torch's AccumulateGrad stream check on later steps)
+            self.loss = self._fwd_bwd(self.static_batch).detach()
             if self.world > 1 and not self.overlap:
                 self.opt.pack_grads()
         g2 = torch.cuda.CUDAGraph()
@@ -354,6 +381,8 @@ class FusionTrainer:
             for dst, src in zip(self.static_batch, batch):
                 dst.copy_(src, non_blocking=True)
         self.opt.sync_hyper()  # scheduler lr / wd changes -> the captured hyper table (same storage)
+        if hasattr(self.lm, "sync_step_scalars"):
+            self.lm.sync_step_scalars()  # the epoch's aux-loss weight -> the scalar the captured loss reads
         g1, g2 = self.graphs
         g1.replay()
         if self.world > 1 and not self.overlap:

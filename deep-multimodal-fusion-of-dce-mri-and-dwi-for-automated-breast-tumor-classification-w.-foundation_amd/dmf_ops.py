@@ -396,6 +396,9 @@ class BnArena:
     def begin(self, zero):
         self.ci = 0
         self.off = 0
+        # a backward holding a slice of an earlier forward checks this: once the owner's next
+        # forward has begun, that slice has been zeroed / handed out again
+        self.gen = getattr(self, "gen", 0) + 1
         if zero:
             for c in self.chunks:
                 c.zero_()
@@ -461,6 +464,25 @@ def _bn_acc(c, dev):
     if ar is not None and ar.device == dev:
         return ar.take(n)
     return torch.zeros(n, dtype=torch.float64, device=dev)  # outside any forward scope (unit tests)
+
+
+class _BwdAcc:
+    """A backward's BN column-sum slice of the forward's arena, usable ONCE and
+    only while no later forward of the same owner has re-begun the arena
+    (retain_graph double backward, or two forwards before one backward, fall
+    back to the per-tile slab form)."""
+
+    __slots__ = ("buf", "arena", "gen")
+
+    def __init__(self, c, dev):
+        self.arena = ARENA[0]
+        self.gen = self.arena.gen
+        self.buf = _bn_acc(c, dev)
+
+    def claim(self):
+        ok = self.buf is not None and self.arena.gen == self.gen
+        buf, self.buf = self.buf, None
+        return buf if ok else None
 
 
 def _bn_desc(bn, acc, count, unbias_count, ss, save):
@@ -801,7 +823,7 @@ class _ConvBNActFn(torch.autograd.Function):
         # the backward's BN column sums: a zeroed slice of this forward's statistics arena
         # (dmf_act_bwd_bn_reduce_acc / dmf_bn_bwd_apply_acc: no finalize launch)
         # (training-mode BN only: the arena is zeroed at the forward's start when a BN trains)
-        ctx.bwd_acc = (_bn_acc(c, y.device) if BWD_BN_ARENA and ARENA[0] is not None and c % 8 == 0
+        ctx.bwd_acc = (_BwdAcc(c, y.device) if BWD_BN_ARENA and ARENA[0] is not None and c % 8 == 0
                        and spec[2].training and any(ctx.needs_input_grad) else None)
         return out
 
@@ -821,7 +843,7 @@ class _ConvBNActFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         dgamma = grad_sink(bn.weight) if need[4] else None
         dbeta = grad_sink(bn.bias) if need[5] else None
-        acc = ctx.bwd_acc
+        acc = ctx.bwd_acc.claim() if ctx.bwd_acc is not None else None
         lddo, lddz = nhwc(dout)[4], nhwc(dz)[4]
         if (acc is not None and ldy % 8 == 0 and lddo % 8 == 0 and (res_t is None or ldr % 8 == 0)
                 and (dout.data_ptr() | y.data_ptr() | (res_t.data_ptr() if res_t is not None else 0)) % 16 == 0):

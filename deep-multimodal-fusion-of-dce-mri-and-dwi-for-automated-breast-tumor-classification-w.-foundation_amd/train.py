@@ -74,6 +74,15 @@ class LightningSingleModel(nn.Module):
     def forward(self, x, masks=None):
         return self.model(x, masks)
 
+    def step_signature(self):
+        """The captured step's structure beyond the optimizer: the aux-loss
+        gate (train.py:391, aux_w > 0)."""
+        return (aux_weight_value(self) > 0.0,)
+
+    def sync_step_scalars(self):
+        """Write the aux-loss weight the captured step reads before a replay."""
+        sync_aux_weight(self)
+
     def configure_optimizers(self):
         """train.py:190-224 (the grad_clip keys are returned but never
         honoured, quirk Q10)."""
@@ -97,7 +106,7 @@ class LightningSingleModel(nn.Module):
         labels = labels.to(dev, non_blocking=True).long()
         if masks is not None:
             masks = masks.to(dev, non_blocking=True)
-        aux_w = max(0.0, 1 - self.current_epoch / self.aux_loss_limit) if self.use_aux_loss_sched else 1.0
+        aux_w = aux_weight_value(self)
 
         outputs, aux, mask_output = self(inputs, masks)
 
@@ -130,11 +139,13 @@ class LightningSingleModel(nn.Module):
         recon_loss_val = torch.zeros((), device=dev)
         mimic_loss_val = torch.zeros((), device=dev)
         if self.recon_enabled and aux_w > 0.0:
-            recon_loss_val, mimic_loss_val = self.compute_aux_losses(aux, inputs, aux_w, is_train)
+            # the device scalar, not the float: a captured step replays with the current epoch's weight
+            w = aux_weight_tensor(self, dev) if inputs.is_cuda else aux_w
+            recon_loss_val, mimic_loss_val = self.compute_aux_losses(aux, inputs, w, is_train)
             if is_train:
                 # the values are already lambda * aux_w weighted (train.py:458-460): weighted twice, as there
-                batch_loss = batch_loss + (self.lambda_recon * recon_loss_val * aux_w
-                                           + self.lambda_mimic * mimic_loss_val * aux_w)
+                batch_loss = batch_loss + (self.lambda_recon * recon_loss_val * w
+                                           + self.lambda_mimic * mimic_loss_val * w)
 
         preds = outputs.argmax(dim=1)
         acc = (preds == labels).float().mean()
@@ -152,7 +163,7 @@ class LightningSingleModel(nn.Module):
         dev = inputs.device
         recon = torch.zeros((), device=dev)
         mimic = torch.zeros((), device=dev)
-        if aux_w <= 0.0:
+        if not torch.is_tensor(aux_w) and aux_w <= 0.0:  # a device weight is only passed while aux_w > 0
             return recon, mimic
         maps = [r for r in (aux.get("recon_feats", []) if aux is not None else []) if r is not None]
         if maps:
@@ -182,6 +193,41 @@ class LightningSingleModel(nn.Module):
     def validation_step(self, batch, batch_idx=0):
         loss, _, _, _ = self._shared_step(batch, batch_idx, phase="val", return_preds=True)
         return loss
+
+
+# ------------------------------------------------------------------ aux-loss schedule
+def aux_weight_value(module):
+    """train_fusion.py:221-224 / train.py:321-324: max(0, 1 - epoch / limit)
+    under the simple aux-loss schedule, else 1."""
+    if not module.use_aux_loss_sched:
+        return 1.0
+    return max(0.0, 1 - module.current_epoch / module.aux_loss_limit)
+
+
+def aux_weight_tensor(module, device):
+    """The aux-loss weight as a device fp32 scalar that the loss multiplies by.
+
+    A Python float would be baked into a captured hipGraph (forward AND the
+    saved backward), so a replay at epoch 10 would still weigh recon / mimic
+    by the capture-time epoch's weight. The step reads this scalar instead;
+    it is rewritten eagerly before every replay (``sync_aux_weight``) the way
+    the optimizer's hyper table is. Outside a capture it is refreshed here."""
+    w = module.__dict__.get("_aux_w_dev")
+    if w is None or w.device != torch.device(device):
+        if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("aux-loss weight scalar must be created by an eager step before capture")
+        w = torch.empty((), dtype=torch.float32, device=device)
+        module.__dict__["_aux_w_dev"] = w
+    if not (device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+        w.fill_(aux_weight_value(module))
+    return w
+
+
+def sync_aux_weight(module):
+    """Write the current epoch's aux weight into the captured step's scalar."""
+    w = module.__dict__.get("_aux_w_dev")
+    if w is not None:
+        w.fill_(aux_weight_value(module))
 
 
 # ------------------------------------------------------------------ TTA flips (train.py:916-923)

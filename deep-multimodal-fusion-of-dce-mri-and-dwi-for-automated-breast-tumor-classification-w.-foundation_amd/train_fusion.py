@@ -16,8 +16,8 @@ import torch.nn as nn
 import dmf_ops as O
 from loss import LabelSmoothing
 from selector_helpers import LightningFusionOptimizerFactory, mask_criterion_selector
-from train import (compute_attn_energy_loss, compute_feat_norm_loss, compute_feature_consistency_loss, tta_flip_lr,
-                   tta_flip_lrud, tta_flip_ud, tta_id)
+from train import (aux_weight_tensor, aux_weight_value, compute_attn_energy_loss, compute_feat_norm_loss,
+                   compute_feature_consistency_loss, sync_aux_weight, tta_flip_lr, tta_flip_lrud, tta_flip_ud, tta_id)
 
 
 class LightningFusionModel(nn.Module):
@@ -87,6 +87,18 @@ class LightningFusionModel(nn.Module):
     def forward(self, dwi_feats, dce_feats, dwi_mask=None, dce_mask=None):
         return self.fusion_model(dwi_feats, dce_feats, dwi_mask, dce_mask)
 
+    # ---------------------------------------------- captured-step hooks
+    def step_signature(self):
+        """What the captured step's graph STRUCTURE depends on beyond the
+        optimizer layout: the aux-loss gate (train_fusion.py:274, aux_w > 0
+        drops the recon and mimic nodes after epoch ``aux_loss_limit``)."""
+        return (aux_weight_value(self) > 0.0,)
+
+    def sync_step_scalars(self):
+        """Write the epoch-dependent scalars the captured step reads (the
+        aux-loss weight) before a replay."""
+        sync_aux_weight(self)
+
     # ------------------------------------------------------------- encoders
     def _encode(self, dwi_inputs, dce_inputs):
         """The two encoder forwards (train_fusion.py:227-230). They are
@@ -141,7 +153,7 @@ class LightningFusionModel(nn.Module):
         labels = labels.long().to(dev, non_blocking=True)
         if masks_batch is not None:
             masks_batch = masks_batch.to(dev, non_blocking=True)
-        aux_w = max(0.0, 1 - self.current_epoch / self.aux_loss_limit) if self.use_aux_loss_sched else 1.0
+        aux_w = aux_weight_value(self)
 
         (_, dwi_aux, dwi_mask_pred), (_, dce_aux, dce_mask_pred) = self._encode(dwi_inputs, dce_inputs)
         logits, fused_mask_logits, aux = self.forward(dwi_aux["raw_feats"], dce_aux["raw_feats"], dwi_mask_pred,
@@ -172,13 +184,17 @@ class LightningFusionModel(nn.Module):
         recon_loss_val = torch.zeros((), device=dev)
         mimic_loss_val = torch.zeros((), device=dev)
         if aux_w > 0.0 and self.recon_enabled and is_train:
+            # the epoch-dependent weight as a device scalar: a captured step replays with the current
+            # epoch's value (FusionTrainer.step writes it before every replay); the aux_w > 0 gate itself
+            # is part of the trainer's capture signature
+            w = aux_weight_tensor(self, dev) if dev.type == "cuda" else aux_w
             recon_loss_val = fused_recon_losses(dwi_aux["recon_feats"], dce_aux["recon_feats"], aux["recon_fused"],
                                                 dwi_inputs.detach(), dce_inputs.detach())
-            total = total + self.lambda_recon * recon_loss_val * aux_w
+            total = total + self.lambda_recon * recon_loss_val * w
             pf = aux.get("proj_fused", None)
             if self.mimic_enabled and pf is not None and len(pf) >= 4:
                 mimic_loss_val = O.mimic_pairs(pf, npairs=2)
-                total = total + self.lambda_mimic * mimic_loss_val * aux_w
+                total = total + self.lambda_mimic * mimic_loss_val * w
 
         preds = torch.argmax(logits, dim=1)
         acc = (preds == labels).float().mean()

@@ -283,6 +283,41 @@ def test_maxpool_recorded_positions_match_rescan(dtype):
     assert torch.equal(torch.nan_to_num(y.detach().float().cpu(), nan=9.0), torch.nan_to_num(ref.detach(), nan=9.0))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool_gradient_routing_matches_torch_on_inf_and_nan_windows(dtype):
+    """Window argmax rule of torch's max_pool2d_with_indices: the
+    index starts at the window's first valid element and moves on
+    ``v > max || isnan(v)``. An all -inf window sends its gradient to that
+    first element (not nowhere), two NaNs in a window route to the later one.
+    Both the recorded-position path (C % 8 == 0) and the re-scan backward are
+    compared with torch's CPU max_pool2d backward, bit for bit."""
+    import dmf_native as N
+    torch.manual_seed(8)
+    x = torch.randn(2, 16, 9, 10)
+    x[0, :, 0:4, 0:4] = float("-inf")   # windows of (0,0), (0,1), (1,0), (1,1) entirely -inf
+    x[1, 3, 4, 4] = float("nan")
+    x[1, 3, 4, 5] = float("nan")        # the later NaN of window (2,2) wins
+    x[1, 7, :, :] = float("-inf")       # a whole -inf channel
+    xr = x.clone().to(dtype).float().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    g = torch.randn(ref.shape).to(dtype).float()  # representable in dtype: both sides sum the same values
+    ref.backward(g)
+    xd = _to_dev(x, dtype).requires_grad_(True)
+    y = O.maxpool2d(xd, 3, 2, 1)
+    y.backward(_to_dev(g, dtype))
+    want = xr.grad.to(dtype).float()
+    assert torch.equal(xd.grad.float().cpu(), want)
+    n, c, h, w = x.shape
+    ho, wo = y.shape[2], y.shape[3]
+    xs = xd.detach()
+    dx2 = O.empty_nhwc(n, c, h, w, dtype, xs.device)
+    gd = _to_dev(g, dtype)
+    N.call("dmf_maxpool2d_bwd", O.dt(xs), xs.data_ptr(), n, h, w, c, c, gd.data_ptr(), ho, wo, c, dx2.data_ptr(), c,
+           3, 2, 1, O._stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx2.float().cpu(), want)
+
+
 def test_maxpool_and_bilinear_and_tokens():
     torch.manual_seed(5)
     x = torch.randn(2, 16, 17, 15)
