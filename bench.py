@@ -54,7 +54,7 @@ def parse():
                          "3: fusion step (default); "
                          "5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
     ap.add_argument("--no-extras", action="store_true",
-                    help="default run only: skip the mode-B and config-2 sub-measurements")
+                    help="default run only: skip the mode-B, config-2 and config-5 sub-measurements")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -587,6 +587,25 @@ def main():
         torch.cuda.empty_cache()
         if world == 1:
             out["config2"] = bench_config2(device, 16, 20, 5, probe=False)
+        # hybrid TransformerStage encoders at S=384 (576 tokens, E=512, depth 6,
+        # 4 heads; parameters_generate.py:71-75) with the fp8-e4m3 MFMA patch-embed, bf16 elsewhere,
+        # mode A, B=32 per GPU -- a DP configuration, so measured on every rank like mode B
+        torch.cuda.empty_cache()
+        P5 = PR.default_parameters()
+        P5["dwi_model_parameters"]["use_hybrid_transformer"] = True
+        P5["dwi_model_parameters"]["patch_embed_fp8"] = True
+        P5["dwi_model_parameters"]["input_size"] = 384
+        n5 = max(10, args.steps // 2)
+        t5, _, dt5 = bench_fusion(P5, device, dtype, "A", args.batch, 384, n5, 3, world, rank,
+                                  use_graph=not args.no_graph)
+        out["config5"] = {"value": round(args.batch * world * n5 / dt5, 2), "unit": "volumes/s",
+                          "ms_per_step": round(dt5 * 1e3 / n5, 3), "steps": n5, "warmup": 3,
+                          "loss": float(t5.loss.item()) if t5.loss is not None else None,
+                          "workload": "fusion training step, config 5 (hybrid TransformerStage encoders, S=384, "
+                                      "fp8-e4m3 patch-embed, bf16 elsewhere), mode A",
+                          "per_gpu_batch": args.batch, "size": 384, "patch_embed": "fp8"}
+        del t5
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args, lambda: _cpu_params(PR, args))

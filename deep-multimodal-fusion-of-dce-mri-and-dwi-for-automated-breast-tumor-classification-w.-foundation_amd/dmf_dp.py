@@ -120,6 +120,9 @@ class FusionTrainer:
             self.scaler = DeviceGradScaler(lm.device)
         cfg = lm.configure_optimizers()
         self.opt = cfg["optimizer"] if isinstance(cfg, dict) else cfg
+        # {"scheduler", "monitor", "interval"} of the factory (selector_helpers.py:148-156), stepped by the
+        # epoch driver (dmf_fit.FusionFit) with the all-reduced val_loss
+        self.lr_scheduler = cfg.get("lr_scheduler") if isinstance(cfg, dict) else None
         self.lm.optimizer = self.opt
         self.graphs = None
         self.static_batch = None
@@ -352,13 +355,14 @@ class FusionTrainer:
         with torch.cuda.graph(g1):
             # detached: keeping the capture pass's autograd graph alive would pin its saved
             # activations (and trips torch's AccumulateGrad stream check on later steps)
-            self.loss = self._fwd_bwd(self.static_batch).detach()
+            self._graph_loss = self._fwd_bwd(self.static_batch).detach()
             if self.world > 1 and not self.overlap:
                 self.opt.pack_grads()
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
             self.opt.step(scaler=self.scaler)
         self.graphs = (g1, g2)
+        self.loss = self._graph_loss
         self._restore(snap)
         torch.cuda.synchronize()
         self._graph_sig = self._signature()
@@ -377,6 +381,9 @@ class FusionTrainer:
                 self.capture(batch)
             else:
                 return self.eager_step(batch)
+        if batch is not None and any(a.shape != b.shape for a, b in zip(batch, self.static_batch)):
+            # a ragged batch (an epoch's last one): the captured shapes do not apply -- run it eagerly
+            return self.eager_step(batch)
         if batch is not None and batch[0].data_ptr() != self.static_batch[0].data_ptr():
             for dst, src in zip(self.static_batch, batch):
                 dst.copy_(src, non_blocking=True)
@@ -389,4 +396,5 @@ class FusionTrainer:
             allreduce_mean_(self.opt.bucket, self.world)
         g2.replay()
         self.lm.global_step += 1
+        self.loss = self._graph_loss  # (an eager ragged step in between rebinds self.loss)
         return self.loss

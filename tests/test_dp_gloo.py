@@ -123,3 +123,51 @@ def test_two_rank_bucket_allreduce_matches_ddp_mean():
     torch.testing.assert_close(bucket, want, rtol=1e-5, atol=1e-6 * want.abs().max().item())
     torch.testing.assert_close(alll, torch.cat(labels))
     assert auc == pytest.approx(MT.multiclass_auroc(allp, alll))
+
+
+def _fit_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dmf_fit import allgather_valid_rows, allreduce_sum, shard
+        import metrics as MT
+
+        n = 11
+        g = torch.Generator().manual_seed(5)
+        probs_all = torch.softmax(torch.randn(n, 4, generator=g), 1)
+        labels_all = torch.arange(n) % 4
+        items, valid = shard(n, rank, world)
+        # the epoch driver's layout: every rank the same row count, padding rows flagged off
+        p = probs_all[items]
+        y = labels_all[items]
+        f = torch.tensor(valid, dtype=torch.uint8)
+        allp = allgather_valid_rows(p, f, world)
+        ally = allgather_valid_rows(y, f, world)
+        cnt = allreduce_sum(torch.tensor([float(sum(valid))], dtype=torch.float64), world)
+        if rank == 0:
+            q.put((items, allp, ally, cnt.item(), MT.multiclass_auroc(allp, ally),
+                   MT.multiclass_auroc(probs_all, labels_all)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_epoch_driver_shards_and_gathers_every_volume_once():
+    """dmf_fit's validation collectives on 3 ranks over 11 volumes (ragged:
+    DistributedSampler pads by wrap-around): every volume is gathered
+    exactly once, so the epoch AUROC equals the single-process one
+    (train.py:682-695)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fit_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    items0, allp, ally, cnt, auc, auc_single = q.get(timeout=250)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(items0) == 4 and cnt == 11 and allp.shape == (11, 4)
+    assert sorted(ally.tolist()) == sorted((torch.arange(11) % 4).tolist())
+    assert auc == pytest.approx(auc_single, abs=1e-12)

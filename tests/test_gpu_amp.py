@@ -104,3 +104,85 @@ def test_trainer_16_mixed_matches_unscaled(mode):
     num = sum((p16[n] - p32[n]).pow(2).sum().item() for n in p32)
     den = sum((p32[n]).pow(2).sum().item() for n in p32)
     assert (num / den) ** 0.5 < 1e-5, (num / den) ** 0.5
+
+
+def test_trainer_16_mixed_bf16_gradients_and_overflow_skip():
+    """"16-mixed" on the reduced-precision path: bf16
+    compute, everything trainable (mode B: bf16 gradients through both
+    encoders), captured step. (1) Against the unscaled "bf16-mixed" trainer
+    on the same batches: the power-of-two scale is exact in bf16, so the
+    parameter updates agree to the backward's float-atomic noise. (2) An
+    overflowing step, injected by raising the device scale to 2^127 (the
+    scaled backward then produces inf / nan): the captured replay leaves
+    every parameter, AdamW moment and step counter untouched and backs the
+    scale off to 2^126; the next step at a sane scale trains again."""
+    import make_golden as MG
+    import foundation_model as FM
+    import model_module as MM
+    import parameters as PR
+    import train_fusion as TF
+    from dmf_dp import FusionTrainer
+    from selector_helpers import get_classification_loss
+
+    batches = [tuple(t.to(DEV) for t in MG.volume_batch(4, 64, 80 + i)) for i in range(4)]
+    runs = {}
+    for prec in ("bf16-mixed", "16-mixed"):
+        P = copy.deepcopy(PR.small_parameters(channels=(16, 32, 64), input_size=64, dropout=0.0))
+        P["backbone_freeze_on_start"] = False
+        P["precision"] = prec
+        P["dwi_model_parameters"]["optimizer_parameters"]["eps"] = 0.1
+        torch.manual_seed(0)
+        dwi = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, FM.build_medical_backbone(P, "cpu", "dwi", 14)),
+                                  True)
+        dce = MM.initialize_model(MM.ModelMaskHeadBackbone("dce", P, FM.build_medical_backbone(P, "cpu", "dce", 6)),
+                                  True)
+        fm = MM.FusionModel(P)
+        init = {**{"dwi_model." + n: p.detach().clone() for n, p in dwi.named_parameters()},
+                **{"dce_model." + n: p.detach().clone() for n, p in dce.named_parameters()}}
+        for m in (dwi, dce, fm):
+            MM.set_compute_dtype(m, torch.bfloat16)
+        crit = get_classification_loss(P, torch.arange(64) % 4, "fusion", DEV)
+        lm = TF.LightningFusionModel(dwi.to(DEV), dce.to(DEV), fm.to(DEV), P, crit)
+        lm.train()
+        tr = FusionTrainer(lm, world=1, use_graph=True)
+        losses = [float(tr.step(b).item()) for b in batches[:3]]
+        torch.cuda.synchronize()
+        runs[prec] = (lm, tr, losses, init)
+    (lm_a, tr_a, la, init), (lm_b, tr_b, lb, _) = runs["bf16-mixed"], runs["16-mixed"]
+    assert tr_b.scaler is not None and tr_b.scaler.get_scale() == 2.0 ** 16
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (la, lb)
+    pa = dict(lm_a.named_parameters())
+    d_a, d_b = [], []
+    for n, p in lm_b.named_parameters():
+        if n.startswith("fusion_model."):
+            continue
+        d_a.append((pa[n].detach().float().cpu() - init[n].float()).reshape(-1))
+        d_b.append((p.detach().float().cpu() - init[n].float()).reshape(-1))
+    da, db = torch.cat(d_a), torch.cat(d_b)
+    rel = ((db - da).norm() / da.norm()).item()
+    print(f"16-mixed vs bf16-mixed, encoder parameter updates after 3 bf16 steps: relative L2 {rel:.2e}")
+    assert da.norm() > 0 and rel < 5e-2, rel
+    # (2) overflow injection into the captured step
+    counts = tr_b.opt.step_counts()
+    with torch.no_grad():
+        tr_b.scaler.amp[0] = 2.0 ** 127
+    before = {n: p.detach().clone() for n, p in lm_b.named_parameters()}
+    moments = {id(t): t.clone() for st in tr_b.opt.state.values() for t in st.values() if torch.is_tensor(t)
+               and t.is_cuda}
+    tr_b.step(batches[3])
+    torch.cuda.synchronize()
+    assert tr_b.scaler.get_scale() == 2.0 ** 126
+    for n, p in lm_b.named_parameters():
+        assert torch.equal(p.detach(), before[n]), n
+    for st in tr_b.opt.state.values():
+        for t in st.values():
+            if torch.is_tensor(t) and t.is_cuda:
+                assert torch.equal(t, moments[id(t)])
+    assert tr_b.opt.step_counts() == counts
+    with torch.no_grad():
+        tr_b.scaler.amp[0] = 2.0 ** 16
+    tr_b.step(batches[3])
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr_b.loss).item()
+    assert any(not torch.equal(p.detach(), before[n]) for n, p in lm_b.named_parameters())
