@@ -1,0 +1,277 @@
+// Shared pieces of the gfx950 implicit-GEMM conv kernels (conv.hip, conv_pp.hip):
+// launch arguments, activation helpers, the XCD-aware block remap, the BN
+// statistics accumulator and the register epilogue of the 256x256 persistent
+// tiles (operands swapped so each lane holds 16 output channels of one pixel).
+#pragma once
+#include "dmf_common.h"
+#include "../../include/dmf_hip.h"
+
+namespace dmf {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+struct ConvArgs {
+  const void* x;      // A source (FWD: input; DGRAD: dy)
+  const void* w;      // B source [Nout][Ktot]
+  const float* bias;  // [Nout] or null
+  void* y;            // output NHWC, channel stride ldy
+  float* partials;    // [mtiles][Nout][2] or null
+  int N, H, W, C, ldx;  // A-source geometry (C = total channels over both sources)
+  const void* x2;       // optional second source concatenated along channels (FWD only)
+  int C1, ldx2;         // channels taken from x (the rest from x2), stride of x2
+  int Ho, Wo, ldy;      // output geometry
+  int Nout;             // GEMM N
+  int KH, KW, stride, pad, dil;
+  int Ktot;             // KH*KW*C
+  int M;                // N*Ho*Wo
+  int act;
+  int act_in;
+  int mtiles, ntiles;
+  // A-operand prologue (FWD, single source): x <- act(x*in_ss[c] + in_ss[C+c])
+  // on every in-bounds element (padding stays zero), i.e. the producer's
+  // batch-norm apply + activation fused into this conv's loads.
+  const float* in_ss;
+  // fused batch-norm finalize: with `tickets` ([ntiles], zero at rest) the
+  // last-arriving block of each output-channel tile reduces that tile's
+  // columns of the partial-statistics slab (fixed order, double) and
+  // finalizes them into `fin`, then re-zeroes its ticket.
+  unsigned* tickets;
+  BnFin fin;
+  // stat_acc: the BN statistics are ADDED into (double*)partials [Nout][2]
+  // (float64 atomics, zeroed by the caller) instead of one slab row per M
+  // tile; the consumer (dmf_bn_apply) finalizes them
+  int stat_acc;
+  // benchmarking only (dmf_conv_tune key 6), k_conv_fwd_ps: bit 1 skips the
+  // DMA (the loop then computes on stale LDS), bit 2 the epilogue, bit 3 its
+  // stores, bit 4 its statistics; bit 5 makes the stores non-temporal (dmf_conv_tune key 6 only)
+  int dbg;
+};
+
+template <int ACT>
+__device__ __forceinline__ float apply_act(float v) {
+  if (ACT == DMF_ACT_RELU) return fmaxf(v, 0.f);
+  if (ACT == DMF_ACT_GELU) return gelu_f(v);
+  if (ACT == DMF_ACT_SIGMOID) return sigmoid_f(v);
+  return v;
+}
+__device__ __forceinline__ float apply_act_rt(int act, float v) {
+  switch (act) {
+    case DMF_ACT_RELU: return fmaxf(v, 0.f);
+    case DMF_ACT_GELU: return gelu_f(v);
+    case DMF_ACT_SIGMOID: return sigmoid_f(v);
+    default: return v;
+  }
+}
+
+// the activation over a whole register group with ONE uniform branch: a
+// per-element apply_act_rt unrolls into a compare-and-branch chain per value
+// and drags every activation's code through the instruction cache (the
+// persistent conv's epilogue was ~40 % of its time that way)
+template <int N>
+__device__ __forceinline__ void apply_act_arr(int act, float (&v)[N]) {
+  switch (act) {
+    case DMF_ACT_RELU:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = fmaxf(v[e], 0.f);
+      break;
+    case DMF_ACT_GELU:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = gelu_f(v[e]);
+      break;
+    case DMF_ACT_SIGMOID:
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = sigmoid_f(v[e]);
+      break;
+    default:
+      break;
+  }
+}
+template <int FM, int FN>
+__device__ __forceinline__ void apply_act_col(int act, f32x4_t (&acc)[FM][FN], int j) {
+  if (act == DMF_ACT_NONE) return;
+  float v[FM * 4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[i * 4 + r] = acc[i][j][r];
+  apply_act_arr(act, v);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[i][j][r] = v[i * 4 + r];
+}
+
+constexpr int CBM = 128, CBN = 128, CTHREADS = 256;
+constexpr int STAGE_BYTES = (CBM + CBN) * 128;  // A + B, 128-byte rows
+// main LDS: two A/B stages, reused for the C staging tile [BM][BN + 16 B pad]
+__host__ __device__ constexpr int conv_lds_main(int esize, int bm = CBM, int bn = CBN) {
+  return 2 * (bm + bn) * 128 > bm * (bn + 16 / esize) * esize ? 2 * (bm + bn) * 128 : bm * (bn + 16 / esize) * esize;
+}
+constexpr int CONV_LDS_EXTRA = 64 + CTHREADS * 2 * 8;  // flag + reducer doubles
+
+// bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
+// an XCD; give each XCD a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, xcd = b % 8, loc = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+constexpr int BUF_FLAGS_EP = 0x00020000;  // buffer descriptor word 3 (as BUF_FLAGS below)
+
+// BN statistics of one column of one M tile into the accumulator (stat_acc):
+// stat_acc = 1: float64 atomics into [Nout][2]; stat_acc = R > 1: into
+// replica (mt % R) of [R][Nout][2] (spreads the same-address contention of
+// the M tiles over R addresses; the consumer sums the replicas);
+// stat_acc < 0: benchmarking variants (-1 f32 atomics, -2 plain slab store)
+__device__ __forceinline__ void acc_stats(const ConvArgs& a, int mt, int col, float2 v) {
+  if (a.stat_acc >= 1) {
+    const int rep = a.stat_acc > 1 ? mt % a.stat_acc : 0;
+    double* d = (double*)a.partials + ((size_t)rep * a.Nout + col) * 2;
+    unsafeAtomicAdd(d, (double)v.x);
+    unsafeAtomicAdd(d + 1, (double)v.y);
+  } else if (a.stat_acc == -1) {
+    unsafeAtomicAdd(a.partials + (size_t)col * 2, v.x);
+    unsafeAtomicAdd(a.partials + (size_t)col * 2 + 1, v.y);
+  } else {
+    *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
+  }
+}
+
+constexpr int QBM = 256, QBN = 256, QSTAGE = (QBM + QBN) * 128;
+constexpr int QWM = 2, QWN = 4, QTHREADS = 64 * QWM * QWN;
+constexpr int QLDS_MAIN = 2 * QSTAGE > QBM * (QBN + 8) * 2 ? 2 * QSTAGE : QBM * (QBN + 8) * 2;
+constexpr int QLDS = QLDS_MAIN + 64 + QTHREADS * 2 * 8;  // + epilogue flag and reducer doubles
+
+constexpr int PS_LDS = 2 * QSTAGE + 2 * 256 * 2 * 4;  // ring + [2 halves][256 cols][2] stats (+ bias: Nout floats)
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+
+// local W-tile row -> channel offset within the 256-column tile: inside each
+// 64-row wave slab, row 16j + 4g + r (bits j1 j0 g1 g0 r1 r0) holds channel
+// 32*j1 + 8g + 4*j0 + r (bits j1 g1 g0 j0 r1 r0): a lane's accumulators of
+// fragments j = 0,1 are channels 8g..8g+7, of j = 2,3 channels 32+8g..+7
+__device__ __forceinline__ int ps_perm(int row) {
+  const int slab = row & ~63, x = row & 63;
+  return slab | (x & 0x23) | (((x >> 2) & 3) << 3) | (((x >> 4) & 1) << 2);
+}
+// channel offset (within the 256-column tile) of accumulator value e = 4j + r of lane group g in wave column wn
+__device__ __forceinline__ int ps_chan(int wn, int g, int e) { return wn * 64 + g * 8 + (e & 7) + ((e >> 3) << 5); }
+
+// Register epilogue of one 256x256 tile of the persistent forms (see
+// k_conv_fwd_ps): bias (+ activation) or BN partial statistics, two 16-B
+// buffer stores per pixel row straight from the accumulators. Every global
+// access is issued unconditionally (out-of-range rows get BUF_OOB offsets) so
+// a wave's vmem count is static: 16 stores (+2 float64 atomics in stat_acc
+// mode, pixel-half wm == 0 only), all YOUNGER than the in-flight DMA, which
+// the caller retires with a counted vmcnt.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+// reduce-scatter over the 16 lanes of a DPP row: returns the row's sum of
+// v[lane & 15]. Four halving rounds (partners lane ^ 15 by row_mirror,
+// (lane & 8) | (7 - lane & 7) by row_half_mirror, then quad xor 2 and xor 1):
+// 15 exchanged values per lane instead of 64 shuffles of a full butterfly.
+__device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int fr) {
+  const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float keep = b3 ? v[k + 8] : v[k], send = b3 ? v[k] : v[k + 8];
+    v[k] = keep + dpp_f<0x140>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float keep = b2 ? v[k + 4] : v[k], send = b2 ? v[k] : v[k + 4];
+    v[k] = keep + dpp_f<0x141>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float keep = b1 ? v[k + 2] : v[k], send = b1 ? v[k] : v[k + 2];
+    v[k] = keep + dpp_f<0x4E>(send);
+  }
+  const float keep = b0 ? v[1] : v[0], send = b0 ? v[0] : v[1];
+  return keep + dpp_f<0xB1>(send);
+}
+
+template <int EPI, int TBN = QBN>
+__device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[8][4], int lin,
+                                            __amdgpu_buffer_rsrc_t ry, float* sred, const float* sbias, int tid,
+                                            int wm, int wn, int fr, int fg) {
+  constexpr int FM = 8, FN = 4;
+  const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+  const int m0 = mt * QBM, n0 = nt * TBN;
+  const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
+  constexpr bool stats = EPI == 0;
+  float bsv[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
+  float s[16], q[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * (QBM / QWM) + i * 16 + fr;
+    const bool ok = m < a.M;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bsv[j * 4 + r];
+    if (stats) {
+      const float w = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
+    } else if constexpr (EPI > 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = apply_act<EPI - 1>(v[e]);
+    }
+    uint32_t w8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+    const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
+    if (a.dbg & 32) {
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 2);
+    } else if (!(a.dbg & 8)) {
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, ok ? off + 64 : BUF_OOB, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  if (stats && !(a.dbg & 16)) {
+    // lane fr of lane group fg ends with the 16 pixel lanes' totals of value fr's channel
+    const float S = row_reduce_scatter16(s, fr), Q = row_reduce_scatter16(q, fr);
+    const int ch = ps_chan(wn, fg, fr);
+    if (a.stat_acc) {
+      // the two pixel-half waves of each channel slab meet in LDS: half the atomics
+      // (the K-step barriers order this slot's reuse by the next tile's epilogue)
+      if (wm == 1) {
+        sred[ch * 2] = S;
+        sred[ch * 2 + 1] = Q;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (wm == 0) acc_stats(a, mt, n0 + ch, make_float2(S + sred[ch * 2], Q + sred[ch * 2 + 1]));
+    } else {
+      // combine the two pixel-half waves through LDS, then one slab row per M tile
+      sred[(wm * TBN + ch) * 2] = S;
+      sred[(wm * TBN + ch) * 2 + 1] = Q;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid < TBN) {
+        const float2 v = make_float2(sred[tid * 2] + sred[(TBN + tid) * 2],
+                                     sred[tid * 2 + 1] + sred[(TBN + tid) * 2 + 1]);
+        *(float2*)(a.partials + ((size_t)mt * a.Nout + n0 + tid) * 2) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+}
+
+// persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 BN statistics, 1 + act: bias + act)
+int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st);
+constexpr int PP_THREADS = 512;
+constexpr int PP_HALF = 128 * 128;  // one half-tile: 128 rows x 128 B
+constexpr int PP_SLOT = 4 * PP_HALF;  // a K-tile: pixel halves P0 P1, channel halves C0 C1
+constexpr int PP_LDS = 2 * PP_SLOT + 2 * 256 * 2 * 4;  // two K-tile slots + epilogue statistics scratch (+ bias)
+
+}  // namespace dmf

@@ -134,6 +134,16 @@ __device__ __forceinline__ void lin_r(int o, int in, int out, int& i0, int& i1, 
   l1 = src - (float)i0;
 }
 
+// lin_r with the scale (float)in / (float)out precomputed (same float, same result)
+__device__ __forceinline__ void lin_rs(int o, int in, float scale, int& i0, int& i1, float& l1) {
+  float src = (o + 0.5f) * scale - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
 struct ReconArgs {
   const void* r[5];      // recon maps [B][h][w] (single channel, channel stride ldr)
   int ldr[5];
@@ -143,6 +153,7 @@ struct ReconArgs {
   const float* tB;
   float ca, cb;          // combination for target 2
   int B, h, w, S;
+  float sc_h, sc_w;      // (float)h / S, (float)w / S
   float* sums;           // [5] loss sums (atomic)
   float* grads[5];       // [B][h][w] fp32 (atomic accumulation, unit-upstream, scaled by 1/(B*S*S))
 };
@@ -288,36 +299,50 @@ __global__ void __launch_bounds__(256) k_recon_band(ReconArgs a) {
   }
 }
 
-// Streaming form (the recon launch of a fusion step at HBM rate): block =
-// (b, band of RECON_RB output rows), thread = output column(s). The band's
-// <= 3 source rows of every map are staged in LDS once; each thread
-// x-interpolates them for its column, then per output row needs one FMA for
-// the bilinear value, the loss term and dL/dv (targets streamed once,
-// coalesced, straight from HBM). The gradient is contracted separably in
-// registers: over the band's rows first (A[k][r][x] = sum_y wy(y, r) g(y,
-// x)), then over x through LDS (each (k, r, j) sums its <= S/w + 2
-// contributing columns), so a band adds <= 3 rows x w values per map with
-// one atomic each and the loss sums with one atomic per map per block.
+// Streaming form (the recon launch of a fusion step at HBM rate), two
+// passes, no atomics (deterministic):
+//  1. k_recon_stream, block = (b, band of RECON_RB output rows), thread =
+//     output column(s). The band's <= 3 source rows of every map are staged
+//     in LDS once; each thread x-interpolates them for its column, then per
+//     output row needs one FMA for the bilinear value, the loss term and
+//     dL/dv (the targets streamed once, coalesced). The gradient contracts
+//     separably: over the band's rows in registers (A[k][r][x] = sum_y
+//     wy(y, r) g(y, x)), then over x through LDS; the band's <= 3 x w
+//     source-row contributions per map and its loss partial sums go to a
+//     workspace slab with plain stores.
+//  2. k_recon_finish: per (map, b) block, every source element sums the
+//     (<= 3) bands covering its row in band order; one more block sums the
+//     loss partials in block order. Same-address atomics (the loss sums of
+//     1024 blocks onto 5 addresses) serialised the one-pass form.
 constexpr int RECON_NR = 3;   // source rows a band may touch
 constexpr int RECON_XPT = 2;  // output columns per thread (S <= 512)
 template <typename T>
-__global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a) {
+__global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __restrict__ ws) {
   __shared__ float Rs[5][RECON_NR][64];
   __shared__ float Acc[5][RECON_NR][RECON_MAXS];
+  __shared__ float Lx[RECON_MAXS];   // column x: bilinear weight of j1
+  __shared__ short J0[RECON_MAXS];   // column x: source columns j0 (j1 = j0 + (j0 < w-1))
   __shared__ float red[16];
-  const int b = blockIdx.x;
-  const int y0 = blockIdx.y * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
+  const int b = blockIdx.x, q = blockIdx.y, nb = gridDim.y;
+  const int y0 = q * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
   const int tid = threadIdx.x;
   const float inv_n = 1.f / ((float)a.B * a.S * a.S);
   int ib0, ie, tmp;
   float ftmp;
-  lin_r(y0, a.h, a.S, ib0, tmp, ftmp);
-  lin_r(y1 - 1, a.h, a.S, tmp, ie, ftmp);
+  lin_rs(y0, a.h, a.sc_h, ib0, tmp, ftmp);
+  lin_rs(y1 - 1, a.h, a.sc_h, tmp, ie, ftmp);
+  for (int x = tid; x < a.S; x += blockDim.x) {
+    int j0, j1;
+    float lx;
+    lin_rs(x, a.w, a.sc_w, j0, j1, lx);
+    J0[x] = (short)j0;
+    Lx[x] = lx;
+  }
   const int nrows = ie - ib0 + 1;  // <= RECON_NR (checked by the launcher)
-  for (int t = tid; t < a.nterms * RECON_NR * 64; t += blockDim.x) {
+  for (int t = tid; t < 5 * RECON_NR * 64; t += blockDim.x) {
     const int k = t / (RECON_NR * 64), rem = t - k * (RECON_NR * 64), r = rem / 64, j = rem - r * 64;
     float v = 0.f;
-    if (r < nrows && j < a.w) {
+    if (k < a.nterms && r < nrows && j < a.w) {
       const T* R = (const T*)a.r[k] + ((size_t)b * a.h * a.w + (size_t)(ib0 + r) * a.w + j) * a.ldr[k];
       v = ld(R);
     }
@@ -331,7 +356,7 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a) {
     if (x >= a.S) break;
     int j0, j1;
     float lx;
-    lin_r(x, a.w, a.S, j0, j1, lx);
+    lin_rs(x, a.w, a.sc_w, j0, j1, lx);
     float rx[5][RECON_NR], A[5][RECON_NR];
 #pragma unroll
     for (int k = 0; k < 5; ++k)
@@ -340,28 +365,41 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a) {
         rx[k][r] = (1.f - lx) * Rs[k][r][j0] + lx * Rs[k][r][j1];
         A[k][r] = 0.f;
       }
-    for (int y = y0; y < y1; ++y) {
+    const float* pA = a.tA ? a.tA + ((size_t)b * a.S + y0) * a.S + x : nullptr;
+    const float* pB = a.tB ? a.tB + ((size_t)b * a.S + y0) * a.S + x : nullptr;
+    // the band's target values of this column: all loads issued up front (one HBM latency, not RB)
+    float tAr[RECON_RB], tBr[RECON_RB];
+#pragma unroll
+    for (int yy = 0; yy < RECON_RB; ++yy) {
+      const bool in = y0 + yy < y1;
+      tAr[yy] = (pA && in) ? pA[(size_t)yy * a.S] : 0.f;
+      tBr[yy] = (pB && in) ? pB[(size_t)yy * a.S] : 0.f;
+    }
+#pragma unroll
+    for (int yy = 0; yy < RECON_RB; ++yy) {
+      const int y = y0 + yy;
+      if (y >= y1) break;
       int i0, i1;
       float ly;
-      lin_r(y, a.h, a.S, i0, i1, ly);
+      lin_rs(y, a.h, a.sc_h, i0, i1, ly);
       const int q0 = i0 - ib0, q1 = i1 - ib0;
-      const size_t tp = ((size_t)b * a.S + y) * a.S + x;
-      const float tAv = a.tA ? a.tA[tp] : 0.f, tBv = a.tB ? a.tB[tp] : 0.f;
+      const float tAv = tAr[yy], tBv = tBr[yy];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         if (k >= a.nterms) break;
-        // the x-interpolated source rows q0 / q1 (<= 3 rows: select without dynamic register indexing)
+        // the x-interpolated source rows q0 / q1 (<= 3 rows: selects, no dynamic register indexing)
         const float r0 = q0 == 0 ? rx[k][0] : (q0 == 1 ? rx[k][1] : rx[k][2]);
         const float r1 = q1 == 0 ? rx[k][0] : (q1 == 1 ? rx[k][1] : rx[k][2]);
         const float v = (1.f - ly) * r0 + ly * r1;
         float tv = a.target[k] == 0 ? tAv : (a.target[k] == 1 ? tBv : a.ca * tAv + a.cb * tBv);
         tv = fminf(fmaxf(tv, 0.f), 1.f);
-        const float sg = sigmoid_f(v);
+        const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-v));
         const float pp = fminf(fmaxf(sg, 0.f), 1.f);
         const float d = pp - tv;
-        const float q = sqrtf(d * d + 1e-6f);
-        part[k] += q;
-        const float g = d / q * sg * (1.f - sg) * inv_n;  // dL/dv (the clamp is the identity on (0,1))
+        const float e2 = d * d + 1e-6f;
+        const float rq = __builtin_amdgcn_rsqf(e2);  // 1 / sqrt(d^2 + eps): the term is e2 * rq, d/term = d * rq
+        part[k] += e2 * rq;
+        const float g = d * rq * sg * (1.f - sg) * inv_n;  // dL/dv (the clamp is the identity on (0,1))
         const float g0 = (1.f - ly) * g, g1 = ly * g;
 #pragma unroll
         for (int r = 0; r < RECON_NR; ++r) A[k][r] += (q0 == r ? g0 : 0.f) + (q1 == r ? g1 : 0.f);
@@ -373,28 +411,70 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a) {
       for (int r = 0; r < RECON_NR; ++r) Acc[k][r][x] = A[k][r];
   }
   __syncthreads();
-  // x-contraction: (k, r, j) sums the columns x whose source column j0 or j1 is j
-  for (int t = tid; t < a.nterms * nrows * a.w; t += blockDim.x) {
-    const int k = t / (nrows * a.w), rem = t - k * (nrows * a.w), r = rem / a.w, j = rem - r * a.w;
-    if (!a.grads[k]) continue;
-    int xl = (int)floorf(((float)j - 1.f + 0.5f) * a.S / a.w - 0.5f) - 1;
-    int xh = (int)ceilf(((float)j + 1.f + 0.5f) * a.S / a.w - 0.5f) + 2;
-    xl = max(xl, 0);
-    xh = min(xh, a.S);
+  // x-contraction: (k, r, j) sums the columns x whose source column j0 or j1 is j -> slab row r of band q
+  float* G = ws + (size_t)a.B * nb * 5;
+  for (int t = tid; t < a.nterms * RECON_NR * a.w; t += blockDim.x) {
+    const int k = t / (RECON_NR * a.w), rem = t - k * (RECON_NR * a.w), r = rem / a.w, j = rem - r * a.w;
     float h = 0.f;
-    for (int x = xl; x < xh; ++x) {
-      int j0, j1;
-      float lx;
-      lin_r(x, a.w, a.S, j0, j1, lx);
-      const float av = Acc[k][r][x];
-      if (j0 == j) h += (1.f - lx) * av;
-      if (j1 == j) h += lx * av;
+    if (r < nrows && a.grads[k]) {
+      int xl = (int)floorf(((float)j - 1.f + 0.5f) * a.S / a.w - 0.5f) - 1;
+      int xh = (int)ceilf(((float)j + 1.f + 0.5f) * a.S / a.w - 0.5f) + 2;
+      xl = max(xl, 0);
+      xh = min(xh, a.S);
+      for (int x = xl; x < xh; ++x) {
+        const int j0 = J0[x], j1 = j0 + (j0 < a.w - 1 ? 1 : 0);
+        const float lx = Lx[x], av = Acc[k][r][x];
+        if (j0 == j) h += (1.f - lx) * av;
+        if (j1 == j) h += lx * av;
+      }
     }
-    if (h != 0.f) atomicAdd(a.grads[k] + ((size_t)b * a.h + ib0 + r) * a.w + j, h);
+    G[(((size_t)k * a.B + b) * nb + q) * RECON_NR * a.w + r * a.w + j] = h;
   }
   for (int k = 0; k < a.nterms; ++k) {
     const float sm = block_sum(part[k], red);
-    if (tid == 0) atomicAdd(a.sums + k, sm);
+    if (tid == 0) ws[((size_t)b * nb + q) * 5 + k] = sm;
+  }
+}
+
+// pass 2: blocks [0, nterms*B) reduce the band slabs of map k = blk / B,
+// item b = blk % B into its gradient [h][w]; block nterms*B sums the loss
+// partials (fixed order: deterministic)
+__global__ void __launch_bounds__(256) k_recon_finish(ReconArgs a, const float* __restrict__ ws, int nb) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x == a.nterms * a.B) {
+    const int nblk = a.B * nb;
+    for (int k = 0; k < a.nterms; ++k) {
+      float s = 0.f;
+      for (int i = tid; i < nblk; i += blockDim.x) s += ws[(size_t)i * 5 + k];
+      s = block_sum(s, red);
+      if (tid == 0) a.sums[k] = s;
+    }
+    return;
+  }
+  const int k = blockIdx.x / a.B, b = blockIdx.x - (blockIdx.x / a.B) * a.B;
+  if (!a.grads[k]) return;
+  __shared__ int band0[RECON_MAXS / RECON_RB + 1], band1[RECON_MAXS / RECON_RB + 1];  // first / last source row
+  for (int q = tid; q < nb; q += blockDim.x) {
+    int ib0, ie, tmp;
+    float ftmp;
+    lin_rs(q * RECON_RB, a.h, a.sc_h, ib0, tmp, ftmp);
+    lin_rs(min(a.S, q * RECON_RB + RECON_RB) - 1, a.h, a.sc_h, tmp, ie, ftmp);
+    band0[q] = ib0;
+    band1[q] = ie;
+  }
+  __syncthreads();
+  const float* G = ws + (size_t)a.B * nb * 5 + ((size_t)k * a.B + b) * nb * RECON_NR * a.w;
+  for (int e = tid; e < a.h * a.w; e += blockDim.x) {
+    const int i = e / a.w, j = e - (e / a.w) * a.w;
+    // bands whose source rows [ib0, ie] contain i: around the band of output row (i + 0.5) * S / h
+    const int qc = (int)(((float)i + 0.5f) * a.S / a.h) / RECON_RB;
+    float s = 0.f;
+    for (int q = max(0, qc - 2); q <= min(nb - 1, qc + 2); ++q) {
+      const int ib0 = band0[q];
+      if (i >= ib0 && i <= band1[q]) s += G[(size_t)q * RECON_NR * a.w + (i - ib0) * a.w + j];
+    }
+    a.grads[k][(size_t)b * a.h * a.w + e] = s;
   }
 }
 
@@ -509,11 +589,23 @@ extern "C" int dmf_soft_dice(int dtype, const void* logits, const float* target,
 
 // recon terms: up to 5 maps r_k ([B][h][w], channel stride ldr_k) against target sel_k in {0:A,1:B,2:ca*A+cb*B}.
 // sums[k] += sum of charbonnier terms (caller divides by B*S*S); grads[k] += unit-upstream grads (scaled 1/(B*S*S)).
+// floats of the two-pass streaming form's workspace, 0 where it does not apply (the caller then passes
+// ws = nullptr and zeroed sums / gradients for the atomic one-pass forms)
+extern "C" int dmf_recon_ws_floats(int nterms, int B, int h, int w, int S) {
+  // source rows a band of RECON_RB output rows touches: ceil(RB*h/S) + 1 (+1 clamp slack) <= RECON_NR
+  const bool ok = nterms >= 1 && nterms <= 5 && B > 0 && S <= RECON_MAXS && S <= 256 * RECON_XPT && h <= S &&
+                  w <= 64 && (RECON_RB * h + S - 1) / S + 2 <= RECON_NR;
+  if (!ok) return 0;
+  const long long nb = cdiv(S, RECON_RB);
+  const long long n = (long long)B * nb * 5 + (long long)nterms * B * nb * RECON_NR * w;
+  return n < (1LL << 30) ? (int)n : 0;
+}
+
 extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const void* r2, const void* r3,
                               const void* r4, int ldr0, int ldr1, int ldr2, int ldr3, int ldr4, int sel0, int sel1,
                               int sel2, int sel3, int sel4, const float* tA, const float* tB, float ca, float cb,
                               int B, int h, int w, int S, float* sums, float* g0, float* g1, float* g2, float* g3,
-                              float* g4, void* stream) {
+                              float* g4, float* ws, void* stream) {
   DMF_CHECK_ARG(nterms >= 1 && nterms <= 5 && sums && w <= 64 && B > 0 && S > 0, "dmf_recon_loss: bad args");
   ReconArgs a{};
   const void* rs[5] = {r0, r1, r2, r3, r4};
@@ -530,16 +622,20 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
   a.nterms = nterms;
   a.tA = tA; a.tB = tB; a.ca = ca; a.cb = cb;
   a.B = B; a.h = h; a.w = w; a.S = S;
+  a.sc_h = (float)h / (float)S;
+  a.sc_w = (float)w / (float)S;
   a.sums = sums;
-  // source rows a band of RECON_RB output rows touches: at most ceil(RB*h/S) + 1 (+1 clamp slack)
-  const bool stream_ok = S <= RECON_MAXS && S <= 256 * RECON_XPT && h <= S && w <= 64 &&
-                         (RECON_RB * h + S - 1) / S + 2 <= RECON_NR;
-  if (stream_ok) {
-    const dim3 g(B, cdiv(S, RECON_RB));
+  if (ws != nullptr) {
+    // two-pass streaming form: sums and gradients are WRITTEN (no zeroing needed)
+    DMF_CHECK_ARG(dmf_recon_ws_floats(nterms, B, h, w, S) > 0, "dmf_recon_loss: workspace given for a shape "
+                  "outside the streaming form (B=%d h=%d w=%d S=%d)", B, h, w, S);
+    const int nb = cdiv(S, RECON_RB);
+    const dim3 g(B, nb);
     if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
     else
-      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
+    hipLaunchKernelGGL(k_recon_finish, dim3(nterms * B + 1), dim3(256), 0, (hipStream_t)stream, a, ws, nb);
   } else if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
     const dim3 g(B, cdiv(S, RECON_RB));
     if (dtype == DMF_BF16)

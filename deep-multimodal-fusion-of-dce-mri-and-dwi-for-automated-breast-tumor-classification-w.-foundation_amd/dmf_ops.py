@@ -1828,16 +1828,20 @@ class _ReconFn(torch.autograd.Function):
         for m in prepared:
             if dt(m) != dtc:
                 raise RuntimeError("recon maps must share a dtype")
-        sums = torch.zeros(5, dtype=torch.float32, device=dev)
+        nws = N.load().dmf_recon_ws_floats(k, b, h, w, s)
+        # two-pass streaming form: sums / gradients are written whole (no zero fills); else atomics
+        alloc = torch.empty if nws > 0 else torch.zeros
+        ws = torch.empty(nws, dtype=torch.float32, device=dev) if nws > 0 else None
+        sums = alloc(5, dtype=torch.float32, device=dev)
         need = any(m.requires_grad for m in maps)
-        grads = [torch.zeros((b, h, w), dtype=torch.float32, device=dev) if (need and maps[i].requires_grad) else None
+        grads = [alloc((b, h, w), dtype=torch.float32, device=dev) if (need and maps[i].requires_grad) else None
                  for i in range(k)]
         ptrs = [m.data_ptr() for m in prepared] + [None] * (5 - k)
         ldl = lds + [0] * (5 - k)
         sel = list(sels) + [0] * (5 - k)
         gp = [_p(g) for g in grads] + [None] * (5 - k)
         N.call("dmf_recon_loss", dtc, k, *ptrs, *ldl, *sel, _p(tA), _p(tB), float(ca), float(cb), b, h, w, s,
-               sums.data_ptr(), *gp, _stream())
+               sums.data_ptr(), *gp, _p(ws), _stream())
         out = sums[:k] / float(b * s * s)
         ctx.save_for_backward(*[g if g is not None else torch.empty(0, device=dev) for g in grads])
         ctx.meta = [(m.shape, m.dtype, g is not None) for m, g in zip(maps, grads)]

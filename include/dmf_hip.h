@@ -361,7 +361,12 @@ int dmf_soft_dice(int dtype, const void* logits, const float* target, int B, int
 int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const void* r2, const void* r3,
                    const void* r4, int ldr0, int ldr1, int ldr2, int ldr3, int ldr4, int sel0, int sel1, int sel2,
                    int sel3, int sel4, const float* tA, const float* tB, float ca, float cb, int B, int h, int w,
-                   int S, float* sums, float* g0, float* g1, float* g2, float* g3, float* g4, void* stream);
+                   int S, float* sums, float* g0, float* g1, float* g2, float* g3, float* g4, float* ws,
+                   void* stream);
+/* recon workspace (floats) of the two-pass streaming form (deterministic; sums and
+ * gradients written, not accumulated); 0 = not applicable: pass ws = NULL with zeroed
+ * sums / gradients (atomic one-pass forms) */
+int dmf_recon_ws_floats(int nterms, int B, int h, int w, int S);
 /* loss must be zeroed by the caller (pairs/channels accumulate) */
 int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long long sstride, long long tstride, int ld,
                    int HW, int C, int npairs, float* loss, void* dstudent, long long dstride, void* stream);
