@@ -1297,8 +1297,9 @@ struct ConvPlan {
   bool ps;    // k_conv_fwd_ps (persistent LDS-DMA 256x256, register epilogue)
   bool pp;    // k_conv_fwd_pp (conv_pp.hip: ping-pong 8-phase 256x256, register epilogue)
 };
-// 7 = ping-pong 256x256 form (conv_pp.hip): 0 off, 1 in place of k_conv_fwd_sq, 2 also in place of k_conv_fwd_ps
-static int g_pp_mode = 0;
+// 7 = ping-pong 256x256 form (conv_pp.hip): 0 off, 1 (default) for 3x3 and K >= 1024 (where it beats the
+// persistent form: tools/conv_bench.py --tunes, profiles/r03h_conv_ab.txt), 2 for every legal shape
+static int g_pp_mode = 1;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
@@ -1379,7 +1380,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const bool sq_ps_ok = dtype == DMF_BF16 && !wide_disabled() && a.tickets == nullptr && a.Nout % QBN == 0 &&
                         a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
                         (long long)a.M * a.ldy * 2 < (1LL << 31);
-  if (sq_ps_ok && (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 2048 && a.KH * a.KW == 1)))) {
+  if (sq_ps_ok && (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 1024 && a.KH * a.KW == 1)))) {
     p.wide = p.sq = p.pp = true;
     p.bm = QBM;
     p.bn = QBN;
@@ -1696,6 +1697,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 4: g_ps_enable = value != 0; return 0;
     case 6: g_ps_dbg = value; return 0;
     case 7: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ping-pong mode %d", value); g_pp_mode = value; return 0;
+    case 8: return conv_pp_tune(value != 0);
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

@@ -269,6 +269,7 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[8]
 
 // persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 BN statistics, 1 + act: bias + act)
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st);
+int conv_pp_tune(int value);  // dmf_conv_tune key 8
 constexpr int PP_THREADS = 512;
 constexpr int PP_HALF = 128 * 128;  // one half-tile: 128 rows x 128 B
 constexpr int PP_SLOT = 4 * PP_HALF;  // a K-tile: pixel halves P0 P1, channel halves C0 C1

@@ -25,6 +25,9 @@
 // slots of LDS (128 KiB), four half-tiles in flight: each phase's wait
 // retires the half its NEXT phase reads (read one phase after the wait),
 // and a half is restaged >= 2 phases after its last read.
+#include <algorithm>
+#include <type_traits>
+
 #include "conv_core.h"
 
 namespace dmf {
@@ -51,25 +54,15 @@ __device__ __forceinline__ void pp_barrier() { asm volatile("s_barrier" ::: "mem
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-}
-// wait until at most 2*younger LDS-DMA pieces of this wave are in flight (uniform)
-__device__ __forceinline__ void vm_wait_halves(int younger) {
-  switch (younger) {
-    case 0: vm_wait<0>(); break;
-    case 1: vm_wait<2>(); break;
-    case 2: vm_wait<4>(); break;
-    case 3: vm_wait<6>(); break;
-    case 4: vm_wait<8>(); break;
-    default: vm_wait<10>(); break;
-  }
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// PERSISTENT grid: gridDim <= tiles, each block walks tiles blockIdx, +gridDim, ... (XCD remap) as ONE
+// flat stream of K-tiles: the staging runs two K-tiles ahead across tile boundaries, so the next
+// tile's first half-tiles are in flight under the finished tile's epilogue (its 16 stores, +2 float64
+// atomics in statistics mode, are then younger than those DMA pieces: the first K-tile after an
+// epilogue waits with 16 more).
 template <bool PADCHK, bool DUAL, int EPI>
 __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   constexpr int ES = 2;
@@ -83,6 +76,8 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   float* sred = (float*)(smem + 2 * PP_SLOT);
   float* sbias = sred + 2 * 256 * 2;
+  const int ntile = a.mtiles * a.ntiles;
+  if ((int)blockIdx.x >= ntile) return;
   if (a.bias) {
     for (int i = tid; i < a.Nout; i += PP_THREADS) sbias[i] = a.bias[i];
     __syncthreads();
@@ -93,58 +88,81 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   const v4i_t rw = buf_rsrc(a.w, (long long)a.Nout * a.Ktot * ES);
   const __amdgpu_buffer_rsrc_t ry =
       __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)((long long)a.M * a.ldy * ES), BUF_FLAGS);
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-  const int m0 = mt * 256, n0 = nt * 256;
   const int nk = a.Ktot / 64;
-  const int taps = a.KH * a.KW;
   const int hw = a.Ho * a.Wo;
+  const int G = ((ntile - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x) * nk;  // this block's K-tiles
+  auto tile_lin = [&](int j) { return xcd_remap((int)blockIdx.x + j * (int)gridDim.x, ntile); };
 
-  // staging rows of this lane: piece q (0, 1) of a half covers half rows 16*wid + 8*q + (0..7)
+  // staging rows of the tile being STAGED: piece q (0, 1) of a half covers half rows 16*wid + 8*q + (0..7)
   int h0[2][2], w0[2][2], b1[2][2], b2[2][2];
   bool mok[2][2];
   unsigned vb[2][2];
+  int meta_tile = -1;
+  auto rows_for = [&](int j) {
+    const int lin = tile_lin(j);
+    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+    const int m0 = mt * 256, n0 = nt * 256;
 #pragma unroll
-  for (int ph = 0; ph < 2; ++ph)
+    for (int ph = 0; ph < 2; ++ph)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rho = 16 * wid + 8 * q + lr;
-      const int m = m0 + pp_pix_row(ph, rho);
-      mok[ph][q] = m < a.M;
-      const int mm = mok[ph][q] ? m : 0;
-      const int n = mm / hw, rem = mm - (mm / hw) * hw;
-      const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
-      h0[ph][q] = ho * a.stride - a.pad;
-      w0[ph][q] = wo * a.stride - a.pad;
-      const int pix = (n * a.H + h0[ph][q]) * a.W + w0[ph][q];
-      b1[ph][q] = pix * a.ldx + lc * 8;
-      b2[ph][q] = DUAL ? pix * a.ldx2 + lc * 8 : 0;
-      const int co = n0 + pp_chan_row(ph, rho);  // (ph doubles as the channel half index here)
-      vb[ph][q] = (unsigned)((co * a.Ktot + lc * 8) * ES);
-    }
+      for (int q = 0; q < 2; ++q) {
+        const int rho = 16 * wid + 8 * q + lr;
+        const int m = m0 + pp_pix_row(ph, rho);
+        mok[ph][q] = m < a.M;
+        const int mm = mok[ph][q] ? m : 0;
+        const int n = mm / hw, rem = mm - (mm / hw) * hw;
+        const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+        h0[ph][q] = ho * a.stride - a.pad;
+        w0[ph][q] = wo * a.stride - a.pad;
+        const int pix = (n * a.H + h0[ph][q]) * a.W + w0[ph][q];
+        b1[ph][q] = pix * a.ldx + lc * 8;
+        b2[ph][q] = DUAL ? pix * a.ldx2 + lc * 8 : 0;
+        const int co = n0 + pp_chan_row(ph, rho);  // (ph doubles as the channel half index here)
+        vb[ph][q] = (unsigned)((co * a.Ktot + lc * 8) * ES);
+      }
+    meta_tile = j;
+  };
 
-  // K-tile kt: channel chunk outer, filter tap inner (the taps of one chunk re-read L2-resident rows)
-  auto stage_p = [&](int kt, int ph) {
-    const int cc = kt / taps, tap = kt - cc * taps;
-    const int r = tap / a.KW, s = tap - r * a.KW;
-    const int c0 = cc * 64, rd = r * a.dil, sd = s * a.dil;
-    const bool hi = DUAL && c0 >= a.C1;
-    const int toff = hi ? (rd * a.W + sd) * a.ldx2 + (c0 - a.C1) : (rd * a.W + sd) * a.ldx + c0;
-    const unsigned dst = lds0 + (kt & 1) * PP_SLOT + ph * PP_HALF + (16 * wid) * 128;
+  // K-tile parameters (wave-uniform) from a division-free cursor over the flat stream: channel chunk
+  // outer, filter tap inner (the taps of one chunk re-read L2-resident rows)
+  struct KP { int toff, rd, sd, tile; unsigned koff; bool hi; };
+  int cur_r = 0, cur_s = 0, cur_cc = 0, cur_tile = 0;
+  auto next_kp = [&]() {
+    KP k;
+    const int c0 = cur_cc * 64;
+    k.rd = cur_r * a.dil;
+    k.sd = cur_s * a.dil;
+    k.koff = (unsigned)(((cur_r * a.KW + cur_s) * a.C + c0) * ES);
+    k.hi = DUAL && c0 >= a.C1;
+    k.toff = k.hi ? (k.rd * a.W + k.sd) * a.ldx2 + (c0 - a.C1) : (k.rd * a.W + k.sd) * a.ldx + c0;
+    k.tile = cur_tile;
+    if (++cur_s == a.KW) {
+      cur_s = 0;
+      if (++cur_r == a.KH) {
+        cur_r = 0;
+        if (++cur_cc * 64 >= a.C) { cur_cc = 0; ++cur_tile; }
+      }
+    }
+    return k;
+  };
+  auto stage_p = [&](const KP& k, int slot, int ph) {
+    if (k.tile != meta_tile) rows_for(k.tile);  // halves are staged in stream order: switch once per tile
+    const unsigned dst = lds0 + slot * PP_SLOT + ph * PP_HALF + (16 * wid) * 128;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       bool ok = mok[ph][q];
-      if (PADCHK) ok = ok && (unsigned)(h0[ph][q] + rd) < (unsigned)a.H && (unsigned)(w0[ph][q] + sd) < (unsigned)a.W;
-      const unsigned vo = ok ? (unsigned)(((hi ? b2[ph][q] : b1[ph][q]) + toff) * ES) : BUF_OOB;
-      dma16u(hi ? rx2 : rx, vo, 0, dst + q * 8 * 128);
+      if (PADCHK)
+        ok = ok && (unsigned)(h0[ph][q] + k.rd) < (unsigned)a.H && (unsigned)(w0[ph][q] + k.sd) < (unsigned)a.W;
+      const unsigned vo = ok ? (unsigned)(((k.hi ? b2[ph][q] : b1[ph][q]) + k.toff) * ES) : BUF_OOB;
+      if (DUAL) dma16u(k.hi ? rx2 : rx, vo, 0, dst + q * 8 * 128);
+      else dma16(rx, vo, 0, dst + q * 8 * 128);
     }
   };
-  auto stage_c = [&](int kt, int ch) {
-    const int cc = kt / taps, tap = kt - cc * taps;
-    const unsigned koff = (unsigned)((tap * a.C + cc * 64) * ES);
-    const unsigned dst = lds0 + (kt & 1) * PP_SLOT + (2 + ch) * PP_HALF + (16 * wid) * 128;
+  auto stage_c = [&](const KP& k, int slot, int ch) {
+    if (k.tile != meta_tile) rows_for(k.tile);
+    const unsigned dst = lds0 + slot * PP_SLOT + (2 + ch) * PP_HALF + (16 * wid) * 128;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) dma16u(rw, vb[ch][q], koff, dst + q * 8 * 128);
+    for (int q = 0; q < 2; ++q) dma16(rw, vb[ch][q], k.koff, dst + q * 8 * 128);
   };
 
   f32x4_t acc[8][4];
@@ -184,53 +202,120 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
           acc[4 * ph + ii][2 * chh + j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               *(const bf16x8_t*)&cv[kk][j0], *(const bf16x8_t*)&pv[kk][ii], acc[4 * ph + ii][2 * chh + j0], 0, 0, 0);
   };
+  // the MFMA segment of phase p: barrier, this wave's fragment reads retired, 16 MFMAs at priority 1, barrier
+  auto mfma_segment = [&](int p) {
+    __builtin_amdgcn_sched_barrier(0);
+    pp_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if (p == 0) mma_q(0, cv0, 0);
+    else if (p == 1) mma_q(0, cv1, 1);
+    else if (p == 2) mma_q(1, cv1, 1);
+    else mma_q(1, cv0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pp_barrier();
+  };
+  // the finished tile's epilogue: realign the two wave groups (the statistics combine has barriers),
+  // store / reduce from the accumulators (ps_epilogue zeroes them), re-stagger
+  auto epilogue = [&](int j, bool restagger) {
+    if (wm == 0) pp_barrier();
+    ps_epilogue<EPI>(a, acc, tile_lin(j), ry, sred, sbias, tid, wm, wn, fr, fg);
+    __builtin_amdgcn_sched_barrier(0);
+    if (restagger && wm == 1) pp_barrier();
+  };
 
   // prologue: P0 C0 C1 P1 of K-tile 0, P0 C0 of K-tile 1 -- issue order == consumption order
-  int issued = 0;
-  stage_p(0, 0); stage_c(0, 0); stage_c(0, 1); stage_p(0, 1);
-  issued = 4;
-  if (nk > 1) { stage_p(1, 0); stage_c(1, 0); issued = 6; }
-  vm_wait_halves(issued - 1 - 1);  // this wave's pieces of P0(0), C0(0) landed
-  pp_barrier();                    // ... and every wave's, before the leading group's first reads
+  KP k1 = next_kp();  // K-tile 0
+  stage_p(k1, 0, 0); stage_c(k1, 0, 0); stage_c(k1, 0, 1); stage_p(k1, 0, 1);
+  KP k2 = k1;
+  if (G > 1) {
+    k1 = next_kp();  // K-tile 1
+    stage_p(k1, 1, 0); stage_c(k1, 1, 0);
+    vm_wait<8>();  // this wave's pieces of P0(0), C0(0) landed
+  } else {
+    vm_wait<4>();
+  }
+  if (G > 2) k2 = next_kp();  // K-tile 2
+  pp_barrier();  // ... and every wave's, before the leading group's first reads
   __builtin_amdgcn_sched_barrier(0);
   if (wm == 1) pp_barrier();  // the stagger: waves 4-7 run one barrier interval behind
 
-  for (int t = 0; t < nk; ++t) {
-    const char* slot = smem + (t & 1) * PP_SLOT;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      // ---- LOAD segment: this phase's fragments, one half-tile of staging, the counted wait
-      if (p == 0) { read_p(slot, 0); read_c(slot, 0, cv0); }
-      else if (p == 1) read_c(slot, 1, cv1);
-      else if (p == 2) read_p(slot, 1);
-      if (p == 0 && t + 1 < nk) { stage_c(t + 1, 1); ++issued; }
-      if (p == 1 && t + 1 < nk) { stage_p(t + 1, 1); ++issued; }
-      if (p == 2 && t + 2 < nk) { stage_p(t + 2, 0); ++issued; }
-      if (p == 3 && t + 2 < nk) { stage_c(t + 2, 0); ++issued; }
-      // the half the NEXT phase reads: C1(t), P1(t), (nothing new), P0/C0(t+1) -> sequence index
-      const int need = p == 0 ? 4 * t + 2 : (p == 1 || p == 2) ? 4 * t + 3 : 4 * t + 5;
-      vm_wait_halves(max(0, min(issued - 1 - need, 5)));
-      __builtin_amdgcn_sched_barrier(0);
-      pp_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- MFMA segment
-      __builtin_amdgcn_s_setprio(1);
-      if (p == 0) mma_q(0, cv0, 0);
-      else if (p == 1) mma_q(0, cv1, 1);
-      else if (p == 2) mma_q(1, cv1, 1);
-      else mma_q(1, cv0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      pp_barrier();
+  // one K-tile g of the steady state (K-tiles g+1 = k1 and g+2 = k2 exist). After an epilogue its
+  // stores (16 per wave, +2 atomics) are younger than this K-tile's halves: the waits count 16 more.
+  int g = 0, kt = 0, j = 0;
+  bool after_epi = false;
+  for (; g + 2 < G; ++g) {
+    const char* slot = smem + (g & 1) * PP_SLOT;
+    const int s1 = (g + 1) & 1, s2 = g & 1;
+    read_p(slot, 0); read_c(slot, 0, cv0);
+    stage_c(k1, s1, 1);
+    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // C1(g) landed
+    mfma_segment(0);
+    read_c(slot, 1, cv1);
+    stage_p(k1, s1, 1);
+    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // P1(g)
+    mfma_segment(1);
+    read_p(slot, 1);
+    stage_p(k2, s2, 0);
+    if (after_epi) vm_wait<26>(); else vm_wait<10>();
+    mfma_segment(2);
+    stage_c(k2, s2, 0);
+    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // P0(g+1), C0(g+1)
+    mfma_segment(3);
+    after_epi = false;
+    k1 = k2;
+    if (g + 3 < G) k2 = next_kp();
+    if (++kt == nk) {
+      epilogue(j, true);
+      kt = 0;
+      ++j;
+      after_epi = true;
     }
   }
-  if (wm == 0) pp_barrier();  // realign the two wave groups for the epilogue's barriers
-  ps_epilogue<EPI>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
+  // the last two K-tiles of the stream: stage what remains, drain every wait
+  for (; g < G; ++g) {
+    const char* slot = smem + (g & 1) * PP_SLOT;
+    const bool more = g + 1 < G;
+    read_p(slot, 0); read_c(slot, 0, cv0);
+    if (more) stage_c(k1, (g + 1) & 1, 1);
+    vm_wait<0>();
+    mfma_segment(0);
+    read_c(slot, 1, cv1);
+    if (more) stage_p(k1, (g + 1) & 1, 1);
+    vm_wait<0>();
+    mfma_segment(1);
+    read_p(slot, 1);
+    vm_wait<0>();
+    mfma_segment(2);
+    vm_wait<0>();
+    mfma_segment(3);
+    if (++kt == nk) {
+      epilogue(j, g + 1 < G);
+      kt = 0;
+      ++j;
+    }
+  }
+}
+
+static int g_pp_persist = 1;  // dmf_conv_tune key 8: 1 persistent grid (<= one block per CU), 0 one block per tile
+
+int conv_pp_tune(int value) {
+  g_pp_persist = value;
+  return 0;
 }
 
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st) {
-  const dim3 g((unsigned)(a.mtiles * a.ntiles)), b(PP_THREADS);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int ntile = a.mtiles * a.ntiles;
+  const dim3 g((unsigned)(g_pp_persist ? std::min(ntile, ncu) : ntile)), b(PP_THREADS);
   const size_t lds = (size_t)PP_LDS + lds_bias;
   DMF_CHECK_ARG(lds <= 160 * 1024, "conv_pp: %d output channels of bias exceed the LDS staging", a.Nout);
   a.dbg = 0;

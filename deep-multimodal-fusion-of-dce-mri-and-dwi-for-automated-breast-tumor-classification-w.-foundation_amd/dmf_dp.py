@@ -40,6 +40,12 @@ def dist_env():
 # topology with aten kernels on the nested stream (tools/capture_fork_probe.py),
 # so by default those segments are launched after backward instead
 NESTED_FORK_OK = os.environ.get("DMF_DP_NESTED_FORK", "0") == "1"
+# PREFORK (default): the comm stream is forked from the step's stream when
+# backward begins, so a segment produced on the DCE encoder's stream only adds
+# an event edge into an already-forked branch (no fork of a fork) and overlaps
+# the rest of backward inside the captured graph too
+# (tests/test_gpu_dp.py::test_overlapped_segment_allreduce_captured[B-True])
+PREFORK = os.environ.get("DMF_DP_PREFORK", "1") == "1"
 
 
 def rank_strided_indices(n_items, rank, world, epoch=0, shuffle=False, seed=0):
@@ -109,6 +115,7 @@ class FusionTrainer:
         self.segment_bytes = int(mb * (1 << 20))
         self._hooks = []
         self._ready_order = []
+        self._fires = {}
         self._armed = False
         self._comm = None
         self._rccl = None
@@ -143,18 +150,27 @@ class FusionTrainer:
 
     # ------------------------------------------------- overlapped exchange
     def _install_hooks(self):
+        import dmf_ops as O
+
         for h in self._hooks:
             h.remove()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self._trainable()]
+        # conv weights and BN gamma / beta get their gradients through grad_sink (no AccumulateGrad,
+        # so no post-accumulate hook): the sink path reports them once their kernels are enqueued
+        if self._on_grad not in O.SINK_HOOKS:
+            O.SINK_HOOKS.append(self._on_grad)
+        self._fires = {}
 
     def _on_grad(self, p):
         if not self._armed:
             return
         if not self._bucket_ready:
-            # first step: learn the gradient-ready order and the stream each
-            # gradient is produced on (DWI / fusion: the step's stream; DCE:
-            # its concurrent encoder stream)
-            self._ready_order.append((p, torch.cuda.current_stream().cuda_stream))
+            # first step: learn the gradient-ready order, the stream each gradient is produced on
+            # (DWI / fusion: the step's stream; DCE: its concurrent encoder stream) and how many
+            # ready events each parameter raises per step
+            if id(p) not in self._fires:
+                self._ready_order.append((p, torch.cuda.current_stream().cuda_stream))
+            self._fires[id(p)] = self._fires.get(id(p), 0) + 1
             return
         k = self._seg_of.get(p)
         if k is None:
@@ -170,7 +186,8 @@ class FusionTrainer:
         backward while a graph is being captured: a fork from a forked stream
         breaks capture end on this stack."""
         cur = torch.cuda.current_stream()
-        if torch.cuda.is_current_stream_capturing() and cur != self._origin and not NESTED_FORK_OK:
+        if (torch.cuda.is_current_stream_capturing() and cur != self._origin and not NESTED_FORK_OK
+                and not PREFORK):
             self._deferred.append(k)
             return
         self._launched.add(k)
@@ -188,8 +205,12 @@ class FusionTrainer:
             rank = dist.get_rank() if dist.is_initialized() else 0
             self._rccl = RcclComm(rank, self.world, self._origin.device)
         if self._bucket_ready:
-            self._pending = [len(s) for s in self.opt.segments]
+            # ready events per segment (a parameter may raise more than one: learned in the first step)
+            self._pending = [sum(self._fires.get(id(self.opt._bucket_params[i]), 1) for i in seg)
+                             for seg in self.opt.segments]
         self._launched, self._deferred = set(), []
+        if PREFORK:
+            self._comm.wait_stream(self._origin)
         self._armed = True
 
     def _end_backward(self):

@@ -604,14 +604,34 @@ def _col_stats(y):
     return part
 
 
+# callables(param) told that a sink-accumulated gradient (grad_sink) has been ENQUEUED on the current
+# stream -- the post-accumulate-grad hooks never fire for such parameters (autograd gets None), so the
+# data-parallel trainer's overlapped exchange listens here too (dmf_dp.FusionTrainer)
+SINK_HOOKS = []
+_SINK_PENDING = []
+
+
 def grad_sink(p):
     """p.grad as the in-place accumulation target of a gradient kernel: the
     conv/BN backward kernels add straight into it (their accumulate mode) and
     hand autograd None, so there is no AccumulateGrad add and no zero fill
-    per parameter. Allocated zeroed on first use."""
+    per parameter. Allocated zeroed on first use. The owning backward calls
+    ``flush_sinks()`` once its kernels are enqueued."""
     if p.grad is None:
         p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    if SINK_HOOKS:
+        _SINK_PENDING.append(p)
     return p.grad
+
+
+def flush_sinks():
+    """Fire SINK_HOOKS for the parameters whose sink kernels this backward enqueued."""
+    if _SINK_PENDING:
+        ps = list(_SINK_PENDING)
+        _SINK_PENDING.clear()
+        for h in list(SINK_HOOKS):
+            for p in ps:
+                h(p)
 
 
 def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2=None, gate_holder=None,
@@ -878,6 +898,7 @@ class _ConvBNActFn(torch.autograd.Function):
         elif res is not None and need[6]:
             dres = dz
         # gamma/beta (and the MFMA conv weights) were accumulated in place (grad_sink)
+        flush_sinks()
         return dx, dx2, dw, db, None, None, dres, dxr, dwr, None, None, None
 
 

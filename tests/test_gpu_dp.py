@@ -251,9 +251,11 @@ def test_trainer_follows_lr_changes_and_unfreeze():
     assert torch.isfinite(tr.loss).item()
 
 
-def _overlap_worker(port, outdir, mode):
+def _overlap_worker(port, outdir, mode, prefork=False):
+    import dmf_dp
     from dmf_dp import FusionTrainer
 
+    dmf_dp.PREFORK = prefork
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     out = {}
@@ -265,15 +267,21 @@ def _overlap_worker(port, outdir, mode):
             losses.append(float(tr.step(_batch(dev, 60 + it)).item()))
         torch.cuda.synchronize()
         out[tag] = {"params": {n: p.detach().cpu() for n, p in lm.named_parameters()}, "losses": losses,
-                    "captures": tr.captures, "segments": len(tr.opt.segments) if overlap else 0}
+                    "captures": tr.captures, "segments": len(tr.opt.segments) if overlap else 0,
+                    # segments whose all-reduce was launched from inside backward (not deferred to its end)
+                    "early": (len(tr.opt.segments) - len(tr._deferred) - len(
+                        [k for k in range(len(tr.opt.segments)) if tr._pending[k] > 0])) if overlap else 0}
     torch.save(out, os.path.join(outdir, "overlap.pt"))
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["A", "B"])
-def test_overlapped_segment_allreduce_captured(tmp_path, mode):
+@pytest.mark.parametrize("mode,prefork", [("A", False), ("B", False), ("B", True)])
+def test_overlapped_segment_allreduce_captured(tmp_path, mode, prefork):
+    """prefork: the comm stream is forked from the step's stream at the start
+    of backward, so the DCE encoder's segments (its own stream) join it by an
+    event edge inside the capture instead of being deferred to the end."""
     ctx = mp.get_context("spawn")
-    pr = ctx.Process(target=_overlap_worker, args=(_free_port(), str(tmp_path), mode))
+    pr = ctx.Process(target=_overlap_worker, args=(_free_port(), str(tmp_path), mode, prefork))
     pr.start()
     pr.join(timeout=500)
     assert pr.exitcode == 0, pr.exitcode
@@ -296,8 +304,8 @@ def test_overlapped_segment_allreduce_captured(tmp_path, mode):
     d_2 = [(r["plain2"]["params"][n] - init[n]).reshape(-1) for n, w in p["params"].items()
            if (w - init[n]).abs().max().item() != 0]
     noise = _rel(torch.cat(d_2), torch.cat(d_p))
-    print(f"mode {mode}: overlapped vs plain update, relative L2 {tot:.2e} over {len(d_o)} tensors "
-          f"(plain vs plain: {noise:.2e})")
+    print(f"mode {mode} prefork {prefork}: overlapped vs plain update, relative L2 {tot:.2e} over {len(d_o)} "
+          f"tensors (plain vs plain: {noise:.2e}); segments {o['segments']}, launched inside backward {o['early']}")
     # within the run-to-run noise of the plain trainer itself (mode B: the
     # float-atomic noise of the backward, amplified by the sign-like first
     # AdamW steps -- see the module docstring)
