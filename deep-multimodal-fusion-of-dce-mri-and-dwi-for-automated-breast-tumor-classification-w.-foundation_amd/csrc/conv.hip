@@ -725,24 +725,28 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
 // bias + DMF_ACT_* activation. The next K-step's DMA pieces are spread over
 // both k-halves (pieces 0-3 in the first, 4-7 in the second; "all 8 in one
 // half" or "all 8 after the barrier" measured no better).
-template <bool PADCHK, bool DUAL, int EPI>
-__global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
+template <bool PADCHK, bool DUAL, int EPI, int TBM = QBM, int TBN = QBN, int TWN = QWN>
+__global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(ConvArgs a) {
   constexpr int ES = 2, BK = 64;
-  constexpr int NW = QTHREADS / 64;
-  constexpr int NA = QBM / 8 / NW;  // pixel row-groups (8 rows) per wave: 4
-  constexpr int NB = QBN / 8 / NW;  // weight row-groups per wave: 4
-  constexpr int FM = QBM / (16 * QWM), FN = QBN / (16 * QWN);  // 8 pixel x 4 channel fragments
+  constexpr int TWM = 2;  // two pixel-half waves per 64-channel slab (ps_epilogue)
+  constexpr int NTH = 64 * TWM * TWN, NW = TWM * TWN;
+  constexpr int STG = (TBM + TBN) * 128;  // one K-step stage: TBM pixel rows + TBN weight rows of 128 B
+  constexpr int NA = TBM / 8 / NW;  // pixel row-groups (8 rows) per wave: 4
+  constexpr int NB = TBN / 8 / NW;  // weight row-groups per wave: 4
+  constexpr int FM = TBM / (16 * TWM), FN = TBN / (16 * TWN);  // 8 (256x256) or 4 (128x128) pixel x 4 channel fragments
+  static_assert(NA == 4 && NB == 4 && FN == 4, "k_conv_fwd_ps geometry");
+  constexpr int EPI_VM = 2 * FM;  // an epilogue's stores per wave (+2 float64 atomics, pixel-half 0, stat_acc)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / QWN, wn = wid % QWN;
+  const int wm = wid / TWN, wn = wid % TWN;
   // (no static priority split between the wave halves here: measured -0.4 % encoder forward
   // without it, interleaved A/B; k_conv_fwd_sq keeps its VAR 1)
   const int lr = lane >> 3;
   const int lc = (lane & 7) ^ lr;  // source-side swizzle (see k_conv_fwd_wide)
   const int fr = lane & 15, fg = lane >> 4;
   const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  float* sred = (float*)(smem + 2 * QSTAGE);
+  float* sred = (float*)(smem + 2 * STG);
 
   const v4i_t rx = buf_rsrc(a.x, (long long)a.N * a.H * a.W * a.ldx * ES);
   const v4i_t rx2 = buf_rsrc(DUAL ? a.x2 : a.x, (long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES);
@@ -754,9 +758,9 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
   const int hw = a.Ho * a.Wo;
   // bias (heads / projections with bias) staged once: the epilogue must issue no vmem load
   // (a compiler-visible load would be waited for behind the in-flight DMA)
-  float* sbias = sred + 2 * 256 * 2;
+  float* sbias = sred + 2 * TBN * 2;
   if (a.bias) {
-    for (int i = tid; i < a.Nout; i += QTHREADS) sbias[i] = a.bias[i];
+    for (int i = tid; i < a.Nout; i += NTH) sbias[i] = a.bias[i];
     __syncthreads();
   }
 
@@ -766,7 +770,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
   unsigned vb[NB];
   auto rows_for = [&](int lin) {
     const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-    const int m0 = mt * QBM, n0 = nt * QBN;
+    const int m0 = mt * TBM, n0 = nt * TBN;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = m0 + wid * (NA * 8) + i * 8 + lr;
@@ -803,8 +807,8 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     p_toff = p_hi ? (rd * a.W + sd) * a.ldx2 + (c0 - a.C1) : (rd * a.W + sd) * a.ldx + c0;
     p_rd = rd;
     p_sd = sd;
-    p_As = lds0 + stage * QSTAGE;
-    p_Bs = p_As + QBM * 128;
+    p_As = lds0 + stage * STG;
+    p_Bs = p_As + TBM * 128;
   };
   auto piece = [&](int p) {
     if (p < NA) {
@@ -839,8 +843,8 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     // step. After an epilogue its 16 stores (+2 atomics) are younger: leave them in flight.
     if (epi) {
       if ((a.stat_acc > 0 || a.stat_acc == -1) && wm == 0)
-        asm volatile("s_waitcnt vmcnt(18)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(EPI_VM + 2) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(EPI_VM) : "memory");
       epi = false;
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -858,25 +862,26 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
     } else {
       more = false;
     }
-    const char* Ps = smem + st * QSTAGE;  // pixel rows
-    const char* Ws = Ps + QBM * 128;      // weight rows (permuted)
+    const char* Ps = smem + st * STG;  // pixel rows
+    const char* Ws = Ps + TBM * 128;   // weight rows (permuted)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + fg;
       uint4 pv[FM], wv[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int row = wn * (QBN / QWN) + j * 16 + fr;
+        const int row = wn * (TBN / TWN) + j * 16 + fr;
         wv[j] = *(const uint4*)(Ws + row * 128 + ((ch ^ (row & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int row = wm * (QBM / QWM) + i * 16 + fr;
+        const int row = wm * (TBM / TWM) + i * 16 + fr;
         pv[i] = *(const uint4*)(Ps + row * 128 + ((ch ^ (row & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if (more && (i & 1) == 0 && !(a.dbg & 2)) piece(kk * 4 + (i >> 1));
+        // the next K-step's 8 pieces, 4 per k-half, spread over the FM fragment rows
+        if (more && i % (FM / 4) == 0 && !(a.dbg & 2)) piece(kk * 4 + i / (FM / 4));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&wv[j], *(bf16x8_t*)&pv[i], acc[i][j], 0,
@@ -889,7 +894,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_ps(ConvArgs a) {
       continue;
     }
     // ---------------- epilogue of tile `lin` (the next tile's step 0 is in flight)
-    if (!(a.dbg & 4)) ps_epilogue<EPI>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
+    if (!(a.dbg & 4)) ps_epilogue<EPI, TBN, FM, TBM>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
     epi = !(a.dbg & 4);
     if (!more) break;
     t = tnext;
@@ -1296,10 +1301,14 @@ struct ConvPlan {
   int bm, bn;
   bool ps;    // k_conv_fwd_ps (persistent LDS-DMA 256x256, register epilogue)
   bool pp;    // k_conv_fwd_pp (conv_pp.hip: ping-pong 8-phase 256x256, register epilogue)
+  bool p2;    // k_conv_fwd_ps at 128x128, two workgroups per CU (ps also set)
 };
 // 7 = ping-pong 256x256 form (conv_pp.hip): 0 off, 1 (default) for 3x3 and K >= 1024 (where it beats the
 // persistent form: tools/conv_bench.py --tunes, profiles/r03h_conv_ab.txt), 2 for every legal shape
 static int g_pp_mode = 1;
+// 9 = the persistent form at 128x128 with two workgroups per CU (one's epilogue runs under the other's
+// K loop; their vmcnt queues are separate): 0 off, 1 for 1x1 convs with K < 1024, 2 every legal shape
+static int g_p2_mode = 0;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
@@ -1347,7 +1356,7 @@ static int cu_count() {
 }
 
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, false, false, CBM, CBN, false, false};
+  ConvPlan p{false, false, false, CBM, CBN, false, false, false};
   const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
   // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
   if (dgrad || fast_disabled() || (a.in_ss != nullptr && !(plain && a.x2 == nullptr && !ina_buf_disabled())))
@@ -1375,6 +1384,16 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
       p.bn = (g_force == 1 || g_force == 2) ? 128 : 64;
       return p;
     }
+  }
+  // persistent 128x128, two workgroups per CU
+  if (dtype == DMF_BF16 && !wide_disabled() && g_p2_mode > 0 && a.tickets == nullptr && a.Nout % 128 == 0 &&
+      a.Ktot >= 64 && (long long)cdiv(a.M, 128) * (a.Nout / 128) >= 2LL * cu_count() &&
+      (long long)a.M * a.ldy * 2 < (1LL << 31) && (a.bias == nullptr || a.Nout <= 2048) &&
+      (g_p2_mode >= 2 || (a.KH * a.KW == 1 && a.Ktot < 1024))) {
+    p.wide = p.sq = p.ps = p.p2 = true;
+    p.bm = 128;
+    p.bn = 128;
+    return p;
   }
   // ping-pong square tile: same legality as the persistent form below
   const bool sq_ps_ok = dtype == DMF_BF16 && !wide_disabled() && a.tickets == nullptr && a.Nout % QBN == 0 &&
@@ -1436,7 +1455,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = dtype == DMF_BF16 ? 2 : 4;
-  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
+  const size_t lds_total = plan.p2 ? (size_t)(2 * 256 * 128 + 2 * 128 * 2 * 4) + (a.bias ? (size_t)a.Nout * 4 : 0)
+                          : plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
@@ -1461,6 +1481,26 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const int epi = a.partials != nullptr ? 0 : 1 + a.act;
     DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st);
+  } else if (plan.p2) {
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const dim3 gp((unsigned)std::min<long long>(nblk, 2LL * cu_count())), bq(256);
+    const int epi = a.partials != nullptr ? 0 : 1 + a.act;
+    a.dbg = g_ps_dbg;
+    DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
+#define DMF_P2(E)                                                                                                \
+  do {                                                                                                           \
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E, 128, 128, 2>), gp, bq, lds_total, st, a); \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E, 128, 128, 2>), gp, bq, lds_total, st, a);   \
+    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, 128, 128, 2>), gp, bq, lds_total, st, a);               \
+  } while (0)
+    switch (epi) {
+      case 0: DMF_P2(0); break;
+      case 1: DMF_P2(1); break;
+      case 2: DMF_P2(2); break;
+      case 3: DMF_P2(3); break;
+      default: DMF_P2(4); break;
+    }
+#undef DMF_P2
   } else if (plan.ps) {
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
@@ -1698,6 +1738,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 6: g_ps_dbg = value; return 0;
     case 7: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ping-pong mode %d", value); g_pp_mode = value; return 0;
     case 8: return conv_pp_tune(value != 0);
+    case 9: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: two-workgroup mode %d", value); g_p2_mode = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

@@ -193,13 +193,15 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int fr) {
   return keep + dpp_f<0xB1>(send);
 }
 
-template <int EPI, int TBN = QBN>
-__device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[8][4], int lin,
+// (FM pixel fragments per wave, TBM pixel rows per tile: 8 / 256 for the 256x256 forms, 4 / 128 for
+// the 128x128 two-workgroup form; two pixel-half waves per channel slab in both)
+template <int EPI, int TBN = QBN, int FM = 8, int TBM = QBM>
+__device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM][4], int lin,
                                             __amdgpu_buffer_rsrc_t ry, float* sred, const float* sbias, int tid,
                                             int wm, int wn, int fr, int fg) {
-  constexpr int FM = 8, FN = 4;
+  constexpr int FN = 4;
   const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-  const int m0 = mt * QBM, n0 = nt * TBN;
+  const int m0 = mt * TBM, n0 = nt * TBN;
   const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
   constexpr bool stats = EPI == 0;
   float bsv[16];
@@ -210,7 +212,7 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[8]
   for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int m = m0 + wm * (QBM / QWM) + i * 16 + fr;
+    const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
     const bool ok = m < a.M;
     float v[16];
 #pragma unroll

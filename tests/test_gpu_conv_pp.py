@@ -1,7 +1,8 @@
-"""The ping-pong 256x256 forward conv (csrc/conv_pp.hip) against a float64
-torch reference of the same bf16 operands, and bit for bit against the
-persistent form it shares operand order, K order and register epilogue with
-(k_conv_fwd_ps). Shapes cover a plain 1x1, padded / dilated 3x3 with an M
+"""The ping-pong 256x256 forward conv (csrc/conv_pp.hip) and the persistent
+form at 128x128 with two workgroups per CU (k_conv_fwd_ps<..., 128, 128, 2>)
+against a float64 torch reference of the same bf16 operands, and bit for bit
+against the 256x256 persistent form they share operand order, K order and
+register epilogue with (k_conv_fwd_ps). Shapes cover a plain 1x1, padded / dilated 3x3 with an M
 tail, the neck's two-source 3x3 (channel concat in the K loop), the bias +
 activation epilogue, and K = 64 (a single K-tile: prologue-only staging)."""
 import copy
@@ -32,11 +33,16 @@ def _q(t):
     return t.bfloat16().float()
 
 
-@pytest.fixture
-def pp_mode():
-    N.call("dmf_conv_tune", 7, 2)
+# (dmf_conv_tune key, value forcing the form on every legal shape, library default)
+FORMS = {"pp": (7, 2, 1), "p2": (9, 2, 0)}
+
+
+@pytest.fixture(params=sorted(FORMS))
+def pp_mode(request):
+    key, on, default = FORMS[request.param]
+    N.call("dmf_conv_tune", key, on)
     yield
-    N.call("dmf_conv_tune", 7, 0)
+    N.call("dmf_conv_tune", key, default)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -74,18 +80,21 @@ def test_pp_forward_matches_reference_and_bn_stats(case, pp_mode):
         assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("form", sorted(FORMS))
 @pytest.mark.parametrize("case", [c for c in CASES if c[5] == 1 and c[8] == 0])
-def test_pp_bitwise_equals_persistent_form(case):
-    """k_conv_fwd_pp and k_conv_fwd_ps accumulate the same MFMAs in the same
-    K order into the same registers: identical raw outputs."""
+def test_pp_bitwise_equals_persistent_form(case, form):
+    """k_conv_fwd_pp / the 128x128 two-workgroup form and the 256x256
+    k_conv_fwd_ps accumulate the same MFMAs in the same K order into the same
+    registers: identical raw outputs."""
+    key, on, default = FORMS[form]
     n, ci, h, w, co, k, p, d, _, act = case
     torch.manual_seed(12)
     conv = nn.Conv2d(ci, co, k, bias=act is not None).to(DEV)
     x = torch.randn(n, ci, h, w, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     g = O.ConvGeom(conv)
     outs = []
-    for mode in (0, 2):
-        N.call("dmf_conv_tune", 7, mode)
+    for mode in ((7, 0), (key, on)):
+        N.call("dmf_conv_tune", *mode)
         try:
             with torch.no_grad():
                 y, _ = O._conv_forward_raw(x, conv.weight, conv.bias, g, (O.WeightCache(), O.WeightCache()), False,
@@ -93,5 +102,6 @@ def test_pp_bitwise_equals_persistent_form(case):
             torch.cuda.synchronize()
             outs.append(y.clone())
         finally:
-            N.call("dmf_conv_tune", 7, 0)
+            N.call("dmf_conv_tune", 7, 1)
+            N.call("dmf_conv_tune", key, default)
     assert torch.equal(outs[0], outs[1])
