@@ -322,11 +322,27 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
   __shared__ float Acc[5][RECON_NR][RECON_MAXS];
   __shared__ float Lx[RECON_MAXS];   // column x: bilinear weight of j1
   __shared__ short J0[RECON_MAXS];   // column x: source columns j0 (j1 = j0 + (j0 < w-1))
-  __shared__ float red[16];
+  __shared__ float red5[5][4];
   const int b = blockIdx.x, q = blockIdx.y, nb = gridDim.y;
   const int y0 = q * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
   const int tid = threadIdx.x;
   const float inv_n = 1.f / ((float)a.B * a.S * a.S);
+  // the band's target values of this thread's columns: every HBM load issued first, so their
+  // latency overlaps the staging below (one exposed latency per block, not two)
+  float tAr[RECON_XPT][RECON_RB], tBr[RECON_XPT][RECON_RB];
+#pragma unroll
+  for (int u = 0; u < RECON_XPT; ++u) {
+    const int x = tid + u * 256;
+    const bool xin = x < a.S;
+    const float* pA = (a.tA && xin) ? a.tA + ((size_t)b * a.S + y0) * a.S + x : nullptr;
+    const float* pB = (a.tB && xin) ? a.tB + ((size_t)b * a.S + y0) * a.S + x : nullptr;
+#pragma unroll
+    for (int yy = 0; yy < RECON_RB; ++yy) {
+      const bool in = y0 + yy < y1;
+      tAr[u][yy] = (pA && in) ? __builtin_nontemporal_load(pA + (size_t)yy * a.S) : 0.f;
+      tBr[u][yy] = (pB && in) ? __builtin_nontemporal_load(pB + (size_t)yy * a.S) : 0.f;
+    }
+  }
   int ib0, ie, tmp;
   float ftmp;
   lin_rs(y0, a.h, a.sc_h, ib0, tmp, ftmp);
@@ -365,16 +381,6 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
         rx[k][r] = (1.f - lx) * Rs[k][r][j0] + lx * Rs[k][r][j1];
         A[k][r] = 0.f;
       }
-    const float* pA = a.tA ? a.tA + ((size_t)b * a.S + y0) * a.S + x : nullptr;
-    const float* pB = a.tB ? a.tB + ((size_t)b * a.S + y0) * a.S + x : nullptr;
-    // the band's target values of this column: all loads issued up front (one HBM latency, not RB)
-    float tAr[RECON_RB], tBr[RECON_RB];
-#pragma unroll
-    for (int yy = 0; yy < RECON_RB; ++yy) {
-      const bool in = y0 + yy < y1;
-      tAr[yy] = (pA && in) ? pA[(size_t)yy * a.S] : 0.f;
-      tBr[yy] = (pB && in) ? pB[(size_t)yy * a.S] : 0.f;
-    }
 #pragma unroll
     for (int yy = 0; yy < RECON_RB; ++yy) {
       const int y = y0 + yy;
@@ -383,7 +389,7 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
       float ly;
       lin_rs(y, a.h, a.sc_h, i0, i1, ly);
       const int q0 = i0 - ib0, q1 = i1 - ib0;
-      const float tAv = tAr[yy], tBv = tBr[yy];
+      const float tAv = tAr[u][yy], tBv = tBr[u][yy];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         if (k >= a.nterms) break;
@@ -430,19 +436,29 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
     }
     G[(((size_t)k * a.B + b) * nb + q) * RECON_NR * a.w + r * a.w + j] = h;
   }
-  for (int k = 0; k < a.nterms; ++k) {
-    const float sm = block_sum(part[k], red);
-    if (tid == 0) ws[((size_t)b * nb + q) * 5 + k] = sm;
+  // the five loss partials in one block reduction (one barrier)
+#pragma unroll
+  for (int k = 0; k < 5; ++k) part[k] = wave_sum(part[k]);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) red5[k][tid >> 6] = part[k];
+  __syncthreads();
+  if (tid < a.nterms) {
+    float sm = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) sm += red5[tid][i];
+    ws[((size_t)b * nb + q) * 5 + tid] = sm;
   }
 }
 
-// pass 2: blocks [0, nterms*B) reduce the band slabs of map k = blk / B,
-// item b = blk % B into its gradient [h][w]; block nterms*B sums the loss
-// partials (fixed order: deterministic)
+// pass 2: one thread per gradient element (map k, item b, source row i,
+// column j) sums the (<= 3) band slabs covering row i, in band order; the
+// last block sums the loss partials in block order (fixed orders:
+// deterministic)
 __global__ void __launch_bounds__(256) k_recon_finish(ReconArgs a, const float* __restrict__ ws, int nb) {
-  __shared__ float red[16];
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x == a.nterms * a.B) {
+  const long long per = (long long)a.B * a.h * a.w;
+  if ((int)blockIdx.x == (int)gridDim.x - 1) {
+    __shared__ float red[16];
     const int nblk = a.B * nb;
     for (int k = 0; k < a.nterms; ++k) {
       float s = 0.f;
@@ -452,30 +468,25 @@ __global__ void __launch_bounds__(256) k_recon_finish(ReconArgs a, const float* 
     }
     return;
   }
-  const int k = blockIdx.x / a.B, b = blockIdx.x - (blockIdx.x / a.B) * a.B;
+  const long long t = (long long)blockIdx.x * blockDim.x + tid;
+  if (t >= per * a.nterms) return;
+  const int k = (int)(t / per);
+  const long long r = t - (long long)k * per;
+  const int b = (int)(r / (a.h * a.w)), e = (int)(r - (long long)b * a.h * a.w);
   if (!a.grads[k]) return;
-  __shared__ int band0[RECON_MAXS / RECON_RB + 1], band1[RECON_MAXS / RECON_RB + 1];  // first / last source row
-  for (int q = tid; q < nb; q += blockDim.x) {
+  const int i = e / a.w, j = e - (e / a.w) * a.w;
+  const float* G = ws + (size_t)a.B * nb * 5 + ((size_t)k * a.B + b) * nb * RECON_NR * a.w;
+  // bands whose source rows [ib0, ie] contain i: around the band of output row (i + 0.5) * S / h
+  const int qc = (int)(((float)i + 0.5f) * a.S / a.h) / RECON_RB;
+  float s = 0.f;
+  for (int q = max(0, qc - 2); q <= min(nb - 1, qc + 2); ++q) {
     int ib0, ie, tmp;
     float ftmp;
     lin_rs(q * RECON_RB, a.h, a.sc_h, ib0, tmp, ftmp);
     lin_rs(min(a.S, q * RECON_RB + RECON_RB) - 1, a.h, a.sc_h, tmp, ie, ftmp);
-    band0[q] = ib0;
-    band1[q] = ie;
+    if (i >= ib0 && i <= ie) s += G[(size_t)q * RECON_NR * a.w + (i - ib0) * a.w + j];
   }
-  __syncthreads();
-  const float* G = ws + (size_t)a.B * nb * 5 + ((size_t)k * a.B + b) * nb * RECON_NR * a.w;
-  for (int e = tid; e < a.h * a.w; e += blockDim.x) {
-    const int i = e / a.w, j = e - (e / a.w) * a.w;
-    // bands whose source rows [ib0, ie] contain i: around the band of output row (i + 0.5) * S / h
-    const int qc = (int)(((float)i + 0.5f) * a.S / a.h) / RECON_RB;
-    float s = 0.f;
-    for (int q = max(0, qc - 2); q <= min(nb - 1, qc + 2); ++q) {
-      const int ib0 = band0[q];
-      if (i >= ib0 && i <= band1[q]) s += G[(size_t)q * RECON_NR * a.w + (i - ib0) * a.w + j];
-    }
-    a.grads[k][(size_t)b * a.h * a.w + e] = s;
-  }
+  a.grads[k][(size_t)b * a.h * a.w + e] = s;
 }
 
 // ------------------------------------------------------------ mimic
@@ -635,7 +646,8 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
       hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
     else
       hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
-    hipLaunchKernelGGL(k_recon_finish, dim3(nterms * B + 1), dim3(256), 0, (hipStream_t)stream, a, ws, nb);
+    hipLaunchKernelGGL(k_recon_finish, dim3(cdiv((long long)nterms * B * h * w, 256) + 1), dim3(256), 0,
+                       (hipStream_t)stream, a, ws, nb);
   } else if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
     const dim3 g(B, cdiv(S, RECON_RB));
     if (dtype == DMF_BF16)
