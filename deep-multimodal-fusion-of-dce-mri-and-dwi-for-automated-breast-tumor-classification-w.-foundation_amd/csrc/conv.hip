@@ -1302,6 +1302,7 @@ struct ConvPlan {
   bool ps;    // k_conv_fwd_ps (persistent LDS-DMA 256x256, register epilogue)
   bool pp;    // k_conv_fwd_pp (conv_pp.hip: ping-pong 8-phase 256x256, register epilogue)
   bool p2;    // k_conv_fwd_ps at 128x128, two workgroups per CU (ps also set)
+  bool stem;  // k_conv_stem (conv_stem.hip): 7x7 / 2 over 8 or 16 channels, 64 out
 };
 // 7 = ping-pong 256x256 form (conv_pp.hip): 0 off, 1 (default) for 3x3 and K >= 1024 (where it beats the
 // persistent form: tools/conv_bench.py --tunes, profiles/r03h_conv_ab.txt), 2 for every legal shape
@@ -1309,6 +1310,8 @@ static int g_pp_mode = 1;
 // 9 = the persistent form at 128x128 with two workgroups per CU (one's epilogue runs under the other's
 // K loop; their vmcnt queues are separate): 0 off, 1 for 1x1 convs with K < 1024, 2 every legal shape
 static int g_p2_mode = 0;
+// 10 = the dedicated 7x7 stem kernel (conv_stem.hip) on (1, default) / off
+static int g_stem_enable = 1;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
@@ -1356,7 +1359,13 @@ static int cu_count() {
 }
 
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, false, false, CBM, CBN, false, false, false};
+  ConvPlan p{false, false, false, CBM, CBN, false, false, false, false};
+  if (g_stem_enable && conv_stem_ok(dtype, dgrad, a)) {
+    p.stem = true;
+    p.bm = conv_stem_m_tile(a);
+    p.bn = 64;
+    return p;
+  }
   const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
   // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
   if (dgrad || fast_disabled() || (a.in_ss != nullptr && !(plain && a.x2 == nullptr && !ina_buf_disabled())))
@@ -1473,7 +1482,9 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, BM, BN>), g, b, lds_total, st, a);  \
     else hipLaunchKernelGGL((k_conv_fwd_buf<TT, true, false, BM, BN>), g, b, lds_total, st, a);              \
   } while (0)
-  if (dgrad) {
+  if (plan.stem) {
+    return launch_conv_stem(a, st);
+  } else if (dgrad) {
     if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
     else DMF_CONV_LAUNCH(float, true, -1);
   } else if (plan.pp) {
@@ -1739,6 +1750,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 7: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ping-pong mode %d", value); g_pp_mode = value; return 0;
     case 8: return conv_pp_tune(value != 0);
     case 9: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: two-workgroup mode %d", value); g_p2_mode = value; return 0;
+    case 10: g_stem_enable = value != 0; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1753,6 +1765,11 @@ extern "C" int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin
   a.x2 = Cin2 > 0 ? (const void*)16 : nullptr;
   a.in_ss = has_in_affine ? (const float*)16 : nullptr;
   a.Nout = Cout; a.KH = KH; a.KW = KW; a.Ktot = KH * KW * a.C; a.M = N * Ho * Wo;
+  a.Ho = Ho; a.Wo = Wo; a.ldy = Cout;
+  // the dilation the output size implies (conv_plan's tile choice depends on it)
+  a.dil = 1;
+  for (int d = 1; KH > 1 && d <= 16; ++d)
+    if ((H + 2 * pad - d * (KH - 1) - 1) / stride + 1 == Ho) { a.dil = d; break; }
   return cdiv(a.M, conv_plan(dtype, false, a).bm);
 }
 

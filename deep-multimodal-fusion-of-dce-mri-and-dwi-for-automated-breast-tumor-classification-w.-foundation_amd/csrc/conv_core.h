@@ -269,6 +269,11 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   }
 }
 
+// 7x7 / stride-2 stem conv (conv_stem.hip): legality, pixels per workgroup (= BN slab rows), launcher
+bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a);
+int conv_stem_m_tile(const ConvArgs& a);
+int launch_conv_stem(ConvArgs& a, hipStream_t st);
+
 // persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 BN statistics, 1 + act: bias + act)
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st);
 int conv_pp_tune(int value);  // dmf_conv_tune key 8

@@ -494,7 +494,8 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dz, int lddz, const T* __re
 // lanes of 8 channels (64 channels), 16-B accesses; x is the BN input (the
 // raw conv output), z = x*ssa + shift (+ residual) recomputed for act'.
 template <typename T, int ACT>
-__global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy, int lddy, const T* __restrict__ x,
+__global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy, int lddy,
+                                                        const T* __restrict__ dy2, int lddy2, const T* __restrict__ x,
                                                         int ldx, const float* __restrict__ ssa,
                                                         const T* __restrict__ res, int ldr,
                                                         const float* __restrict__ ssr, float p,
@@ -526,6 +527,14 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
       if (m >= M) break;
       float g[8], xv[8];
       ld8(dy + m * lddy + c0, g);
+      if (dy2) {
+        // a second gradient of the same output (the next block's shortcut), summed here in fp32
+        // instead of by a separate add pass
+        float g2[8];
+        ld8(dy2 + m * lddy2 + c0, g2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] += g2[e];
+      }
       ld8(x + m * ldx + c0, xv);
       if (p > 0.f) {
         bool keep[4];
@@ -947,24 +956,25 @@ extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void*
   return 0;
 }
 
-static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* x, int ldx,
-                                  const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
-                                  int act, float dropout_p, const unsigned long long* rng, int site,
-                                  const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
-                                  float* partials, double* acc, int replicas, void* stream);
+static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* dy2, int lddy2, const void* x,
+                                  int ldx, const float* scale_shift, const void* res, int ldr,
+                                  const float* res_scale_shift, int act, float dropout_p,
+                                  const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz,
+                                  int lddz, long long M, int C, float* partials, double* acc, int replicas,
+                                  void* stream);
 
-extern "C" int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, int ldx,
-                                     const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
-                                     int act, float dropout_p, const unsigned long long* rng, int site,
-                                     const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
-                                     float* partials, void* stream) {
+extern "C" int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* dy2, int lddy2, const void* x,
+                                     int ldx, const float* scale_shift, const void* res, int ldr,
+                                     const float* res_scale_shift, int act, float dropout_p,
+                                     const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz,
+                                     int lddz, long long M, int C, float* partials, void* stream) {
   DMF_CHECK_ARG(partials, "dmf_act_bwd_bn_reduce: bad args");
-  return act_bwd_bn_reduce_impl(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng,
-                                site, save_mean_invstd, dz, lddz, M, C, partials, nullptr, 0, stream);
+  return act_bwd_bn_reduce_impl(dtype, dy, lddy, dy2, lddy2, x, ldx, scale_shift, res, ldr, res_scale_shift, act,
+                                dropout_p, rng, site, save_mean_invstd, dz, lddz, M, C, partials, nullptr, 0, stream);
 }
 
-extern "C" int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* x, int ldx,
-                                         const float* scale_shift, const void* res, int ldr,
+extern "C" int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* dy2, int lddy2,
+                                         const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
                                          const float* res_scale_shift, int act, float dropout_p,
                                          const unsigned long long* rng, int site, const float* save_mean_invstd,
                                          void* dz, int lddz, long long M, int C, double* acc, int replicas,
@@ -974,8 +984,8 @@ extern "C" int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, co
   DMF_CHECK_ARG(C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
                     ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz)) % 16 == 0,
                 "dmf_act_bwd_bn_reduce_acc: needs 8-channel vectors (C=%d)", C);
-  return act_bwd_bn_reduce_impl(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng,
-                                site, save_mean_invstd, dz, lddz, M, C, nullptr, acc, replicas, stream);
+  return act_bwd_bn_reduce_impl(dtype, dy, lddy, dy2, lddy2, x, ldx, scale_shift, res, ldr, res_scale_shift, act,
+                                dropout_p, rng, site, save_mean_invstd, dz, lddz, M, C, nullptr, acc, replicas, stream);
 }
 
 extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int ldx, const double* acc,
@@ -1004,16 +1014,20 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
   return 0;
 }
 
-static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* x, int ldx,
-                                  const float* scale_shift, const void* res, int ldr, const float* res_scale_shift,
-                                  int act, float dropout_p, const unsigned long long* rng, int site,
-                                  const float* save_mean_invstd, void* dz, int lddz, long long M, int C,
-                                  float* partials, double* acc, int replicas, void* stream) {
+static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const void* dy2, int lddy2, const void* x,
+                                  int ldx, const float* scale_shift, const void* res, int ldr,
+                                  const float* res_scale_shift, int act, float dropout_p,
+                                  const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz,
+                                  int lddz, long long M, int C, float* partials, double* acc, int replicas,
+                                  void* stream) {
   DMF_CHECK_ARG(dy && x && scale_shift && save_mean_invstd && dz && (partials || acc) && M > 0 && C > 0,
                 "dmf_act_bwd_bn_reduce: bad args");
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_act_bwd_bn_reduce: dropout needs rng state");
   const bool vec8 = C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
-                    ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz)) % 16 == 0;
+                    (!dy2 || lddy2 % 8 == 0) &&
+                    ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz) |
+                     (uintptr_t)(dy2 ? dy2 : dz)) % 16 == 0;
+  DMF_CHECK_ARG(vec8 || !dy2, "dmf_act_bwd_bn_reduce: a second gradient needs 8-channel vectors (C=%d)", C);
   if (!vec8) {
     int rc = dmf_act_bwd(dtype, dy, lddy, x, ldx, scale_shift, res, ldr, res_scale_shift, act, dropout_p, rng, site,
                          dz, lddz, M, C, stream);
@@ -1024,7 +1038,7 @@ static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const voi
   DMF_CHECK_ARG(tiles < 65536LL * 32768LL, "dmf_act_bwd_bn_reduce: too many rows");
   dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
   hipStream_t s = (hipStream_t)stream;
-#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
+#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)dy2, lddy2, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
   if (dtype == DMF_BF16) {
     switch (act) {
       case DMF_ACT_RELU: DMF_ABR(bf16_t, DMF_ACT_RELU); break;

@@ -399,9 +399,15 @@ class BnArena:
         # a backward holding a slice of an earlier forward checks this: once the owner's next
         # forward has begun, that slice has been zeroed / handed out again
         self.gen = getattr(self, "gen", 0) + 1
-        if zero:
-            for c in self.chunks:
-                c.zero_()
+        if len(self.chunks) > 1:
+            # the previous forward (+ its backward's BN column sums) outgrew the first chunk: one
+            # zeroed chunk of the whole size from now on, so each forward costs ONE fill launch
+            # (mode B grew ~20 chunks per encoder: ~40 fills per step). Runs during the eager
+            # warm-up steps, before a graph captures the addresses.
+            total = sum(c.numel() for c in self.chunks)
+            self.chunks = [torch.zeros(total, dtype=torch.float64, device=self.device)]
+        elif zero:
+            self.chunks[0].zero_()
 
     def take(self, n):
         n = (n + 7) // 8 * 8
@@ -624,6 +630,11 @@ def grad_sink(p):
     return p.grad
 
 
+def _sinkable(*ps):
+    """grad_sink needs leaf parameters (their .grad is the accumulation target)."""
+    return all(p is None or (isinstance(p, torch.nn.Parameter) and p.is_leaf) for p in ps)
+
+
 def flush_sinks():
     """Fire SINK_HOOKS for the parameters whose sink kernels this backward enqueued."""
     if _SINK_PENDING:
@@ -670,7 +681,8 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
                    1 if dw_sink else 0, _stream())
             dw = None if dw_sink else dwt
         if need_db:
-            db = _colsum_nhwc(dy)
+            db = _colsum_nhwc(dy, grad_sink(bias) if dw_sink else None)
+            db = None if dw_sink else db
         dx = torch.zeros((), dtype=x.dtype, device=dev).expand(n, cx, h, w)
         return dx, dw, db
     if need_dx:
@@ -730,18 +742,20 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
                        1 if dw_sink else 0, _stream())
                 dw = None if dw_sink else dwt
             if need_db:
-                db = _colsum_nhwc(dy)
+                db = _colsum_nhwc(dy, grad_sink(bias) if dw_sink else None)
+                db = None if dw_sink else db
     return dx, dw, db
 
 
-def _colsum_nhwc(t):
-    """sum over (N,H,W) per channel -> fp32 [C]"""
+def _colsum_nhwc(t, out=None):
+    """sum over (N,H,W) per channel -> fp32 [C]; with ``out`` (a grad_sink) added into it"""
     n, c, h, w, ld = nhwc(t)
     m = n * h * w
     tiles = (m + 255) // 256
     part = torch.empty((tiles, c, 2), dtype=torch.float32, device=t.device)
     N.call("dmf_bn_bwd_reduce", dt(t), t.data_ptr(), ld, None, 0, None, m, c, part.data_ptr(), _stream())
-    out = torch.zeros(c, dtype=torch.float32, device=t.device)
+    if out is None:
+        out = torch.zeros(c, dtype=torch.float32, device=t.device)
     N.call("dmf_bn_bwd_finalize", part.data_ptr(), tiles, c, float(m), 1, None, None, None, out.data_ptr(), None,
            _stream())
     return out
@@ -760,8 +774,11 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias = ctx.saved_tensors
+        # weight / bias gradients added straight into .grad (grad_sink): no AccumulateGrad add per parameter
         dx, dw, db = _conv_backward(x, weight, bias, ctx.g, ctx.caches, dy, ctx.needs_input_grad[0],
-                                    ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
+                                    ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2],
+                                    dw_sink=_sinkable(weight, bias))
+        flush_sinks()
         return dx, dw, db, None, None, None
 
 
@@ -813,7 +830,7 @@ class _ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x2, w, b, gamma, beta, res, xr, wr, gamma_r, beta_r, spec):
-        (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act) = spec
+        (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act, _key, _handoff) = spec
         defer = in_ss is None and (res is None or _bn_apply_ok(res))
         y, ss, save, desc = _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss, in_act=in_act,
                                              defer=defer)
@@ -850,10 +867,14 @@ class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng) = ctx.saved_tensors
-        (g, caches, bn, act, p, _rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, _ia) = ctx.spec
+        (g, caches, bn, act, p, _rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, _ia, key, handoff) = ctx.spec
         if in_ss is not None:
             raise RuntimeError("conv_bn_act with a fused input affine is forward-only")
         dout = as_nhwc(dout)
+        # the next block's shortcut gradient of this output, handed over by that block's backward (below)
+        extra = GRAD_STASH.pop(key, None)
+        if extra is not None:
+            extra = as_nhwc(extra)
         n, c, ho, wo, ldy = nhwc(y)
         m = n * ho * wo
         dtc = dt(y)
@@ -866,9 +887,12 @@ class _ConvBNActFn(torch.autograd.Function):
         acc = ctx.bwd_acc.claim() if ctx.bwd_acc is not None else None
         lddo, lddz = nhwc(dout)[4], nhwc(dz)[4]
         if (acc is not None and ldy % 8 == 0 and lddo % 8 == 0 and (res_t is None or ldr % 8 == 0)
-                and (dout.data_ptr() | y.data_ptr() | (res_t.data_ptr() if res_t is not None else 0)) % 16 == 0):
-            # act/dropout backward + column sums into the arena, then the apply finalizes per block
-            N.call("dmf_act_bwd_bn_reduce_acc", dtc, dout.data_ptr(), lddo, y.data_ptr(), ldy, ss.data_ptr(),
+                and (dout.data_ptr() | y.data_ptr() | (res_t.data_ptr() if res_t is not None else 0)) % 16 == 0
+                and (extra is None or (nhwc(extra)[4] % 8 == 0 and extra.data_ptr() % 16 == 0))):
+            # act/dropout backward (of dout + the handed-over shortcut gradient) + column sums into the
+            # arena, then the apply finalizes per block
+            N.call("dmf_act_bwd_bn_reduce_acc", dtc, dout.data_ptr(), lddo, _p(extra),
+                   nhwc(extra)[4] if extra is not None else 0, y.data_ptr(), ldy, ss.data_ptr(),
                    _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
                    lddz, m, c, acc.data_ptr(), BN_ACC_REPLICAS, _stream())
             dy = empty_nhwc(n, c, ho, wo, y.dtype, y.device)
@@ -876,10 +900,13 @@ class _ConvBNActFn(torch.autograd.Function):
                    BN_ACC_REPLICAS, float(m), 1 if bn.training else 0, _p(bn.weight), save.data_ptr(), _p(dgamma),
                    _p(dbeta), dy.data_ptr(), nhwc(dy)[4], m, c, _stream())
         else:
+            if extra is not None:
+                dout = as_nhwc(dout + extra)
+                lddo = nhwc(dout)[4]
             # act/dropout backward and the BN column partials in one pass
             tiles = N.load().dmf_bn_bwd_tiles(m)
             part = torch.empty((tiles, c, 2), dtype=torch.float32, device=y.device)
-            N.call("dmf_act_bwd_bn_reduce", dtc, dout.data_ptr(), lddo, y.data_ptr(), ldy, ss.data_ptr(),
+            N.call("dmf_act_bwd_bn_reduce", dtc, dout.data_ptr(), lddo, None, 0, y.data_ptr(), ldy, ss.data_ptr(),
                    _p(res_t), ldr, _p(ss_r), ACT[act], float(p), _p(rng), site, save.data_ptr(), dz.data_ptr(),
                    lddz, m, c, part.data_ptr(), _stream())
             dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
@@ -895,8 +922,14 @@ class _ConvBNActFn(torch.autograd.Function):
             dbr = grad_sink(bn_r.bias) if need[10] else None
             dyr = _bn_backward(dz, yr, save_r, bn_r, dgr, dbr, training=bn_r.training)
             dxr, dwr, _ = _conv_backward(xr, wr, None, gr, caches_r, dyr, need[7], need[8], False, dw_sink=True)
+            if handoff is not None and dxr is not None:
+                GRAD_STASH[handoff] = dxr
+                dxr = None
         elif res is not None and need[6]:
             dres = dz
+            if handoff is not None:
+                GRAD_STASH[handoff] = dz
+                dres = None
         # gamma/beta (and the MFMA conv weights) were accumulated in place (grad_sink)
         flush_sinks()
         return dx, dx2, dw, db, None, None, dres, dxr, dwr, None, None, None
@@ -947,7 +980,17 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
     else:
         xr = wr = gamma_r = beta_r = None
         gr = caches_r = bn_r = None
-    spec = (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act)
+    key = handoff = None
+    if SHORTCUT_HANDOFF and in_ss is None and torch.is_grad_enabled():
+        key = next(_GKEYS)
+        sc = xr if xr is not None else res
+        # the shortcut input is another conv_bn_act's output whose only shortcut consumer is this one: its
+        # gradient is handed to that producer's backward instead of going through an autograd add
+        if (sc is not None and sc.requires_grad and getattr(sc, "_dmf_gkey", None) is not None
+                and not getattr(sc, "_dmf_gclaimed", False)):
+            handoff = sc._dmf_gkey
+            sc._dmf_gclaimed = True
+    spec = (g, caches, bn, act, p, rng, site, gr, caches_r, bn_r, unbias_mult, in_ss, in_act, key, handoff)
     if in_ss is not None:
         # forward-only form: x is the producer's raw conv output, its BN apply
         # + activation run inside this conv's loads
@@ -956,7 +999,20 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
         with torch.no_grad():
             return _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r,
                                       beta_r, spec)
-    return _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r, beta_r, spec)
+    out = _ConvBNActFn.apply(x, x2, conv.weight, conv.bias, bn.weight, bn.bias, res, xr, wr, gamma_r, beta_r, spec)
+    if key is not None:
+        out._dmf_gkey = key
+    return out
+
+
+# Shortcut-gradient hand-off (mode B backward): a Bottleneck's shortcut gradient (dz of its last
+# conv_bn_act, or the projection's input gradient) is parked here under the key of the conv_bn_act
+# that produced the block input; that producer's backward sums it with the gradient autograd hands
+# it inside dmf_act_bwd_bn_reduce(_acc) (dy2), so the block input's gradient is never formed by a
+# separate bf16 add pass. DMF_SHORTCUT_HANDOFF=0 restores the autograd add.
+SHORTCUT_HANDOFF = os.environ.get("DMF_SHORTCUT_HANDOFF", "1") == "1"
+GRAD_STASH = {}
+_GKEYS = itertools.count(1)
 
 
 def conv_bn_stats(x, conv, caches, bn, in_ss=None, in_act="none", x2=None, unbias_mult=1):

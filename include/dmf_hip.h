@@ -213,8 +213,12 @@ int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void* x, int ldx
  * y = drop(act(x*scale_shift + residual)) written once, plus the BN column
  * partials [dmf_bn_bwd_tiles(M)][C][2] of x (the BN input) with the saved
  * (mean, invstd); ResNetLite/Bottleneck conv->BN->act backward
- * (model_module.py:259-280, timm Bottleneck) */
-int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+ * (model_module.py:259-280, timm Bottleneck). dy2 (may be null; then lddy2
+ * is ignored): a second gradient of the same output, summed with dy in fp32
+ * -- the next Bottleneck's shortcut gradient, handed over by that block's
+ * backward instead of an autograd add pass (needs 8-channel vectors). */
+int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* dy2, int lddy2, const void* x, int ldx,
+                          const float* scale_shift,
                           const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
                           const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz, int lddz,
                           long long M, int C, float* partials, void* stream);
@@ -224,7 +228,8 @@ int dmf_act_bwd_bn_reduce(int dtype, const void* dy, int lddy, const void* x, in
  * block (dgamma / dbeta added once) -- the backward of conv -> BatchNorm2d ->
  * act of timm Bottleneck / BackboneAdapter (foundation_model.py:260-267,
  * model_module.py:440-447). C and strides multiples of 8. */
-int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* scale_shift,
+int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* dy2, int lddy2, const void* x, int ldx,
+                              const float* scale_shift,
                               const void* res, int ldr, const float* res_scale_shift, int act, float dropout_p,
                               const unsigned long long* rng, int site, const float* save_mean_invstd, void* dz,
                               int lddz, long long M, int C, double* acc, int replicas, void* stream);

@@ -163,14 +163,18 @@ def test_trainer_16_mixed_bf16_gradients_and_overflow_skip():
     rel = ((db - da).norm() / da.norm()).item()
     print(f"16-mixed vs bf16-mixed, encoder parameter updates after 3 bf16 steps: relative L2 {rel:.2e}")
     assert da.norm() > 0 and rel < 5e-2, rel
-    # (2) overflow injection into the captured step
+    # (2) a non-finite gradient inside the captured step: a huge scale plus one NaN input voxel (whether
+    # 2^127 alone overflows depends on where the backward rounds to bf16 -- the fused shortcut-gradient
+    # sums in fp32 keep some products finite that a bf16 add pass overflowed)
     counts = tr_b.opt.step_counts()
     with torch.no_grad():
         tr_b.scaler.amp[0] = 2.0 ** 127
     before = {n: p.detach().clone() for n, p in lm_b.named_parameters()}
     moments = {id(t): t.clone() for st in tr_b.opt.state.values() for t in st.values() if torch.is_tensor(t)
                and t.is_cuda}
-    tr_b.step(batches[3])
+    bad = [t.clone() if torch.is_tensor(t) else t for t in batches[3]]
+    bad[0].view(-1)[0] = float("nan")
+    tr_b.step(type(batches[3])(bad) if isinstance(batches[3], tuple) else bad)
     torch.cuda.synchronize()
     assert tr_b.scaler.get_scale() == 2.0 ** 126
     for n, p in lm_b.named_parameters():

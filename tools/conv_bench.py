@@ -32,6 +32,7 @@ SHAPES = [
     ((32, 64, 64, 64, 256, 1, 1, 1), 8),
     ((32, 64, 64, 64, 64, 3, 1, 1), 6),
     ((32, 256, 256, 16, 64, 7, 2, 1), 1),
+    ((32, 256, 256, 8, 64, 7, 2, 1), 1),
     ((32, 32, 32, 64, 64, 1, 1, 1), 9),
 ]
 
