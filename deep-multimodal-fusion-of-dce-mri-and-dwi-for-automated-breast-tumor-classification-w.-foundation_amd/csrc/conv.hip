@@ -1312,6 +1312,8 @@ static int g_pp_mode = 1;
 static int g_p2_mode = 0;
 // 10 = the dedicated 7x7 stem kernel (conv_stem.hip) on (1, default) / off
 static int g_stem_enable = 1;
+// 11 = the statistics epilogue without bias adds / row masks for whole-tile launches (EPI 5) on / off
+static int g_fast_epi = 1;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
@@ -1489,15 +1491,17 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     else DMF_CONV_LAUNCH(float, true, -1);
   } else if (plan.pp) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const int epi = a.partials != nullptr ? 0 : 1 + a.act;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
+    // statistics without bias over whole tiles: the fast epilogue (EPI 5)
+    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
+    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st);
   } else if (plan.p2) {
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 gp((unsigned)std::min<long long>(nblk, 2LL * cu_count())), bq(256);
-    const int epi = a.partials != nullptr ? 0 : 1 + a.act;
+    // statistics without bias over whole tiles: the fast epilogue (EPI 5)
+    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 128 == 0) ? 5 : 0) : 1 + a.act;
     a.dbg = g_ps_dbg;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
+    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
 #define DMF_P2(E)                                                                                                \
   do {                                                                                                           \
     if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E, 128, 128, 2>), gp, bq, lds_total, st, a); \
@@ -1509,6 +1513,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
       case 1: DMF_P2(1); break;
       case 2: DMF_P2(2); break;
       case 3: DMF_P2(3); break;
+      case 5: DMF_P2(5); break;
       default: DMF_P2(4); break;
     }
 #undef DMF_P2
@@ -1516,9 +1521,10 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
-    const int epi = a.partials != nullptr ? 0 : 1 + a.act;
+    // statistics without bias over whole tiles: the fast epilogue (EPI 5)
+    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
     a.dbg = g_ps_dbg;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 4, "%s: activation %d", what, a.act);
+    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
 #define DMF_PS(E)                                                                                      \
   do {                                                                                                 \
     if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E>), gp, bq, lds_total, st, a);  \
@@ -1530,6 +1536,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
       case 1: DMF_PS(1); break;
       case 2: DMF_PS(2); break;
       case 3: DMF_PS(3); break;
+      case 5: DMF_PS(5); break;
       default: DMF_PS(4); break;
     }
 #undef DMF_PS
@@ -1751,6 +1758,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 8: return conv_pp_tune(value != 0);
     case 9: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: two-workgroup mode %d", value); g_p2_mode = value; return 0;
     case 10: g_stem_enable = value != 0; return 0;
+    case 11: g_fast_epi = value != 0; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

@@ -203,29 +203,34 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
   const int m0 = mt * TBM, n0 = nt * TBN;
   const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
-  constexpr bool stats = EPI == 0;
+  // EPI 0: BN statistics; EPI 5: the same for a launch without bias whose M is a multiple of the tile
+  // height (every row in range: no bias adds, no row masks -- half the VALU of EPI 0)
+  constexpr bool stats = EPI == 0 || EPI == 5, fast = EPI == 5;
   float bsv[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) bsv[e] = a.bias ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
+  for (int e = 0; e < 16; ++e) bsv[e] = (!fast && a.bias) ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
   float s[16], q[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
-    const bool ok = m < a.M;
+    const bool ok = fast || m < a.M;
     float v[16];
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = acc[i][j][r] + bsv[j * 4 + r];
-    if (stats) {
+      for (int r = 0; r < 4; ++r) v[j * 4 + r] = fast ? acc[i][j][r] : acc[i][j][r] + bsv[j * 4 + r];
+    if (fast) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { s[e] += v[e]; q[e] = __builtin_fmaf(v[e], v[e], q[e]); }
+    } else if (stats) {
       const float w = ok ? 1.f : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
-    } else if constexpr (EPI > 1) {
+    } else if constexpr (EPI > 1 && EPI < 5) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = apply_act<EPI - 1>(v[e]);
+      for (int e = 0; e < 16; ++e) v[e] = apply_act<(EPI < 5 ? EPI - 1 : 0)>(v[e]);
     }
     uint32_t w8[8];
 #pragma unroll

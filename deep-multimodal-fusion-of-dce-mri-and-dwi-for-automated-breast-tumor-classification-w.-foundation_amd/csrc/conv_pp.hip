@@ -330,6 +330,7 @@ int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_
     case 1: DMF_PP(1); break;
     case 2: DMF_PP(2); break;
     case 3: DMF_PP(3); break;
+    case 5: DMF_PP(5); break;
     default: DMF_PP(4); break;
   }
 #undef DMF_PP
