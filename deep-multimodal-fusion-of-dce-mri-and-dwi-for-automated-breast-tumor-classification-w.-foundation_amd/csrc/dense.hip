@@ -629,6 +629,79 @@ __global__ void k_gate_bwd(const float* __restrict__ pa, const float* __restrict
   }
 }
 
+
+// ------------------------------------------------ SE / excitation MLP, one launch
+// The whole excitation of an SEBlock (model_module.py:25-43) or of the input
+// modality attention for ONE batch row per workgroup: pooled = scale * sum of
+// the S partial planes ws[z][n][:] (the squeeze's stage-1 sums, or S = 1 /
+// scale = 1 for a finished pool), hpre = pooled W1^T + b1, hact = gelu(hpre),
+// gate = sigmoid(hact W2^T + b2). Replaces squeeze-finish + 2 x (GEMM + split
+// reduce + activation) = 6 latency-bound launches. Each wave computes 4
+// outputs at a time: the 64 lanes stride the input vector (float4 loads of the
+// weight rows when K % 4 == 0), a wave sum per output. fp32 throughout.
+template <int ACT>
+__device__ __forceinline__ void se_layer(const float* __restrict__ W, const float* __restrict__ b,
+                                         const float* vin, int K, int J, float* __restrict__ pre_out,
+                                         float* act_lds, float* __restrict__ act_out, int n) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const bool v4 = (K & 3) == 0;
+  for (int j0 = wv * 4; j0 < J; j0 += nw * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (v4) {
+      for (int i = lane * 4; i < K; i += 256) {
+        const float4 x = *(const float4*)(vin + i);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j0 + u < J) {
+            const float4 w = *(const float4*)(W + (size_t)(j0 + u) * K + i);
+            acc[u] = fmaf(w.x, x.x, fmaf(w.y, x.y, fmaf(w.z, x.z, fmaf(w.w, x.w, acc[u]))));
+          }
+        }
+      }
+    } else {
+      for (int i = lane; i < K; i += 64) {
+        const float x = vin[i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (j0 + u < J) acc[u] = fmaf(W[(size_t)(j0 + u) * K + i], x, acc[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float z = wave_sum(acc[u]) + ((b && j0 + u < J) ? b[j0 + u] : 0.f);
+      if (lane == 0 && j0 + u < J) {
+        const float a = ACT == DMF_ACT_GELU ? gelu_f(z) : sigmoid_f(z);
+        if (pre_out) pre_out[(size_t)n * J + j0 + u] = z;
+        if (act_lds) act_lds[j0 + u] = a;
+        act_out[(size_t)n * J + j0 + u] = a;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(512) k_se_mlp(const float* __restrict__ ws, int S, int N, int C, float scale,
+                                                const float* __restrict__ w1, const float* __restrict__ b1, int mid,
+                                                const float* __restrict__ w2, const float* __restrict__ b2,
+                                                float* __restrict__ pooled, float* __restrict__ hpre,
+                                                float* __restrict__ hact, float* __restrict__ gate) {
+  extern __shared__ __attribute__((aligned(16))) float se_lds[];
+  float* pv = se_lds;                 // [C] pooled vector (padded to 4)
+  float* hv = se_lds + ((C + 3) & ~3);  // [mid] hidden activations
+  const int n = blockIdx.x;
+  const size_t plane = (size_t)N * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += ws[(size_t)z * plane + (size_t)n * C + c];
+    v *= scale;
+    pv[c] = v;
+    if (pooled) pooled[(size_t)n * C + c] = v;
+  }
+  __syncthreads();
+  se_layer<DMF_ACT_GELU>(w1, b1, pv, C, mid, hpre, hv, hact, n);
+  __syncthreads();
+  se_layer<DMF_ACT_SIGMOID>(w2, b2, hv, mid, C, nullptr, nullptr, gate, n);
+}
+
 }  // namespace dmf
 
 using namespace dmf;
@@ -872,5 +945,19 @@ extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const floa
   hipLaunchKernelGGL(k_gate_bwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pv_dwi, pv_dce, conf_dwi, conf_dce, C, W,
                      gates, dgates, dW, db, dpv_dwi, dpv_dce, dconf_dwi, dconf_dce);
   DMF_LAUNCH_CHECK("dmf_gate_bwd");
+  return 0;
+}
+
+extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1,
+                          int mid, const float* w2, const float* b2, float* pooled, float* hpre, float* hact,
+                          float* gate, void* stream) {
+  DMF_CHECK_ARG(ws && w1 && w2 && hact && gate && S >= 1 && N >= 1 && C >= 1 && mid >= 1 && C <= 16384 &&
+                    mid <= 16384,
+                "dmf_se_mlp: bad args");
+  DMF_CHECK_ARG(((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0, "dmf_se_mlp: weights must be 16-B aligned");
+  const size_t lds = (size_t)(((C + 3) & ~3) + mid) * sizeof(float);
+  hipLaunchKernelGGL(k_se_mlp, dim3(N), dim3(512), lds, (hipStream_t)stream, ws, S, N, C, scale, w1, b1, mid, w2, b2,
+                     pooled, hpre, hact, gate);
+  DMF_LAUNCH_CHECK("dmf_se_mlp");
   return 0;
 }

@@ -477,6 +477,48 @@ __global__ void k_col_stats(const T* __restrict__ x, int ldx, long long M, int C
                     red[0][cl][1] + red[1][cl][1] + red[2][cl][1] + red[3][cl][1]);
 }
 
+// the same partials from 8-channel vectors (16-B bf16 loads): block = CVt
+// channel vectors x R = 256 / CVt row lanes over one 256-row tile, every
+// thread's rows in flight together (the scalar form issued one 2-B load per
+// row and channel: ~20 us for a 32k x 64 map)
+template <typename T>
+__global__ void __launch_bounds__(256) k_col_stats8(const T* __restrict__ x, int ldx, long long M, int C, int CVt,
+                                                    float* __restrict__ part) {
+  __shared__ float red[256 * 16];
+  const int R = 256 / CVt;
+  const int cvl = threadIdx.x % CVt, rl = threadIdx.x / CVt;
+  const int cv = blockIdx.y * CVt + cvl;
+  const long long r0 = (long long)blockIdx.x * 256;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  if (cv * 8 < C) {
+#pragma unroll 4
+    for (int r = rl; r < 256; r += R) {
+      const long long m = r0 + r;
+      if (m < M) {
+        float v[8];
+        ld8(x + m * ldx + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] += v[j]; q[j] = fmaf(v[j], v[j], q[j]); }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x * 16 + j] = s[j]; red[threadIdx.x * 16 + 8 + j] = q[j]; }
+  __syncthreads();
+  for (int t = threadIdx.x; t < CVt * 8; t += 256) {
+    const int v = t >> 3, j = t & 7;
+    float ss = 0.f, qq = 0.f;
+    for (int r = 0; r < R; ++r) {
+      ss += red[(r * CVt + v) * 16 + j];
+      qq += red[(r * CVt + v) * 16 + 8 + j];
+    }
+    const int c = (blockIdx.y * CVt + v) * 8 + j;
+    if (c < C) *(float2*)(part + ((size_t)blockIdx.x * C + c) * 2) = make_float2(ss, qq);
+  }
+}
+
 // ------------------------------------------ mask-guided spatial attention
 // mask m[n][p] (single channel, already at the feature resolution)
 // h[c] = w1[c]*m ; GroupNorm(1,16) over (c,p) per sample: mean = mean(w1)*mean(m),
@@ -896,6 +938,13 @@ static void nhwc_reduce_plan(int N, int HW, int C, int& CVt, int& groups, int& S
   S = cdiv(HW, rpb);
 }
 
+extern "C" int dmf_nhwc_reduce_splits(int N, int HW, int C) {
+  if (C % 8 != 0) return 0;
+  int CVt, groups, S, rpb;
+  nhwc_reduce_plan(N, HW, C, CVt, groups, S, rpb);
+  return S;
+}
+
 extern "C" int dmf_nhwc_reduce_ws_size(int N, int HW, int C) {
   if (C % 8 != 0) return 0;
   int CVt, groups, S, rpb;
@@ -906,7 +955,9 @@ extern "C" int dmf_nhwc_reduce_ws_size(int N, int HW, int C) {
 extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C,
                                float scale, float* out, float* out_sq, int accumulate, float* workspace,
                                void* stream) {
-  DMF_CHECK_ARG(a && out && N > 0 && HW > 0 && C > 0, "dmf_nhwc_reduce: bad args");
+  DMF_CHECK_ARG(a && (out || workspace) && N > 0 && HW > 0 && C > 0, "dmf_nhwc_reduce: bad args");
+  DMF_CHECK_ARG(out || (v8ok(C, lda, b ? ldb : 8, a, b) && !out_sq),
+                "dmf_nhwc_reduce: the stage-1-only form (out == NULL) needs the 8-channel vector layout");
   DMF_CHECK_ARG(!(b && out_sq), "dmf_nhwc_reduce: out_sq is for the plain (b == NULL) form");
   hipStream_t st = (hipStream_t)stream;
   if (workspace && v8ok(C, lda, b ? ldb : 8, a, b)) {
@@ -920,6 +971,10 @@ extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b,
       hipLaunchKernelGGL(k_nhwc_reduce8<float>, g8, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, HW,
                          C, CVt, rpb, out_sq ? 1 : 0, workspace);
     const long long nc = (long long)N * C;
+    if (!out) {  // stage 1 only: the consumer (dmf_se_mlp) sums the S partial planes itself
+      DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
+      return 0;
+    }
     hipLaunchKernelGGL(k_nhwc_reduce_fin, dim3(gsz(nc * (out_sq ? 2 : 1))), dim3(256), 0, st, workspace, S, nc, scale,
                        out, out_sq, accumulate);
     DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
@@ -1194,6 +1249,19 @@ extern "C" int dmf_col_stats_tiles(long long M) { return (int)((M + 255) / 256);
 
 extern "C" int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream) {
   DMF_CHECK_ARG(x && partials && M > 0 && C > 0, "dmf_col_stats: bad args");
+  const int es = dtype == DMF_BF16 ? 2 : 4;
+  if (C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % (8 * es)) == 0) {
+    const int CVt = std::min(32, C / 8);
+    dim3 g8((unsigned)((M + 255) / 256), (unsigned)cdiv(C / 8, CVt));
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_col_stats8<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, C, CVt,
+                         partials);
+    else
+      hipLaunchKernelGGL(k_col_stats8<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, M, C, CVt,
+                         partials);
+    DMF_LAUNCH_CHECK("dmf_col_stats");
+    return 0;
+  }
   dim3 grid((unsigned)((M + 255) / 256), (unsigned)cdiv(C, 64));
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_col_stats<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, C,

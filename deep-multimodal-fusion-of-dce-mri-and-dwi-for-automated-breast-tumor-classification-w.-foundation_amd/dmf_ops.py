@@ -1152,24 +1152,47 @@ def linear(x, w, b=None, act="none"):
 
 
 # --------------------------------------------------------------------- SE
+def excite_mlp(src, splits, scale, w1, b1, w2, b2, keep=True):
+    """gate = sigmoid(gelu(pooled w1^T + b1) w2^T + b2) with pooled = scale *
+    sum of ``splits`` partial planes [S][N][C] in ``src`` (dmf_se_mlp, one
+    launch). Returns (pooled, hpre, hact, gate) fp32 [N][*]; pooled / hpre are
+    None unless ``keep`` (what a backward needs)."""
+    mid, c = w1.shape
+    n = src.numel() // (splits * c)
+    dev = src.device
+    w1c, w2c = w1.contiguous().float(), w2.contiguous().float()
+    pooled = torch.empty((n, c), dtype=torch.float32, device=dev) if keep else None
+    hpre = torch.empty((n, mid), dtype=torch.float32, device=dev) if keep else None
+    hact = torch.empty((n, mid), dtype=torch.float32, device=dev)
+    gate = torch.empty((n, c), dtype=torch.float32, device=dev)
+    N.call("dmf_se_mlp", src.data_ptr(), splits, n, c, float(scale), w1c.data_ptr(), _p(b1), mid, w2c.data_ptr(),
+           _p(b2), _p(pooled), _p(hpre), hact.data_ptr(), gate.data_ptr(), _stream())
+    return pooled, hpre, hact, gate
+
+
+def se_excite(x, w1, b1, w2, b2, keep=True):
+    """SEBlock squeeze + excitation of an NHWC map: the squeeze's stage-1
+    partial sums feed dmf_se_mlp directly (no finish pass)."""
+    n, c, h, w, ld = nhwc(x)
+    s = N.load().dmf_nhwc_reduce_splits(n, h * w, c)
+    if s > 0 and ld % 8 == 0 and x.data_ptr() % 16 == 0:
+        ws = torch.empty((s, n, c), dtype=torch.float32, device=x.device)
+        N.call("dmf_nhwc_reduce", dt(x), x.data_ptr(), ld, None, 0, n, h * w, c, 1.0, None, None, 0, ws.data_ptr(),
+               _stream())
+        return excite_mlp(ws, s, 1.0 / (h * w), w1, b1, w2, b2, keep)
+    return excite_mlp(spatial_mean(x), 1, 1.0, w1, b1, w2, b2, keep)
+
+
 class _SEFn(torch.autograd.Function):
     """SEBlock (model_module.py:25-43) on an NHWC map: returns (x*w, w)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
         n, c, h, w, ld = nhwc(x)
-        pooled = spatial_mean(x)
         mid = w1.shape[0]
-        hpre = torch.empty((n, mid), dtype=torch.float32, device=x.device)
-        _sgemm(0, 1, n, mid, c, 1.0, pooled.data_ptr(), c, w1.detach().reshape(mid, c).contiguous()
-               .data_ptr(), c, 0.0, hpre.data_ptr(), mid, _p(b1), N.ACT_NONE, _stream())
-        hact = torch.empty_like(hpre)
-        _act_f32(hpre, hact, "gelu")
-        z2 = torch.empty((n, c), dtype=torch.float32, device=x.device)
-        _sgemm(0, 1, n, c, mid, 1.0, hact.data_ptr(), mid, w2.detach().reshape(c, mid).contiguous()
-               .data_ptr(), mid, 0.0, z2.data_ptr(), c, _p(b2), N.ACT_NONE, _stream())
-        gate = torch.empty_like(z2)
-        _act_f32(z2, gate, "sigmoid")
+        # squeeze (stage-1 partial sums) + the whole excitation MLP in one launch
+        pooled, hpre, hact, gate = se_excite(x, w1.detach().reshape(mid, c), b1, w2.detach().reshape(c, mid), b2,
+                                             keep=any(ctx.needs_input_grad))
         y = empty_nhwc(n, c, h, w, x.dtype, x.device)
         N.call("dmf_channel_scale", dt(x), x.data_ptr(), ld, gate.data_ptr(), y.data_ptr(), nhwc(y)[4], n, h * w, c,
                _stream())

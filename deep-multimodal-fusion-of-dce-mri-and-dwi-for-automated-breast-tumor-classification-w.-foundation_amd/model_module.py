@@ -492,8 +492,13 @@ class ModelMaskHeadBackbone(nn.Module):
         if self.modality_attention is not None:
             fc = self.modality_attention.fc
             pooled = O.nchw_mean(x)
-            hmid = O.linear(pooled, fc[1].weight, fc[1].bias, act="gelu")
-            gate = O.linear(hmid, fc[3].weight, fc[3].bias, act="sigmoid")
+            if O.needs_grad(fc[1].weight, fc[1].bias, fc[3].weight, fc[3].bias):
+                hmid = O.linear(pooled, fc[1].weight, fc[1].bias, act="gelu")
+                gate = O.linear(hmid, fc[3].weight, fc[3].bias, act="sigmoid")
+            else:  # frozen encoder: the excitation MLP in one launch
+                c, mid = pooled.shape[1], fc[1].weight.shape[0]
+                gate = O.excite_mlp(pooled, 1, 1.0, fc[1].weight.detach().reshape(mid, c), fc[1].bias,
+                                    fc[3].weight.detach().reshape(c, mid), fc[3].bias, keep=False)[3]
             x_in, _ = O.input_stage(x, dt, gate)
             return x_in, gate.view(gate.shape[0], gate.shape[1], 1, 1)
         x_in, _ = O.input_stage(x, dt, None)

@@ -249,8 +249,12 @@ int dmf_nchw_mean(const float* x, int NC, long long HW, float* out, void* stream
 /* out[n][c] (+)= scale * sum_hw a*(b or 1); out_sq (nullable, b == NULL only)
  * also gets scale * sum_hw a^2 in the same pass. workspace (nullable):
  * dmf_nhwc_reduce_ws_size(N, HW, C) floats enable the chip-wide split form
- * (partials + ordered combine, deterministic). */
+ * (partials + ordered combine, deterministic). out == NULL (vector layout,
+ * no out_sq): stage 1 only -- workspace receives dmf_nhwc_reduce_splits(N,
+ * HW, C) partial planes [S][N][C] (unscaled) for a consumer that sums them
+ * (dmf_se_mlp). */
 int dmf_nhwc_reduce_ws_size(int N, int HW, int C);
+int dmf_nhwc_reduce_splits(int N, int HW, int C);
 int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b, int ldb, int N, int HW, int C, float scale,
                     float* out, float* out_sq, int accumulate, float* workspace, void* stream);
 int dmf_channel_scale(int dtype, const void* x, int ldx, const float* gate, void* y, int ldy, int N, int HW, int C,
@@ -322,6 +326,14 @@ int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumu
 int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
 int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream);
 int dmf_sig_grad_f32(const float* dg, const float* s, float* dz, long long n, void* stream);
+/* SEBlock excitation in one launch (model_module.py:25-43; the modality
+ * attention of :584-591): pooled[n] = scale * sum_z ws[z][n][:] over S partial
+ * planes of [N][C] (dmf_nhwc_reduce's stage-1 layout; S = 1, scale = 1 for a
+ * finished pool), hpre = pooled w1^T + b1 ([mid][C]), hact = gelu(hpre),
+ * gate = sigmoid(hact w2^T + b2) ([C][mid]). pooled / hpre / b1 / b2 nullable;
+ * weights 16-B aligned. */
+int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1, int mid,
+               const float* w2, const float* b2, float* pooled, float* hpre, float* hact, float* gate, void* stream);
 int dmf_row_l2norm(const float* x, int R, int C, float eps, float* y, float* norms, void* stream);
 int dmf_row_l2norm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float eps, float* dx,
                        void* stream);

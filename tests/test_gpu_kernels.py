@@ -383,6 +383,44 @@ def test_se_block_grads():
     assert torch.allclose(sed.fc[1].weight.grad.cpu(), ref_g1, atol=1e-5, rtol=1e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(32, 512, 32, 32), (5, 128, 16, 16), (3, 14, 9, 7), (2, 6, 4, 4)])
+def test_se_excite_one_launch_matches_torch(shape, dtype):
+    """dmf_se_mlp (squeeze partials -> fc1 -> GELU -> fc2 -> sigmoid in one launch)
+    against torch fp32, with grad off (the frozen-encoder path) and on (its saved
+    pooled / hpre / hact feed the SE backward)."""
+    import model_module as MM
+
+    n, c, h, w = shape
+    torch.manual_seed(11)
+    se = MM.SEBlock(c, 2)
+    MM.set_compute_dtype(se, dtype)
+    x = torch.randn(n, c, h, w)
+    xq = x.to(dtype).float()  # the input the kernel sees
+    fc = se.fc
+    pooled = xq.mean((2, 3))
+    hpre = F.linear(pooled, fc[1].weight.flatten(1), fc[1].bias)
+    gate = torch.sigmoid(F.linear(F.gelu(hpre), fc[3].weight.flatten(1), fc[3].bias))
+    sed = copy.deepcopy(se).to(DEV)
+    xd = _to_dev(x, dtype)
+    mid = fc[1].weight.shape[0]
+    with torch.no_grad():
+        p, hp, ha, g = O.se_excite(xd, sed.fc[1].weight.reshape(mid, c), sed.fc[1].bias, sed.fc[3].weight.reshape(c, mid),
+                                   sed.fc[3].bias, keep=True)
+        y, wg = sed(xd)
+    torch.testing.assert_close(p.cpu(), pooled, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(hp.cpu(), hpre, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(ha.cpu(), F.gelu(hpre), atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(g.cpu(), gate, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(wg.reshape(n, c).cpu(), gate, atol=2e-5, rtol=1e-4)
+    rt = 2e-5 if dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(y.float().cpu(), (xq * gate[:, :, None, None]), atol=rt, rtol=rt)
+    # modality-attention form: a finished pool (S = 1) through the same kernel
+    g1 = O.excite_mlp(pooled.to(DEV), 1, 1.0, sed.fc[1].weight.reshape(mid, c), sed.fc[1].bias,
+                      sed.fc[3].weight.reshape(c, mid), sed.fc[3].bias, keep=False)[3]
+    torch.testing.assert_close(g1.cpu(), gate, atol=2e-5, rtol=1e-4)
+
+
 def test_mask_attention_fwd_bwd():
     torch.manual_seed(7)
     import model_module as MM
@@ -585,3 +623,22 @@ def test_conv_fused_input_affine(dtype, shape):
     assert err <= atol * 4 + rtol * ref.abs().max().item(), err
     assert torch.allclose(bns[1].running_mean.cpu(), b2.running_mean, rtol=1e-3,
                           atol=1e-4 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(32, 64, 32, 32), (3, 24, 7, 9), (2, 520, 5, 6), (1, 3, 4, 4)])
+def test_col_stats_partials(shape, dtype):
+    """dmf_col_stats (vector and scalar forms): per-256-row-tile column (sum, sum^2)."""
+    n, c, h, w = shape
+    torch.manual_seed(12)
+    x = torch.randn(n, c, h, w)
+    xd = _to_dev(x, dtype)
+    part = O._col_stats(xd).cpu().double()
+    xr = xd.float().cpu().permute(0, 2, 3, 1).reshape(-1, c).double()
+    m = xr.shape[0]
+    tiles = (m + 255) // 256
+    assert part.shape == (tiles, c, 2)
+    for t in range(tiles):
+        blk = xr[t * 256:(t + 1) * 256]
+        torch.testing.assert_close(part[t, :, 0], blk.sum(0), atol=1e-3, rtol=1e-4)
+        torch.testing.assert_close(part[t, :, 1], (blk * blk).sum(0), atol=1e-3, rtol=1e-4)
