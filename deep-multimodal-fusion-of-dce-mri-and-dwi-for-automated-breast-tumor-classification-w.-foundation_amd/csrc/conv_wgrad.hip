@@ -628,6 +628,48 @@ __global__ void k_conv_cout1_dgrad(const T* __restrict__ dy, int lddy, const flo
   }
 }
 
+// 8-channel vector form of the same: thread = one pixel x 8 input channels,
+// 32-bit index math (the scalar form's 64-bit divisions per element cost
+// ~50 us on a 32k x 128 map), the 8 weights of every tap from L1
+template <typename T>
+__global__ void __launch_bounds__(256) k_conv_cout1_dgrad8(const T* __restrict__ dy, int lddy,
+                                                           const float* __restrict__ w, int N, int H, int W, int Cin,
+                                                           int KH, int KW, int stride, int pad, int dil, int Ho, int Wo,
+                                                           T* __restrict__ dx, int lddx) {
+  const int CV = Cin >> 3;
+  const int total = N * H * W * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV, pix = i / CV;
+    const int n = pix / (H * W), rem = pix - n * (H * W);
+    const int h = rem / W, wq = rem - (rem / W) * W;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < KH; ++r) {
+      const int hn = h + pad - r * dil;
+      if (hn < 0 || hn % stride) continue;
+      const int ho = hn / stride;
+      if (ho >= Ho) continue;
+      for (int s2 = 0; s2 < KW; ++s2) {
+        const int wn = wq + pad - s2 * dil;
+        if (wn < 0 || wn % stride) continue;
+        const int wo = wn / stride;
+        if (wo >= Wo) continue;
+        const float g = ld(dy + ((n * Ho + ho) * Wo + wo) * lddy);
+        const float4* wp = (const float4*)(w + (r * KW + s2) * Cin + cv * 8);
+        const float4 a = wp[0], b = wp[1];
+        acc[0] = fmaf(g, a.x, acc[0]);
+        acc[1] = fmaf(g, a.y, acc[1]);
+        acc[2] = fmaf(g, a.z, acc[2]);
+        acc[3] = fmaf(g, a.w, acc[3]);
+        acc[4] = fmaf(g, b.x, acc[4]);
+        acc[5] = fmaf(g, b.y, acc[5]);
+        acc[6] = fmaf(g, b.z, acc[6]);
+        acc[7] = fmaf(g, b.w, acc[7]);
+      }
+    }
+    st8(dx + (size_t)pix * lddx + cv * 8, acc);
+  }
+}
+
 // dw[(r,s,ci)] partial over a pixel chunk: block = (tap-chunk of 256 columns, split)
 template <typename T>
 __global__ void k_conv_cout1_wgrad(const T* __restrict__ x, int N, int H, int W, int Cin, int ldx,
@@ -702,6 +744,91 @@ __global__ void __launch_bounds__(256) k_conv_cout1_wgrad8(const T* __restrict__
     *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
   if (dbias_ws && blockIdx.x == 0 && threadIdx.x == 0) dbias_ws[blockIdx.y] = accb;
+}
+
+// pixel-lane form for 1-output-channel weight gradients: block = CVt 8-channel
+// slices (of all KH*KW*Cin/8) x R = 256 / CVt pixel lanes, so a short K (a
+// 1x1 head over 64 channels: 8 slices) still fills the block; each split's
+// partial is reduced over the R lanes in LDS (fixed order). Writes
+// ws[split][K] and the bias partials wsb[split].
+template <typename T>
+__global__ void __launch_bounds__(256) k_conv_cout1_wgrad8r(const T* __restrict__ x, int N, int H, int W, int Cin,
+                                                            int ldx, const T* __restrict__ dy, int lddy, int KH, int KW,
+                                                            int stride, int pad, int dil, int Ho, int Wo, int ppsplit,
+                                                            int CVt, float* __restrict__ ws,
+                                                            float* __restrict__ dbias_ws) {
+  __shared__ float red[256 * 9];
+  const int CV = Cin >> 3;
+  const int KV = KH * KW * CV;
+  const int R = 256 / CVt;
+  const int cl = threadIdx.x % CVt, rl = threadIdx.x / CVt;
+  const int kv = blockIdx.x * CVt + cl;
+  const bool kok = kv < KV && rl < R;
+  const int tap = kok ? kv / CV : 0, cv = kv - tap * CV, r = tap / KW, s = tap - (tap / KW) * KW;
+  const int M = N * Ho * Wo;
+  const int p0 = blockIdx.y * ppsplit, p1 = min(M, p0 + ppsplit);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  if (rl < R) {
+#pragma unroll 2
+    for (int p = p0 + rl; p < p1; p += R) {
+      const int n = p / (Ho * Wo), rem = p - n * (Ho * Wo);
+      const int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+      const float g = ld(dy + p * lddy);
+      accb += g;
+      const int hi = ho * stride - pad + r * dil, wi = wo * stride - pad + s * dil;
+      if (kok && hi >= 0 && hi < H && wi >= 0 && wi < W) {
+        float v[8];
+        ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(g, v[j], acc[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 9 + j] = acc[j];
+  red[threadIdx.x * 9 + 8] = accb;
+  __syncthreads();
+  for (int t = threadIdx.x; t < CVt * 8; t += 256) {
+    const int c = t >> 3, j = t & 7;
+    float v = 0.f;
+    for (int q = 0; q < R; ++q) v += red[(q * CVt + c) * 9 + j];
+    if (blockIdx.x * CVt + c < KV) ws[(size_t)blockIdx.y * KV * 8 + (size_t)(blockIdx.x * CVt + c) * 8 + j] = v;
+  }
+  if (dbias_ws && blockIdx.x == 0 && threadIdx.x == 0) {
+    float v = 0.f;  // every pixel lane of the first slice saw its pixels' dy once
+    for (int q = 0; q < R; ++q) v += red[(q * CVt) * 9 + 8];
+    dbias_ws[blockIdx.y] = v;
+  }
+}
+
+// out[k] (+)= sum over splits of ws[s][k]: block = 64 columns x 16 split lanes,
+// 8 loads in flight per thread, the 16 lanes combined in LDS in a fixed order
+// (the one-thread-per-column form ran 40 us over 512 splits)
+__global__ void __launch_bounds__(1024) k_sum_splits16(const float* __restrict__ ws, int splits, int K,
+                                                       float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + c;
+  float v = 0.f;
+  if (k < K) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int s = q;
+    for (; s + 7 * 16 < splits; s += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += ws[(size_t)(s + u * 16) * K + k];
+    }
+    for (; s < splits; s += 16) a[0] += ws[(size_t)s * K + k];
+    v = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  }
+  red[q][c] = v;
+  __syncthreads();
+  if (q == 0 && k < K) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    out[k] = accumulate ? out[k] + t : t;
+  }
 }
 
 __global__ void k_sum_splits(const float* __restrict__ ws, int splits, int K, float* __restrict__ out, int accumulate) {
@@ -935,6 +1062,17 @@ extern "C" int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const f
   DMF_CHECK_ARG(dy && w && dx, "dmf_conv_cout1_dgrad: null pointer");
   const long long total = (long long)N * H * W * Cin;
   if (total == 0) return 0;
+  if (Cin % 8 == 0 && lddx % 8 == 0 && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)w % 16) == 0 && total < (1LL << 31)) {
+    const long long t8 = total / 8;
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_conv_cout1_dgrad8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (bf16_t*)dx, lddx);
+    else
+      hipLaunchKernelGGL(k_conv_cout1_dgrad8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (float*)dx, lddx);
+    DMF_LAUNCH_CHECK("dmf_conv_cout1_dgrad");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_conv_cout1_dgrad<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (bf16_t*)dx, lddx);
@@ -946,7 +1084,8 @@ extern "C" int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const f
 }
 
 extern "C" int dmf_conv_cout1_wgrad_splits(long long M) {
-  long long s = (M + 63) / 64;
+  // 128 pixels per split (the pixel-lane form walks them with 256 / CVt lanes), at most 512
+  long long s = (M + 127) / 128;
   if (s > 512) s = 512;
   return (int)(s < 1 ? 1 : s);
 }
@@ -961,14 +1100,17 @@ extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int 
   const int pps = (int)((M + splits - 1) / splits);
   dim3 grid(cdiv(K, 256), splits);
   float* wsb = workspace + (size_t)splits * K;
-  if (Cin % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0) {
-    const dim3 g8(cdiv(K / 8, 256), splits);
+  if (Cin % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0 && M < (1LL << 31)) {
+    const int KV = K / 8;
+    const int CVt = KV >= 64 ? 64 : (KV >= 32 ? 32 : (KV >= 16 ? 16 : (KV >= 8 ? 8 : (KV >= 4 ? 4 : (KV >= 2 ? 2 : 1)))));
+    const dim3 g8(cdiv(KV, CVt), splits);
     if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_conv_cout1_wgrad8<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
-                         W, Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+      hipLaunchKernelGGL(k_conv_cout1_wgrad8r<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
+                         W, Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, CVt, workspace,
+                         wsb);
     else
-      hipLaunchKernelGGL(k_conv_cout1_wgrad8<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
-                         Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+      hipLaunchKernelGGL(k_conv_cout1_wgrad8r<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
+                         Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, CVt, workspace, wsb);
   } else if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_conv_cout1_wgrad<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
                        Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
@@ -976,8 +1118,8 @@ extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int 
     hipLaunchKernelGGL(k_conv_cout1_wgrad<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
                        Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
   DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad");
-  if (dw) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, workspace, splits, K, dw, 1);
-  if (db) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, (hipStream_t)stream, wsb, splits, 1, db, 1);
+  if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(K, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, splits, K, dw, 1);
+  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(1), dim3(1024), 0, (hipStream_t)stream, wsb, splits, 1, db, 1);
   DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad(reduce)");
   return 0;
 }
@@ -1027,8 +1169,8 @@ extern "C" int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void
                        (const float*)dy, lddy, M, Cout, workspace, wsb);
   DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad");
   // reduce tiles: treat [tiles][Cout] as splits x K
-  if (dw) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(Cout, 256)), dim3(256), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1);
-  if (db) hipLaunchKernelGGL(k_sum_splits, dim3(cdiv(Cout, 256)), dim3(256), 0, (hipStream_t)stream, wsb, tiles, Cout, db, 1);
+  if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1);
+  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, wsb, tiles, Cout, db, 1);
   DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad(reduce)");
   return 0;
 }

@@ -111,8 +111,8 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
     }
 }
 
-__global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __restrict__ ws, float* __restrict__ C,
-                               int ldc, const float* __restrict__ bias, int act) {
+__global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __restrict__ ws, float beta,
+                               float* __restrict__ C, int ldc, const float* __restrict__ bias, int act) {
   const long long total = (long long)M * N;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -120,6 +120,7 @@ __global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __
     float v = 0.f;
     for (int z = 0; z < S; ++z) v += ws[(size_t)z * total + i];
     v *= alpha;
+    if (beta != 0.f) v += beta * C[(size_t)m * ldc + n];
     if (bias) v += bias[n];
     C[(size_t)m * ldc + n] = actf(act, v);
   }
@@ -630,76 +631,116 @@ __global__ void k_gate_bwd(const float* __restrict__ pa, const float* __restrict
 }
 
 
-// ------------------------------------------------ SE / excitation MLP, one launch
-// The whole excitation of an SEBlock (model_module.py:25-43) or of the input
-// modality attention for ONE batch row per workgroup: pooled = scale * sum of
-// the S partial planes ws[z][n][:] (the squeeze's stage-1 sums, or S = 1 /
-// scale = 1 for a finished pool), hpre = pooled W1^T + b1, hact = gelu(hpre),
-// gate = sigmoid(hact W2^T + b2). Replaces squeeze-finish + 2 x (GEMM + split
-// reduce + activation) = 6 latency-bound launches. Each wave computes 4
-// outputs at a time: the 64 lanes stride the input vector (float4 loads of the
-// weight rows when K % 4 == 0), a wave sum per output. fp32 throughout.
+// ------------------------------------------------ SE / excitation MLP
+// The excitation of an SEBlock (model_module.py:25-43) or of the input
+// modality attention: hpre = pooled W1^T + b1, hact = gelu(hpre), gate =
+// sigmoid(hact W2^T + b2), as two launches of one small dense-layer kernel
+// (was 2 x (GEMM + split reduce + activation)). Each wave owns ONE output
+// column j for every row: its weight row is held in registers (float4 slices,
+// lanes stride K), the block's input rows are staged once in LDS, and each
+// (row, j) dot product ends in one wave sum. Outputs are spread over J/4
+// workgroups so the weight rows stream from L2 in parallel (a one-workgroup-
+// per-row form ran ~57 us, latency-bound on its weight reads).
+constexpr int DR_LDS = 64 * 1024;  // input-row staging per block
+constexpr int DR_TMAX = 8;         // K <= 8 * 256
+
 template <int ACT>
-__device__ __forceinline__ void se_layer(const float* __restrict__ W, const float* __restrict__ b,
-                                         const float* vin, int K, int J, float* __restrict__ pre_out,
-                                         float* act_lds, float* __restrict__ act_out, int n) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+__global__ void __launch_bounds__(256) k_dense_rows(const float* __restrict__ in, int N, int K,
+                                                    const float* __restrict__ W, const float* __restrict__ b, int J,
+                                                    float* __restrict__ pre, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = blockIdx.x * 4 + wv;
+  const int K4 = (K + 3) & ~3;
+  const int T = (K4 + 255) / 256;
+  const int NC = max(1, min(N, DR_LDS / (K4 * 4)));
   const bool v4 = (K & 3) == 0;
-  for (int j0 = wv * 4; j0 < J; j0 += nw * 4) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (v4) {
-      for (int i = lane * 4; i < K; i += 256) {
-        const float4 x = *(const float4*)(vin + i);
+  float4 wr[DR_TMAX];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (j0 + u < J) {
-            const float4 w = *(const float4*)(W + (size_t)(j0 + u) * K + i);
-            acc[u] = fmaf(w.x, x.x, fmaf(w.y, x.y, fmaf(w.z, x.z, fmaf(w.w, x.w, acc[u]))));
+  for (int t = 0; t < DR_TMAX; ++t) {
+    const int k = lane * 4 + t * 256;
+    wr[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < T && j < J && k < K) {
+      if (v4) {
+        wr[t] = *(const float4*)(W + (size_t)j * K + k);
+      } else {
+        const float* wp = W + (size_t)j * K;
+        wr[t].x = wp[k];
+        if (k + 1 < K) wr[t].y = wp[k + 1];
+        if (k + 2 < K) wr[t].z = wp[k + 2];
+        if (k + 3 < K) wr[t].w = wp[k + 3];
+      }
+    }
+  }
+  const float bj = (b && j < J) ? b[j] : 0.f;
+  for (int n0 = 0; n0 < N; n0 += NC) {
+    const int nn = min(NC, N - n0);
+    __syncthreads();
+    if (v4) {
+      // all of a thread's staging loads in flight before its LDS stores (a load -> store
+      // chain per element serialises on the L2 latency)
+      const int kv = K >> 2, tot = nn * kv;
+      for (int e0 = 0; e0 < tot; e0 += 256 * 8) {
+        float4 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256 + threadIdx.x;
+          if (e < tot) {
+            const int r = e / kv, k = (e - r * kv) * 4;
+            t[u] = *(const float4*)(in + (size_t)(n0 + r) * K + k);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int e = e0 + u * 256 + threadIdx.x;
+          if (e < tot) {
+            const int r = e / kv, k = (e - r * kv) * 4;
+            *(float4*)(xs + r * K4 + k) = t[u];
           }
         }
       }
     } else {
-      for (int i = lane; i < K; i += 64) {
-        const float x = vin[i];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (j0 + u < J) acc[u] = fmaf(W[(size_t)(j0 + u) * K + i], x, acc[u]);
+      for (int e = threadIdx.x; e < nn * K4; e += 256) {
+        const int r = e / K4, k = e - r * K4;
+        xs[r * K4 + k] = k < K ? in[(size_t)(n0 + r) * K + k] : 0.f;
       }
     }
+    __syncthreads();
+    if (j >= J) continue;
+    for (int r0 = 0; r0 < nn; r0 += 4) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float z = wave_sum(acc[u]) + ((b && j0 + u < J) ? b[j0 + u] : 0.f);
-      if (lane == 0 && j0 + u < J) {
-        const float a = ACT == DMF_ACT_GELU ? gelu_f(z) : sigmoid_f(z);
-        if (pre_out) pre_out[(size_t)n * J + j0 + u] = z;
-        if (act_lds) act_lds[j0 + u] = a;
-        act_out[(size_t)n * J + j0 + u] = a;
+      for (int u = 0; u < 4; ++u) {
+        const int r = min(r0 + u, nn - 1);
+#pragma unroll
+        for (int t = 0; t < DR_TMAX; ++t) {
+          const int k = lane * 4 + t * 256;
+          if (t < T && k < K4) {
+            const float4 x = *(const float4*)(xs + r * K4 + k);
+            acc[u] = fmaf(wr[t].x, x.x, fmaf(wr[t].y, x.y, fmaf(wr[t].z, x.z, fmaf(wr[t].w, x.w, acc[u]))));
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = wave_sum(acc[u]);
+      if (lane < 4 && r0 + lane < nn) {
+        const float a = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
+        const float z = a + bj;
+        const size_t o = (size_t)(n0 + r0 + lane) * J + j;
+        if (pre) pre[o] = z;
+        out[o] = ACT == DMF_ACT_GELU ? gelu_f(z) : sigmoid_f(z);
       }
     }
   }
 }
 
-__global__ void __launch_bounds__(512) k_se_mlp(const float* __restrict__ ws, int S, int N, int C, float scale,
-                                                const float* __restrict__ w1, const float* __restrict__ b1, int mid,
-                                                const float* __restrict__ w2, const float* __restrict__ b2,
-                                                float* __restrict__ pooled, float* __restrict__ hpre,
-                                                float* __restrict__ hact, float* __restrict__ gate) {
-  extern __shared__ __attribute__((aligned(16))) float se_lds[];
-  float* pv = se_lds;                 // [C] pooled vector (padded to 4)
-  float* hv = se_lds + ((C + 3) & ~3);  // [mid] hidden activations
-  const int n = blockIdx.x;
-  const size_t plane = (size_t)N * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+// pooled[n][c] = scale * sum_z ws[z][n][c] (the squeeze's stage-1 partial planes)
+__global__ void k_sum_planes(const float* __restrict__ ws, int S, long long NC, float scale, float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < NC; i += (long long)gridDim.x * blockDim.x) {
     float v = 0.f;
-    for (int z = 0; z < S; ++z) v += ws[(size_t)z * plane + (size_t)n * C + c];
-    v *= scale;
-    pv[c] = v;
-    if (pooled) pooled[(size_t)n * C + c] = v;
+    for (int z = 0; z < S; ++z) v += ws[(size_t)z * NC + i];
+    out[i] = v * scale;
   }
-  __syncthreads();
-  se_layer<DMF_ACT_GELU>(w1, b1, pv, C, mid, hpre, hv, hact, n);
-  __syncthreads();
-  se_layer<DMF_ACT_SIGMOID>(w2, b2, hv, mid, C, nullptr, nullptr, gate, n);
 }
 
 }  // namespace dmf
@@ -707,10 +748,12 @@ __global__ void __launch_bounds__(512) k_se_mlp(const float* __restrict__ ws, in
 using namespace dmf;
 
 // K splits used for an (M, N, K) problem: enough blocks to cover the chip,
-// >= 64 K per split (1 = no split)
+// >= 128 K per split (1 = no split)
 static int sgemm_splits(int M, int N, int K) {
   const int tiles = cdiv(N, 64) * cdiv(M, 64);
-  int S = std::max(1, std::min(cdiv(512, tiles), K / 64));
+  // >= 128 K per split: a split of a short K (the fusion's 128-wide token linears) costs a reduce
+  // launch for less than it saves
+  int S = std::max(1, std::min(cdiv(512, tiles), K / 128));
   if (S <= 1) return 1;
   const int kchunk = cdiv(cdiv(K, S), 16) * 16;
   return std::max(1, cdiv(K, kchunk));
@@ -727,15 +770,16 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
   DMF_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "dmf_sgemm: bad args");
   if (M == 0 || N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  int S = (workspace && beta == 0.f) ? sgemm_splits(M, N, K) : 1;
+  // (beta != 0 -- an accumulating weight gradient -- splits too: the ordered reduce adds beta * C)
+  int S = workspace ? sgemm_splits(M, N, K) : 1;
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);
   S = S > 1 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
   hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb, beta, C,
                      ldc, bias, act, workspace);
   if (S > 1)
-    hipLaunchKernelGGL(k_sgemm_reduce, dim3(gsz((long long)M * N)), dim3(256), 0, st, S, M, N, alpha, workspace, C,
-                       ldc, bias, act);
+    hipLaunchKernelGGL(k_sgemm_reduce, dim3(gsz((long long)M * N)), dim3(256), 0, st, S, M, N, alpha, workspace, beta,
+                       C, ldc, bias, act);
   DMF_LAUNCH_CHECK("dmf_sgemm");
   return 0;
 }
@@ -951,13 +995,23 @@ extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const floa
 extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1,
                           int mid, const float* w2, const float* b2, float* pooled, float* hpre, float* hact,
                           float* gate, void* stream) {
-  DMF_CHECK_ARG(ws && w1 && w2 && hact && gate && S >= 1 && N >= 1 && C >= 1 && mid >= 1 && C <= 16384 &&
-                    mid <= 16384,
-                "dmf_se_mlp: bad args");
-  DMF_CHECK_ARG(((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0, "dmf_se_mlp: weights must be 16-B aligned");
-  const size_t lds = (size_t)(((C + 3) & ~3) + mid) * sizeof(float);
-  hipLaunchKernelGGL(k_se_mlp, dim3(N), dim3(512), lds, (hipStream_t)stream, ws, S, N, C, scale, w1, b1, mid, w2, b2,
-                     pooled, hpre, hact, gate);
+  DMF_CHECK_ARG(ws && w1 && w2 && hact && gate && S >= 1 && N >= 1 && C >= 1 && mid >= 1, "dmf_se_mlp: bad args");
+  DMF_CHECK_ARG(C <= DR_TMAX * 256 && mid <= DR_TMAX * 256, "dmf_se_mlp: C and mid must be <= 2048");
+  DMF_CHECK_ARG(((uintptr_t)w1 & 15) == 0 && ((uintptr_t)w2 & 15) == 0 && ((uintptr_t)ws & 15) == 0 &&
+                    ((uintptr_t)hact & 15) == 0 && (!pooled || ((uintptr_t)pooled & 15) == 0),
+                "dmf_se_mlp: weights and vectors must be 16-B aligned");
+  DMF_CHECK_ARG(pooled || (S == 1 && scale == 1.f), "dmf_se_mlp: a split / scaled squeeze needs `pooled`");
+  hipStream_t st = (hipStream_t)stream;
+  const float* x = ws;
+  if (pooled && (S > 1 || scale != 1.f || pooled != ws)) {
+    const long long nc = (long long)N * C;
+    hipLaunchKernelGGL(k_sum_planes, dim3(gsz(nc)), dim3(256), 0, st, ws, S, nc, scale, pooled);
+    x = pooled;
+  }
+  hipLaunchKernelGGL(k_dense_rows<DMF_ACT_GELU>, dim3(cdiv(mid, 4)), dim3(256), DR_LDS, st, x, N, C, w1, b1, mid, hpre,
+                     hact);
+  hipLaunchKernelGGL(k_dense_rows<DMF_ACT_SIGMOID>, dim3(cdiv(C, 4)), dim3(256), DR_LDS, st, (const float*)hact, N,
+                     mid, w2, b2, C, (float*)nullptr, gate);
   DMF_LAUNCH_CHECK("dmf_se_mlp");
   return 0;
 }

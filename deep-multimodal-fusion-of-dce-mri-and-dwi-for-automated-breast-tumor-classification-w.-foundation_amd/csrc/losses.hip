@@ -557,6 +557,69 @@ static inline int gsz(long long n) {
   return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
 }
 
+
+// ------------------------------------------------ loss assembly of one step
+// total = sum_i coef_i * v_i * (w if flagged) over the scalar criterion values of
+// _shared_step (train_fusion.py:246-300: cls + lambda_mask * mean of the three
+// mask losses + aux_w * (lambda_recon * recon + lambda_mimic * mimic)), plus the
+// reported group sums (mask / recon / mimic values), in one launch; the
+// backward writes every term's gradient in one more (was ~40 scalar aten
+// launches forward + backward).
+struct LossPlan {
+  const float* p[DMF_LOSS_MAX];
+  float coef[DMF_LOSS_MAX];
+  float gcoef[DMF_LOSS_MAX];
+  int flags[DMF_LOSS_MAX];  // bit 0: times w; bits 1..: group + 1 (0 = none)
+  int n, ng;
+};
+
+__global__ void k_loss_combine(LossPlan pl, const float* __restrict__ w, float* __restrict__ total_out,
+                               float* __restrict__ groups) {
+  if (threadIdx.x != 0) return;
+  const float wv = w ? *w : 1.f;
+  float total = 0.f, g[DMF_LOSS_MAX];
+  for (int k = 0; k < pl.ng; ++k) g[k] = 0.f;
+  for (int i = 0; i < pl.n; ++i) {
+    const float v = *pl.p[i];
+    total += pl.coef[i] * v * ((pl.flags[i] & 1) ? wv : 1.f);
+    const int grp = (pl.flags[i] >> 1) - 1;
+    if (grp >= 0 && grp < pl.ng) g[grp] += pl.gcoef[i] * v;
+  }
+  total_out[0] = total;
+  for (int k = 0; k < pl.ng; ++k) groups[k] = g[k];
+}
+
+__global__ void k_loss_combine_bwd(LossPlan pl, const float* __restrict__ w, const float* __restrict__ dtotal,
+                                   float* __restrict__ grads) {
+  const int i = threadIdx.x;
+  if (i >= pl.n) return;
+  const float wv = w ? *w : 1.f;
+  grads[i] = *dtotal * pl.coef[i] * ((pl.flags[i] & 1) ? wv : 1.f);
+}
+
+// torch.argmax(logits, 1) == labels, averaged (train_fusion.py:302-303): first maximum, NaN
+// counts as the maximum (torch's rule)
+__global__ void k_batch_accuracy(const float* __restrict__ z, const long long* __restrict__ labels, int B, int K,
+                                 float* __restrict__ out) {
+  __shared__ float red[16];
+  float hit = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* r = z + (size_t)b * K;
+    int best = 0;
+    float bv = r[0];
+    for (int k = 1; k < K; ++k) {
+      const float v = r[k];
+      if (!(bv != bv) && ((v != v) || v > bv)) {
+        bv = v;
+        best = k;
+      }
+    }
+    hit += best == labels[b] ? 1.f : 0.f;
+  }
+  hit = block_sum(hit, red);
+  if (threadIdx.x == 0) out[0] = hit / (float)B;
+}
+
 }  // namespace dmf
 
 using namespace dmf;
@@ -699,5 +762,51 @@ extern "C" int dmf_scale_by_cast(int dtype, const float* src, long long M, int C
     hipLaunchKernelGGL(k_scale_by_cast<float>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
                        (float*)dst, ldd, C);
   DMF_LAUNCH_CHECK("dmf_scale_by_cast");
+  return 0;
+}
+
+static int loss_plan(int n, const unsigned long long* ptrs, const float* coef, const int* flags, const float* gcoef,
+                     int ng, LossPlan& pl) {
+  if (n < 1 || n > DMF_LOSS_MAX || ng < 0 || ng > DMF_LOSS_MAX || !ptrs || !coef || !flags) return -1;
+  pl.n = n;
+  pl.ng = ng;
+  for (int i = 0; i < n; ++i) {
+    pl.p[i] = (const float*)(uintptr_t)ptrs[i];
+    pl.coef[i] = coef[i];
+    pl.gcoef[i] = gcoef ? gcoef[i] : 0.f;
+    pl.flags[i] = flags[i];
+    if (!pl.p[i]) return -1;
+  }
+  return 0;
+}
+
+extern "C" int dmf_loss_combine(int n, const unsigned long long* ptrs, const float* coef, const int* flags,
+                                const float* gcoef, int ngroups, const float* w, float* total, float* groups,
+                                void* stream) {
+  LossPlan pl;
+  DMF_CHECK_ARG(total && (groups || ngroups == 0) && loss_plan(n, ptrs, coef, flags, gcoef, ngroups, pl) == 0,
+                "dmf_loss_combine: bad args");
+  hipLaunchKernelGGL(k_loss_combine, dim3(1), dim3(64), 0, (hipStream_t)stream, pl, w, total, groups);
+  DMF_LAUNCH_CHECK("dmf_loss_combine");
+  return 0;
+}
+
+extern "C" int dmf_loss_combine_bwd(int n, const float* coef, const int* flags, const float* w, const float* dtotal,
+                                    float* grads, void* stream) {
+  LossPlan pl;
+  unsigned long long dummy[DMF_LOSS_MAX];
+  for (int i = 0; i < DMF_LOSS_MAX; ++i) dummy[i] = 1;
+  DMF_CHECK_ARG(dtotal && grads && loss_plan(n, dummy, coef, flags, nullptr, 0, pl) == 0,
+                "dmf_loss_combine_bwd: bad args");
+  hipLaunchKernelGGL(k_loss_combine_bwd, dim3(1), dim3(64), 0, (hipStream_t)stream, pl, w, dtotal, grads);
+  DMF_LAUNCH_CHECK("dmf_loss_combine_bwd");
+  return 0;
+}
+
+extern "C" int dmf_batch_accuracy(const float* logits, const long long* labels, int B, int K, float* out,
+                                  void* stream) {
+  DMF_CHECK_ARG(logits && labels && out && B > 0 && K > 0, "dmf_batch_accuracy: bad args");
+  hipLaunchKernelGGL(k_batch_accuracy, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, B, K, out);
+  DMF_LAUNCH_CHECK("dmf_batch_accuracy");
   return 0;
 }

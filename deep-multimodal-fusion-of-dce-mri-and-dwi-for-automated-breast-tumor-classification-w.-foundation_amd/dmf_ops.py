@@ -239,7 +239,7 @@ class WeightCache:
 
 def _sgemm(tA, tB, M, N_, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act, stream):
     """dmf_sgemm with its split-K workspace (deterministic ordered reduce)."""
-    wsn = N.load().dmf_sgemm_ws_size(M, N_, K) if beta == 0.0 else 0
+    wsn = N.load().dmf_sgemm_ws_size(M, N_, K)
     ws = torch.empty(wsn, dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device())) \
         if wsn > 0 else None
     N.call("dmf_sgemm", tA, tB, M, N_, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act, _p(ws), stream)
@@ -1128,15 +1128,31 @@ class _LinearFn(torch.autograd.Function):
             dx = torch.empty((r, k), dtype=torch.float32, device=x.device)
             _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
                    None, N.ACT_NONE, _stream())
+        # leaf parameters: the weight / bias gradients accumulate straight into p.grad (grad_sink:
+        # no AccumulateGrad add per parameter; in_proj's two uses per step just add twice)
+        sink = LINEAR_SINK and _sinkable(w, b) and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty((nout, k), dtype=torch.float32, device=x.device)
-            _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 0.0, dw.data_ptr(), k,
-                   None, N.ACT_NONE, _stream())
-            dw = dw.view_as(w)
+            if sink:
+                _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 1.0, grad_sink(w).data_ptr(),
+                       k, None, N.ACT_NONE, _stream())
+            else:
+                dw = torch.empty((nout, k), dtype=torch.float32, device=x.device)
+                _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 0.0, dw.data_ptr(), k,
+                       None, N.ACT_NONE, _stream())
+                dw = dw.view_as(w)
         if b is not None and ctx.needs_input_grad[2]:
-            db = torch.empty(nout, dtype=torch.float32, device=x.device)
-            N.call("dmf_colsum_f32", dpre.data_ptr(), nout, r, nout, db.data_ptr(), 0, _stream())
+            if sink:
+                N.call("dmf_colsum_f32", dpre.data_ptr(), nout, r, nout, grad_sink(b).data_ptr(), 1, _stream())
+            else:
+                db = torch.empty(nout, dtype=torch.float32, device=x.device)
+                N.call("dmf_colsum_f32", dpre.data_ptr(), nout, r, nout, db.data_ptr(), 0, _stream())
+        if sink:
+            flush_sinks()
         return dx, dw, db, None
+
+
+LINEAR_SINK = os.environ.get("DMF_LINEAR_SINK", "1") != "0"  # A/B knob
+SE_FUSED = os.environ.get("DMF_SE_FUSED", "1") != "0"  # A/B knob
 
 
 def _act_f32(x, out, act):
@@ -1154,14 +1170,15 @@ def linear(x, w, b=None, act="none"):
 # --------------------------------------------------------------------- SE
 def excite_mlp(src, splits, scale, w1, b1, w2, b2, keep=True):
     """gate = sigmoid(gelu(pooled w1^T + b1) w2^T + b2) with pooled = scale *
-    sum of ``splits`` partial planes [S][N][C] in ``src`` (dmf_se_mlp, one
-    launch). Returns (pooled, hpre, hact, gate) fp32 [N][*]; pooled / hpre are
-    None unless ``keep`` (what a backward needs)."""
+    sum of ``splits`` partial planes [S][N][C] in ``src`` (dmf_se_mlp, <= 3
+    launches: partial-plane sum, fc1 + GELU, fc2 + sigmoid). Returns (pooled,
+    hpre, hact, gate) fp32 [N][*]; hpre is None unless ``keep`` (what a
+    backward needs)."""
     mid, c = w1.shape
     n = src.numel() // (splits * c)
     dev = src.device
     w1c, w2c = w1.contiguous().float(), w2.contiguous().float()
-    pooled = torch.empty((n, c), dtype=torch.float32, device=dev) if keep else None
+    pooled = torch.empty((n, c), dtype=torch.float32, device=dev) if (keep or splits > 1 or scale != 1.0) else None
     hpre = torch.empty((n, mid), dtype=torch.float32, device=dev) if keep else None
     hact = torch.empty((n, mid), dtype=torch.float32, device=dev)
     gate = torch.empty((n, c), dtype=torch.float32, device=dev)
@@ -1170,9 +1187,29 @@ def excite_mlp(src, splits, scale, w1, b1, w2, b2, keep=True):
     return pooled, hpre, hact, gate
 
 
+def _se_excite_chain(x, w1, b1, w2, b2):
+    """The unfused excitation (squeeze, GEMM + activation twice) -- A/B reference of se_excite."""
+    n, c, h, w, ld = nhwc(x)
+    pooled = spatial_mean(x)
+    mid = w1.shape[0]
+    hpre = torch.empty((n, mid), dtype=torch.float32, device=x.device)
+    _sgemm(0, 1, n, mid, c, 1.0, pooled.data_ptr(), c, w1.contiguous().data_ptr(), c, 0.0, hpre.data_ptr(), mid,
+           _p(b1), N.ACT_NONE, _stream())
+    hact = torch.empty_like(hpre)
+    _act_f32(hpre, hact, "gelu")
+    z2 = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    _sgemm(0, 1, n, c, mid, 1.0, hact.data_ptr(), mid, w2.contiguous().data_ptr(), mid, 0.0, z2.data_ptr(), c,
+           _p(b2), N.ACT_NONE, _stream())
+    gate = torch.empty_like(z2)
+    _act_f32(z2, gate, "sigmoid")
+    return pooled, hpre, hact, gate
+
+
 def se_excite(x, w1, b1, w2, b2, keep=True):
     """SEBlock squeeze + excitation of an NHWC map: the squeeze's stage-1
     partial sums feed dmf_se_mlp directly (no finish pass)."""
+    if not SE_FUSED:
+        return _se_excite_chain(x, w1, b1, w2, b2)
     n, c, h, w, ld = nhwc(x)
     s = N.load().dmf_nhwc_reduce_splits(n, h * w, c)
     if s > 0 and ld % 8 == 0 and x.data_ptr() % 16 == 0:
@@ -1269,6 +1306,7 @@ class _InputFn(torch.autograd.Function):
                cmean.data_ptr(), _stream())
         ctx.save_for_backward(x)
         ctx.mark_non_differentiable(cmean)
+        _remember_chan_mean(x, cmean)
         # the consuming conv (the backbone stem) may deliver the gate gradient
         # directly (_conv_backward gate_holder) instead of d(x*gate)
         ctx.holder = {"gate": g} if g is not None else None
@@ -1798,9 +1836,31 @@ def cross_attention(qf, kvf, heads, e):
     return _CrossAttnFn.apply(qf, kvf, heads, e)
 
 
+# per-pixel channel means input_stage computed (the encoders' dmf_input_prep sums the raw
+# channels anyway): the recon targets of the same step reuse them instead of re-reading the
+# inputs (2 launches, ~58 us per fusion step). Keyed by storage, shape and version counter, so an
+# in-place refill of the input (a graph's static batch) is never served a stale mean; the few
+# newest entries are kept.
+_CHAN_MEAN = {}
+
+
+def _chan_mean_key(x):
+    return (x.data_ptr(), tuple(x.shape), tuple(x.stride()), x._version, x.device)
+
+
+def _remember_chan_mean(x, cmean):
+    _CHAN_MEAN[_chan_mean_key(x)] = cmean
+    while len(_CHAN_MEAN) > 4:
+        _CHAN_MEAN.pop(next(iter(_CHAN_MEAN)))
+
+
 def channel_mean_map(x):
     """mean over channels of an NCHW fp32 tensor -> [N, H, W] fp32 (recon target)."""
     x = x.contiguous().float()
+    hit = _CHAN_MEAN.get(_chan_mean_key(x))
+    if hit is not None:
+        record_tree(hit, torch.cuda.current_stream(x.device))
+        return hit
     n, c, h, w = x.shape
     out = torch.empty((n, h, w), dtype=torch.float32, device=x.device)
     N.call("dmf_input_prep", F32, x.data_ptr(), n, c, h, w, None, None, c, out.data_ptr(), _stream())
@@ -1808,6 +1868,78 @@ def channel_mean_map(x):
 
 
 # ================================================================ criteria
+LOSS_MAX = 16
+
+
+class _LossCombineFn(torch.autograd.Function):
+    """total = sum over terms of sum_e coef[e] * term[e] * (w if use_w) in one
+    launch (dmf_loss_combine), plus per-group weighted sums (the logged values,
+    non-differentiable); the backward writes every term's gradient in one more.
+    meta: per term (coefs, use_w, group, gcoefs)."""
+
+    @staticmethod
+    def forward(ctx, meta, ngroups, w, *terms):
+        ptrs, coef, flags, gco = [], [], [], []
+        for t, (cs, uw, grp, gcs) in zip(terms, meta):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == len(cs)):
+                raise RuntimeError("loss_combine: terms must be contiguous fp32 device tensors matching their coefs")
+            for e in range(t.numel()):
+                ptrs.append(t.data_ptr() + 4 * e)
+                coef.append(float(cs[e]))
+                flags.append(int(bool(uw)) | ((int(grp) + 1) << 1))
+                gco.append(float(gcs[e]))
+        n = len(ptrs)
+        if n > LOSS_MAX:
+            raise RuntimeError(f"loss_combine: at most {LOSS_MAX} scalar terms")
+        dev = terms[0].device
+        a_p = (ctypes.c_ulonglong * n)(*ptrs)
+        a_c = (ctypes.c_float * n)(*coef)
+        a_f = (ctypes.c_int * n)(*flags)
+        a_g = (ctypes.c_float * n)(*gco)
+        total = torch.empty((), dtype=torch.float32, device=dev)
+        groups = torch.empty(max(ngroups, 1), dtype=torch.float32, device=dev)
+        N.call("dmf_loss_combine", n, ctypes.addressof(a_p), ctypes.addressof(a_c), ctypes.addressof(a_f),
+               ctypes.addressof(a_g), ngroups, _p(w), total.data_ptr(), groups.data_ptr(), _stream())
+        ctx.coef, ctx.flags, ctx.n = coef, flags, n
+        ctx.shapes = [t.shape for t in terms]
+        ctx.w = w
+        ctx.mark_non_differentiable(groups)
+        return total, groups
+
+    @staticmethod
+    def backward(ctx, dtotal, _dgroups):
+        n = ctx.n
+        d = dtotal.contiguous().float()
+        grads = torch.empty(n, dtype=torch.float32, device=d.device)
+        a_c = (ctypes.c_float * n)(*ctx.coef)
+        a_f = (ctypes.c_int * n)(*ctx.flags)
+        N.call("dmf_loss_combine_bwd", n, ctypes.addressof(a_c), ctypes.addressof(a_f), _p(ctx.w), d.data_ptr(),
+               grads.data_ptr(), _stream())
+        out, off = [], 0
+        for shp in ctx.shapes:
+            k = 1
+            for s_ in shp:
+                k *= s_
+            out.append(grads[off:off + k].view(shp))
+            off += k
+        return (None, None, None, *out)
+
+
+def loss_combine(parts, ngroups, w=None):
+    """parts: list of (term tensor, coefs, use_w, group, gcoefs). Returns
+    (total 0-d tensor, groups [ngroups] tensor)."""
+    meta = tuple((tuple(c), bool(u), int(g), tuple(gc)) for _, c, u, g, gc in parts)
+    return _LossCombineFn.apply(meta, ngroups, w, *[p[0].contiguous().float() for p in parts])
+
+
+def batch_accuracy(logits, labels):
+    """(argmax(logits, 1) == labels).float().mean() in one launch."""
+    z = logits.detach().contiguous().float()
+    lab = labels.contiguous().long()
+    out = torch.empty((), dtype=torch.float32, device=z.device)
+    N.call("dmf_batch_accuracy", z.data_ptr(), lab.data_ptr(), z.shape[0], z.shape[1], out.data_ptr(), _stream())
+    return out
+
 class _FocalFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, soft, cw, gamma, smoothing, use_smoothing, reduction):

@@ -492,7 +492,7 @@ class ModelMaskHeadBackbone(nn.Module):
         if self.modality_attention is not None:
             fc = self.modality_attention.fc
             pooled = O.nchw_mean(x)
-            if O.needs_grad(fc[1].weight, fc[1].bias, fc[3].weight, fc[3].bias):
+            if not O.SE_FUSED or O.needs_grad(fc[1].weight, fc[1].bias, fc[3].weight, fc[3].bias):
                 hmid = O.linear(pooled, fc[1].weight, fc[1].bias, act="gelu")
                 gate = O.linear(hmid, fc[3].weight, fc[3].bias, act="sigmoid")
             else:  # frozen encoder: the excitation MLP in one launch

@@ -10,6 +10,8 @@ reconstruction terms of one step share a single launch.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -165,6 +167,13 @@ class LightningFusionModel(nn.Module):
             cls_loss = self.criterion_clf(logits, smoothed)  # Q7: undefined without smoothing, as in the reference
         else:
             cls_loss = self.criterion_clf(logits, labels)
+        # the device assembly covers the default terms; the fusion aux has no raw_feats, so the
+        # feat-norm term is the constant 0 of compute_feat_norm_loss and drops out
+        feat_norm_zero = not self.feat_norm_reg_enabled or aux.get("raw_feats", None) is None
+        if DEVICE_LOSS and dev.type == "cuda" and not self.attn_reg_enabled and feat_norm_zero and cls_loss.dim() == 0:
+            return self._assemble_on_device(cls_loss, logits, labels, fused_mask_logits, aux, dwi_aux, dce_aux,
+                                            dwi_mask_pred, dce_mask_pred, masks_batch, dwi_inputs, dce_inputs,
+                                            aux_w, is_train, return_preds)
         total = cls_loss
 
         mask_loss_val = torch.zeros((), device=dev)
@@ -201,6 +210,39 @@ class LightningFusionModel(nn.Module):
         self.last_metrics = {"loss": total.detach(), "acc": acc.detach(), "cls": cls_loss.detach(),
                              "mask": mask_loss_val.detach(), "recon": recon_loss_val.detach(),
                              "mimic": mimic_loss_val.detach()}
+        if return_preds:
+            return total.detach(), logits.detach(), aux, fused_mask_logits
+        return total
+
+    def _assemble_on_device(self, cls_loss, logits, labels, fused_mask_logits, aux, dwi_aux, dce_aux, dwi_mask_pred,
+                            dce_mask_pred, masks_batch, dwi_inputs, dce_inputs, aux_w, is_train, return_preds):
+        """The rest of _shared_step (train_fusion.py:246-303) with the loss
+        arithmetic in one launch (O.loss_combine) instead of ~40 scalar aten
+        launches forward + backward: total = cls + lambda_mask * (m_dwi + m_dce
+        + m_fused) / 3 + aux_w * (lambda_recon * recon + lambda_mimic * mimic),
+        recon = ((t0 + t1) / 2 + (t2 + t3) / 2 + t4) / 3 over the five
+        reconstruction terms; the logged mask / recon / mimic values are the
+        launch's group sums."""
+        dev = logits.device
+        parts = [(cls_loss, (1.0,), False, -1, (0.0,))]
+        if self.mask_enabled:
+            lm = self.lambda_mask / 3.0 if is_train else 0.0
+            for pred in (dwi_mask_pred, dce_mask_pred, fused_mask_logits):
+                parts.append((safe_mask_loss(pred, masks_batch, self.mask_criterion), (lm,), False, 0, (1.0 / 3,)))
+        w = None
+        with_aux = aux_w > 0.0 and self.recon_enabled and is_train
+        if with_aux:
+            w = aux_weight_tensor(self, dev)
+            t, rc = fused_recon_terms(dwi_aux["recon_feats"], dce_aux["recon_feats"], aux["recon_fused"],
+                                      dwi_inputs.detach(), dce_inputs.detach())
+            parts.append((t, tuple(self.lambda_recon * c for c in rc), True, 1, rc))
+            pf = aux.get("proj_fused", None)
+            if self.mimic_enabled and pf is not None and len(pf) >= 4:
+                parts.append((O.mimic_pairs(pf, npairs=2), (self.lambda_mimic,), True, 2, (1.0,)))
+        total, groups = O.loss_combine(parts, 3, w)
+        # (a group with no term sums to 0, as the reference's torch.zeros placeholders)
+        self.last_metrics = {"loss": total.detach(), "acc": O.batch_accuracy(logits, labels),
+                             "cls": cls_loss.detach(), "mask": groups[0], "recon": groups[1], "mimic": groups[2]}
         if return_preds:
             return total.detach(), logits.detach(), aux, fused_mask_logits
         return total
@@ -368,6 +410,25 @@ def compute_recon_list_loss(recon_list, input_img):
     tgt = O.channel_mean_map(input_img)
     terms = O.recon_terms(maps, [0] * len(maps), tgt)
     return terms.sum() / len(maps)
+
+
+DEVICE_LOSS = os.environ.get("DMF_DEVICE_LOSS", "1") != "0"  # A/B knob: the one-launch loss assembly
+
+
+def fused_recon_terms(dwi_recons, dce_recons, fused_recon, dwi_img, dce_img):
+    """The five reconstruction terms of fused_recon_losses as a [5] tensor with
+    the weights that make recon = sum(w * t), ((t0 + t1) / 2 + (t2 + t3) / 2 +
+    t4) / 3 (train_fusion.py:281-285); other layouts: ([recon], (1,))."""
+    dw = [r for r in dwi_recons if r is not None]
+    dc = [r for r in dce_recons if r is not None]
+    if fused_recon is None or len(dw) != 2 or len(dc) != 2:
+        return fused_recon_losses(dwi_recons, dce_recons, fused_recon, dwi_img, dce_img).reshape(1), (1.0,)
+    ta = O.channel_mean_map(dwi_img)
+    tb = O.channel_mean_map(dce_img)
+    ca, cb = dwi_img.shape[1], dce_img.shape[1]
+    t = O.recon_terms([dw[0], dw[1], dc[0], dc[1], fused_recon], [0, 0, 1, 1, 2], ta, tb, ca / (ca + cb),
+                      cb / (ca + cb))
+    return t, (1.0 / 6, 1.0 / 6, 1.0 / 6, 1.0 / 6, 1.0 / 3)
 
 
 def fused_recon_losses(dwi_recons, dce_recons, fused_recon, dwi_img, dce_img):

@@ -317,8 +317,8 @@ int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, con
  * LayerNorm/Linear FFN), gated combine + bilinear upsample-add (:952-973);
  * nn.Linear layers (classifier, SE excitations) via dmf_sgemm. */
 /* workspace (nullable): dmf_sgemm_ws_size(M, N, K) floats enable a
- * deterministic split-K (partial tiles + ordered reduce) for small-output,
- * long-K problems; without it (or with beta != 0) one pass over K. */
+ * deterministic split-K (partial tiles + ordered reduce, which also applies
+ * beta * C) for small-output, long-K problems; without it one pass over K. */
 int dmf_sgemm_ws_size(int M, int N, int K);
 int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
               int ldb, float beta, float* C, int ldc, const float* bias, int act, float* workspace, void* stream);
@@ -326,12 +326,13 @@ int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumu
 int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
 int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream);
 int dmf_sig_grad_f32(const float* dg, const float* s, float* dz, long long n, void* stream);
-/* SEBlock excitation in one launch (model_module.py:25-43; the modality
- * attention of :584-591): pooled[n] = scale * sum_z ws[z][n][:] over S partial
- * planes of [N][C] (dmf_nhwc_reduce's stage-1 layout; S = 1, scale = 1 for a
- * finished pool), hpre = pooled w1^T + b1 ([mid][C]), hact = gelu(hpre),
- * gate = sigmoid(hact w2^T + b2) ([C][mid]). pooled / hpre / b1 / b2 nullable;
- * weights 16-B aligned. */
+/* SEBlock excitation (model_module.py:25-43; the modality attention of
+ * :584-591) in <= 3 launches: pooled[n] = scale * sum_z ws[z][n][:] over S
+ * partial planes of [N][C] (dmf_nhwc_reduce's stage-1 layout; S = 1, scale = 1
+ * for a finished pool), hpre = pooled w1^T + b1 ([mid][C]), hact = gelu(hpre),
+ * gate = sigmoid(hact w2^T + b2) ([C][mid]). pooled (required when S > 1 or
+ * scale != 1), hpre, b1, b2 nullable; C, mid <= 2048; weights and vectors
+ * 16-B aligned. */
 int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1, int mid,
                const float* w2, const float* b2, float* pooled, float* hpre, float* hact, float* gate, void* stream);
 int dmf_row_l2norm(const float* x, int R, int C, float eps, float* y, float* norms, void* stream);
@@ -390,6 +391,21 @@ int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long lon
 int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream);
 int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul, void* dst,
                       int ldd, void* stream);
+/* Loss assembly of LightningFusionModel._shared_step (train_fusion.py:246-300):
+ * total = sum_i coef[i] * v_i * (w if flags[i] & 1) over n <= DMF_LOSS_MAX scalar
+ * criterion values v_i = *ptrs[i]; groups[g] = sum of gcoef[i] * v_i over the
+ * elements of group g = (flags[i] >> 1) - 1 (the logged mask / recon / mimic
+ * values). ptrs, coef, flags, gcoef are HOST arrays (ptrs holds device
+ * addresses); w (nullable = 1) is the device aux-loss weight. The backward
+ * writes grads[i] = *dtotal * coef[i] * (w or 1). */
+#define DMF_LOSS_MAX 16
+int dmf_loss_combine(int n, const unsigned long long* ptrs, const float* coef, const int* flags, const float* gcoef,
+                     int ngroups, const float* w, float* total, float* groups, void* stream);
+int dmf_loss_combine_bwd(int n, const float* coef, const int* flags, const float* w, const float* dtotal, float* grads,
+                         void* stream);
+/* mean over rows of (argmax(logits[b]) == labels[b]), torch's argmax rule (first
+ * maximum, NaN is the maximum); logits fp32 [B][K] (train_fusion.py:302-303) */
+int dmf_batch_accuracy(const float* logits, const long long* labels, int B, int K, float* out, void* stream);
 
 /* ------------------------------------------ batched bf16 GEMM, attention
  * Hybrid TransformerStage, configuration 5 (transformer_model.py:68-134):

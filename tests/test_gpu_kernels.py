@@ -642,3 +642,31 @@ def test_col_stats_partials(shape, dtype):
         blk = xr[t * 256:(t + 1) * 256]
         torch.testing.assert_close(part[t, :, 0], blk.sum(0), atol=1e-3, rtol=1e-4)
         torch.testing.assert_close(part[t, :, 1], (blk * blk).sum(0), atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(4, 128, 16, 16, 3, 1, 1), (5, 64, 12, 12, 1, 1, 0), (3, 12, 9, 7, 3, 1, 1),
+                                  (2, 16, 10, 10, 3, 2, 1)])
+def test_conv_cout1_backward(case, dtype):
+    """1-output-channel convs (mask / recon heads): input gradient (8-channel
+    vector form), weight and bias gradients (pixel-lane partials + the 16-lane
+    split sum) against torch fp32."""
+    n, ci, h, w, k, s, p = case
+    torch.manual_seed(13)
+    conv = nn.Conv2d(ci, 1, k, stride=s, padding=p, bias=True)
+    x = torch.randn(n, ci, h, w).to(dtype).float()
+    xr = x.clone().requires_grad_(True)
+    yr = F.conv2d(xr, conv.weight, conv.bias, s, p)
+    gy = torch.randn_like(yr).to(dtype).float()
+    yr.backward(gy)
+    cd = copy.deepcopy(conv).to(DEV)
+    cd.zero_grad(set_to_none=True)
+    xd = _to_dev(x, dtype).requires_grad_(True)
+    y = O.conv2d(xd, cd, (O.WeightCache(), O.WeightCache()))
+    y.backward(_to_dev(gy, dtype))
+    rt = 2e-4 if dtype == torch.float32 else 2e-2
+    gx = xr.grad.abs().max().item()
+    torch.testing.assert_close(xd.grad.float().cpu(), xr.grad, rtol=rt, atol=rt * gx)
+    gw = conv.weight.grad.abs().max().item()
+    torch.testing.assert_close(cd.weight.grad.cpu(), conv.weight.grad, rtol=1e-3, atol=1e-4 * gw)
+    torch.testing.assert_close(cd.bias.grad.cpu(), conv.bias.grad, rtol=1e-4, atol=1e-4)

@@ -58,3 +58,43 @@ def test_conv_refuses_wrong_channel_count():
     bad = O.as_nhwc(torch.randn(2, 12, 12, 12, device=DEV))
     with pytest.raises(RuntimeError):
         O.conv2d(bad, conv, (O.WeightCache(), O.WeightCache()))
+
+
+def test_loss_combine_and_batch_accuracy_match_torch():
+    """dmf_loss_combine (total + group sums in one launch, term gradients in one
+    more) and dmf_batch_accuracy against plain torch arithmetic."""
+    import dmf_ops as O
+
+    torch.manual_seed(3)
+    dev = "cuda"
+    a = torch.rand((), device=dev, requires_grad=True)
+    m = [torch.rand((), device=dev, requires_grad=True) for _ in range(3)]
+    t = torch.rand(5, device=dev, requires_grad=True)
+    mi = torch.rand((), device=dev, requires_grad=True)
+    w = torch.tensor(0.8, device=dev)
+    rc = (1 / 6, 1 / 6, 1 / 6, 1 / 6, 1 / 3)
+    parts = [(a, (1.0,), False, -1, (0.0,))] + [(x, (0.2 / 3,), False, 0, (1 / 3,)) for x in m] + \
+        [(t, tuple(0.1 * c for c in rc), True, 1, rc), (mi, (0.2,), True, 2, (1.0,))]
+    total, groups = O.loss_combine(parts, 3, w)
+    g = torch.tensor(1.7, device=dev)
+    total.backward(g)
+    grads = [a.grad.clone()] + [x.grad.clone() for x in m] + [t.grad.clone(), mi.grad.clone()]
+    for x in [a, *m, t, mi]:
+        x.grad = None
+    recon = ((t[0] + t[1]) / 2 + (t[2] + t[3]) / 2 + t[4]) / 3
+    ref = a + 0.2 * (m[0] + m[1] + m[2]) / 3 + 0.1 * recon * w + 0.2 * mi * w
+    ref.backward(g)
+    torch.testing.assert_close(total, ref.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(groups[0], ((m[0] + m[1] + m[2]) / 3).detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(groups[1], recon.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(groups[2], mi.detach(), rtol=1e-6, atol=1e-7)
+    for got, x in zip(grads, [a, *m, t, mi]):
+        torch.testing.assert_close(got, x.grad, rtol=1e-6, atol=1e-7)
+    # accuracy: first maximum on ties, NaN counts as the maximum (torch.argmax)
+    z = torch.randn(37, 4, device=dev)
+    z[3] = torch.tensor([1.0, 1.0, 0.0, -1.0])
+    z[5, 2] = float("nan")
+    lab = torch.randint(0, 4, (37,), device=dev)
+    lab[3], lab[5] = 0, 2
+    ref_acc = (torch.argmax(z, dim=1) == lab).float().mean()
+    torch.testing.assert_close(O.batch_accuracy(z, lab), ref_acc)
