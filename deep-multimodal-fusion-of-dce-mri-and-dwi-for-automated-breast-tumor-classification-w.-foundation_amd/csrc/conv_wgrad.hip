@@ -805,8 +805,9 @@ __global__ void __launch_bounds__(256) k_conv_cout1_wgrad8r(const T* __restrict_
 // out[k] (+)= sum over splits of ws[s][k]: block = 64 columns x 16 split lanes,
 // 8 loads in flight per thread, the 16 lanes combined in LDS in a fixed order
 // (the one-thread-per-column form ran 40 us over 512 splits)
+// cin > 0: column k = tap * cin + ci lands at out[ci * (K / cin) + tap] (torch [Cin][KH][KW])
 __global__ void __launch_bounds__(1024) k_sum_splits16(const float* __restrict__ ws, int splits, int K,
-                                                       float* __restrict__ out, int accumulate) {
+                                                       float* __restrict__ out, int accumulate, int cin) {
   __shared__ float red[16][64];
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + c;
@@ -827,7 +828,8 @@ __global__ void __launch_bounds__(1024) k_sum_splits16(const float* __restrict__
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][c];
-    out[k] = accumulate ? out[k] + t : t;
+    const int o = cin > 0 ? (k % cin) * (K / cin) + k / cin : k;
+    out[o] = accumulate ? out[o] + t : t;
   }
 }
 
@@ -1091,9 +1093,27 @@ extern "C" int dmf_conv_cout1_wgrad_splits(long long M) {
 }
 
 // ws: [splits][KH*KW*Cin] + [splits] (bias partials); dw (layout [KH][KW][Cin]) and db accumulate
+static int cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int lddy,
+                       int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits, float* workspace,
+                       float* dw, float* db, bool torch_layout, void* stream);
+
 extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy,
                                     int lddy, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits,
                                     float* workspace, float* dw, float* db, void* stream) {
+  return cout1_wgrad(dtype, x, N, H, W, Cin, ldx, dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, splits, workspace, dw, db,
+                     false, stream);
+}
+
+extern "C" int dmf_conv_cout1_wgrad_torch(int dtype, const void* x, int N, int H, int W, int Cin, int ldx,
+                                          const void* dy, int lddy, int KH, int KW, int stride, int pad, int dil, int Ho,
+                                          int Wo, int splits, float* workspace, float* dw, float* db, void* stream) {
+  return cout1_wgrad(dtype, x, N, H, W, Cin, ldx, dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, splits, workspace, dw, db,
+                     true, stream);
+}
+
+static int cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int lddy,
+                       int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits, float* workspace,
+                       float* dw, float* db, bool torch_layout, void* stream) {
   DMF_CHECK_ARG(x && dy && workspace && splits >= 1, "dmf_conv_cout1_wgrad: bad args");
   const long long M = (long long)N * Ho * Wo;
   const int K = KH * KW * Cin;
@@ -1118,8 +1138,10 @@ extern "C" int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int 
     hipLaunchKernelGGL(k_conv_cout1_wgrad<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
                        Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
   DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad");
-  if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(K, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, splits, K, dw, 1);
-  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(1), dim3(1024), 0, (hipStream_t)stream, wsb, splits, 1, db, 1);
+  if (dw)
+    hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(K, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, splits, K, dw,
+                       1, torch_layout ? Cin : 0);
+  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(1), dim3(1024), 0, (hipStream_t)stream, wsb, splits, 1, db, 1, 0);
   DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad(reduce)");
   return 0;
 }
@@ -1169,8 +1191,8 @@ extern "C" int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void
                        (const float*)dy, lddy, M, Cout, workspace, wsb);
   DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad");
   // reduce tiles: treat [tiles][Cout] as splits x K
-  if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1);
-  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, wsb, tiles, Cout, db, 1);
+  if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1, 0);
+  if (db) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, wsb, tiles, Cout, db, 1, 0);
   DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad(reduce)");
   return 0;
 }

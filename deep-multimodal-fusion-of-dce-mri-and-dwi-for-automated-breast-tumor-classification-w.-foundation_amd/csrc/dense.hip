@@ -127,17 +127,29 @@ __global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __
 }
 
 // column sums: out[n] (+)= sum_m X[m][n]
-__global__ void k_colsum(const float* __restrict__ X, int ldx, int M, int N, float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
+// block = 64 columns x 16 row lanes, 8 rows in flight per thread, the lanes
+// combined in LDS in a fixed order (4 lanes with one load in flight took
+// ~27 us over 512 rows: latency-bound)
+__global__ void __launch_bounds__(1024) k_colsum(const float* __restrict__ X, int ldx, int M, int N,
+                                                 float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (n < N)
-    for (int m = rl; m < M; m += 4) s += X[(size_t)m * ldx + n];
-  red[rl][cl] = s;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int m = rl;
+    for (; m + 7 * 16 < M; m += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += X[(size_t)(m + u * 16) * ldx + n];
+    }
+    for (; m < M; m += 16) a[0] += X[(size_t)m * ldx + n];
+  }
+  red[rl][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (rl == 0 && n < N) {
-    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += red[i][cl];
     out[n] = accumulate ? out[n] + v : v;
   }
 }
@@ -380,6 +392,65 @@ __global__ void k_tokens_bwd(const float* __restrict__ dtok, int B, int H, int W
   }
 }
 
+// 8-channel vector forms (C % 8 == 0, 64 % (C / 8) == 0): one wave per token,
+// lanes = C/8 channel slices x PL = 64 / (C/8) pixel lanes over the cell, the
+// pixel lanes combined by shuffles (the scalar form looped 64 pixels per
+// channel per thread: ~18 us on a 32 x 32 x 32 x 128 map)
+template <typename T>
+__global__ void __launch_bounds__(256) k_tokens_fwd8(const T* __restrict__ x, int ldx, int B, int H, int W, int C,
+                                                     int Hp, int Wp, float* __restrict__ tok) {
+  const int CV = C >> 3, PL = 64 / CV;
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);  // token index b*Hp*Wp + i*Wp + j
+  if (t >= B * Hp * Wp) return;
+  const int j = t % Wp, i = (t / Wp) % Hp, b = t / (Wp * Hp);
+  const int kh = H / Hp, kw = W / Wp;
+  const int cv = lane % CV, pl = lane / CV;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int q = pl; q < kh * kw; q += PL) {
+    const int a = q / kw, e = q - (q / kw) * kw;
+    float v[8];
+    ld8(x + ((size_t)(b * H + i * kh + a) * W + j * kw + e) * ldx + cv * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += v[k];
+  }
+  for (int o = CV; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+  if (pl == 0) {
+    const float inv = 1.f / (float)(kh * kw);
+    float* o = tok + (size_t)t * C + cv * 8;
+    *(float4*)o = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    *(float4*)(o + 4) = make_float4(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
+  }
+}
+
+// thread = one pixel x 8 channels, 32-bit index math
+template <typename T>
+__global__ void __launch_bounds__(256) k_tokens_bwd8(const float* __restrict__ dtok, int B, int H, int W, int C, int Hp,
+                                                     int Wp, T* __restrict__ dx, int lddx, int accumulate) {
+  const int CV = C >> 3;
+  const int total = B * H * W * CV;
+  const int kh = H / Hp, kw = W / Wp;
+  const float inv = 1.f / (float)(kh * kw);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int cv = t % CV, pix = t / CV;
+    const int w = pix % W, h = (pix / W) % H, b = pix / (W * H);
+    const float* src = dtok + (((size_t)b * Hp + h / kh) * Wp + w / kw) * C + cv * 8;
+    const float4 g0 = *(const float4*)src, g1 = *(const float4*)(src + 4);
+    float v[8] = {g0.x * inv, g0.y * inv, g0.z * inv, g0.w * inv, g1.x * inv, g1.y * inv, g1.z * inv, g1.w * inv};
+    T* p = dx + (size_t)pix * lddx + cv * 8;
+    if (accumulate) {
+      float o[8];
+      ld8(p, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += o[k];
+    }
+    st8(p, v);
+  }
+}
+
 // ----------------------------------------------------------- combine
 __device__ __forceinline__ void lin_w(int o, int in, int out, int& i0, int& i1, float& l1) {
   const float scale = (float)in / (float)out;
@@ -564,6 +635,52 @@ __global__ void k_combine_bwd_low8(const T* __restrict__ dy, int lddy, int B, in
       }
     }
     float* o = dlow + (size_t)t * 8;
+    *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+// the same as one wave per low-res token: lanes = C/8 channel slices x PL pixel
+// lanes over the token's bilinear support, combined by shuffles (the
+// thread-per-slice form walked ~360 positions serially on 32 blocks: ~67 us)
+template <typename T>
+__global__ void __launch_bounds__(256) k_combine_bwd_low8w(const T* __restrict__ dy, int lddy, int B, int H, int W,
+                                                           int C, int Hp, int Wp, float* __restrict__ dlow) {
+  const int CV = C >> 3, PL = 64 / CV;
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= B * Hp * Wp) return;
+  const int j = t % Wp, i = (t / Wp) % Hp, n = t / (Wp * Hp);
+  const int cv = lane % CV, pl = lane / CV;
+  const int hl = max(0, (int)floorf(((float)i - 0.5f) * H / Hp - 0.5f) - 1);
+  const int hh = min(H, (int)ceilf(((float)i + 1.5f) * H / Hp - 0.5f) + 2);
+  const int wl = max(0, (int)floorf(((float)j - 0.5f) * W / Wp - 0.5f) - 1);
+  const int wh = min(W, (int)ceilf(((float)j + 1.5f) * W / Wp - 0.5f) + 2);
+  const int nw = wh - wl, npos = (hh - hl) * nw;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int q = pl; q < npos; q += PL) {
+    const int h = hl + q / nw, w = wl + (q - (q / nw) * nw);
+    int h0, h1, w0, w1;
+    float lh, lw;
+    lin_w(h, Hp, H, h0, h1, lh);
+    lin_w(w, Wp, W, w0, w1, lw);
+    float wgh = 0.f, ww = 0.f;
+    if (h0 == i) wgh += 1.f - lh;
+    if (h1 == i) wgh += lh;
+    if (w0 == j) ww += 1.f - lw;
+    if (w1 == j) ww += lw;
+    const float wt = wgh * ww;
+    if (wt == 0.f) continue;
+    float v[8];
+    ld8(dy + ((size_t)(n * H + h) * W + w) * lddy + cv * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = fmaf(wt, v[k], acc[k]);
+  }
+  for (int o = CV; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+  if (pl == 0) {
+    float* o = dlow + (size_t)t * C + cv * 8;
     *(float4*)o = make_float4(acc[0], acc[1], acc[2], acc[3]);
     *(float4*)(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
@@ -787,7 +904,7 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
 extern "C" int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream) {
   DMF_CHECK_ARG(X && out, "dmf_colsum_f32: bad args");
   if (N == 0) return 0;
-  hipLaunchKernelGGL(k_colsum, dim3(cdiv(N, 64)), dim3(256), 0, (hipStream_t)stream, X, ldx, M, N, out, accumulate);
+  hipLaunchKernelGGL(k_colsum, dim3(cdiv(N, 64)), dim3(1024), 0, (hipStream_t)stream, X, ldx, M, N, out, accumulate);
   DMF_LAUNCH_CHECK("dmf_colsum_f32");
   return 0;
 }
@@ -877,6 +994,19 @@ extern "C" int dmf_tokens_fwd(int dtype, const void* x, int ldx, int B, int H, i
   DMF_CHECK_ARG(x && tokens && Hp > 0 && Wp > 0 && H % Hp == 0 && W % Wp == 0,
                 "dmf_tokens_fwd: map %dx%d must divide into %dx%d tokens", H, W, Hp, Wp);
   const long long total = (long long)B * Hp * Wp * C;
+  const int CV = C / 8;
+  if (C % 8 == 0 && CV <= 64 && 64 % CV == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0 &&
+      ((uintptr_t)tokens % 16) == 0 && (long long)B * H * W * ldx < (1LL << 31)) {
+    const dim3 g(cdiv((long long)B * Hp * Wp, 4));
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_tokens_fwd8<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, B, H, W, C,
+                         Hp, Wp, tokens);
+    else
+      hipLaunchKernelGGL(k_tokens_fwd8<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, B, H, W, C,
+                         Hp, Wp, tokens);
+    DMF_LAUNCH_CHECK("dmf_tokens_fwd");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_tokens_fwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        ldx, B, H, W, C, Hp, Wp, tokens);
@@ -891,6 +1021,18 @@ extern "C" int dmf_tokens_bwd(int dtype, const float* dtokens, int B, int H, int
                               int lddx, int accumulate, void* stream) {
   DMF_CHECK_ARG(dtokens && dx && H % Hp == 0 && W % Wp == 0, "dmf_tokens_bwd: bad args");
   const long long total = (long long)B * H * W * C;
+  if (C % 8 == 0 && lddx % 8 == 0 && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)dtokens % 16) == 0 &&
+      (long long)B * H * W * lddx < (1LL << 31)) {
+    const long long t8 = total / 8;
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_tokens_bwd8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                         Hp, Wp, (bf16_t*)dx, lddx, accumulate);
+    else
+      hipLaunchKernelGGL(k_tokens_bwd8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                         Hp, Wp, (float*)dx, lddx, accumulate);
+    DMF_LAUNCH_CHECK("dmf_tokens_bwd");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_tokens_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
                        Hp, Wp, (bf16_t*)dx, lddx, accumulate);
@@ -924,7 +1066,8 @@ extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const
   DMF_CHECK_ARG(dy && p_dwi && p_dce && gates, "dmf_fusion_combine_bwd: bad args");
   const long long total = (long long)B * H * W * C;
   hipStream_t st_ = (hipStream_t)stream;
-  const bool v8 = C % 8 == 0 && lddy % 8 == 0 && ld % 8 == 0 && ((uintptr_t)dy % 16) == 0 &&
+  const bool v8 = C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0 && lddy % 8 == 0 && ld % 8 == 0 &&
+                  ((uintptr_t)dy % 16) == 0 && (!dlowres || ((uintptr_t)dlowres % 16) == 0) &&
                   ((uintptr_t)p_dwi % 16) == 0 && ((uintptr_t)p_dce % 16) == 0;
   if (v8 && dtype == DMF_BF16) {
     if (dp_dwi || dp_dce)
@@ -934,7 +1077,7 @@ extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const
       hipLaunchKernelGGL(k_combine_bwd_gate8<bf16_t>, dim3(B), dim3(1024), 0, st_, (const bf16_t*)dy, lddy,
                          (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, H * W, C, dgates);
     if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low8<bf16_t>, dim3(gsz((long long)B * Hp * Wp * C / 8)), dim3(256), 0, st_,
+      hipLaunchKernelGGL(k_combine_bwd_low8w<bf16_t>, dim3(cdiv((long long)B * Hp * Wp, 4)), dim3(256), 0, st_,
                          (const bf16_t*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
   } else if (v8) {
     if (dp_dwi || dp_dce)
@@ -944,7 +1087,7 @@ extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const
       hipLaunchKernelGGL(k_combine_bwd_gate8<float>, dim3(B), dim3(1024), 0, st_, (const float*)dy, lddy,
                          (const float*)p_dwi, (const float*)p_dce, ld, H * W, C, dgates);
     if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low8<float>, dim3(gsz((long long)B * Hp * Wp * C / 8)), dim3(256), 0, st_,
+      hipLaunchKernelGGL(k_combine_bwd_low8w<float>, dim3(cdiv((long long)B * Hp * Wp, 4)), dim3(256), 0, st_,
                          (const float*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
   } else if (dtype == DMF_BF16) {
     if (dp_dwi || dp_dce)

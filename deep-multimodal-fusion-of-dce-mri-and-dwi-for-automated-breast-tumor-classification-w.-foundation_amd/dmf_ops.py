@@ -710,7 +710,22 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
         if x2 is not None:
             dx = (dx[:, :cx], dx[:, cx:])
     if need_dw or need_db:
-        if co == 1:
+        if co == 1 and dw_sink and cx == ci:
+            # straight into .grad in torch layout: no zero fills, re-layout copy or AccumulateGrad adds
+            splits = N.load().dmf_conv_cout1_wgrad_splits(m)
+            k = kh * kw * cx
+            ws = torch.empty(splits * k + splits, dtype=torch.float32, device=dev)
+            N.call("dmf_conv_cout1_wgrad_torch", dtc, x.data_ptr(), n, h, w, cx, ldx, dy.data_ptr(), lddy, kh, kw,
+                   g.stride, g.pad, g.dil, ho, wo, splits, ws.data_ptr(),
+                   grad_sink(weight).data_ptr() if need_dw else None,
+                   grad_sink(bias).data_ptr() if need_db else None, _stream())
+        elif ci == 1 and kh == 1 and kw == 1 and g.stride == 1 and dw_sink:
+            tiles = (n * h * w + 255) // 256
+            ws = torch.empty(2 * tiles * co, dtype=torch.float32, device=dev)
+            N.call("dmf_conv_cin1_wgrad", dtc, x.data_ptr(), ldx, dy.data_ptr(), lddy, n * h * w, co, ws.data_ptr(),
+                   grad_sink(weight).data_ptr() if need_dw else None,
+                   grad_sink(bias).data_ptr() if need_db else None, _stream())
+        elif co == 1:
             splits = N.load().dmf_conv_cout1_wgrad_splits(m)
             k = kh * kw * cx
             ws = torch.empty(splits * k + splits, dtype=torch.float32, device=dev)
@@ -1130,7 +1145,8 @@ class _LinearFn(torch.autograd.Function):
                    None, N.ACT_NONE, _stream())
         # leaf parameters: the weight / bias gradients accumulate straight into p.grad (grad_sink:
         # no AccumulateGrad add per parameter; in_proj's two uses per step just add twice)
-        sink = LINEAR_SINK and _sinkable(w, b) and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32)
+        sink = (LINEAR_SINK and _sinkable(w, b) and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32)
+                and ctx.needs_input_grad[1] and (b is None or ctx.needs_input_grad[2]))
         if ctx.needs_input_grad[1]:
             if sink:
                 _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 1.0, grad_sink(w).data_ptr(),
@@ -1234,6 +1250,7 @@ class _SEFn(torch.autograd.Function):
         N.call("dmf_channel_scale", dt(x), x.data_ptr(), ld, gate.data_ptr(), y.data_ptr(), nhwc(y)[4], n, h * w, c,
                _stream())
         ctx.save_for_backward(x, w1, w2, pooled, hpre, hact, gate)
+        ctx.biases = (b1, b2)
         ctx.mark_non_differentiable(gate)
         return y, gate.view(n, c, 1, 1)
 
@@ -1251,21 +1268,25 @@ class _SEFn(torch.autograd.Function):
         N.call("dmf_sig_grad_f32", dg.data_ptr(), gate.data_ptr(), dz2.data_ptr(), dg.numel(), _stream())
         w2m = w2.detach().reshape(c, mid).contiguous()
         w1m = w1.detach().reshape(mid, c).contiguous()
-        dw2 = torch.empty((c, mid), dtype=torch.float32, device=dev)
-        _sgemm(1, 0, c, mid, n, 1.0, dz2.data_ptr(), c, hact.data_ptr(), mid, 0.0, dw2.data_ptr(), mid,
-               None, N.ACT_NONE, _stream())
-        db2 = torch.empty(c, dtype=torch.float32, device=dev)
-        N.call("dmf_colsum_f32", dz2.data_ptr(), c, n, c, db2.data_ptr(), 0, _stream())
+        # the four parameter gradients go straight into .grad (grad_sink) when they are leaves
+        b1, b2 = ctx.biases
+        sink = (LINEAR_SINK and _sinkable(w1, b1, w2, b2) and b1 is not None and b2 is not None
+                and all(ctx.needs_input_grad[1:5]))
+        dw2 = grad_sink(w2) if sink else torch.empty((c, mid), dtype=torch.float32, device=dev)
+        _sgemm(1, 0, c, mid, n, 1.0, dz2.data_ptr(), c, hact.data_ptr(), mid, 1.0 if sink else 0.0, dw2.data_ptr(),
+               mid, None, N.ACT_NONE, _stream())
+        db2 = grad_sink(b2) if sink else torch.empty(c, dtype=torch.float32, device=dev)
+        N.call("dmf_colsum_f32", dz2.data_ptr(), c, n, c, db2.data_ptr(), 1 if sink else 0, _stream())
         dh = torch.empty((n, mid), dtype=torch.float32, device=dev)
         _sgemm(0, 0, n, mid, c, 1.0, dz2.data_ptr(), c, w2m.data_ptr(), mid, 0.0, dh.data_ptr(), mid,
                None, N.ACT_NONE, _stream())
         dh1 = torch.empty_like(dh)
         N.call("dmf_act_grad_f32", dh.data_ptr(), hpre.data_ptr(), dh1.data_ptr(), dh.numel(), N.ACT_GELU, _stream())
-        dw1 = torch.empty((mid, c), dtype=torch.float32, device=dev)
-        _sgemm(1, 0, mid, c, n, 1.0, dh1.data_ptr(), mid, pooled.data_ptr(), c, 0.0, dw1.data_ptr(), c,
-               None, N.ACT_NONE, _stream())
-        db1 = torch.empty(mid, dtype=torch.float32, device=dev)
-        N.call("dmf_colsum_f32", dh1.data_ptr(), mid, n, mid, db1.data_ptr(), 0, _stream())
+        dw1 = grad_sink(w1) if sink else torch.empty((mid, c), dtype=torch.float32, device=dev)
+        _sgemm(1, 0, mid, c, n, 1.0, dh1.data_ptr(), mid, pooled.data_ptr(), c, 1.0 if sink else 0.0, dw1.data_ptr(),
+               c, None, N.ACT_NONE, _stream())
+        db1 = grad_sink(b1) if sink else torch.empty(mid, dtype=torch.float32, device=dev)
+        N.call("dmf_colsum_f32", dh1.data_ptr(), mid, n, mid, db1.data_ptr(), 1 if sink else 0, _stream())
         dx = None
         if ctx.needs_input_grad[0]:
             dpooled = torch.empty((n, c), dtype=torch.float32, device=dev)
@@ -1274,6 +1295,9 @@ class _SEFn(torch.autograd.Function):
             dx = empty_nhwc(n, c, h, w, x.dtype, dev)
             N.call("dmf_channel_affine", dt(x), dy.data_ptr(), nhwc(dy)[4], gate.data_ptr(), dpooled.data_ptr(),
                    1.0 / (h * w), dx.data_ptr(), nhwc(dx)[4], n, h * w, c, _stream())
+        if sink:
+            flush_sinks()
+            return dx, None, None, None, None
         return dx, dw1.view_as(w1), db1, dw2.view_as(w2), db2
 
 
@@ -1616,6 +1640,7 @@ class _GateFn(torch.autograd.Function):
         N.call("dmf_gate_fwd", pa.data_ptr(), pb.data_ptr(), _p(ca), _p(cb), n, c, W.data_ptr(), b.data_ptr(),
                g.data_ptr(), _stream())
         ctx.save_for_backward(pa, pb, ca, cb, W, g)
+        ctx.bias = b
         return g
 
     @staticmethod
@@ -1624,8 +1649,11 @@ class _GateFn(torch.autograd.Function):
         dg = dg.contiguous()
         n, c = pa.shape
         dev = pa.device
-        dW = torch.zeros_like(W)
-        db = torch.zeros(2, dtype=torch.float32, device=dev)
+        # (the kernel adds into dW / db: with leaf parameters that is their .grad -- no fill, no add)
+        b = ctx.bias
+        sink = LINEAR_SINK and _sinkable(W, b) and ctx.needs_input_grad[4] and ctx.needs_input_grad[5]
+        dW = grad_sink(W) if sink else torch.zeros_like(W)
+        db = grad_sink(b) if sink else torch.zeros(2, dtype=torch.float32, device=dev)
         dpa = torch.empty_like(pa)
         dpb = torch.empty_like(pb)
         dca = torch.empty_like(ca) if ca is not None else None
@@ -1633,6 +1661,9 @@ class _GateFn(torch.autograd.Function):
         N.call("dmf_gate_bwd", pa.data_ptr(), pb.data_ptr(), _p(ca), _p(cb), n, c, W.data_ptr(), g.data_ptr(),
                dg.data_ptr(), dW.data_ptr(), db.data_ptr(), dpa.data_ptr(), dpb.data_ptr(), _p(dca), _p(dcb),
                _stream())
+        if sink:
+            flush_sinks()
+            return dpa, dpb, dca, dcb, None, None
         return dpa, dpb, dca, dcb, dW, db
 
 
@@ -1689,6 +1720,7 @@ class _LayerNormFn(torch.autograd.Function):
         N.call("dmf_layernorm_fwd", x2.data_ptr(), r, e, gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(),
                save.data_ptr(), _stream())
         ctx.save_for_backward(x2, gamma, save)
+        ctx.beta = beta
         return y.view(shp)
 
     @staticmethod
@@ -1698,10 +1730,15 @@ class _LayerNormFn(torch.autograd.Function):
         r, e = x2.shape
         dy2 = dy.reshape(r, e).contiguous()
         dx = torch.empty_like(x2)
-        dg = torch.zeros_like(gamma)
-        db = torch.zeros_like(gamma)
+        beta = ctx.beta
+        sink = LINEAR_SINK and _sinkable(gamma, beta) and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]
+        dg = grad_sink(gamma) if sink else torch.zeros_like(gamma)  # the kernel adds into dg / db
+        db = grad_sink(beta) if sink else torch.zeros_like(gamma)
         N.call("dmf_layernorm_bwd", dy2.data_ptr(), x2.data_ptr(), save.data_ptr(), r, e, gamma.data_ptr(),
                dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _stream())
+        if sink:
+            flush_sinks()
+            return dx.view(shp), None, None, None
         return dx.view(shp), dg, db, None
 
 
@@ -1838,9 +1875,10 @@ def cross_attention(qf, kvf, heads, e):
 
 # per-pixel channel means input_stage computed (the encoders' dmf_input_prep sums the raw
 # channels anyway): the recon targets of the same step reuse them instead of re-reading the
-# inputs (2 launches, ~58 us per fusion step). Keyed by storage, shape and version counter, so an
-# in-place refill of the input (a graph's static batch) is never served a stale mean; the few
-# newest entries are kept.
+# inputs (2 launches, ~58 us per fusion step). Keyed by storage, shape and version counter, and
+# valid only while the tensor the mean was computed from is alive (a weak reference): a freed
+# input's address reused by a new tensor, or an in-place refill (a graph's static batch), is never
+# served a stale mean. The few newest entries are kept.
 _CHAN_MEAN = {}
 
 
@@ -1849,7 +1887,7 @@ def _chan_mean_key(x):
 
 
 def _remember_chan_mean(x, cmean):
-    _CHAN_MEAN[_chan_mean_key(x)] = cmean
+    _CHAN_MEAN[_chan_mean_key(x)] = (weakref.ref(x), cmean)
     while len(_CHAN_MEAN) > 4:
         _CHAN_MEAN.pop(next(iter(_CHAN_MEAN)))
 
@@ -1857,8 +1895,9 @@ def _remember_chan_mean(x, cmean):
 def channel_mean_map(x):
     """mean over channels of an NCHW fp32 tensor -> [N, H, W] fp32 (recon target)."""
     x = x.contiguous().float()
-    hit = _CHAN_MEAN.get(_chan_mean_key(x))
-    if hit is not None:
+    ent = _CHAN_MEAN.get(_chan_mean_key(x))
+    if ent is not None and ent[0]() is not None:
+        hit = ent[1]
         record_tree(hit, torch.cuda.current_stream(x.device))
         return hit
     n, c, h, w = x.shape

@@ -148,6 +148,10 @@ int dmf_conv_cout1_wgrad_splits(long long M);
 int dmf_conv_cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy, int lddy,
                          int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits, float* workspace,
                          float* dw, float* db, void* stream);
+/* the same with dw in torch layout [1][Cin][KH][KW] (accumulated: a parameter's .grad) */
+int dmf_conv_cout1_wgrad_torch(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* dy,
+                               int lddy, int KH, int KW, int stride, int pad, int dil, int Ho, int Wo, int splits,
+                               float* workspace, float* dw, float* db, void* stream);
 /* single-input-channel 1x1 convs: mask_processor[0] (model_module.py:68),
  * proj_r1/proj_r2 first conv (:639-640) */
 int dmf_conv_cin1_fwd(int dtype, const void* x, int ldx, const float* w, const float* bias, void* y, int ldy,

@@ -670,3 +670,21 @@ def test_conv_cout1_backward(case, dtype):
     gw = conv.weight.grad.abs().max().item()
     torch.testing.assert_close(cd.weight.grad.cpu(), conv.weight.grad, rtol=1e-3, atol=1e-4 * gw)
     torch.testing.assert_close(cd.bias.grad.cpu(), conv.bias.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_channel_mean_reuse_never_stale():
+    """channel_mean_map reuses input_stage's channel means only for the live tensor they came
+    from: an in-place refill (version bump) or a new tensor at a freed input's address recomputes."""
+    torch.manual_seed(14)
+    x = torch.rand(2, 6, 8, 8, device=DEV)
+    _, cm = O.input_stage(x, torch.bfloat16)
+    assert O.channel_mean_map(x) is cm
+    torch.testing.assert_close(cm, x.mean(1))
+    x.copy_(torch.rand_like(x))  # same storage, new contents
+    torch.testing.assert_close(O.channel_mean_map(x), x.mean(1))
+    ptr = x.data_ptr()
+    O.input_stage(x, torch.bfloat16)
+    del x
+    y = torch.rand(2, 6, 8, 8, device=DEV)  # may land on the freed block
+    torch.testing.assert_close(O.channel_mean_map(y), y.mean(1))
+    assert ptr is not None
