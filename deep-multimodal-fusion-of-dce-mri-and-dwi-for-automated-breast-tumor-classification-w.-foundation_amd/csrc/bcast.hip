@@ -46,6 +46,30 @@ __global__ void k_broadcast_hw(const float* __restrict__ vec, float scale, T* __
   }
 }
 
+// 8-channel vector form, 32-bit index math (the scalar form's 64-bit divisions
+// per element: ~12 us on a 32 x 32 x 32 x 128 map)
+template <typename T>
+__global__ void __launch_bounds__(256) k_broadcast_hw8(const float* __restrict__ vec, float scale, T* __restrict__ y,
+                                                       int ldy, int N, int HW, int C, int accumulate) {
+  const int CV = C >> 3;
+  const int total = N * HW * CV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cv = i % CV, row = i / CV, n = row / HW;
+    const float* src = vec + (size_t)n * C + cv * 8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[k] * scale;
+    T* p = y + (size_t)row * ldy + cv * 8;
+    if (accumulate) {
+      float o[8];
+      ld8(p, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += o[k];
+    }
+    st8(p, v);
+  }
+}
+
 // block per (n, c)
 template <typename T>
 __global__ void k_gate_grad_nchw(const T* __restrict__ dy, int lddy, const float* __restrict__ x, int C, int HW,
@@ -84,6 +108,17 @@ extern "C" int dmf_broadcast_hw(int dtype, const float* vec, float scale, void* 
   DMF_CHECK_ARG(vec && y, "dmf_broadcast_hw: bad args");
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
+  if (C % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 && (long long)N * HW * ldy < (1LL << 31)) {
+    const long long t8 = total / 8;
+    if (dtype == DMF_BF16)
+      hipLaunchKernelGGL(k_broadcast_hw8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, vec, scale,
+                         (bf16_t*)y, ldy, N, HW, C, accumulate);
+    else
+      hipLaunchKernelGGL(k_broadcast_hw8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, vec, scale,
+                         (float*)y, ldy, N, HW, C, accumulate);
+    DMF_LAUNCH_CHECK("dmf_broadcast_hw");
+    return 0;
+  }
   if (dtype == DMF_BF16)
     hipLaunchKernelGGL(k_broadcast_hw<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, vec, scale,
                        (bf16_t*)y, ldy, (long long)N, HW, C, accumulate);

@@ -63,24 +63,35 @@ __global__ void k_nchw_mean(const float* __restrict__ x, long long HW, float* __
 
 // out[n][c] = scale * sum_hw a[n,hw,c] * (b ? b[n,hw,c] : 1); block = (n, 64-channel group), 4 row lanes
 template <typename T>
+// block = CW channel lanes x R = 256 / CW pixel lanes (CW = C rounded up to a
+// power of two, <= 64): a 1-channel map (the gating's mask-logit means) uses
+// all 256 threads instead of 4; pixel lanes combined by a fixed-order tree
 __global__ void k_nhwc_reduce(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb, int HW, int C,
                               float scale, float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  __shared__ float red[256];
+  int CW = 1;
+  while (CW < C && CW < 64) CW <<= 1;
+  const int R = 256 / CW;
+  const int cl = threadIdx.x % CW, rl = threadIdx.x / CW;
   const int n = blockIdx.x, c = blockIdx.y * 64 + cl;
   float s = 0.f;
-  if (c < C) {
+  if (c < C && cl < 64) {
     const T* pa = a + (long long)n * HW * lda + c;
     const T* pb = b ? b + (long long)n * HW * ldb + c : nullptr;
-    for (int p = rl; p < HW; p += 4) {
+#pragma unroll 4
+    for (int p = rl; p < HW; p += R) {
       const float v = ld(pa + (long long)p * lda);
       s += pb ? v * ld(pb + (long long)p * ldb) : v;
     }
   }
-  red[rl][cl] = s;
+  red[threadIdx.x] = s;
   __syncthreads();
+  for (int st = R >> 1; st > 0; st >>= 1) {
+    if (rl < st) red[threadIdx.x] += red[threadIdx.x + st * CW];
+    __syncthreads();
+  }
   if (rl == 0 && c < C) {
-    const float r = (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]) * scale;
+    const float r = red[cl] * scale;
     out[n * C + c] = accumulate ? out[n * C + c] + r : r;
   }
 }
