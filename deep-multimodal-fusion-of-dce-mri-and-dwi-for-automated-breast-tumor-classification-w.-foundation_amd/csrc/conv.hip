@@ -1746,6 +1746,8 @@ using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
+int sgemm_tune(int deep_k);  // dense.hip
+
 extern "C" int dmf_conv_tune(int key, int value) {
   switch (key) {
     case 0: g_sq_enable = value != 0; return 0;
@@ -1759,6 +1761,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 9: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: two-workgroup mode %d", value); g_p2_mode = value; return 0;
     case 10: g_stem_enable = value != 0; return 0;
     case 11: g_fast_epi = value != 0; return 0;
+    case 12: return sgemm_tune(value);
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

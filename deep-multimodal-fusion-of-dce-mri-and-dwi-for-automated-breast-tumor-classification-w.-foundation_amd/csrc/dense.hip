@@ -40,48 +40,53 @@ __device__ __forceinline__ float actf(int act, float z) {
 // [z*kchunk, (z+1)*kchunk); with gridDim.z > 1 each split stores its
 // partial tile into ws[z][M][N] and k_sgemm_reduce sums the splits in a
 // fixed order and applies alpha, bias and act (deterministic).
+// BK = K rows staged per barrier: 16, or 64 for K >= 64 when enabled (the
+// fusion's 128-deep token linears: 2 global-latency rounds instead of 8;
+// measured neutral on the step, see g_sgemm_deep)
+template <int BK>
 __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, int kchunk, float alpha,
                                                const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                int ldb, float beta, float* __restrict__ C, int ldc,
                                                const float* __restrict__ bias, int act, float* __restrict__ ws) {
-  __shared__ float As[16][68], Bs[16][68];
+  constexpr int NR = BK * 64 / 256;  // staged elements per thread and operand
+  __shared__ float As[BK][68], Bs[BK][68];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
   const bool split = gridDim.z > 1;
   // load mapping: contiguous-K operands walk k fastest (16 lanes x 1 row)
-  float ra[4], rb[4];
+  float ra[NR], rb[NR];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int i = threadIdx.x + 256 * r;
       int kk, mm;
-      if (tA) { kk = i >> 6; mm = i & 63; } else { kk = i & 15; mm = i >> 4; }
+      if (tA) { kk = i >> 6; mm = i & 63; } else { kk = i % BK; mm = i / BK; }
       const int m = m0 + mm, k = k0 + kk;
       ra[r] = (m < M && k < ke) ? (tA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k]) : 0.f;
       int kk2, nn;
-      if (tB) { kk2 = i & 15; nn = i >> 4; } else { kk2 = i >> 6; nn = i & 63; }
+      if (tB) { kk2 = i % BK; nn = i / BK; } else { kk2 = i >> 6; nn = i & 63; }
       const int n = n0 + nn, k2 = k0 + kk2;
       rb[r] = (n < N && k2 < ke) ? (tB ? B[(size_t)n * ldb + k2] : B[(size_t)k2 * ldb + n]) : 0.f;
     }
   };
   auto sstore = [&]() {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int i = threadIdx.x + 256 * r;
-      if (tA) As[i >> 6][i & 63] = ra[r]; else As[i & 15][i >> 4] = ra[r];
-      if (tB) Bs[i & 15][i >> 4] = rb[r]; else Bs[i >> 6][i & 63] = rb[r];
+      if (tA) As[i >> 6][i & 63] = ra[r]; else As[i % BK][i / BK] = ra[r];
+      if (tB) Bs[i % BK][i / BK] = rb[r]; else Bs[i >> 6][i & 63] = rb[r];
     }
   };
   float acc[4][4] = {};
   if (kb < ke) gload(kb);
-  for (int k0 = kb; k0 < ke; k0 += 16) {
+  for (int k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
     sstore();
     __syncthreads();
-    if (k0 + 16 < ke) gload(k0 + 16);
+    if (k0 + BK < ke) gload(k0 + BK);
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
+    for (int kk = 0; kk < BK; ++kk) {
       float a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
@@ -876,6 +881,14 @@ static int sgemm_splits(int M, int N, int K) {
   return std::max(1, cdiv(K, kchunk));
 }
 
+// 64-deep K staging where K allows (dmf_conv_tune key 12): measured neutral on the mode-A step
+// (interleaved A/B, 3108 vs 3100 vol/s), off by default
+static bool g_sgemm_deep = false;
+int sgemm_tune(int deep_k) {
+  g_sgemm_deep = deep_k != 0;
+  return 0;
+}
+
 extern "C" int dmf_sgemm_ws_size(int M, int N, int K) {
   const int S = sgemm_splits(M, N, K);
   return S > 1 ? S * M * N : 0;
@@ -892,8 +905,12 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);
   S = S > 1 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
-  hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb, beta, C,
-                     ldc, bias, act, workspace);
+  if (kchunk >= 64 && g_sgemm_deep)
+    hipLaunchKernelGGL(k_sgemm<64>, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb,
+                       beta, C, ldc, bias, act, workspace);
+  else
+    hipLaunchKernelGGL(k_sgemm<16>, grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb,
+                       beta, C, ldc, bias, act, workspace);
   if (S > 1)
     hipLaunchKernelGGL(k_sgemm_reduce, dim3(gsz((long long)M * N)), dim3(256), 0, st, S, M, N, alpha, workspace, beta,
                        C, ldc, bias, act);

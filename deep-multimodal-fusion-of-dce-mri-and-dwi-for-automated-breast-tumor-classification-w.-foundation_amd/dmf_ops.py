@@ -1168,6 +1168,8 @@ class _LinearFn(torch.autograd.Function):
 
 
 LINEAR_SINK = os.environ.get("DMF_LINEAR_SINK", "1") != "0"  # A/B knob
+if os.environ.get("DMF_SGEMM_DEEP", "0") == "1":  # A/B knob: 64-deep K staging in the fp32 GEMMs
+    N.call("dmf_conv_tune", 12, 1)
 SE_FUSED = os.environ.get("DMF_SE_FUSED", "1") != "0"  # A/B knob
 
 
