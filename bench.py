@@ -178,7 +178,7 @@ def roofline_probe(trainer, batch, dtype):
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = pmc_traffic()
     return {
-        "kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm, %s)" %
+        "kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_pp / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_stem / k_conv_igemm, %s)" %
                   ("bf16" if dtype == torch.bfloat16 else "f32"),
         "bound": "mfma",
         "achieved": round(achieved, 2),
@@ -326,7 +326,7 @@ def conv_probe(fn, dtype):
     peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
     achieved = flops / n / (avg_ms * 1e-3) / 1e12
     recs.clear()
-    return {"kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_igemm)",
+    return {"kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_pp / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_stem / k_conv_igemm)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None, "launches_per_step": n,
             "avg_launch_us": round(avg_ms * 1e3, 2), "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),

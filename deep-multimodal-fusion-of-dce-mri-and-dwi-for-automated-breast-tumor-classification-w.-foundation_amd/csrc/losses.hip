@@ -319,10 +319,14 @@ constexpr int RECON_XPT = 2;  // output columns per thread (S <= 512)
 template <typename T>
 __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __restrict__ ws) {
   __shared__ float Rs[5][RECON_NR][64];
-  __shared__ float Acc[5][RECON_NR][RECON_MAXS];
-  __shared__ float Lx[RECON_MAXS];   // column x: bilinear weight of j1
-  __shared__ short J0[RECON_MAXS];   // column x: source columns j0 (j1 = j0 + (j0 < w-1))
   __shared__ float red5[5][4];
+  // sized by S at launch (5 * 3 * S + S floats + S shorts): at S = 256 half the static
+  // RECON_MAXS footprint, so twice the resident blocks per CU
+  extern __shared__ __attribute__((aligned(16))) float rdyn[];
+  float* AccF = rdyn;                                     // [5][RECON_NR][S]
+  float* Lx = rdyn + 5 * RECON_NR * a.S;                  // column x: bilinear weight of j1
+  short* J0 = (short*)(rdyn + 5 * RECON_NR * a.S + a.S);  // column x: source column j0 (j1 = j0 + (j0 < w-1))
+#define Acc(k, r, x) AccF[((k) * RECON_NR + (r)) * a.S + (x)]
   const int b = blockIdx.x, q = blockIdx.y, nb = gridDim.y;
   const int y0 = q * RECON_RB, y1 = min(a.S, y0 + RECON_RB);
   const int tid = threadIdx.x;
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
-      for (int r = 0; r < RECON_NR; ++r) Acc[k][r][x] = A[k][r];
+      for (int r = 0; r < RECON_NR; ++r) Acc(k, r, x) = A[k][r];
   }
   __syncthreads();
   // x-contraction: (k, r, j) sums the columns x whose source column j0 or j1 is j -> slab row r of band q
@@ -429,7 +433,7 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
       xh = min(xh, a.S);
       for (int x = xl; x < xh; ++x) {
         const int j0 = J0[x], j1 = j0 + (j0 < a.w - 1 ? 1 : 0);
-        const float lx = Lx[x], av = Acc[k][r][x];
+        const float lx = Lx[x], av = Acc(k, r, x);
         if (j0 == j) h += (1.f - lx) * av;
         if (j1 == j) h += lx * av;
       }
@@ -449,6 +453,8 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
     ws[((size_t)b * nb + q) * 5 + tid] = sm;
   }
 }
+
+#undef Acc
 
 // pass 2: one thread per gradient element (map k, item b, source row i,
 // column j) sums the (<= 3) band slabs covering row i, in band order; the
@@ -705,10 +711,11 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
                   "outside the streaming form (B=%d h=%d w=%d S=%d)", B, h, w, S);
     const int nb = cdiv(S, RECON_RB);
     const dim3 g(B, nb);
+    const size_t lds = (size_t)(5 * RECON_NR * S + S) * sizeof(float) + (size_t)S * sizeof(short);
     if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
+      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), lds, (hipStream_t)stream, a, ws);
     else
-      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), 0, (hipStream_t)stream, a, ws);
+      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), lds, (hipStream_t)stream, a, ws);
     hipLaunchKernelGGL(k_recon_finish, dim3(cdiv((long long)nterms * B * h * w, 256) + 1), dim3(256), 0,
                        (hipStream_t)stream, a, ws, nb);
   } else if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {

@@ -23,7 +23,7 @@ def load(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--match", default=r"k_conv_fwd_ps|k_conv_fwd_sq|k_conv_fwd_wide|k_conv_fwd_buf|k_conv_fwd_pers|k_conv_igemm<unsigned short, false")
+    ap.add_argument("--match", default=r"k_conv_fwd_ps|k_conv_fwd_pp|k_conv_fwd_sq|k_conv_fwd_wide|k_conv_fwd_buf|k_conv_stem|k_conv_igemm<unsigned short, false")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     fe = load(f"{a.dir}/FETCH_SIZE/run_counter_collection.csv")
