@@ -362,6 +362,10 @@ class BackboneAdapter(nn.Module):
 PARALLEL_NECKS = os.environ.get("DMF_PAR_NECK", "0") != "0"  # opt-in: measured slower (r01w)
 PARALLEL_PROJ = os.environ.get("DMF_PAR_PROJ", "0") != "0"  # opt-in: measured slower (r01w)
 PARALLEL_DEAD = os.environ.get("DMF_PAR_DEAD", "1") != "0"
+# opt-in: measured slower (interleaved A/B, 3 rounds: mode A 3150 -> 2941 vol/s with the three
+# fusion heads on side streams -- the cross-stream joins of the captured forward and backward cost
+# more than the overlap of their short chains)
+PARALLEL_HEADS = os.environ.get("DMF_PAR_HEADS", "0") != "0"
 
 
 def _inline_branch(owner, name, fn, *inputs):
@@ -673,11 +677,18 @@ class FusionModel(nn.Module):
                 low, attn_weights = self.cross_attn_block(t_dwi, t_dce)
             fused = O.fusion_combine(p_dwi, p_dce, gating_weights, low, hp, wp)
             fused_refined = O.se_block(fused, self.fusion_se)[0] if self.fusion_se is not None else fused
-            fused_mask_logits = self.mask_head(fused_refined)
+            # the four heads read fused_refined independently: with DMF_PAR_HEADS=1 the mask, recon
+            # and projection heads run on side streams beside the classifier (off: measured slower)
+            br = O.branch if PARALLEL_HEADS else _inline_branch
+            fused_mask_logits, join_mask = br(self, "head_mask", lambda: self.mask_head(fused_refined), fused_refined)
+            recon_fused, join_recon = br(
+                self, "head_recon",
+                lambda: self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None,
+                fused_refined)
+            proj_fused, join_proj = br(self, "head_proj", lambda: self.projF(fused_refined), fused_refined)
             cl = self.classifier[2]
             logits = O.linear(O.gap(fused_refined), cl.weight, cl.bias)
-            recon_fused = self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None
-            proj_fused = self.projF(fused_refined)
+            fused_mask_logits, recon_fused, proj_fused = join_mask(), join_recon(), join_proj()
             join_dead()
         aux = {"proj_fused": proj_fused, "recon_fused": recon_fused, "gating_weights": gating_weights,
                "attn_weights": attn_weights, "p_dwi": p_dwi, "p_dce": p_dce}
