@@ -1114,6 +1114,15 @@ class _LinearFn(torch.autograd.Function):
         nout = w.shape[0]
         y = torch.empty((r, nout), dtype=torch.float32, device=x.device)
         wc = w.detach().contiguous()
+        x = x.float()
+        if _linear_mfma(k, nout) and x.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0:
+            # exact f32 MFMA GEMM with bias + activation (+ the pre-activation for backward) in its epilogue
+            pre = torch.empty_like(y) if act != "none" else None
+            _gemm_f32(0, 0, r, nout, k, x.data_ptr(), k, wc.data_ptr(), k, y.data_ptr(), nout, bias=_p(b),
+                      act=ACT[act], aux=_p(pre), ldaux=nout)
+            ctx.save_for_backward(x, w, b, pre)
+            ctx.act = act
+            return y
         _sgemm(0, 1, r, nout, k, 1.0, x.data_ptr(), k, wc.data_ptr(), k, 0.0, y.data_ptr(), nout, _p(b),
                N.ACT_NONE, _stream())
         pre = y
@@ -1139,16 +1148,25 @@ class _LinearFn(torch.autograd.Function):
             dpre = dy
         dx = dw = db = None
         wc = w.detach().contiguous()
+        mfma = (_linear_mfma(k, nout) and r % 4 == 0 and x.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0
+                and dpre.data_ptr() % 16 == 0)
         if ctx.needs_input_grad[0]:
             dx = torch.empty((r, k), dtype=torch.float32, device=x.device)
-            _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
-                   None, N.ACT_NONE, _stream())
+            if mfma:  # dX = dpre [r x nout] . W [nout x k]
+                _gemm_f32(0, 1, r, k, nout, dpre.data_ptr(), nout, wc.data_ptr(), k, dx.data_ptr(), k)
+            else:
+                _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
+                       None, N.ACT_NONE, _stream())
         # leaf parameters: the weight / bias gradients accumulate straight into p.grad (grad_sink:
         # no AccumulateGrad add per parameter; in_proj's two uses per step just add twice)
         sink = (LINEAR_SINK and _sinkable(w, b) and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32)
                 and ctx.needs_input_grad[1] and (b is None or ctx.needs_input_grad[2]))
         if ctx.needs_input_grad[1]:
-            if sink:
+            if sink and mfma:  # dW += dpre^T [nout x r] . x [r x k] (the GEMM's residual input aliases dW)
+                g = grad_sink(w)
+                _gemm_f32(1, 1, nout, k, r, dpre.data_ptr(), nout, x.data_ptr(), k, g.data_ptr(), k,
+                          res=g.data_ptr(), ldr=k)
+            elif sink:
                 _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 1.0, grad_sink(w).data_ptr(),
                        k, None, N.ACT_NONE, _stream())
             else:
@@ -1168,6 +1186,17 @@ class _LinearFn(torch.autograd.Function):
 
 
 LINEAR_SINK = os.environ.get("DMF_LINEAR_SINK", "1") != "0"  # A/B knob
+LINEAR_MFMA = os.environ.get("DMF_LINEAR_MFMA", "0") == "1"  # A/B knob: fp32 linears on the f32 MFMA GEMM
+
+
+def _linear_mfma(k, nout):
+    return LINEAR_MFMA and k % 4 == 0 and nout % 4 == 0
+
+
+def _gemm_f32(ta, tb, M, N_, K, A, lda, B, ldb, C, ldc, bias=None, act=0, aux=None, ldaux=0, res=None, ldr=0):
+    """dmf_gemm_f32, unbatched: C = act(op(A) op(B) + bias) [+ res], aux = pre-activation."""
+    N.call("dmf_gemm_f32", N.F32, ta, tb, M, N_, K, 1.0, A, lda, 0, 0, B, ldb, 0, 0, C, ldc, 0, 0, 1, 1, bias, act,
+           None, res, ldr, aux, ldaux, None, 0, 0.0, None, 0, None, _stream())
 if os.environ.get("DMF_SGEMM_DEEP", "0") == "1":  # A/B knob: 64-deep K staging in the fp32 GEMMs
     N.call("dmf_conv_tune", 12, 1)
 SE_FUSED = os.environ.get("DMF_SE_FUSED", "1") != "0"  # A/B knob
