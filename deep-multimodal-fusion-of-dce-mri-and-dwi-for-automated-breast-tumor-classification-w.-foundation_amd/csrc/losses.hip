@@ -359,14 +359,27 @@ __global__ void __launch_bounds__(256) k_recon_stream(ReconArgs a, float* __rest
     Lx[x] = lx;
   }
   const int nrows = ie - ib0 + 1;  // <= RECON_NR (checked by the launcher)
-  for (int t = tid; t < 5 * RECON_NR * 64; t += blockDim.x) {
+  // the band's source rows: all of a thread's (<= 4) loads in flight before its LDS stores (a
+  // load -> store chain per element paid the load latency four times)
+  static_assert(5 * RECON_NR * 64 <= 4 * 256, "recon staging: 4 elements per thread");
+  float sv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = tid + u * 256;
     const int k = t / (RECON_NR * 64), rem = t - k * (RECON_NR * 64), r = rem / 64, j = rem - r * 64;
-    float v = 0.f;
-    if (k < a.nterms && r < nrows && j < a.w) {
+    sv[u] = 0.f;
+    if (t < 5 * RECON_NR * 64 && k < a.nterms && r < nrows && j < a.w) {
       const T* R = (const T*)a.r[k] + ((size_t)b * a.h * a.w + (size_t)(ib0 + r) * a.w + j) * a.ldr[k];
-      v = ld(R);
+      sv[u] = ld(R);
     }
-    Rs[k][r][j] = v;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = tid + u * 256;
+    if (t < 5 * RECON_NR * 64) {
+      const int k = t / (RECON_NR * 64), rem = t - k * (RECON_NR * 64), r = rem / 64, j = rem - r * 64;
+      Rs[k][r][j] = sv[u];
+    }
   }
   __syncthreads();
   float part[5] = {0.f, 0.f, 0.f, 0.f, 0.f};

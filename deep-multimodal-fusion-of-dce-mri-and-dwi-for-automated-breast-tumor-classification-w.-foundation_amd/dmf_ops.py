@@ -1186,7 +1186,9 @@ class _LinearFn(torch.autograd.Function):
 
 
 LINEAR_SINK = os.environ.get("DMF_LINEAR_SINK", "1") != "0"  # A/B knob
-LINEAR_MFMA = os.environ.get("DMF_LINEAR_MFMA", "0") == "1"  # A/B knob: fp32 linears on the f32 MFMA GEMM
+# A/B knob: fp32 linears on the f32 MFMA GEMM -- parity-green, measured 5.6 % slower on the mode-A step
+# (interleaved A/B: 2953 vs 3124 vol/s; latency-bound big tiles on 512-row token problems), off
+LINEAR_MFMA = os.environ.get("DMF_LINEAR_MFMA", "0") == "1"
 
 
 def _linear_mfma(k, nout):
