@@ -1747,6 +1747,7 @@ using namespace dmf;
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
 int sgemm_tune(int deep_k);  // dense.hip
+int sgemm_tune_v4(int v4);   // dense.hip
 
 extern "C" int dmf_conv_tune(int key, int value) {
   switch (key) {
@@ -1762,6 +1763,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 10: g_stem_enable = value != 0; return 0;
     case 11: g_fast_epi = value != 0; return 0;
     case 12: return sgemm_tune(value);
+    case 13: return sgemm_tune_v4(value);
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

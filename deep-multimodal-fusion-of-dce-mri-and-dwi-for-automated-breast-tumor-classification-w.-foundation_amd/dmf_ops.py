@@ -1201,6 +1201,8 @@ def _gemm_f32(ta, tb, M, N_, K, A, lda, B, ldb, C, ldc, bias=None, act=0, aux=No
            None, res, ldr, aux, ldaux, None, 0, 0.0, None, 0, None, _stream())
 if os.environ.get("DMF_SGEMM_DEEP", "0") == "1":  # A/B knob: 64-deep K staging in the fp32 GEMMs
     N.call("dmf_conv_tune", 12, 1)
+if os.environ.get("DMF_SGEMM_V4", "0") == "1":  # A/B knob: the vector 4 x 4 fp32 GEMM micro-tile
+    N.call("dmf_conv_tune", 13, 1)
 SE_FUSED = os.environ.get("DMF_SE_FUSED", "1") != "0"  # A/B knob
 
 
