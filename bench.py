@@ -9,7 +9,12 @@ state at epoch 0 ("mode A": both encoders frozen but in train mode -- dropout
 on, BN batch statistics -- backward + AdamW through FusionModel only,
 selector_helpers.py:437-443 / :632-685). ``--mode B`` unfreezes everything.
 
-  python bench.py --gpus N --steps K --warmup W      (N>1 under torchrun)
+  python bench.py --gpus N --steps K --warmup W
+
+--gpus N > 1 without a launcher's WORLD_SIZE starts N worker processes of this
+script itself (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE set, rendezvous on
+127.0.0.1) before anything touches the GPU, and exits with their status; under
+torch.distributed.run (WORLD_SIZE set) it is one of the ranks.
 
 Prints ONE JSON line (rank 0) including the roofline of the dominant kernel
 (the implicit-GEMM conv forward, timed per launch with HIP events on the
@@ -61,7 +66,42 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="flip a measured variant for an A/B run (dmf_ops.KNOBS; DESIGN.md 'Knobs')")
     return ap.parse_args()
+
+
+def spawn_ranks(n):
+    """``--gpus N`` with no launcher: N processes of this script, one per GPU,
+    each with the torchrun environment (the parent never touches the GPU).
+    Rank 0 prints the JSON line; the first failing rank stops the others."""
+    import signal
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:  # a rank died: the others would wait in a collective forever
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
 
 
 def build(P, device, dtype, mode, seed=0):
@@ -141,6 +181,84 @@ def encoder_forward_probe(trainer, batch, args):
         t_roof = T_ROOF_ENC_FWD_MS_B32 * args.batch / 32
         out.update({"t_roof_ms": round(t_roof, 3), "frac": round(t_roof / ms, 4),
                     "roof": "SURVEY 8(d): sum_k max(F_k / 2.5 PFLOP/s, B_k / 8 TB/s)"})
+    return out
+
+
+def wgrad_probe(trainer, batch, dtype):
+    """Mode B's dominant kernel family, the MFMA weight gradient
+    (k_conv_wgrad_dma / _tr + its split-K reduce): one eager mode-B step
+    records every dmf_conv2d_wgrad + dmf_conv2d_wgrad_reduce pair; the pairs
+    are replayed GPU-only from a hipGraph with HIP events around the replay
+    (as roofline_probe). achieved = algorithmic 2*Cout*K*pixels per pair /
+    average pair duration."""
+    import dmf_ops as O
+
+    recs = []
+    O.PROBE["conv_wgrad"] = recs
+    torch.cuda.synchronize()
+    trainer.eager_step(batch)
+    torch.cuda.synchronize()
+    O.PROBE["conv_wgrad"] = None
+    if not recs:
+        return None
+    flops = sum(r["flops"] for r in recs)
+    byt = sum(r["bytes"] for r in recs)
+    n = len(recs)
+    avg_ms, per = O.probe_replay(recs)
+    wg_only = [dict(r, calls=r["calls"][:1]) for r in recs]
+    avg_ms_wg, _ = O.probe_replay(wg_only)
+    recs.clear()
+    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    achieved = flops / n / (avg_ms * 1e-3) / 1e12
+    return {"kernel": "conv2d weight gradient (k_conv_wgrad_dma / k_conv_wgrad_tr + k_wgrad_reduce), %s" %
+                      ("bf16" if dtype == torch.bfloat16 else "f32"),
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
+            "avg_wgrad_kernel_us": round(avg_ms_wg * 1e3, 2),
+            "avg_reduce_us": round((avg_ms - avg_ms_wg) * 1e3, 2),
+            "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
+            "algorithmic_mb_per_launch": round(byt / n / 1e6, 2),
+            "per_launch": "one launch = dmf_conv2d_wgrad + its dmf_conv2d_wgrad_reduce"}
+
+
+FP8_MFMA_PEAK_TFLOPS = 5000.0  # dense e4m3 (spec, no sparsity)
+
+
+def gemm_probes(trainer, batch):
+    """Config 5's rooflines: one eager step records the e4m3 patch-embed GEMM
+    launches (dmf_gemm_fp8) and the bf16 token GEMMs (dmf_tokens.gemm:
+    qkv / QK^T / PV / proj / fc1 / fc2), replayed GPU-only from a hipGraph
+    (as roofline_probe); each family against its own dense MFMA peak."""
+    import dmf_ops as O
+
+    fam = {"fp8_gemm": ("e4m3 patch-embed GEMM (k_gemm_fp8, v_mfma_f32_16x16x32_fp8_fp8)", FP8_MFMA_PEAK_TFLOPS),
+           "tok_gemm": ("token GEMMs (k_gemm_bf16: qkv, QK^T, PV, proj, fc1, fc2)", BF16_MFMA_PEAK_TFLOPS)}
+    recs = {k: [] for k in fam}
+    for k in fam:
+        O.PROBE[k] = recs[k]
+    torch.cuda.synchronize()
+    try:
+        trainer.eager_step(batch)
+        torch.cuda.synchronize()
+    finally:
+        for k in fam:
+            O.PROBE[k] = None
+    out = {}
+    for k, (name, peak) in fam.items():
+        r = recs[k]
+        if not r:
+            continue
+        n = len(r)
+        avg_ms, _ = O.probe_replay(r)
+        flops = sum(x["flops"] for x in r)
+        byt = sum(x["bytes"] for x in r)
+        ach = flops / n / (avg_ms * 1e-3) / 1e12
+        out[k] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                  "frac": round(ach / peak, 4), "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
+                  "algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
+                  "algorithmic_mb_per_launch": round(byt / n / 1e6, 3)}
+        r.clear()
     return out
 
 
@@ -476,8 +594,14 @@ GFLOP_PER_VOL = {"A": 155.0, "B": 458.0}
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if os.environ.get("DMF_BENCH_SHARE_GPU") != "1" and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(spawn_ranks(args.gpus))
     rank, local_rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), \
         int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} rank(s)", file=sys.stderr)
     # one process per GPU over RCCL ("nccl"). DMF_DIST_BACKEND=gloo with
     # DMF_BENCH_SHARE_GPU=1 rehearses the multi-rank control flow on a 1-GPU box.
     dev_idx = local_rank % torch.cuda.device_count() if os.environ.get("DMF_BENCH_SHARE_GPU") == "1" else local_rank
@@ -491,6 +615,11 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", dev_idx)
     import parameters as PR
+
+    if args.knob:
+        import dmf_ops as O
+
+        O.set_knobs(**dict(k.split("=", 1) for k in args.knob))
 
     if args.config in (1, 2):
         if world > 1:
@@ -521,6 +650,7 @@ def main():
     trainer, batch, dt = bench_fusion(P, device, dtype, args.mode, args.batch, args.size, args.steps, args.warmup,
                                       world, rank, use_graph=not args.no_graph)
     loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
+    comm_ranks = trainer._rccl.count() if getattr(trainer, "_rccl", None) is not None else None
     if loss_val is not None and loss_val != loss_val:
         raise RuntimeError("training loss is NaN: the benchmarked step is numerically broken")
     med = _median_step_ms(lambda: trainer.step(batch), min(args.steps, 50)) if world == 1 else None
@@ -550,6 +680,8 @@ def main():
                                f"({'encoders frozen, train-mode' if args.mode == 'A' else 'all trainable'})",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch, "size": args.size,
                    "parallelism": f"dp{world}", "hipgraph": not args.no_graph,
+                   "collective": ("RCCL all-reduce over %d ranks (ncclCommCount), overlapped with backward" % comm_ranks
+                                  if comm_ranks else ("gloo host all-reduce" if world > 1 else "none (1 rank)")),
                    **({"patch_embed": args.patch_embed if args.dtype == "bf16" else "f32"}
                       if args.config == 5 else {})},
         "loss": loss_val,
@@ -574,6 +706,7 @@ def main():
                                     max(10, args.steps // 2), 3, world, rank, use_graph=not args.no_graph)
         nb = max(10, args.steps // 2)
         msb = dtb * 1e3 / nb
+        roof_b = wgrad_probe(tb, bb_, dtype) if not args.no_roofline else None
         tfb = GFLOP_PER_VOL["B"] * args.batch / (msb * 1e-3) / 1e3
         out["mode_b"] = {"value": round(args.batch * world * nb / dtb, 2), "unit": "volumes/s",
                          "ms_per_step": round(msb, 3), "steps": nb, "warmup": 3,
@@ -582,7 +715,8 @@ def main():
                          "step_roofline": {"bound": "mfma", "achieved": round(tfb, 1),
                                            "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                            "frac": round(tfb / BF16_MFMA_PEAK_TFLOPS, 4),
-                                           "algorithmic_gflop_per_volume": GFLOP_PER_VOL["B"]}}
+                                           "algorithmic_gflop_per_volume": GFLOP_PER_VOL["B"]},
+                         "roofline": roof_b}
         del tb, bb_
         torch.cuda.empty_cache()
         if world == 1:
@@ -596,15 +730,17 @@ def main():
         P5["dwi_model_parameters"]["patch_embed_fp8"] = True
         P5["dwi_model_parameters"]["input_size"] = 384
         n5 = max(10, args.steps // 2)
-        t5, _, dt5 = bench_fusion(P5, device, dtype, "A", args.batch, 384, n5, 3, world, rank,
-                                  use_graph=not args.no_graph)
+        t5, b5, dt5 = bench_fusion(P5, device, dtype, "A", args.batch, 384, n5, 3, world, rank,
+                                   use_graph=not args.no_graph)
+        roof5 = gemm_probes(t5, b5) if not args.no_roofline else None
         out["config5"] = {"value": round(args.batch * world * n5 / dt5, 2), "unit": "volumes/s",
                           "ms_per_step": round(dt5 * 1e3 / n5, 3), "steps": n5, "warmup": 3,
                           "loss": float(t5.loss.item()) if t5.loss is not None else None,
                           "workload": "fusion training step, config 5 (hybrid TransformerStage encoders, S=384, "
                                       "fp8-e4m3 patch-embed, bf16 elsewhere), mode A",
-                          "per_gpu_batch": args.batch, "size": 384, "patch_embed": "fp8"}
-        del t5
+                          "per_gpu_batch": args.batch, "size": 384, "patch_embed": "fp8",
+                          "roofline": roof5}
+        del t5, b5
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -903,230 +903,6 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
   }
 }
 
-// ---------------------------------------- forward, persistent buffer-load form
-// 128x128 tiles, gridDim = resident blocks; each block walks its tiles as ONE
-// flat stream of K-steps, so the two-tile register pipeline runs across tile
-// boundaries: the loads of the next tile's first K-steps are in flight while
-// the finished tile's epilogue (bias/act or BN partials, C staging in row
-// passes through the free LDS stage, 16-B stores) runs. Used when a launch
-// needs more than one round of blocks; no fused BN finalize (tickets).
-template <typename T>
-__device__ __forceinline__ void conv_epilogue_stage(const ConvArgs& a, f32x4_t (&acc)[4][4], char* st, int tid,
-                                                    int mt, int m0, int n0) {
-  constexpr int ES = sizeof(T);
-  constexpr int EPC = 16 / ES;
-  constexpr int RP = ES == 2 ? 64 : 32;  // rows per staging pass (fits a 32 KB stage)
-  constexpr int CST = 128 + 16 / ES;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int fr = lane & 15, fg = lane >> 4;
-  const bool stats = a.partials != nullptr;
-  float* red = (float*)st;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + fr;
-    const float bsv = (a.bias != nullptr && col < a.Nout) ? a.bias[col] : 0.f;
-    float s = 0.f, ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + fg * 4 + r;
-        float v = acc[i][j][r] + bsv;
-        if (stats && row < a.M) { s += v; ss += v * v; }
-        acc[i][j][r] = v;
-      }
-    }
-    if (!stats) apply_act_col(a.act, acc, j);
-    if (stats) {
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
-      if (fg == 0) {
-        const int lc = wn * 64 + j * 16 + fr;
-        red[(wm * 128 + lc) * 2 + 0] = s;
-        red[(wm * 128 + lc) * 2 + 1] = ss;
-      }
-    }
-  }
-  if (stats) {
-    __syncthreads();
-    if (tid < 128) {
-      const int col = n0 + tid;
-      if (col < a.Nout) {
-        float2 v;
-        v.x = red[tid * 2 + 0] + red[(128 + tid) * 2 + 0];
-        v.y = red[tid * 2 + 1] + red[(128 + tid) * 2 + 1];
-        if (a.stat_acc) {
-          acc_stats(a, mt, col, v);
-        } else {
-          *(float2*)(a.partials + ((size_t)mt * a.Nout + col) * 2) = v;
-        }
-      }
-    }
-  }
-  T* Cs = (T*)st;
-  T* Y = (T*)a.y;
-#pragma unroll
-  for (int pass = 0; pass < 128 / RP; ++pass) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if ((wm * 64 + i * 16) / RP != pass) continue;  // wave-uniform
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * 64 + i * 16 + fg * 4 + r - pass * RP;
-          const int col = wn * 64 + j * 16 + fr;
-          Cs[row * CST + col] = Cvt<T>::store(acc[i][j][r]);
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = 128 / EPC;
-#pragma unroll
-    for (int idx = tid; idx < RP * CPR; idx += CTHREADS) {
-      const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
-      const int m = m0 + pass * RP + row, n = n0 + chn * EPC;
-      if (m < a.M && n < a.Nout) *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
-    }
-  }
-}
-
-template <typename T, bool PADCHK, bool DUAL>
-__global__ void __launch_bounds__(CTHREADS, 2) k_conv_fwd_pers(ConvArgs a) {
-  constexpr int ES = sizeof(T);
-  constexpr int EPC = 16 / ES;
-  constexpr int BK = 8 * EPC;
-  constexpr int SB = 256 * 128;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int q = tid & 7, rbase = tid >> 3;
-  const int nk = a.Ktot / BK;
-  // tiles of this block: XCD x = blockIdx % 8 owns a contiguous range of logical tiles
-  const int T_ = a.mtiles * a.ntiles, G = gridDim.x;
-  const int x = blockIdx.x & 7, jb = blockIdx.x >> 3;
-  const int gx = G / 8 + (x < G % 8 ? 1 : 0);  // blocks on this XCD
-  const int r0 = (int)((long long)T_ * x / 8), r1 = (int)((long long)T_ * (x + 1) / 8);
-  const int cnt = jb < (r1 - r0) ? (r1 - r0 - jb + gx - 1) / gx : 0;
-  if (cnt == 0) return;
-  const int S = cnt * nk;  // flat K-steps of this block
-
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(a.x), 0, (int)((long long)a.N * a.H * a.W * a.ldx * ES), BUF_FLAGS);
-  const __amdgpu_buffer_rsrc_t rx2 = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(DUAL ? a.x2 : a.x), 0, (int)((long long)a.N * a.H * a.W * (DUAL ? a.ldx2 : a.ldx) * ES),
-      BUF_FLAGS);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(a.w), 0, (int)((long long)a.Nout * a.Ktot * ES), BUF_FLAGS);
-
-  // loader state: row metadata of the tile being loaded
-  int ltile = -1;
-  int h0[4], w0[4], b1[4], b2[4];
-  bool mok[4];
-  unsigned vb[4];
-  auto set_tile = [&](int li) {
-    const int lin = r0 + jb + li * gx;
-    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-    const int m0 = mt * 128, n0 = nt * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + rbase + 32 * i;
-      mok[i] = m < a.M;
-      const int mm = mok[i] ? m : 0;
-      const int hw = a.Ho * a.Wo;
-      const int n = mm / hw, rem = mm - (mm / hw) * hw;
-      const int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
-      h0[i] = ho * a.stride - a.pad;
-      w0[i] = wo * a.stride - a.pad;
-      const int pix = (n * a.H + h0[i]) * a.W + w0[i];
-      b1[i] = pix * a.ldx + q * EPC;
-      b2[i] = DUAL ? pix * a.ldx2 + q * EPC : 0;
-      const int nn = n0 + rbase + 32 * i;
-      vb[i] = nn < a.Nout ? (unsigned)((nn * a.Ktot + q * EPC) * ES) : BUF_OOB;
-    }
-  };
-  uint4 ra0[4], rb0[4], ra1[4], rb1[4];
-  auto gload = [&](int sidx, uint4 (&ra)[4], uint4 (&rb)[4]) {
-    const int li = sidx / nk, kt = sidx - (sidx / nk) * nk;  // uniform
-    if (li != ltile) {
-      set_tile(li);
-      ltile = li;
-    }
-    const int k0 = kt * BK;
-    const int tap = k0 / a.C;
-    const int c0 = k0 - tap * a.C;
-    const int r = tap / a.KW, s = tap - (tap / a.KW) * a.KW;
-    const int rd = r * a.dil, sd = s * a.dil;
-    if (DUAL && c0 >= a.C1) {
-      const int toff = (rd * a.W + sd) * a.ldx2 + (c0 - a.C1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        bool ok = mok[i];
-        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
-        const unsigned vo = ok ? (unsigned)((b2[i] + toff) * ES) : BUF_OOB;
-        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx2, vo, 0, 0));
-      }
-    } else {
-      const int toff = (rd * a.W + sd) * a.ldx + c0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        bool ok = mok[i];
-        if (PADCHK) ok = ok && (unsigned)(h0[i] + rd) < (unsigned)a.H && (unsigned)(w0[i] + sd) < (unsigned)a.W;
-        const unsigned vo = ok ? (unsigned)((b1[i] + toff) * ES) : BUF_OOB;
-        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, vb[i], k0 * ES, 0));
-  };
-  auto lds_store = [&](char* base, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rbase + 32 * i;
-      *(uint4*)(base + row * 128 + ((q ^ (row & 7)) << 4)) = ra[i];
-      *(uint4*)(base + 128 * 128 + row * 128 + ((q ^ (row & 7)) << 4)) = rb[i];
-    }
-  };
-  f32x4_t acc[4][4];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  };
-  // after computing flat step sidx from stage `st`: a finished tile's epilogue
-  // runs in that stage (free once every wave is past the next barrier)
-  auto finish = [&](int sidx, char* st) {
-    if (sidx - (sidx / nk) * nk != nk - 1) return;  // uniform
-    const int lin = r0 + jb + (sidx / nk) * gx;
-    const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-    conv_epilogue_stage<T>(a, acc, st, tid, mt, mt * 128, nt * 128);
-    zero_acc();
-    __syncthreads();
-  };
-
-  zero_acc();
-  gload(0, ra0, rb0);
-  gload(min(1, S - 1), ra1, rb1);
-  lds_store(smem, ra0, rb0);
-  __syncthreads();
-  for (int sidx = 0; sidx < S; sidx += 2) {
-    gload(min(sidx + 2, S - 1), ra0, rb0);
-    conv_mma<T>(smem, acc, wm, wn, lane);
-    lds_store(smem + SB, ra1, rb1);
-    __syncthreads();
-    finish(sidx, smem);
-    if (sidx + 1 >= S) break;
-    gload(min(sidx + 3, S - 1), ra1, rb1);
-    conv_mma<T>(smem + SB, acc, wm, wn, lane);
-    lds_store(smem, ra0, rb0);
-    __syncthreads();
-    finish(sidx + 1, smem + SB);
-  }
-}
-
 // INA: A-prologue activation (-1 = no prologue, else DMF_ACT_*)
 // FASTC: C (and the concat split C1) are multiples of BK, so every K-step
 // lies inside one filter tap: the tap/channel decode is block-uniform
@@ -1265,31 +1041,6 @@ __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
   conv_epilogue<T>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
-#include <cstdlib>
-// persistent 1x1 form: opt-in (DMF_CONV_PERS=1); measured slower than the
-// one-tile-per-block launch on the hot path's shapes (tools/conv_sweep.sh)
-static bool pers_disabled() {
-  static const int v = [] {
-    const char* e = std::getenv("DMF_CONV_PERS");
-    return e && e[0] == '1' ? 0 : 1;
-  }();
-  return v != 0;
-}
-static bool ina_buf_disabled() {
-  static const int v = [] {
-    const char* e = std::getenv("DMF_CONV_INA_BUF");
-    return e && e[0] == '0' ? 1 : 0;
-  }();
-  return v != 0;
-}
-static bool fast_disabled() {
-  static const int v = [] {
-    const char* e = std::getenv("DMF_CONV_LEGACY");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 // Which kernel/tile a forward launch uses. The buffer-load kernel needs C
 // (and C1) multiples of BK, no input prologue and < 2 GiB operands. Tile:
 // BN = 64 when Cout <= 64 (no wasted MFMA columns), BM = 64 when 128-row
@@ -1301,15 +1052,11 @@ struct ConvPlan {
   int bm, bn;
   bool ps;    // k_conv_fwd_ps (persistent LDS-DMA 256x256, register epilogue)
   bool pp;    // k_conv_fwd_pp (conv_pp.hip: ping-pong 8-phase 256x256, register epilogue)
-  bool p2;    // k_conv_fwd_ps at 128x128, two workgroups per CU (ps also set)
   bool stem;  // k_conv_stem (conv_stem.hip): 7x7 / 2 over 8 or 16 channels, 64 out
 };
 // 7 = ping-pong 256x256 form (conv_pp.hip): 0 off, 1 (default) for 3x3 and K >= 1024 (where it beats the
 // persistent form: tools/conv_bench.py --tunes, profiles/r03h_conv_ab.txt), 2 for every legal shape
 static int g_pp_mode = 1;
-// 9 = the persistent form at 128x128 with two workgroups per CU (one's epilogue runs under the other's
-// K loop; their vmcnt queues are separate): 0 off, 1 for 1x1 convs with K < 1024, 2 every legal shape
-static int g_p2_mode = 0;
 // 10 = the dedicated 7x7 stem kernel (conv_stem.hip) on (1, default) / off
 static int g_stem_enable = 1;
 // 11 = the statistics epilogue without bias adds / row masks for whole-tile launches (EPI 5) on / off
@@ -1322,33 +1069,16 @@ static int g_force = 0;
 // 3 = dmf_conv2d_fwd_acc accumulation mode (benchmarking; see acc_stats): 0 default
 static int g_stat_mode = 0;
 // 4 = persistent square form (k_conv_fwd_ps) on (1, default) / off
-static int g_ps_enable = [] {
-  const char* e = std::getenv("DMF_PS");
-  return e && e[0] == '0' ? 0 : 1;
-}();
+static int g_ps_enable = 1;
 // benchmarking bits of k_conv_fwd_ps (skip DMA / epilogue / stores / statistics): set only through
-// dmf_conv_tune key 6 by the A/B tools, never from the environment (a stray variable would
-// silently corrupt outputs)
+// dmf_conv_tune key 6 by the A/B tools (a stray setting would silently corrupt outputs)
 static int g_ps_dbg = 0;
-// tiles a launch needs before the wide (256x128) / square (256x256) forms take it: one per
+// 14 / 15 = tiles a launch needs before the wide (256x128) / square (256x256) forms take it: one per
 // CU. At 128 (half a tile per CU, the other encoder stream filling the rest) the two-stream
 // mode-A step measured -1.2 %, but every single-stream launch runs on half the GPU: config 2
 // (one stream) -14 %, conv-forward roofline fraction 0.27 -> 0.23 (profiles/r02s_bench.json)
-static long long g_wide_min_tiles = [] {
-  const char* e = std::getenv("DMF_WIDE_MIN_TILES");
-  return e ? std::atoll(e) : 256LL;
-}();
-static long long g_min_tiles = [] {
-  const char* e = std::getenv("DMF_SQ_MIN_TILES");
-  return e ? std::atoll(e) : 256LL;
-}();
-static bool wide_disabled() {
-  static const int v = [] {
-    const char* e = std::getenv("DMF_CONV_WIDE");
-    return e && e[0] == '0' ? 1 : 0;
-  }();
-  return v != 0;
-}
+static long long g_wide_min_tiles = 256;
+static long long g_min_tiles = 256;
 static int cu_count() {
   static int cached = 0;
   if (!cached) {
@@ -1361,7 +1091,7 @@ static int cu_count() {
 }
 
 static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
-  ConvPlan p{false, false, false, CBM, CBN, false, false, false, false};
+  ConvPlan p{false, false, false, CBM, CBN, false, false, false};
   if (g_stem_enable && conv_stem_ok(dtype, dgrad, a)) {
     p.stem = true;
     p.bm = conv_stem_m_tile(a);
@@ -1370,7 +1100,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   }
   const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
   // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
-  if (dgrad || fast_disabled() || (a.in_ss != nullptr && !(plain && a.x2 == nullptr && !ina_buf_disabled())))
+  if (dgrad || (a.in_ss != nullptr && !(plain && a.x2 == nullptr)))
     return p;
   const int es = dtype == DMF_BF16 ? 2 : 4;
   const int bk = dtype == DMF_BF16 ? 64 : 32;
@@ -1396,18 +1126,8 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
       return p;
     }
   }
-  // persistent 128x128, two workgroups per CU
-  if (dtype == DMF_BF16 && !wide_disabled() && g_p2_mode > 0 && a.tickets == nullptr && a.Nout % 128 == 0 &&
-      a.Ktot >= 64 && (long long)cdiv(a.M, 128) * (a.Nout / 128) >= 2LL * cu_count() &&
-      (long long)a.M * a.ldy * 2 < (1LL << 31) && (a.bias == nullptr || a.Nout <= 2048) &&
-      (g_p2_mode >= 2 || (a.KH * a.KW == 1 && a.Ktot < 1024))) {
-    p.wide = p.sq = p.ps = p.p2 = true;
-    p.bm = 128;
-    p.bn = 128;
-    return p;
-  }
   // ping-pong square tile: same legality as the persistent form below
-  const bool sq_ps_ok = dtype == DMF_BF16 && !wide_disabled() && a.tickets == nullptr && a.Nout % QBN == 0 &&
+  const bool sq_ps_ok = dtype == DMF_BF16 && a.tickets == nullptr && a.Nout % QBN == 0 &&
                         a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
                         (long long)a.M * a.ldy * 2 < (1LL << 31);
   if (sq_ps_ok && (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 1024 && a.KH * a.KW == 1)))) {
@@ -1418,7 +1138,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   }
   // persistent square LDS-DMA tile: whole 256-column tiles, >= one tile per CU, no fused-finalize
   // tickets, output addressable by a 32-bit buffer offset
-  if (dtype == DMF_BF16 && !wide_disabled() && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
+  if (dtype == DMF_BF16 && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
       a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
       (long long)a.M * a.ldy * 2 < (1LL << 31)) {
     p.wide = p.sq = p.ps = true;
@@ -1429,7 +1149,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   // square LDS-DMA tile: whole 256-column tiles and >= one block per CU
   // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
   // bound at one 256x256 block per CU and stays on the 256x128 form)
-  if (dtype == DMF_BF16 && !wide_disabled() && g_sq_enable && a.Nout % QBN == 0 &&
+  if (dtype == DMF_BF16 && g_sq_enable && a.Nout % QBN == 0 &&
       (a.KH * a.KW > 1 ? a.Ktot >= 512 : a.Ktot >= 2048) && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles) {
     p.wide = p.sq = true;
     p.bm = QBM;
@@ -1437,7 +1157,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
     return p;
   }
   // wide LDS-DMA tile: bf16, whole 128-column tiles, long enough K, >= one block per CU
-  if (dtype == DMF_BF16 && !wide_disabled() && a.Nout % WBN == 0 && a.Ktot >= 512 &&
+  if (dtype == DMF_BF16 && a.Nout % WBN == 0 && a.Ktot >= 512 &&
       (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= g_wide_min_tiles) {
     p.wide = true;
     p.bm = WBM;
@@ -1450,6 +1170,10 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   return p;
 }
 
+// the body the most recent forward / dgrad launch on this host thread ran (dmf_conv_last_form: tests
+// assert which forms a model-level parity run exercised)
+static thread_local int g_last_form = -1;
+
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
   const int epc = dtype == DMF_BF16 ? 8 : 4;
   DMF_CHECK_ARG(a.C % epc == 0 && a.ldx % epc == 0, "%s: input channels (%d) and stride (%d) must be multiples of %d",
@@ -1461,13 +1185,15 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   DMF_CHECK_ARG(a.M > 0 && a.Nout > 0 && a.Ktot > 0, "%s: empty problem (M=%d N=%d K=%d)", what, a.M, a.Nout,
                 a.Ktot);
   const ConvPlan plan = conv_plan(dtype, dgrad, a);
+  g_last_form = plan.stem ? DMF_FORM_STEM : dgrad ? DMF_FORM_IGEMM : plan.pp ? DMF_FORM_PP : plan.ps ? DMF_FORM_PS
+              : plan.sq ? DMF_FORM_SQ : plan.wide ? DMF_FORM_WIDE
+              : plan.buf ? (a.in_ss != nullptr ? DMF_FORM_BUF_INA : DMF_FORM_BUF) : DMF_FORM_IGEMM;
   a.mtiles = cdiv(a.M, plan.bm);
   a.ntiles = cdiv(a.Nout, plan.bn);
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = dtype == DMF_BF16 ? 2 : 4;
-  const size_t lds_total = plan.p2 ? (size_t)(2 * 256 * 128 + 2 * 128 * 2 * 4) + (a.bias ? (size_t)a.Nout * 4 : 0)
-                          : plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
+  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   const dim3 g((unsigned)nblk), b(CTHREADS);
@@ -1495,28 +1221,6 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
     DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st);
-  } else if (plan.p2) {
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const dim3 gp((unsigned)std::min<long long>(nblk, 2LL * cu_count())), bq(256);
-    // statistics without bias over whole tiles: the fast epilogue (EPI 5)
-    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 128 == 0) ? 5 : 0) : 1 + a.act;
-    a.dbg = g_ps_dbg;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
-#define DMF_P2(E)                                                                                                \
-  do {                                                                                                           \
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E, 128, 128, 2>), gp, bq, lds_total, st, a); \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E, 128, 128, 2>), gp, bq, lds_total, st, a);   \
-    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, 128, 128, 2>), gp, bq, lds_total, st, a);               \
-  } while (0)
-    switch (epi) {
-      case 0: DMF_P2(0); break;
-      case 1: DMF_P2(1); break;
-      case 2: DMF_P2(2); break;
-      case 3: DMF_P2(3); break;
-      case 5: DMF_P2(5); break;
-      default: DMF_P2(4); break;
-    }
-#undef DMF_P2
   } else if (plan.ps) {
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
@@ -1577,31 +1281,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     const bool dual = a.x2 != nullptr;
     const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
-    int ncu = 256;
-    {
-      static int cached = 0;
-      if (!cached) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cached <= 0) cached = 256;
-      }
-      ncu = cached;
-    }
-    const long long resident = 2LL * ncu;
-    // persistent form: measured to pay for 1x1 (plain) convs only
-    if (cfg == 3 && plain && !dual && a.tickets == nullptr && nblk > resident && !pers_disabled()) {
-      const dim3 gp((unsigned)resident);
-#define DMF_PERS_LAUNCH(TT)                                                                         \
-  do {                                                                                              \
-    if (dual) hipLaunchKernelGGL((k_conv_fwd_pers<TT, true, true>), gp, b, lds_total, st, a);       \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_pers<TT, false, false>), gp, b, lds_total, st, a); \
-    else hipLaunchKernelGGL((k_conv_fwd_pers<TT, true, false>), gp, b, lds_total, st, a);           \
-  } while (0)
-      if (dtype == DMF_BF16) DMF_PERS_LAUNCH(bf16_t);
-      else DMF_PERS_LAUNCH(float);
-#undef DMF_PERS_LAUNCH
-    } else if (dtype == DMF_BF16) {
+    if (dtype == DMF_BF16) {
       switch (cfg) {
         case 3: DMF_BUF_LAUNCH(bf16_t, 128, 128); break;
         case 2: DMF_BUF_LAUNCH(bf16_t, 128, 64); break;
@@ -1746,7 +1426,8 @@ using namespace dmf;
 
 extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
-int sgemm_tune(int deep_k);  // dense.hip
+extern "C" int dmf_conv_last_form(void) { return g_last_form; }
+
 int sgemm_tune_v4(int v4);   // dense.hip
 
 extern "C" int dmf_conv_tune(int key, int value) {
@@ -1759,11 +1440,11 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 6: g_ps_dbg = value; return 0;
     case 7: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ping-pong mode %d", value); g_pp_mode = value; return 0;
     case 8: return conv_pp_tune(value != 0);
-    case 9: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: two-workgroup mode %d", value); g_p2_mode = value; return 0;
     case 10: g_stem_enable = value != 0; return 0;
     case 11: g_fast_epi = value != 0; return 0;
-    case 12: return sgemm_tune(value);
     case 13: return sgemm_tune_v4(value);
+    case 14: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: wide min tiles %d", value); g_wide_min_tiles = value; return 0;
+    case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1791,7 +1472,6 @@ extern "C" int dmf_conv2d_fwd_stat_tiles(int dtype, int N, int H, int W, int Cin
 // buffer-load tile as without it -- i.e. the unfused launch would not pick
 // the 256-wide LDS-DMA tiles, which have no input-affine form
 extern "C" int dmf_conv2d_fwd_input_affine_fusable(int dtype, int N, int H, int W, int Cin, int Cout) {
-  if (ina_buf_disabled()) return 0;
   ConvArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = Cin; a.C1 = Cin;
   a.Nout = Cout; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0; a.Ktot = Cin; a.M = N * H * W;

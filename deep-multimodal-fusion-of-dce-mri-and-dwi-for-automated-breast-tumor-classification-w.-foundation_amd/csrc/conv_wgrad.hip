@@ -908,30 +908,24 @@ static inline int gsz(long long n) {
 
 using namespace dmf;
 
-static int wgrad_tr_enabled() {
-  static int v = [] {
-    const char* e = std::getenv("DMF_WGRAD_TR");
-    return e && e[0] == '0' ? 0 : (e && e[0] == '2' ? 2 : 1);
-  }();
-  return v;
-}
-
-// LDS-DMA staging for the bf16 transposed-read weight gradient (k_conv_wgrad_dma);
-// DMF_WGRAD_DMA=0 keeps the register-staged k_conv_wgrad_tr, dmf_conv_wgrad_tune(0, v) switches at run time
-static int g_wgrad_dma = [] {
-  const char* e = std::getenv("DMF_WGRAD_DMA");
-  return e && e[0] == '0' ? 0 : 1;
-}();
+// bf16 weight-gradient forms (dmf_conv_wgrad_tune): key 2 = transposed-read kernels on (1, default: the
+// LDS-DMA form below), 2 = its 128 x 256 register-staged variant, 0 = the plain gather kernel; key 0 = LDS-DMA
+// staging (k_conv_wgrad_dma, default) vs register-staged k_conv_wgrad_tr; key 1 = the 128 x 256 LDS-DMA tile
+// for 1x1 convs with K <= 1024 (default on)
+static int g_wgrad_tr = 1;
+static int wgrad_tr_enabled() { return g_wgrad_tr; }
+static int g_wgrad_dma = 1;
 static int wgrad_dma_enabled() { return g_wgrad_dma; }
-static int g_wgrad_wide = [] {
-  const char* e = std::getenv("DMF_WGRAD_WIDE");
-  return e && e[0] == '0' ? 0 : 1;
-}();
+static int g_wgrad_wide = 1;
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
-  DMF_CHECK_ARG(key == 0 || key == 1, "dmf_conv_wgrad_tune: unknown key %d", key);
+  DMF_CHECK_ARG(key >= 0 && key <= 2, "dmf_conv_wgrad_tune: unknown key %d", key);
   if (key == 0) g_wgrad_dma = value != 0;
-  else g_wgrad_wide = value != 0;
+  else if (key == 1) g_wgrad_wide = value != 0;
+  else {
+    DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_wgrad_tune: transposed-read mode %d", value);
+    g_wgrad_tr = value;
+  }
   return 0;
 }
 

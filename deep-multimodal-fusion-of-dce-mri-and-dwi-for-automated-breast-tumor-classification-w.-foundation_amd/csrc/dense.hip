@@ -40,9 +40,8 @@ __device__ __forceinline__ float actf(int act, float z) {
 // [z*kchunk, (z+1)*kchunk); with gridDim.z > 1 each split stores its
 // partial tile into ws[z][M][N] and k_sgemm_reduce sums the splits in a
 // fixed order and applies alpha, bias and act (deterministic).
-// BK = K rows staged per barrier: 16, or 64 for K >= 64 when enabled (the
-// fusion's 128-deep token linears: 2 global-latency rounds instead of 8;
-// measured neutral on the step, see g_sgemm_deep)
+// BK = K rows staged per barrier (16; a 64-deep form measured neutral on the
+// mode-A step, interleaved A/B 3108 vs 3100 vol/s, and was removed)
 // V4: each thread owns 4 consecutive rows x 4 consecutive columns, so its A and B fragments are two
 // 16-B LDS reads per k (the strided 4 x 4 mapping issued 8 scalar reads); V4 = false keeps the
 // strided form (A/B, dmf_conv_tune key 13)
@@ -890,14 +889,7 @@ static int sgemm_splits(int M, int N, int K) {
   return std::max(1, cdiv(K, kchunk));
 }
 
-// 64-deep K staging where K allows (dmf_conv_tune key 12): measured neutral on the mode-A step
-// (interleaved A/B, 3108 vs 3100 vol/s), off by default
-static bool g_sgemm_deep = false;
 static bool g_sgemm_v4 = false;  // vector 4 x 4 micro-tile (dmf_conv_tune key 13)
-int sgemm_tune(int deep_k) {
-  g_sgemm_deep = deep_k != 0;
-  return 0;
-}
 int sgemm_tune_v4(int v4) {
   g_sgemm_v4 = v4 != 0;
   return 0;
@@ -919,10 +911,7 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);
   S = S > 1 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
-  if (kchunk >= 64 && g_sgemm_deep)
-    hipLaunchKernelGGL((k_sgemm<64, true>), grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda,
-                       B, ldb, beta, C, ldc, bias, act, workspace);
-  else if (g_sgemm_v4)
+  if (g_sgemm_v4)
     hipLaunchKernelGGL((k_sgemm<16, true>), grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda,
                        B, ldb, beta, C, ldc, bias, act, workspace);
   else

@@ -7,7 +7,7 @@ Replaces the Lightning Trainer that ``run_training.run_fusion_model``
   * the gradients of every trainable parameter go to ONE flat fp32 bucket
     that the AdamW kernel reads directly with scale 1/world (no unpack pass);
   * with RCCL (backend "nccl") the exchange OVERLAPS the backward: the bucket
-    is laid out in gradient-ready order and cut into ~DMF_DP_BUCKET_MB
+    is laid out in gradient-ready order and cut into ~bucket_mb (32 MB)
     segments; a post-accumulate-grad hook launches pack + ``all_reduce`` of a
     segment on a communication stream the moment its last gradient lands,
     while autograd keeps computing the earlier layers' gradients (fusion
@@ -24,6 +24,7 @@ Replaces the Lightning Trainer that ``run_training.run_fusion_model``
 from __future__ import annotations
 
 import os
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -35,17 +36,16 @@ def dist_env():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
-# a comm stream forked from the concurrent DCE encoder stream during capture
-# (a fork of a fork): torch 2.10 + HIP 7 crash at capture end on such a
-# topology with aten kernels on the nested stream (tools/capture_fork_probe.py),
-# so by default those segments are launched after backward instead
-NESTED_FORK_OK = os.environ.get("DMF_DP_NESTED_FORK", "0") == "1"
-# PREFORK (default): the comm stream is forked from the step's stream when
-# backward begins, so a segment produced on the DCE encoder's stream only adds
-# an event edge into an already-forked branch (no fork of a fork) and overlaps
-# the rest of backward inside the captured graph too
-# (tests/test_gpu_dp.py::test_overlapped_segment_allreduce_captured[B-True])
-PREFORK = os.environ.get("DMF_DP_PREFORK", "1") == "1"
+# PREFORK (knob "dp_prefork", default): the comm stream is forked from the step's
+# stream when backward begins, so a segment produced on the DCE encoder's stream
+# only adds an event edge into an already-forked branch and overlaps the rest of
+# backward inside the captured graph too
+# (tests/test_gpu_dp.py::test_overlapped_segment_allreduce_captured[B-True]).
+# Without it such segments are deferred to the end of backward during capture: a
+# comm stream forked from the concurrent DCE encoder stream (a fork of a fork)
+# crashes torch 2.10 + HIP 7 at capture end when aten kernels run on the nested
+# stream (tools/capture_fork_probe.py)
+PREFORK = True
 
 
 def rank_strided_indices(n_items, rank, world, epoch=0, shuffle=False, seed=0):
@@ -111,7 +111,7 @@ class FusionTrainer:
         # overlap=True with world=1 runs the same hooks / segments / captured
         # collectives over a 1-rank communicator (the single-GPU test of the path)
         self.overlap = bool(overlap)
-        mb = bucket_mb if bucket_mb is not None else float(os.environ.get("DMF_DP_BUCKET_MB", "32"))
+        mb = bucket_mb if bucket_mb is not None else 32.0
         self.segment_bytes = int(mb * (1 << 20))
         self._hooks = []
         self._ready_order = []
@@ -138,6 +138,8 @@ class FusionTrainer:
         self._graph_sig = None
         self.loss = None
         self.captures = 0
+        self.eager_steps = 0  # steps that ran eagerly beside a captured graph (shape mismatch)
+        self.early_segments = 0
 
     # ------------------------------------------------------------ signature
     def _trainable(self):
@@ -156,9 +158,10 @@ class FusionTrainer:
             h.remove()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self._trainable()]
         # conv weights and BN gamma / beta get their gradients through grad_sink (no AccumulateGrad,
-        # so no post-accumulate hook): the sink path reports them once their kernels are enqueued
-        if self._on_grad not in O.SINK_HOOKS:
-            O.SINK_HOOKS.append(self._on_grad)
+        # so no post-accumulate hook): the sink path reports them once their kernels are enqueued.
+        # Registered weakly: a dropped trainer (and its model / optimizer) is not kept alive by the
+        # module-global list
+        O.add_sink_hook(self._on_grad)
         self._fires = {}
 
     def _on_grad(self, p):
@@ -186,8 +189,7 @@ class FusionTrainer:
         backward while a graph is being captured: a fork from a forked stream
         breaks capture end on this stack."""
         cur = torch.cuda.current_stream()
-        if (torch.cuda.is_current_stream_capturing() and cur != self._origin and not NESTED_FORK_OK
-                and not PREFORK):
+        if torch.cuda.is_current_stream_capturing() and cur != self._origin and not PREFORK:
             self._deferred.append(k)
             return
         self._launched.add(k)
@@ -215,6 +217,9 @@ class FusionTrainer:
 
     def _end_backward(self):
         self._armed = False
+        # segments whose exchange was launched from inside backward (overlapped); of a captured step,
+        # this is the count its graph holds
+        self.early_segments = len(self._launched)
         if not self._bucket_ready or self._bucket_sig != self._signature()[:2]:
             self._setup_bucket()
         # segments whose params got no gradient this step, and deferred ones
@@ -234,6 +239,13 @@ class FusionTrainer:
             self._end_backward()
         else:
             bwd(loss)
+        import dmf_ops as O
+
+        if O.GRAD_STASH:
+            # a full backward consumes every shortcut-gradient hand-off (dmf_ops.conv_bn_act)
+            n = len(O.GRAD_STASH)
+            O.GRAD_STASH.clear()
+            raise RuntimeError(f"{n} shortcut gradient hand-off(s) left undelivered by the training backward")
         return loss
 
     def _exchange_and_update(self):
@@ -273,7 +285,11 @@ class FusionTrainer:
         self._bucket_sig = self._signature()[:2]
 
     def eager_step(self, batch):
-        if self.overlap and (not self._hooks or self._bucket_sig != self._signature()[:2]):
+        if self.overlap and (not self._hooks or not self._bucket_ready or self._bucket_sig != self._signature()[:2]):
+            # a (re-)learning step: fresh hooks and per-parameter ready-event counts. Every re-capture
+            # (aux-loss gate flip, optimizer tables) clears _bucket_ready and lands here, so its warm-up
+            # never adds a second round of counts on top of the old ones (doubled
+            # _pending totals never reach 0 and every segment would wait for _end_backward)
             self._install_hooks()
             self._bucket_ready = False
             self._ready_order = []
@@ -389,22 +405,39 @@ class FusionTrainer:
         self._graph_sig = self._signature()
         self.captures += 1
 
+    def _rows(self, batch):
+        return batch[0].shape[0] if batch is not None else 0
+
     def step(self, batch=None):
         if self.graphs is not None and self._graph_sig != self._signature():
             # unfreeze / new param group / reloaded optimizer: the captured
-            # pointers are stale -- rebuild the bucket and capture again
+            # pointers are stale -- rebuild the bucket and capture again, on a
+            # full-size batch: a ragged one (an epoch's last) would make every later
+            # full batch miss the captured shapes; the previous static batch is
+            # full-size, and capture leaves the training state untouched
             self.graphs = None
             self._bucket_ready = False
             if self.use_graph:
-                self.capture(batch if batch is not None else self.static_batch)
+                full = batch if self._rows(batch) >= self._rows(self.static_batch) else self.static_batch
+                self.capture(full)
         if self.graphs is None:
             if self.use_graph and self.captures == 0 and batch is not None:
                 self.capture(batch)
             else:
                 return self.eager_step(batch)
         if batch is not None and any(a.shape != b.shape for a, b in zip(batch, self.static_batch)):
-            # a ragged batch (an epoch's last one): the captured shapes do not apply -- run it eagerly
-            return self.eager_step(batch)
+            if self.use_graph and self._rows(batch) > self._rows(self.static_batch):
+                # the first capture landed on a short batch: capture again on this larger one, so the
+                # full-size batches replay instead of falling back to eager for the rest of training
+                warnings.warn(f"re-capturing the training step: batch of {self._rows(batch)} volumes after a capture "
+                              f"on {self._rows(self.static_batch)}", RuntimeWarning)
+                self.graphs = None
+                self._bucket_ready = False
+                self.capture(batch)
+            else:
+                # a ragged batch (an epoch's last one): the captured shapes do not apply -- run it eagerly
+                self.eager_steps += 1
+                return self.eager_step(batch)
         if batch is not None and batch[0].data_ptr() != self.static_batch[0].data_ptr():
             for dst, src in zip(self.static_batch, batch):
                 dst.copy_(src, non_blocking=True)

@@ -131,18 +131,24 @@ class FusionFit:
             nsum = torch.zeros((), dtype=torch.float64, device=lm.device)
             for idx, ok in _batches(items, valid, self.batch_size):
                 nv = sum(ok)
+                pad = len(idx) - nv
+                flags.append(torch.tensor(ok, dtype=torch.uint8, device=lm.device))
+                if nv == 0:
+                    # a batch of padding copies only (e.g. n_val=65, world=2, batch 32: rank 1's last
+                    # batch): nothing to score, but every rank must gather the same row count
+                    probs.append(torch.zeros(pad, lm.class_num, dtype=torch.float32, device=lm.device))
+                    labels.append(torch.zeros(pad, dtype=torch.long, device=lm.device))
+                    continue
                 # padding copies sit only at the end of the last batch: score the valid prefix
                 batch = _take(self.val_data, idx[:nv], lm.device)
                 loss, logits, _, _ = lm._shared_step(batch, phase="val", return_preds=True)
                 wsum += loss.double() * nv
                 nsum += nv
                 p = torch.softmax(logits.float(), dim=1)
-                pad = len(idx) - nv
                 if pad:
                     p = torch.cat([p, p.new_zeros(pad, p.shape[1])], 0)
                 probs.append(p)
                 labels.append(torch.cat([batch[-1].long(), batch[-1].new_zeros(pad).long()]))
-                flags.append(torch.tensor(ok, dtype=torch.uint8, device=lm.device))
             probs = torch.cat(probs, 0)
             labels = torch.cat(labels, 0)
             flags = torch.cat(flags, 0)

@@ -25,6 +25,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dmf_hip.h")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3
+# conv kernel bodies (dmf_conv_last_form, include/dmf_hip.h DMF_FORM_*)
+FORMS = {0: "igemm", 1: "buf", 2: "buf_ina", 3: "wide", 4: "sq", 5: "ps", 6: "pp", 7: "stem"}
 
 _lib = None
 _lock = threading.Lock()

@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import itertools
 import math
-import os
+import warnings
 import weakref
 
 import torch
@@ -137,7 +137,7 @@ class PrepPlan:
         self.gen = 0
         self.fresh = False
         self.tables = {}  # (device, signature) -> (jobs tensor, blk tensor, nblocks)
-        self.enabled = os.environ.get("DMF_PREP_PLAN", "1") != "0"
+        self.enabled = True  # knob "prep_plan" (set_knobs)
 
     class Entry:
         __slots__ = ("ref", "out", "version", "gen", "serial")
@@ -289,7 +289,8 @@ def _conv_launch(fn, args, keep, x, n, h, w, cxt, co, kh, kw, g, ho, wo):
         flops = 2.0 * n * ho * wo * co * k_tot
         byts = es * (n * h * w * cxt + co * k_tot + n * ho * wo * co)
         probe.append({"fn": fn, "args": args, "keep": keep, "flops": flops, "bytes": byts,
-                      "shape": (n, h, w, cxt, co, kh, g.stride, g.dil)})
+                      "shape": (n, h, w, cxt, co, kh, g.stride, g.dil),
+                      "form": N.FORMS.get(N.load().dmf_conv_last_form(), "?")})
 
 
 def _is_mfma_conv(weight, g):
@@ -351,13 +352,13 @@ def _conv_forward_raw(x, weight, bias, g, caches, want_stats, act, out=None, x2=
     return y, partials
 
 
-DGRAD_AS_FWD = os.environ.get("DMF_DGRAD_FWD", "1") != "0"
+DGRAD_AS_FWD = True  # knob "dgrad_as_fwd": stride-1 dgrad on the forward kernels
 # no-grad forwards: a BN apply + activation feeding a 1x1 conv runs in that
 # conv's loads (conv_bn_stats + in_ss) instead of its own pass. Opt-in
-# (DMF_FUSE_INA=1): measured 1-2 % slower on the mode-A step (r01zi: 2470 vs
+# (knob "fuse_input_affine"): measured 1-2 % slower on the mode-A step (r01zi: 2470 vs
 # 2500 vol/s) -- the affine on the load path costs the 128x128 buffer-load
 # tile more than the saved BN-apply pass
-FUSE_INPUT_AFFINE = os.environ.get("DMF_FUSE_INA", "0") == "1"
+FUSE_INPUT_AFFINE = False
 FUSED_BN_MAX_MTILES = 32
 
 def fuse_input_affine(x, producer, consumer, *params):
@@ -438,6 +439,13 @@ class bn_scope:
     def __enter__(self):
         if ARENA[0] is not None or self.device.type != "cuda":
             return self
+        if GRAD_STASH:
+            # a backward that reached a block but was pruned before the block input's producer
+            # (torch.autograd.grad(..., inputs=[intermediate]), a checkpoint boundary) left a handed-over
+            # shortcut gradient undelivered: say so, and do not leak it into this forward's backward
+            warnings.warn(f"{len(GRAD_STASH)} shortcut gradient hand-off(s) of an earlier backward were never "
+                          "consumed (partial backward?); dropped", RuntimeWarning)
+            GRAD_STASH.clear()
         key = "_dmf_bn_arena"
         ar = self.owner.__dict__.get(key)
         if ar is None or ar.device != self.device:
@@ -613,8 +621,22 @@ def _col_stats(y):
 # callables(param) told that a sink-accumulated gradient (grad_sink) has been ENQUEUED on the current
 # stream -- the post-accumulate-grad hooks never fire for such parameters (autograd gets None), so the
 # data-parallel trainer's overlapped exchange listens here too (dmf_dp.FusionTrainer)
-SINK_HOOKS = []
+SINK_HOOKS = []  # weakref.WeakMethod / weakref.ref entries (add_sink_hook)
 _SINK_PENDING = []
+
+
+def add_sink_hook(fn):
+    """Register fn(param) in SINK_HOOKS without keeping its owner alive (bound
+    methods are held by weakref.WeakMethod); registering the same callable
+    twice is a no-op."""
+    ref = weakref.WeakMethod(fn) if hasattr(fn, "__self__") else weakref.ref(fn)
+    if all(r() != fn for r in SINK_HOOKS):
+        SINK_HOOKS.append(ref)
+    return ref
+
+
+def remove_sink_hook(fn):
+    SINK_HOOKS[:] = [r for r in SINK_HOOKS if r() is not None and r() != fn]
 
 
 def grad_sink(p):
@@ -640,7 +662,12 @@ def flush_sinks():
     if _SINK_PENDING:
         ps = list(_SINK_PENDING)
         _SINK_PENDING.clear()
-        for h in list(SINK_HOOKS):
+        live = [r() for r in SINK_HOOKS]
+        if any(h is None for h in live):
+            SINK_HOOKS[:] = [r for r, h in zip(SINK_HOOKS, live) if h is not None]
+        for h in live:
+            if h is None:
+                continue
             for p in ps:
                 h(p)
 
@@ -749,12 +776,21 @@ def _conv_backward(x, weight, bias, g, caches, dy, need_dx, need_dw, need_db, x2
                 ct = cx + cx2
                 splits = N.load().dmf_conv2d_wgrad_splits(dtc, co, ct, kh, kw, m)
                 ws = torch.empty(splits * co * kh * kw * ct, dtype=torch.float32, device=dev)
-                N.call("dmf_conv2d_wgrad", dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, dy.data_ptr(), ho,
-                       wo, co, lddy, kh, kw, g.stride, g.pad, g.dil, splits, ws.data_ptr(), _stream())
+                wargs = (dtc, x.data_ptr(), n, h, w, cx, ldx, _p(x2), cx2, ldx2, dy.data_ptr(), ho, wo, co, lddy, kh,
+                         kw, g.stride, g.pad, g.dil, splits, ws.data_ptr())
+                N.call("dmf_conv2d_wgrad", *wargs, _stream())
                 dwt = grad_sink(weight) if dw_sink else torch.empty((co, ci, kh, kw), dtype=torch.float32,
                                                                       device=dev)
-                N.call("dmf_conv2d_wgrad_reduce", ws.data_ptr(), splits, co, ci, ct, kh, kw, dwt.data_ptr(),
-                       1 if dw_sink else 0, _stream())
+                rargs = (ws.data_ptr(), splits, co, ci, ct, kh, kw, dwt.data_ptr(), 1 if dw_sink else 0)
+                N.call("dmf_conv2d_wgrad_reduce", *rargs, _stream())
+                probe = PROBE["conv_wgrad"]
+                if probe is not None:
+                    es = x.element_size()
+                    k_tot = kh * kw * ct
+                    probe.append({"calls": (("dmf_conv2d_wgrad", wargs), ("dmf_conv2d_wgrad_reduce", rargs)),
+                                  "keep": (x, x2, dy, ws, dwt), "flops": 2.0 * m * co * k_tot,
+                                  "bytes": es * (n * h * w * ct + m * co) + 4 * co * k_tot,
+                                  "shape": (n, h, w, ct, co, kh, g.stride, g.dil)})
                 dw = None if dw_sink else dwt
             if need_db:
                 db = _colsum_nhwc(dy, grad_sink(bias) if dw_sink else None)
@@ -951,8 +987,8 @@ class _ConvBNActFn(torch.autograd.Function):
 
 
 # backward BN column sums into the forward's statistics arena (no finalize launch);
-# DMF_BWD_BN_ARENA=0 restores the per-tile slab + finalize form
-BWD_BN_ARENA = os.environ.get("DMF_BWD_BN_ARENA", "1") != "0"
+# knob "bwd_bn_arena" = False restores the per-tile slab + finalize form
+BWD_BN_ARENA = True
 
 
 def _bn_backward(dz, y, save, bn, dgamma, dbeta, training=True, part=None):
@@ -1024,8 +1060,8 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
 # conv_bn_act, or the projection's input gradient) is parked here under the key of the conv_bn_act
 # that produced the block input; that producer's backward sums it with the gradient autograd hands
 # it inside dmf_act_bwd_bn_reduce(_acc) (dy2), so the block input's gradient is never formed by a
-# separate bf16 add pass. DMF_SHORTCUT_HANDOFF=0 restores the autograd add.
-SHORTCUT_HANDOFF = os.environ.get("DMF_SHORTCUT_HANDOFF", "1") == "1"
+# separate bf16 add pass. Knob "shortcut_handoff" = False restores the autograd add.
+SHORTCUT_HANDOFF = True
 GRAD_STASH = {}
 _GKEYS = itertools.count(1)
 
@@ -1115,14 +1151,6 @@ class _LinearFn(torch.autograd.Function):
         y = torch.empty((r, nout), dtype=torch.float32, device=x.device)
         wc = w.detach().contiguous()
         x = x.float()
-        if _linear_mfma(k, nout) and x.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0:
-            # exact f32 MFMA GEMM with bias + activation (+ the pre-activation for backward) in its epilogue
-            pre = torch.empty_like(y) if act != "none" else None
-            _gemm_f32(0, 0, r, nout, k, x.data_ptr(), k, wc.data_ptr(), k, y.data_ptr(), nout, bias=_p(b),
-                      act=ACT[act], aux=_p(pre), ldaux=nout)
-            ctx.save_for_backward(x, w, b, pre)
-            ctx.act = act
-            return y
         _sgemm(0, 1, r, nout, k, 1.0, x.data_ptr(), k, wc.data_ptr(), k, 0.0, y.data_ptr(), nout, _p(b),
                N.ACT_NONE, _stream())
         pre = y
@@ -1148,25 +1176,16 @@ class _LinearFn(torch.autograd.Function):
             dpre = dy
         dx = dw = db = None
         wc = w.detach().contiguous()
-        mfma = (_linear_mfma(k, nout) and r % 4 == 0 and x.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0
-                and dpre.data_ptr() % 16 == 0)
         if ctx.needs_input_grad[0]:
             dx = torch.empty((r, k), dtype=torch.float32, device=x.device)
-            if mfma:  # dX = dpre [r x nout] . W [nout x k]
-                _gemm_f32(0, 1, r, k, nout, dpre.data_ptr(), nout, wc.data_ptr(), k, dx.data_ptr(), k)
-            else:
-                _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
-                       None, N.ACT_NONE, _stream())
+            _sgemm(0, 0, r, k, nout, 1.0, dpre.data_ptr(), nout, wc.data_ptr(), k, 0.0, dx.data_ptr(), k,
+                   None, N.ACT_NONE, _stream())
         # leaf parameters: the weight / bias gradients accumulate straight into p.grad (grad_sink:
         # no AccumulateGrad add per parameter; in_proj's two uses per step just add twice)
         sink = (LINEAR_SINK and _sinkable(w, b) and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32)
                 and ctx.needs_input_grad[1] and (b is None or ctx.needs_input_grad[2]))
         if ctx.needs_input_grad[1]:
-            if sink and mfma:  # dW += dpre^T [nout x r] . x [r x k] (the GEMM's residual input aliases dW)
-                g = grad_sink(w)
-                _gemm_f32(1, 1, nout, k, r, dpre.data_ptr(), nout, x.data_ptr(), k, g.data_ptr(), k,
-                          res=g.data_ptr(), ldr=k)
-            elif sink:
+            if sink:
                 _sgemm(1, 0, nout, k, r, 1.0, dpre.data_ptr(), nout, x.data_ptr(), k, 1.0, grad_sink(w).data_ptr(),
                        k, None, N.ACT_NONE, _stream())
             else:
@@ -1185,25 +1204,19 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
-LINEAR_SINK = os.environ.get("DMF_LINEAR_SINK", "1") != "0"  # A/B knob
-# A/B knob: fp32 linears on the f32 MFMA GEMM -- parity-green, measured 5.6 % slower on the mode-A step
-# (interleaved A/B: 2953 vs 3124 vol/s; latency-bound big tiles on 512-row token problems), off
-LINEAR_MFMA = os.environ.get("DMF_LINEAR_MFMA", "0") == "1"
-
-
-def _linear_mfma(k, nout):
-    return LINEAR_MFMA and k % 4 == 0 and nout % 4 == 0
+# knob "linear_sink": Linear / LayerNorm / SE parameter gradients accumulated in place (grad_sink).
+# (The fp32 linears on the exact f32 MFMA GEMM were measured 5.6 % slower on the mode-A step --
+# interleaved A/B 2953 vs 3124 vol/s, big tiles latency-bound on 512-row token problems -- and removed.)
+LINEAR_SINK = True
 
 
 def _gemm_f32(ta, tb, M, N_, K, A, lda, B, ldb, C, ldc, bias=None, act=0, aux=None, ldaux=0, res=None, ldr=0):
     """dmf_gemm_f32, unbatched: C = act(op(A) op(B) + bias) [+ res], aux = pre-activation."""
     N.call("dmf_gemm_f32", N.F32, ta, tb, M, N_, K, 1.0, A, lda, 0, 0, B, ldb, 0, 0, C, ldc, 0, 0, 1, 1, bias, act,
            None, res, ldr, aux, ldaux, None, 0, 0.0, None, 0, None, _stream())
-if os.environ.get("DMF_SGEMM_DEEP", "0") == "1":  # A/B knob: 64-deep K staging in the fp32 GEMMs
-    N.call("dmf_conv_tune", 12, 1)
-if os.environ.get("DMF_SGEMM_V4", "0") == "1":  # A/B knob: the vector 4 x 4 fp32 GEMM micro-tile
-    N.call("dmf_conv_tune", 13, 1)
-SE_FUSED = os.environ.get("DMF_SE_FUSED", "1") != "0"  # A/B knob
+
+
+SE_FUSED = True  # knob "se_fused": the one-launch SE excitation (dmf_se_mlp)
 
 
 def _act_f32(x, out, act):
@@ -2218,7 +2231,7 @@ class _MimicFn(torch.autograd.Function):
 
 # the Philox snapshot shared by the dropout sites of one top-level forward
 # ------------------------------------------------------ concurrent branches
-PARALLEL_BRANCHES = os.environ.get("DMF_PAR_ENC", "1") != "0"
+PARALLEL_BRANCHES = True  # knob "parallel_encoders": the DCE encoder on a second stream
 
 
 def record_tree(obj, stream):
@@ -2368,8 +2381,11 @@ def mimic_pairs(feats, npairs=2):
 
 
 # bench.py's roofline probe: when PROBE["conv_fwd"] is a list, every MFMA conv
-# forward launch appends its record (see _conv_launch).
-PROBE = {"conv_fwd": None}
+# forward launch appends its record (see _conv_launch); PROBE["conv_wgrad"] the
+# same for every MFMA weight gradient (dmf_conv2d_wgrad + its split reduce, one
+# record holding both calls)
+PROBE = {"conv_fwd": None, "conv_wgrad": None, "tok_gemm": None, "fp8_gemm": None}
+# (tok_gemm: dmf_tokens.gemm launches; fp8_gemm: the e4m3 patch-embed GEMM -- config 5's rooflines)
 
 
 def probe_replay(recs, reps=3):
@@ -2382,7 +2398,8 @@ def probe_replay(recs, reps=3):
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for r in items:
-                N.call(r["fn"], *r["args"], _stream())
+                for fn, args in (r["calls"] if "calls" in r else ((r["fn"], r["args"]),)):
+                    N.call(fn, *args, _stream())
         return graph
 
     def timed(graph):
@@ -2404,3 +2421,57 @@ def probe_replay(recs, reps=3):
     for shp, items in groups.items():
         per.append((shp, len(items), timed(capture(items)) / len(items)))
     return total / len(recs), per
+
+
+# ------------------------------------------------------------------ knobs
+# Switches between measured variants. The package reads none of them from the
+# environment: an A/B tool or a test sets them from code (set_knobs; bench.py
+# --knob NAME=VALUE). Each is listed with its test in DESIGN.md "Knobs".
+# name -> (module, attribute) for Python switches, ("tune", key) / ("wgrad_tune", key)
+# for the library's run-time tunables (dmf_conv_tune / dmf_conv_wgrad_tune).
+KNOBS = {
+    "prep_plan": ("dmf_ops", "PREP.enabled"),
+    "dgrad_as_fwd": ("dmf_ops", "DGRAD_AS_FWD"),
+    "fuse_input_affine": ("dmf_ops", "FUSE_INPUT_AFFINE"),
+    "bwd_bn_arena": ("dmf_ops", "BWD_BN_ARENA"),
+    "shortcut_handoff": ("dmf_ops", "SHORTCUT_HANDOFF"),
+    "linear_sink": ("dmf_ops", "LINEAR_SINK"),
+    "se_fused": ("dmf_ops", "SE_FUSED"),
+    "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),
+    "parallel_dead": ("model_module", "PARALLEL_DEAD"),
+    "device_loss": ("train_fusion", "DEVICE_LOSS"),
+    "dp_prefork": ("dmf_dp", "PREFORK"),
+    "conv_sq": ("tune", 0),
+    "conv_sq_var": ("tune", 1),
+    "conv_ps": ("tune", 4),
+    "conv_pp_mode": ("tune", 7),
+    "conv_pp_persist": ("tune", 8),
+    "conv_stem": ("tune", 10),
+    "conv_fast_epi": ("tune", 11),
+    "sgemm_v4": ("tune", 13),
+    "conv_wide_min_tiles": ("tune", 14),
+    "conv_sq_min_tiles": ("tune", 15),
+    "wgrad_dma": ("wgrad_tune", 0),
+    "wgrad_wide": ("wgrad_tune", 1),
+    "wgrad_tr": ("wgrad_tune", 2),
+}
+
+
+def set_knobs(**kw):
+    """set_knobs(name=value, ...): flip measured variants from code (A/B tools, tests)."""
+    import importlib
+
+    for name, value in kw.items():
+        if name not in KNOBS:
+            raise ValueError(f"unknown knob {name!r}; known: {sorted(KNOBS)}")
+        where, attr = KNOBS[name]
+        if where == "tune":
+            N.call("dmf_conv_tune", attr, int(value))
+        elif where == "wgrad_tune":
+            N.call("dmf_conv_wgrad_tune", attr, int(value))
+        else:
+            obj = importlib.import_module(where)
+            *path, last = attr.split(".")
+            for p in path:
+                obj = getattr(obj, p)
+            setattr(obj, last, bool(int(value)) if isinstance(value, (str, int)) else value)

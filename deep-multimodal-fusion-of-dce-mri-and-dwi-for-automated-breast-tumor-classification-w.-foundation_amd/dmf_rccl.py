@@ -37,6 +37,7 @@ def _lib():
     lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p]
     lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+    lib.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     lib.ncclGetErrorString.argtypes = [ctypes.c_int]
     lib.ncclGetErrorString.restype = ctypes.c_char_p
     return lib
@@ -76,6 +77,12 @@ class RcclComm:
         self._check(self.lib.ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_FLOAT32, NCCL_SUM,
                                            self.comm, s), "ncclAllReduce")
         return t
+
+    def count(self):
+        """Ranks of the communicator as RCCL reports them (ncclCommCount)."""
+        n = ctypes.c_int(0)
+        self._check(self.lib.ncclCommCount(self.comm, ctypes.byref(n)), "ncclCommCount")
+        return n.value
 
     def close(self):
         if self.comm:

@@ -48,14 +48,22 @@ def gemm(out, a, b, M, Nn, K, ta=0, tb=0, lda=None, ldb=None, ldc=None, batch=(1
         if t is not None and t.dtype != a.dtype:
             raise TypeError("gemm: aux / pre must have the operand dtype")
     esz_c = out.element_size()
-    N.call(fn, F32 if out.dtype == torch.float32 else BF16, int(ta), int(tb), int(M), int(Nn), int(K),
-           float(alpha), a.data_ptr() + esz * a_off, int(lda), int(sa[0]), int(sa[1]),
-           b.data_ptr() + esz * b_off, int(ldb), int(sb[0]), int(sb[1]),
-           out.data_ptr() + esz_c * c_off, int(ldc), int(sc[0]), int(sc[1]), int(batch[0]), int(batch[1]),
-           O._p(bias), O.ACT[act], O._p(colscale), O._p(res), int(res.stride(0)) if res is not None else 0,
-           O._p(aux), int(aux.stride(0)) if aux is not None else 0,
-           O._p(pre), int(pre.stride(0)) if pre is not None else 0,
-           float(dropout_p), O._p(rng), int(site), O._p(dbias), _s())
+    args = (F32 if out.dtype == torch.float32 else BF16, int(ta), int(tb), int(M), int(Nn), int(K),
+            float(alpha), a.data_ptr() + esz * a_off, int(lda), int(sa[0]), int(sa[1]),
+            b.data_ptr() + esz * b_off, int(ldb), int(sb[0]), int(sb[1]),
+            out.data_ptr() + esz_c * c_off, int(ldc), int(sc[0]), int(sc[1]), int(batch[0]), int(batch[1]),
+            O._p(bias), O.ACT[act], O._p(colscale), O._p(res), int(res.stride(0)) if res is not None else 0,
+            O._p(aux), int(aux.stride(0)) if aux is not None else 0,
+            O._p(pre), int(pre.stride(0)) if pre is not None else 0,
+            float(dropout_p), O._p(rng), int(site), O._p(dbias))
+    N.call(fn, *args, _s())
+    probe = O.PROBE["tok_gemm"]
+    if probe is not None and res is None and dbias is None:
+        # (an epilogue that reads res / accumulates dbias changes state on a replay: not probed)
+        nb = int(batch[0]) * int(batch[1])
+        probe.append({"fn": fn, "args": args, "keep": (out, a, b, bias, colscale, aux, pre, rng),
+                      "flops": 2.0 * M * Nn * K * nb,
+                      "bytes": nb * (esz * (M * K + K * Nn) + esz_c * M * Nn), "shape": (fn, M, Nn, K, nb)})
     return out
 
 
@@ -140,8 +148,13 @@ class _PatchEmbedFp8Fn(torch.autograd.Function):
         wc = weight.detach().float().contiguous()
         N.call("dmf_weight_quant_fp8", wc.data_ptr(), e, c, p, wq.data_ptr(), cs.data_ptr(), _s())
         y = O.empty_nhwc(n, e, ho, wo, torch.bfloat16, dev)
-        N.call("dmf_gemm_fp8", m, e, k, q.data_ptr(), k, rs.data_ptr(), wq.data_ptr(), k, cs.data_ptr(),
-               O._p(bias), y.data_ptr(), O.nhwc(y)[4], _s())
+        args = (m, e, k, q.data_ptr(), k, rs.data_ptr(), wq.data_ptr(), k, cs.data_ptr(), O._p(bias), y.data_ptr(),
+                O.nhwc(y)[4])
+        N.call("dmf_gemm_fp8", *args, _s())
+        probe = O.PROBE["fp8_gemm"]
+        if probe is not None:
+            probe.append({"fn": "dmf_gemm_fp8", "args": args, "keep": (q, rs, wq, cs, bias, y),
+                          "flops": 2.0 * m * e * k, "bytes": m * k + e * k + 2 * m * e, "shape": (m, e, k)})
         ctx.save_for_backward(x, weight, bias)
         ctx.conv, ctx.caches = conv, caches
         return y

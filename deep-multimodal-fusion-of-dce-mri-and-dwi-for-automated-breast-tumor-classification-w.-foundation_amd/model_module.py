@@ -11,7 +11,6 @@ are NCHW-shaped tensors with NHWC storage in the model's compute dtype
 from __future__ import annotations
 
 import contextlib
-import os
 from dataclasses import dataclass
 
 import torch
@@ -335,37 +334,17 @@ class BackboneAdapter(nn.Module):
         return O.conv_bn_act(h, nk[3], _caches(nk[3]), nk[4], "gelu")
 
     def forward(self, x):
-        chains = self.selected_indices_chains
-        if not (PARALLEL_NECKS and x.is_cuda and getattr(self.backbone, "supports_feature_callback", False)):
-            feats = self.backbone(x)
-            outs = [self._neck(i, feats) for i in range(len(chains))]
-            return outs[0], outs[1], outs[2]
-        # a neck chain whose maps are all out starts on a side stream while the
-        # backbone's deeper layers still run; the last chain stays on this stream
-        outs, joins = [None] * len(chains), {}
-
-        def on_feature(k, feats):
-            for i, chain in enumerate(chains):
-                if i != len(chains) - 1 and i not in joins and max(chain) == k:
-                    outs[i], joins[i] = O.branch(self, f"neck{i}", lambda i=i: self._neck(i, feats),
-                                                 *[feats[j] for j in chain])
-
-        feats = self.backbone(x, on_feature=on_feature)
-        for i in range(len(chains)):
-            if i in joins:
-                outs[i] = joins[i]()
-            elif outs[i] is None:
-                outs[i] = self._neck(i, feats)
+        # (neck chains on side streams beside the deeper backbone layers were measured slower, r01w,
+        # and removed; so were the projectors beside block3 and the fusion heads beside the classifier:
+        # mode A 3150 -> 2941 vol/s, the cross-stream joins of the captured step cost more than the
+        # overlap of their short chains)
+        feats = self.backbone(x)
+        outs = [self._neck(i, feats) for i in range(len(self.selected_indices_chains))]
         return outs[0], outs[1], outs[2]
 
 
-PARALLEL_NECKS = os.environ.get("DMF_PAR_NECK", "0") != "0"  # opt-in: measured slower (r01w)
-PARALLEL_PROJ = os.environ.get("DMF_PAR_PROJ", "0") != "0"  # opt-in: measured slower (r01w)
-PARALLEL_DEAD = os.environ.get("DMF_PAR_DEAD", "1") != "0"
-# opt-in: measured slower (interleaved A/B, 3 rounds: mode A 3150 -> 2941 vol/s with the three
-# fusion heads on side streams -- the cross-stream joins of the captured forward and backward cost
-# more than the overlap of their short chains)
-PARALLEL_HEADS = os.environ.get("DMF_PAR_HEADS", "0") != "0"
+# knob "parallel_dead": FusionModel's dead reduce + refine branch (Q4) on a side stream
+PARALLEL_DEAD = True
 
 
 def _inline_branch(owner, name, fn, *inputs):
@@ -527,12 +506,9 @@ class ModelMaskHeadBackbone(nn.Module):
                 f1_aligned = self.f1_to_f2(f1)
                 mask_pred = self.mask_head(O.act_nhwc(f2, "none", res=f1_aligned))
                 f2, mask_attn_map = self.mask_spatial_attention(f2, mask_pred)
-            # the four projectors (their outputs only feed aux["proj_pairs"]) run
-            # on a side stream beside block3 / the transformer stage
-            (p1, p2, p1_r, p2_r), join_proj = (O.branch if PARALLEL_PROJ else _inline_branch)(
-                self, "proj", lambda: (self._projector(self.proj_f1, f1), self._projector(self.proj_f2, f2),
-                                       self._projector(self.proj_r1, r1), self._projector(self.proj_r2, r2)),
-                f1, f2, r1, r2)
+            # the four projectors (their outputs only feed aux["proj_pairs"])
+            p1, p2 = self._projector(self.proj_f1, f1), self._projector(self.proj_f2, f2)
+            p1_r, p2_r = self._projector(self.proj_r1, r1), self._projector(self.proj_r2, r2)
             if not self.use_hybrid_transformer:
                 f3_in = O.gn_mix(f3_b, f2, self.f3_weight, self.norm_f3) if self.use_backbone else f2
                 f3, _ = self.block3(f3_in)
@@ -543,7 +519,6 @@ class ModelMaskHeadBackbone(nn.Module):
             else:
                 f3 = O.conv2d(self.transformer(f2), self.trans_out_proj, _caches(self.trans_out_proj))
             logits = self.classification_head(f3)
-            p1, p2, p1_r, p2_r = join_proj()
         aux = {"raw_feats": [f1, f2, f3], "recon_feats": [r1, r2], "proj_pairs": [p1, p1_r, p2, p2_r],
                "mask_attn_map": mask_attn_map, "mod_attn_map": mod_attn_map}
         return logits, aux, mask_pred
@@ -677,18 +652,12 @@ class FusionModel(nn.Module):
                 low, attn_weights = self.cross_attn_block(t_dwi, t_dce)
             fused = O.fusion_combine(p_dwi, p_dce, gating_weights, low, hp, wp)
             fused_refined = O.se_block(fused, self.fusion_se)[0] if self.fusion_se is not None else fused
-            # the four heads read fused_refined independently: with DMF_PAR_HEADS=1 the mask, recon
-            # and projection heads run on side streams beside the classifier (off: measured slower)
-            br = O.branch if PARALLEL_HEADS else _inline_branch
-            fused_mask_logits, join_mask = br(self, "head_mask", lambda: self.mask_head(fused_refined), fused_refined)
-            recon_fused, join_recon = br(
-                self, "head_recon",
-                lambda: self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None,
-                fused_refined)
-            proj_fused, join_proj = br(self, "head_proj", lambda: self.projF(fused_refined), fused_refined)
+            # the four heads read fused_refined independently
+            fused_mask_logits = self.mask_head(fused_refined)
+            recon_fused = self.fusion_reconstruct(fused_refined) if self.fusion_reconstruct is not None else None
+            proj_fused = self.projF(fused_refined)
             cl = self.classifier[2]
             logits = O.linear(O.gap(fused_refined), cl.weight, cl.bias)
-            fused_mask_logits, recon_fused, proj_fused = join_mask(), join_recon(), join_proj()
             join_dead()
         aux = {"proj_fused": proj_fused, "recon_fused": recon_fused, "gating_weights": gating_weights,
                "attn_weights": attn_weights, "p_dwi": p_dwi, "p_dce": p_dce}

@@ -10,7 +10,6 @@ reconstruction terms of one step share a single launch.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -111,7 +110,7 @@ class LightningFusionModel(nn.Module):
         snapshots are taken up front in the sequential order (DWI, DCE), so
         the masks match a sequential run; autograd replays each encoder's
         backward on the stream its forward ran on."""
-        if not (dwi_inputs.is_cuda and PARALLEL_ENCODERS):
+        if not (dwi_inputs.is_cuda and O.PARALLEL_BRANCHES):
             return self.dwi_model(dwi_inputs), self.dce_model(dce_inputs)
         main = torch.cuda.current_stream(dwi_inputs.device)
         side = self.__dict__.get("_side_stream")
@@ -387,7 +386,7 @@ class LightningFusionModel(nn.Module):
 
 
 # ------------------------------------------------------------------ helpers
-PARALLEL_ENCODERS = O.PARALLEL_BRANCHES
+
 
 
 def _draws_dropout(model):
@@ -412,7 +411,7 @@ def compute_recon_list_loss(recon_list, input_img):
     return terms.sum() / len(maps)
 
 
-DEVICE_LOSS = os.environ.get("DMF_DEVICE_LOSS", "1") != "0"  # A/B knob: the one-launch loss assembly
+DEVICE_LOSS = True  # knob "device_loss": the one-launch loss assembly (dmf_loss_combine)
 
 
 def fused_recon_terms(dwi_recons, dce_recons, fused_recon, dwi_img, dce_img):

@@ -55,12 +55,24 @@ int dmf_rng_advance(unsigned long long* state, unsigned long long inc, void* str
  * FeatureDownAlign (:386-390), FusionModel.proj_in_* / reduce (:857-862,
  * :788-792), PatchEmbed.proj (transformer_model.py:17-22). */
 int dmf_conv_m_tile(void);
-/* forward-conv tuning knobs (benchmarks / A-B runs): key 0 = 256x256 LDS-DMA
- * tile on (1, default) / off; key 1 = its scheduling variant 0..3 */
+/* the kernel body of the most recent conv launch (forward, fused-BN forward or
+ * dgrad) made from this host thread: one of DMF_FORM_* (-1 before any) */
+enum { DMF_FORM_IGEMM = 0, DMF_FORM_BUF = 1, DMF_FORM_BUF_INA = 2, DMF_FORM_WIDE = 3, DMF_FORM_SQ = 4,
+       DMF_FORM_PS = 5, DMF_FORM_PP = 6, DMF_FORM_STEM = 7 };
+int dmf_conv_last_form(void);
+/* forward-conv tuning knobs, set only from code (benchmarks / A-B runs; the
+ * library reads no environment): 0 = 256x256 LDS-DMA tile on (1, default) / off;
+ * 1 = its scheduling variant 0..3; 2 = forced tile; 3 = statistics accumulation
+ * mode; 4 = persistent 256x256 form on / off; 6 = benchmark-only skip bits of the
+ * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
+ * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 13 = fp32 GEMM 4x4 vector
+ * micro-tile; 14 / 15 = tiles a launch needs for the 256x128 / 256x256 forms.
+ * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
  * bf16 transposed-read kernel on (1, default) / off; key 1 = its 128x256 tile
- * (one workgroup per CU) where K >= 256 on (1, default) / off. */
+ * (one workgroup per CU) where K >= 256 on (1, default) / off; key 2 = the
+ * transposed-read kernels 1 (default) / 2 (register-staged 128x256) / 0 (off). */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */

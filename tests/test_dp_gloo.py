@@ -171,3 +171,71 @@ def test_epoch_driver_shards_and_gathers_every_volume_once():
     assert len(items0) == 4 and cnt == 11 and allp.shape == (11, 4)
     assert sorted(ally.tolist()) == sorted((torch.arange(11) % 4).tolist())
     assert auc == pytest.approx(auc_single, abs=1e-12)
+
+
+class _StubFusionLM(torch.nn.Module):
+    """Just the surface FusionFit.validate uses (CPU): _shared_step refuses an
+    empty batch, as dmf_batch_accuracy does on the device."""
+
+    class_num = 4
+    device = torch.device("cpu")
+
+    def _shared_step(self, batch, phase="val", return_preds=False):
+        x = batch[0]
+        assert x.shape[0] > 0, "empty batch scored"
+        logits = x.flatten(1)[:, :4] * 3.0
+        loss = torch.nn.functional.cross_entropy(logits, batch[-1])
+        return loss, logits, None, None
+
+
+class _StubTrainer:
+    lr_scheduler = None
+
+
+def _val_data(n):
+    g = torch.Generator().manual_seed(9)
+    return (torch.randn(n, 2, 3, 3, generator=g), torch.arange(n) % 4)
+
+
+def _validate_worker(rank, world, port, n, bs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dmf_fit import FusionFit
+
+        fit = FusionFit(_StubFusionLM(), None, _val_data(n), batch_size=bs, world=world, rank=rank,
+                        trainer=_StubTrainer())
+        out = fit.validate()
+        if rank == 0:
+            q.put((out["val_loss"], out["val_roc_auc"], out["n_val"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_validate_skips_padding_only_batch():
+    """n_val=65, world=2, batch 32 leaves rank 1 a last batch that
+    holds only a wrap-around padding copy. It must not be scored (no empty
+    forward), yet every rank gathers the same row count, so val_loss and the
+    AUROC equal the single-process values over the 65 volumes."""
+    import metrics as MT
+    from dmf_fit import shard
+
+    n, bs, world = 65, 32, 2
+    items, valid = shard(n, 1, world)
+    assert len(items) == 33 and valid[32] is False  # the padding-only batch exists
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_validate_worker, args=(r, world, port, n, bs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    val_loss, auc, n_val = q.get(timeout=250)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x, y = _val_data(n)
+    logits = x.flatten(1)[:, :4] * 3.0
+    assert n_val == n
+    assert val_loss == pytest.approx(torch.nn.functional.cross_entropy(logits, y).item(), rel=1e-6)
+    assert auc == pytest.approx(MT.multiclass_auroc(torch.softmax(logits, 1), y), abs=1e-12)

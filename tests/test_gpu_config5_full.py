@@ -108,8 +108,8 @@ def test_config5_full_shape_fusion_step_f32_and_fp8_report():
         assert torch.isfinite(lg).all()
         assert e <= 5e-2, (tag, e)
     print("config 5 numerics vs fp32 oracle:", json.dumps(report))
-    out = os.environ.get("DMF_REPORT_DIR")
-    if out:
-        os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, "config5_numerics.json"), "w") as f:
-            json.dump(report, f, indent=1)
+    # SURVEY 8(d) "Tolerances": fp8 reported separately -- always written (copied into profiles/ per round)
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "config5_numerics.json"), "w") as f:
+        json.dump(report, f, indent=1)

@@ -34,7 +34,7 @@ def _q(t):
 
 
 # (dmf_conv_tune key, value forcing the form on every legal shape, library default)
-FORMS = {"pp": (7, 2, 1), "p2": (9, 2, 0)}
+FORMS = {"pp": (7, 2, 1)}  # (the 128x128 two-workgroup persistent form was removed in round 4)
 
 
 @pytest.fixture(params=sorted(FORMS))

@@ -310,3 +310,91 @@ def test_overlapped_segment_allreduce_captured(tmp_path, mode, prefork):
     # float-atomic noise of the backward, amplified by the sign-like first
     # AdamW steps -- see the module docstring)
     assert tot < max(2 * noise, 1e-4) and tot < 0.1, (tot, noise)
+
+
+def _aux_flip_worker(port, outdir):
+    from dmf_dp import FusionTrainer
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    _, lm = _build(dev, freeze=True, eps=EPS)
+    tr = FusionTrainer(lm, world=1, use_graph=True, overlap=True, bucket_mb=0.05)
+    b = _batch(dev, 70)
+    tr.step(b)
+    before = (tr.captures, len(tr.opt.segments), tr.early_segments)
+    lm.current_epoch = lm.aux_loss_limit  # aux_w = 0: the recon / mimic nodes drop out -> re-capture
+    tr.step(b)
+    tr.step(b)
+    torch.cuda.synchronize()
+    after = (tr.captures, len(tr.opt.segments), tr.early_segments)
+    torch.save({"before": before, "after": after, "finite": bool(torch.isfinite(tr.loss).item())},
+               os.path.join(outdir, "aux_flip.pt"))
+
+
+@pytest.mark.timeout(600)
+def test_overlap_survives_aux_gate_recapture(tmp_path):
+    """a re-capture triggered by the aux-loss gate (epoch >= the
+    aux limit) must re-learn the per-parameter ready-event counts. Doubled
+    counts never reach zero, so every segment would be launched only at the
+    end of backward and the overlap would be silently lost."""
+    ctx = mp.get_context("spawn")
+    pr = ctx.Process(target=_aux_flip_worker, args=(_free_port(), str(tmp_path)))
+    pr.start()
+    pr.join(timeout=500)
+    assert pr.exitcode == 0, pr.exitcode
+    r = torch.load(tmp_path / "aux_flip.pt", weights_only=True)
+    (c0, s0, e0), (c1, s1, e1) = r["before"], r["after"]
+    assert c0 == 1 and c1 == 2, (c0, c1)
+    assert s0 > 3 and e0 > 0, (s0, e0)
+    # segments still launch from inside backward after the re-capture (doubled counts: none would; the
+    # recon / mimic heads' segments, without gradient once aux_w = 0, launch at its end)
+    print(f"segments {s0} -> {s1}, launched inside backward {e0} -> {e1}")
+    assert e1 > 0 and e1 >= s1 // 2, (s1, e1)
+    assert r["finite"]
+
+
+def test_short_first_batch_recaptures_on_full_batch():
+    """a capture that lands on a short (ragged) batch must not make
+    every later full-size batch run eagerly: the first larger batch re-captures
+    the step; later short batches run eagerly beside the graph."""
+    from dmf_dp import FusionTrainer
+
+    dev = torch.device("cuda", 0)
+    _, lm = _build(dev, freeze=True)
+    tr = FusionTrainer(lm, world=1, use_graph=True)
+    full = _batch(dev, 80)
+    short = tuple(t[:3] for t in full)
+    tr.step(short)
+    assert tr.captures == 1
+    with pytest.warns(RuntimeWarning, match="re-capturing"):
+        tr.step(full)
+    assert tr.captures == 2 and tr.static_batch[0].shape[0] == B
+    tr.step(full)
+    assert tr.captures == 2 and tr.eager_steps == 0
+    tr.step(short)
+    assert tr.eager_steps == 1 and tr.captures == 2
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.loss).item()
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus_2_spawns_two_ranks():
+    """``bench.py --gpus N`` with no launcher starts N
+    ranks itself (before touching the GPU) and rank 0 reports the whole job.
+    Rehearsed on one GPU: two ranks share cuda:0 over gloo."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    env.update(DMF_DIST_BACKEND="gloo", DMF_BENCH_SHARE_GPU="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "8", "--size", "128", "--no-extras", "--no-cpu-baseline", "--no-roofline"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16, d
+    assert d["value"] > 0 and d["loss"] == d["loss"]

@@ -216,3 +216,41 @@ def test_rank_strided_indices(n, world):
     assert len(flat) == -(-n // world) * world
     sh = [rank_strided_indices(n, r, world, epoch=3, shuffle=True, seed=1) for r in range(world)]
     assert set(i for p in sh for i in p) == set(range(n))
+
+
+def test_knobs_are_set_from_code_only():
+    """no kernel selection reads the environment; every
+    switch is a documented knob set from code (dmf_ops.set_knobs, bench.py
+    --knob). The package's only environment reads are the library path
+    (DMF_HIP_LIB), a local checkpoint path and the torchrun rank variables."""
+    import glob
+    import importlib
+    import os
+    import re
+
+    import dmf_ops as O
+
+    pkg = os.path.dirname(O.__file__)
+    allowed = {"DMF_HIP_LIB", "DMF_RADIMAGENET_CKPT", "RANK", "LOCAL_RANK", "WORLD_SIZE"}
+    seen = set()
+    for f in glob.glob(os.path.join(pkg, "*.py")) + glob.glob(os.path.join(pkg, "csrc", "*.hip")) + \
+            glob.glob(os.path.join(pkg, "csrc", "*.h")):
+        src = open(f).read()
+        seen |= set(re.findall(r"""(?:environ\.get|environ\[|getenv)\(\s*["']([A-Z_0-9]+)""", src))
+        assert "std::getenv" not in src or f.endswith(".py"), f
+    assert seen <= allowed, sorted(seen - allowed)
+    for name, (where, attr) in O.KNOBS.items():
+        if where in ("tune", "wgrad_tune"):
+            continue
+        obj = importlib.import_module(where)
+        *path, last = attr.split(".")
+        for p in path:
+            obj = getattr(obj, p)
+        old = getattr(obj, last)
+        assert isinstance(old, bool), name
+        O.set_knobs(**{name: "0"})
+        assert getattr(obj, last) is False
+        O.set_knobs(**{name: int(old)})
+        assert getattr(obj, last) is old
+    with pytest.raises(ValueError):
+        O.set_knobs(no_such_knob=1)

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Interleaved A/B of environment settings on the bench's encoder-forward north star and step
-# throughput (same library): usage: bash tools/ab_env.sh ROUNDS "VAR=a" "VAR=b" ...
+# Interleaved A/B of knob settings (dmf_ops.KNOBS, passed as bench.py --knob) on the bench's
+# encoder-forward north star and step throughput (same library):
+#   bash tools/ab_env.sh ROUNDS "sgemm_v4=0" "sgemm_v4=1" ...   (a setting may hold several: "a=1,b=0"; "-" = defaults)
 set -o pipefail
 R=${1:?rounds}; shift
 mkdir -p gpurun_out/abenv
@@ -8,7 +9,9 @@ for r in $(seq 1 $R); do
   i=0
   for e in "$@"; do
     i=$((i + 1))
-    env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 > gpurun_out/abenv/$i.$r.json 2> gpurun_out/abenv/$i.$r.err || { echo "bench $e failed"; tail -20 gpurun_out/abenv/$i.$r.err; exit 1; }
+    K=""
+    if [ "$e" != "-" ]; then for kv in ${e//,/ }; do K="$K --knob $kv"; done; fi
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 $K > gpurun_out/abenv/$i.$r.json 2> gpurun_out/abenv/$i.$r.err || { echo "bench $e failed"; tail -20 gpurun_out/abenv/$i.$r.err; exit 1; }
     python - "$e" gpurun_out/abenv/$i.$r.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
