@@ -274,6 +274,24 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (the instruction takes an immediate): one
+// scalar branch per call
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+#define DMF_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    DMF_VMW(0) DMF_VMW(1) DMF_VMW(2) DMF_VMW(3) DMF_VMW(4) DMF_VMW(5) DMF_VMW(6) DMF_VMW(7)
+    DMF_VMW(8) DMF_VMW(9) DMF_VMW(10) DMF_VMW(11) DMF_VMW(12) DMF_VMW(13) DMF_VMW(14) DMF_VMW(15)
+    DMF_VMW(16) DMF_VMW(17) DMF_VMW(18) DMF_VMW(19) DMF_VMW(20) DMF_VMW(21) DMF_VMW(22) DMF_VMW(23)
+    DMF_VMW(24) DMF_VMW(25) DMF_VMW(26) DMF_VMW(27) DMF_VMW(28) DMF_VMW(29) DMF_VMW(30) DMF_VMW(31)
+    DMF_VMW(32) DMF_VMW(33) DMF_VMW(34) DMF_VMW(35) DMF_VMW(36) DMF_VMW(37) DMF_VMW(38) DMF_VMW(39)
+    DMF_VMW(40) DMF_VMW(41) DMF_VMW(42) DMF_VMW(43) DMF_VMW(44) DMF_VMW(45) DMF_VMW(46) DMF_VMW(47)
+    DMF_VMW(48) DMF_VMW(49) DMF_VMW(50) DMF_VMW(51) DMF_VMW(52) DMF_VMW(53) DMF_VMW(54) DMF_VMW(55)
+    DMF_VMW(56) DMF_VMW(57) DMF_VMW(58) DMF_VMW(59) DMF_VMW(60) DMF_VMW(61) DMF_VMW(62)
+#undef DMF_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 // 7x7 / stride-2 stem conv (conv_stem.hip): legality, pixels per workgroup (= BN slab rows), launcher
 bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a);
 int conv_stem_m_tile(const ConvArgs& a);

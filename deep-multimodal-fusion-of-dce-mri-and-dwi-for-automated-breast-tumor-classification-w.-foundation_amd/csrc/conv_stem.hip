@@ -35,20 +35,6 @@ namespace dmf {
 
 constexpr int STEM_SLOTS = 9;  // 7 rows in use + the next step's 2
 
-// s_waitcnt vmcnt with a run-time count (the immediate must be a constant)
-__device__ __forceinline__ void vm_wait_rt(int n) {
-  switch (n) {
-#define DMF_VMW(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    DMF_VMW(1) DMF_VMW(2) DMF_VMW(3) DMF_VMW(4) DMF_VMW(5) DMF_VMW(6) DMF_VMW(7) DMF_VMW(8) DMF_VMW(9)
-    DMF_VMW(10) DMF_VMW(11) DMF_VMW(12) DMF_VMW(13) DMF_VMW(14) DMF_VMW(15) DMF_VMW(16) DMF_VMW(17)
-    DMF_VMW(18) DMF_VMW(19) DMF_VMW(20) DMF_VMW(21) DMF_VMW(22) DMF_VMW(23) DMF_VMW(24) DMF_VMW(25)
-    DMF_VMW(26) DMF_VMW(27) DMF_VMW(28) DMF_VMW(29) DMF_VMW(30) DMF_VMW(31) DMF_VMW(32)
-#undef DMF_VMW
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
 // C: padded input channels (8 / 16); STATS: BN statistics epilogue (a.partials)
 template <int C, bool STATS>
 __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plane) {

@@ -18,10 +18,14 @@ oracle.model / oracle.losses on the same state_dict and inputs:
 
 Tolerances: bf16 logits within 5e-2 absolute of the fp32 oracle (the gate;
 the measured max-abs / relative errors go to gpurun_out/bf16_errors.json and
-profiles/); per-channel f1..f3 statistics within 3e-2 of the map's scale;
-running-stat sums within 1e-2 relative; the step's loss within 3e-2 and the
-fusion gradients no further from the fp32 oracle than 1.25x the reference's
-own bf16 autocast (+0.01) -- the reference-AMP yardstick of
+profiles/). Everything else against the reference's own bf16-mixed AMP (the
+fp32 oracle under CPU bf16 autocast, parameters_generate.py:211): the masks,
+gating / attention weights, per-channel f1..f3 statistics and running-stat
+sums no further from the fp32 oracle than 1.5x the reference-AMP error (+ a
+small floor) -- train-mode BN renormalises every layer by batch statistics,
+so bf16 rounding moves e.g. the mask logits by ~0.1 in the reference's AMP
+too. The step: loss within 3e-2 and the fusion gradients no further from the
+fp32 oracle than 1.25x the reference-AMP gradients (+0.01), the yardstick of
 test_gpu_golden_full.test_mode_b_bf16_full_width_step_vs_oracle."""
 import copy
 import json
@@ -115,33 +119,54 @@ def test_config3_b32_bf16_forward_vs_oracle(mode):
     assert BENCH_FORMS <= set(forms), forms
 
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    with torch.no_grad():
-        lr_d, ar_d, mr_d = dwi_r(x_dwi)
-        lr_c, ar_c, mr_c = dce_r(x_dce)
-        lr_f, mr_f, ar_f = fr(ar_d["raw_feats"], ar_c["raw_feats"], mr_d, mr_c)
-    out = {"forms": forms}
-    for name, got, want in (("dwi_logits", lo_d, lr_d), ("dce_logits", lo_c, lr_c), ("fusion_logits", logits, lr_f),
-                            ("dwi_mask", mp_d, mr_d), ("dce_mask", mp_c, mr_c), ("fused_mask", fmask, mr_f),
-                            ("gating", aux["gating_weights"], ar_f["gating_weights"]),
-                            ("attn", aux["attn_weights"], ar_f["attn_weights"])):
-        out[name] = _err(got, want)
-    out["feature_stats_rel"] = {f"{tag}_f{i + 1}": _stats_err(a, b)
-                                for tag, ga, wa in (("dwi", aux_d, ar_d), ("dce", aux_c, ar_c))
-                                for i, (a, b) in enumerate(zip(ga["raw_feats"], wa["raw_feats"]))}
-    if mode == "train":
-        got = np.array([b.double().sum().item() for m in (dwi, dce, fm) for n, b in m.named_buffers()
-                        if n.endswith("running_mean") or n.endswith("running_var")])
-        want = np.array([b.double().sum().item() for m in (dwi_r, dce_r, fr) for n, b in m.named_buffers()
+    # the reference's own bf16-mixed (parameters_generate.py:211, run.py:59-76): the fp32 oracle under CPU bf16
+    # autocast, from the same state (copied before the fp32 forward moves the running statistics)
+    amp = [copy.deepcopy(m) for m in (dwi_r, dce_r, fr)]
+
+    def oracle(mods):
+        with torch.no_grad():
+            lo1, a1, m1 = mods[0](x_dwi)
+            lo2, a2, m2 = mods[1](x_dce)
+            lf, mf, af = mods[2](a1["raw_feats"], a2["raw_feats"], m1, m2)
+        return (lo1, lo2, lf, m1, m2, mf, af["gating_weights"], af["attn_weights"]), (a1, a2)
+
+    want, (ar_d, ar_c) = oracle((dwi_r, dce_r, fr))
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ref_amp, (am_d, am_c) = oracle(amp)
+    names = ("dwi_logits", "dce_logits", "fusion_logits", "dwi_mask", "dce_mask", "fused_mask", "gating", "attn")
+    mine = (lo_d, lo_c, logits, mp_d, mp_c, fmask, aux["gating_weights"], aux["attn_weights"])
+    out = {"forms": forms, "hip_bf16": {}, "reference_bf16_autocast": {}}
+    for name, got, w, r in zip(names, mine, want, ref_amp):
+        out["hip_bf16"][name] = _err(got, w)
+        out["reference_bf16_autocast"][name] = _err(r, w)
+    out["hip_bf16"]["feature_stats_rel"] = {f"{tag}_f{i + 1}": _stats_err(a, b)
+                                            for tag, ga, wa in (("dwi", aux_d, ar_d), ("dce", aux_c, ar_c))
+                                            for i, (a, b) in enumerate(zip(ga["raw_feats"], wa["raw_feats"]))}
+    out["reference_bf16_autocast"]["feature_stats_rel"] = {
+        f"{tag}_f{i + 1}": _stats_err(a, b) for tag, ga, wa in (("dwi", am_d, ar_d), ("dce", am_c, ar_c))
+        for i, (a, b) in enumerate(zip(ga["raw_feats"], wa["raw_feats"]))}
+
+    def stat_sums(mods):
+        return np.array([b.double().sum().item() for m in mods for n, b in m.named_buffers()
                          if n.endswith("running_mean") or n.endswith("running_var")])
-        assert got.shape == want.shape
-        out["running_stat_sums_rel"] = float((np.abs(got - want) / np.maximum(1.0, np.abs(want))).max())
-    _report(f"config3_b32_{mode}_forward_bf16_vs_fp32_oracle", out)
-    for name in ("dwi_logits", "dce_logits", "fusion_logits"):
-        assert out[name]["max_abs"] < 5e-2, (name, out[name])
-    for k, v in out["feature_stats_rel"].items():
-        assert v < 3e-2, (k, v)
+
     if mode == "train":
-        assert out["running_stat_sums_rel"] < 1e-2, out["running_stat_sums_rel"]
+        w = stat_sums((dwi_r, dce_r, fr))
+        for tag, mods in (("hip_bf16", (dwi, dce, fm)), ("reference_bf16_autocast", amp)):
+            g = stat_sums(mods)
+            assert g.shape == w.shape
+            out[tag]["running_stat_sums_rel"] = float((np.abs(g - w) / np.maximum(1.0, np.abs(w))).max())
+    _report(f"config3_b32_{mode}_forward_bf16_vs_fp32_oracle", out)
+    h, r = out["hip_bf16"], out["reference_bf16_autocast"]
+    for name in ("dwi_logits", "dce_logits", "fusion_logits"):
+        assert h[name]["max_abs"] < 5e-2, (name, h[name])
+    # everything else: no further from the fp32 oracle than the reference's own bf16 autocast (x1.5, + a floor)
+    for name in names:
+        assert h[name]["rel"] <= 1.5 * r[name]["rel"] + 1e-2, (name, h[name], r[name])
+    for k, v in h["feature_stats_rel"].items():
+        assert v <= 1.5 * r["feature_stats_rel"][k] + 1e-2, (k, v, r["feature_stats_rel"][k])
+    if mode == "train":
+        assert h["running_stat_sums_rel"] <= 1.5 * r["running_stat_sums_rel"] + 1e-3, (h, r)
 
 
 def _fusion_grads(fm):

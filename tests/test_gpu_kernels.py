@@ -688,3 +688,52 @@ def test_channel_mean_reuse_never_stale():
     y = torch.rand(2, 6, 8, 8, device=DEV)  # may land on the freed block
     torch.testing.assert_close(O.channel_mean_map(y), y.mean(1))
     assert ptr is not None
+
+
+# the persistent 256x256 form's flat K-step stream (k_conv_fwd_ps): one step staged under the current
+# step's MFMAs, one more ahead of every tile's epilogue stores. Shapes with 1 (K = 64), 2, 4 and 8 K-steps
+# per tile, 2..3 tiles per block, an M tail (the statistics epilogue with row masks) and the bias +
+# activation epilogue; the form is asserted from the launch record (dmf_conv_last_form)
+PS_CASES = [
+    # (N, Cin, H, W, Cout, bias+act epilogue)
+    (33, 64, 64, 64, 256, False),
+    (33, 128, 32, 32, 512, False),
+    (35, 256, 31, 31, 1024, False),
+    (34, 512, 32, 32, 1024, False),
+    (33, 64, 64, 64, 256, True),
+    (35, 256, 31, 31, 512, True),
+]
+
+
+@pytest.mark.parametrize("case", PS_CASES)
+def test_conv_ps_stream_forward(case):
+    import dmf_native as N
+
+    n, ci, h, w, co, with_bias = case
+    torch.manual_seed(9)
+    conv = nn.Conv2d(ci, co, 1, bias=with_bias)
+    a = torch.randn(n, ci, h, w).bfloat16().float()
+    wq = conv.weight.detach().bfloat16().float()
+    cd = copy.deepcopy(conv).to(DEV)
+    xd = _to_dev(a, torch.bfloat16)
+    if with_bias:
+        ref = F.relu(F.conv2d(a.double(), wq.double(), conv.bias.detach().double())).float()
+        with torch.no_grad():
+            y = O.conv2d(xd, cd, (O.WeightCache(), O.WeightCache()), act="relu")
+        assert N.FORMS[N.load().dmf_conv_last_form()] == "ps"
+        err = (y.float().cpu() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item(), err
+        return
+    bn = nn.BatchNorm2d(co)
+    with torch.no_grad():
+        raw = F.conv2d(a.double(), wq.double()).float()
+        ref = F.relu(bn(raw))
+    bd = nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        with O.bn_scope(cd, DEV):  # the training forward's statistics arena (dmf_conv2d_fwd_acc)
+            y = O.conv_bn_act(xd, cd, (O.WeightCache(), O.WeightCache()), bd, "relu")
+    assert N.FORMS[N.load().dmf_conv_last_form()] == "ps"
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 3e-2 * ref.abs().max().item(), err
+    assert torch.allclose(bd.running_mean.cpu(), bn.running_mean, rtol=1e-2, atol=1e-3 * raw.abs().max().item())
+    assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)

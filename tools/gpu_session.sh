@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 ROOT=$(pwd)
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $OUT/tests.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rf --durations=25 --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -40 $OUT/tests.log; exit 1; }
   tail -3 $OUT/tests.log
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail -30 $OUT/smoke.log; exit 1; }
   tail -2 $OUT/smoke.log
