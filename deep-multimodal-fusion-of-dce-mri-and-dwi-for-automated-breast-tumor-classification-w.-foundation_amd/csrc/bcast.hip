@@ -93,12 +93,8 @@ extern "C" int dmf_channel_affine(int dtype, const void* x, int ldx, const float
   DMF_CHECK_ARG(y && (x || add), "dmf_channel_affine: bad args");
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_channel_affine<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)x, ldx, gate, add, add_scale, (bf16_t*)y, ldy, (long long)N, HW, C);
-  else
-    hipLaunchKernelGGL(k_channel_affine<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
-                       ldx, gate, add, add_scale, (float*)y, ldy, (long long)N, HW, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_channel_affine<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)x, ldx, gate, add, add_scale, (T*)y, ldy, (long long)N, HW, C));
   DMF_LAUNCH_CHECK("dmf_channel_affine");
   return 0;
 }
@@ -110,21 +106,13 @@ extern "C" int dmf_broadcast_hw(int dtype, const float* vec, float scale, void* 
   if (total == 0) return 0;
   if (C % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 && (long long)N * HW * ldy < (1LL << 31)) {
     const long long t8 = total / 8;
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_broadcast_hw8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, vec, scale,
-                         (bf16_t*)y, ldy, N, HW, C, accumulate);
-    else
-      hipLaunchKernelGGL(k_broadcast_hw8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, vec, scale,
-                         (float*)y, ldy, N, HW, C, accumulate);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_broadcast_hw8<T>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, vec, scale,
+                         (T*)y, ldy, N, HW, C, accumulate));
     DMF_LAUNCH_CHECK("dmf_broadcast_hw");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_broadcast_hw<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, vec, scale,
-                       (bf16_t*)y, ldy, (long long)N, HW, C, accumulate);
-  else
-    hipLaunchKernelGGL(k_broadcast_hw<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, vec, scale,
-                       (float*)y, ldy, (long long)N, HW, C, accumulate);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_broadcast_hw<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, vec, scale,
+                       (T*)y, ldy, (long long)N, HW, C, accumulate));
   DMF_LAUNCH_CHECK("dmf_broadcast_hw");
   return 0;
 }
@@ -132,12 +120,8 @@ extern "C" int dmf_broadcast_hw(int dtype, const float* vec, float scale, void* 
 extern "C" int dmf_gate_grad_nchw(int dtype, const void* dy, int lddy, const float* x, int N, int C, int HW,
                                   float* out, void* stream) {
   DMF_CHECK_ARG(dy && x && out && N > 0 && C > 0, "dmf_gate_grad_nchw: bad args");
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_gate_grad_nchw<bf16_t>, dim3(N * C), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                       lddy, x, C, HW, out);
-  else
-    hipLaunchKernelGGL(k_gate_grad_nchw<float>, dim3(N * C), dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
-                       x, C, HW, out);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gate_grad_nchw<T>, dim3(N * C), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                       lddy, x, C, HW, out));
   DMF_LAUNCH_CHECK("dmf_gate_grad_nchw");
   return 0;
 }

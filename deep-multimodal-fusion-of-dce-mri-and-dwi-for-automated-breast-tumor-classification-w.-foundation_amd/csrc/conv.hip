@@ -43,10 +43,10 @@ __device__ __forceinline__ void chunk_affine(uint4& u, const float* sc, const fl
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+      float lo = B16<T>::lo(w[i]), hi = B16<T>::hi(w[i]);
       lo = in_act_f<INA>(lo * sc[2 * i] + sh[2 * i]);
       hi = in_act_f<INA>(hi * sc[2 * i + 1] + sh[2 * i + 1]);
-      w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+      w[i] = B16<T>::pack(lo, hi);
     }
     u = make_uint4(w[0], w[1], w[2], w[3]);
   } else {
@@ -85,8 +85,7 @@ __device__ __forceinline__ void conv_mma(const char* As, f32x4_t (&acc)[BM / (16
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
-                                                              0, 0);
+          acc[i][j] = mfma16<T>(av[i], bv[j], acc[i][j]);
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
@@ -450,7 +449,7 @@ constexpr int WBM = 256, WBN = 128, WSTAGE = (WBM + WBN) * 128, WNSTAGE = 3;
 constexpr int WWM = 4, WWN = 2, WTHREADS = 64 * WWM * WWN;  // 8 waves of 64x64: two per SIMD
 constexpr int WLDS = WNSTAGE * WSTAGE;  // 147456 B: also holds the C staging tile
 
-template <bool PADCHK, bool DUAL>
+template <bool PADCHK, bool DUAL, typename T = bf16_t>
 __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
   constexpr int ES = 2, EPC = 8, BK = 64;
   constexpr int NW = WTHREADS / 64;
@@ -550,11 +549,11 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
     if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);
-    conv_mma<bf16_t, WBM, WBN, WWM, WWN>(smem + st * WSTAGE, acc, wm, wn, lane);
+    conv_mma<T, WBM, WBN, WWM, WWN>(smem + st * WSTAGE, acc, wm, wn, lane);
     st = st == 2 ? 0 : st + 1;
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  conv_epilogue<bf16_t, WBM, WBN, WWM, WWN>(a, acc, smem, tid, mt, nt, m0, n0);
+  conv_epilogue<T, WBM, WBN, WWM, WWN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
 // --------------------------------------- forward, LDS-DMA square form (bf16)
@@ -570,7 +569,7 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
 // the other stage. Requires Nout % 256 == 0 plus the wide form's conditions.
 
 // VAR bit 0: waves 4-7 at static priority 1; bit 1: s_setprio around each MFMA group
-template <bool PADCHK, bool DUAL, int VAR>
+template <bool PADCHK, bool DUAL, int VAR, typename T = bf16_t>
 __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
   constexpr int ES = 2, EPC = 8, BK = 64;
   constexpr int NW = QTHREADS / 64;
@@ -689,14 +688,13 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
         if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&av[i], *(bf16x8_t*)&bv[j], acc[i][j], 0,
-                                                              0, 0);
+          acc[i][j] = mfma16<T>(av[i], bv[j], acc[i][j]);
         if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(0);
       }
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  conv_epilogue<bf16_t, QBM, QBN, QWM, QWN>(a, acc, smem, tid, mt, nt, m0, n0);
+  conv_epilogue<T, QBM, QBN, QWM, QWN>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
 // ------------------------------- forward, persistent LDS-DMA square form (bf16)
@@ -725,7 +723,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
 // bias + DMF_ACT_* activation. The next K-step's DMA pieces are spread over
 // both k-halves (pieces 0-3 in the first, 4-7 in the second; "all 8 in one
 // half" or "all 8 after the barrier" measured no better).
-template <bool PADCHK, bool DUAL, int EPI, int TBM = QBM, int TBN = QBN, int TWN = QWN>
+template <bool PADCHK, bool DUAL, int EPI, int TBM = QBM, int TBN = QBN, int TWN = QWN, typename T = bf16_t>
 __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(ConvArgs a) {
   constexpr int ES = 2, BK = 64;
   constexpr int TWM = 2;  // two pixel-half waves per 64-channel slab (ps_epilogue)
@@ -884,8 +882,7 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
         if (more && i % (FM / 4) == 0 && !(a.dbg & 2)) piece(kk * 4 + i / (FM / 4));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_t*)&wv[j], *(bf16x8_t*)&pv[i], acc[i][j], 0,
-                                                              0, 0);
+          acc[i][j] = mfma16<T>(wv[j], pv[i], acc[i][j]);
       }
     }
     st ^= 1;
@@ -894,7 +891,7 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
       continue;
     }
     // ---------------- epilogue of tile `lin` (the next tile's step 0 is in flight)
-    if (!(a.dbg & 4)) ps_epilogue<EPI, TBN, FM, TBM>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
+    if (!(a.dbg & 4)) ps_epilogue<EPI, TBN, FM, TBM, T>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
     epi = !(a.dbg & 4);
     if (!more) break;
     t = tnext;
@@ -1102,8 +1099,8 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   // an input affine runs on the buffer-load kernel for plain 1x1 convs, else on k_conv_igemm
   if (dgrad || (a.in_ss != nullptr && !(plain && a.x2 == nullptr)))
     return p;
-  const int es = dtype == DMF_BF16 ? 2 : 4;
-  const int bk = dtype == DMF_BF16 ? 64 : 32;
+  const int es = is16(dtype) ? 2 : 4;
+  const int bk = is16(dtype) ? 64 : 32;
   const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
   const long long xbytes = (long long)a.N * a.H * a.W * a.ldx * es;
   const long long x2bytes = a.x2 ? (long long)a.N * a.H * a.W * a.ldx2 * es : 0;
@@ -1116,8 +1113,8 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
     return p;
   }
   if (g_force) {
-    const bool wide_ok = dtype == DMF_BF16 && a.Nout % WBN == 0 && a.Ktot >= 512;
-    const bool sq_ok = dtype == DMF_BF16 && a.Nout % QBN == 0 && a.Ktot >= 512;
+    const bool wide_ok = is16(dtype) && a.Nout % WBN == 0 && a.Ktot >= 512;
+    const bool sq_ok = is16(dtype) && a.Nout % QBN == 0 && a.Ktot >= 512;
     if (g_force == 6 && sq_ok) { p.wide = p.sq = true; p.bm = QBM; p.bn = QBN; return p; }
     if (g_force == 5 && wide_ok) { p.wide = true; p.bm = WBM; p.bn = WBN; return p; }
     if (g_force >= 1 && g_force <= 4) {
@@ -1127,7 +1124,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
     }
   }
   // ping-pong square tile: same legality as the persistent form below
-  const bool sq_ps_ok = dtype == DMF_BF16 && a.tickets == nullptr && a.Nout % QBN == 0 &&
+  const bool sq_ps_ok = is16(dtype) && a.tickets == nullptr && a.Nout % QBN == 0 &&
                         a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
                         (long long)a.M * a.ldy * 2 < (1LL << 31);
   if (sq_ps_ok && (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 1024 && a.KH * a.KW == 1)))) {
@@ -1138,7 +1135,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   }
   // persistent square LDS-DMA tile: whole 256-column tiles, >= one tile per CU, no fused-finalize
   // tickets, output addressable by a 32-bit buffer offset
-  if (dtype == DMF_BF16 && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
+  if (is16(dtype) && g_ps_enable && a.tickets == nullptr && a.Nout % QBN == 0 &&
       a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
       (long long)a.M * a.ldy * 2 < (1LL << 31)) {
     p.wide = p.sq = p.ps = true;
@@ -1149,7 +1146,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   // square LDS-DMA tile: whole 256-column tiles and >= one block per CU
   // (measured: +15 % on the dilated 3x3s; a short-K 1x1 (K <= 1024) is epilogue-
   // bound at one 256x256 block per CU and stays on the 256x128 form)
-  if (dtype == DMF_BF16 && g_sq_enable && a.Nout % QBN == 0 &&
+  if (is16(dtype) && g_sq_enable && a.Nout % QBN == 0 &&
       (a.KH * a.KW > 1 ? a.Ktot >= 512 : a.Ktot >= 2048) && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles) {
     p.wide = p.sq = true;
     p.bm = QBM;
@@ -1157,7 +1154,7 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
     return p;
   }
   // wide LDS-DMA tile: bf16, whole 128-column tiles, long enough K, >= one block per CU
-  if (dtype == DMF_BF16 && a.Nout % WBN == 0 && a.Ktot >= 512 &&
+  if (is16(dtype) && a.Nout % WBN == 0 && a.Ktot >= 512 &&
       (long long)cdiv(a.M, WBM) * (a.Nout / WBN) >= g_wide_min_tiles) {
     p.wide = true;
     p.bm = WBM;
@@ -1174,8 +1171,121 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
 // assert which forms a model-level parity run exercised)
 static thread_local int g_last_form = -1;
 
+// the forward / dgrad body of a plan for one storage type T (bf16, f16 or f32; the LDS-DMA forms exist for
+// the 16-bit types only -- conv_plan never picks them for f32)
+template <typename T>
+static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long long nblk, size_t lds_total,
+                          hipStream_t st) {
+  const dim3 g((unsigned)nblk), b(CTHREADS);
+  const int bk = sizeof(T) == 2 ? 64 : 32;
+  const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
+  const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  const bool dual = a.x2 != nullptr;
+#define DMF_CONV_LAUNCH(DG, INA)                                                                \
+  do {                                                                                          \
+    if (fastc) hipLaunchKernelGGL((k_conv_igemm<T, DG, INA, true>), g, b, lds_total, st, a);   \
+    else hipLaunchKernelGGL((k_conv_igemm<T, DG, INA, false>), g, b, lds_total, st, a);        \
+  } while (0)
+#define DMF_BUF_LAUNCH(BM, BN)                                                                              \
+  do {                                                                                                      \
+    if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<T, true, true, BM, BN>), g, b, lds_total, st, a);          \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<T, false, false, BM, BN>), g, b, lds_total, st, a);  \
+    else hipLaunchKernelGGL((k_conv_fwd_buf<T, true, false, BM, BN>), g, b, lds_total, st, a);              \
+  } while (0)
+  if (dgrad) {
+    DMF_CONV_LAUNCH(true, -1);
+    return;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (plan.ps) {
+      const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
+      // statistics without bias over whole tiles: the fast epilogue (EPI 5)
+      const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
+      a.dbg = g_ps_dbg;
+#define DMF_PS(E)                                                                                                \
+  do {                                                                                                           \
+    if (dual) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);    \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a); \
+    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);        \
+  } while (0)
+      switch (epi) {
+        case 0: DMF_PS(0); break;
+        case 1: DMF_PS(1); break;
+        case 2: DMF_PS(2); break;
+        case 3: DMF_PS(3); break;
+        case 5: DMF_PS(5); break;
+        default: DMF_PS(4); break;
+      }
+#undef DMF_PS
+      return;
+    }
+    if (plan.sq) {
+      const dim3 bq(QTHREADS);
+#define DMF_SQ(V)                                                                                         \
+  do {                                                                                                    \
+    if (dual) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, V, T>), g, bq, lds_total, st, a);             \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_sq<false, false, V, T>), g, bq, lds_total, st, a);     \
+    else hipLaunchKernelGGL((k_conv_fwd_sq<true, false, V, T>), g, bq, lds_total, st, a);                 \
+  } while (0)
+      switch (g_sq_var) {
+        case 1: DMF_SQ(1); break;
+        case 2: DMF_SQ(2); break;
+        case 3: DMF_SQ(3); break;
+        default: DMF_SQ(0); break;
+      }
+#undef DMF_SQ
+      return;
+    }
+    if (plan.wide) {
+      const dim3 bw(WTHREADS);
+      if (dual) hipLaunchKernelGGL((k_conv_fwd_wide<true, true, T>), g, bw, lds_total, st, a);
+      else if (plain) hipLaunchKernelGGL((k_conv_fwd_wide<false, false, T>), g, bw, lds_total, st, a);
+      else hipLaunchKernelGGL((k_conv_fwd_wide<true, false, T>), g, bw, lds_total, st, a);
+      return;
+    }
+  }
+  if (plan.buf && a.in_ss != nullptr) {
+    const size_t lds_ina = lds_total + (size_t)a.C * 8;
+    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
+#define DMF_INA_BUF(IA)                                                                                   \
+  do {                                                                                                    \
+    switch (cfg) {                                                                                        \
+      case 3: hipLaunchKernelGGL((k_conv_fwd_buf<T, false, false, 128, 128, IA>), g, b, lds_ina, st, a); break; \
+      case 2: hipLaunchKernelGGL((k_conv_fwd_buf<T, false, false, 128, 64, IA>), g, b, lds_ina, st, a); break;  \
+      case 1: hipLaunchKernelGGL((k_conv_fwd_buf<T, false, false, 64, 128, IA>), g, b, lds_ina, st, a); break;  \
+      default: hipLaunchKernelGGL((k_conv_fwd_buf<T, false, false, 64, 64, IA>), g, b, lds_ina, st, a);         \
+    }                                                                                                     \
+  } while (0)
+    switch (a.act_in) {
+      case DMF_ACT_NONE: DMF_INA_BUF(DMF_ACT_NONE); break;
+      case DMF_ACT_RELU: DMF_INA_BUF(DMF_ACT_RELU); break;
+      default: DMF_INA_BUF(DMF_ACT_GELU); break;
+    }
+#undef DMF_INA_BUF
+  } else if (plan.buf) {
+    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
+    switch (cfg) {
+      case 3: DMF_BUF_LAUNCH(128, 128); break;
+      case 2: DMF_BUF_LAUNCH(128, 64); break;
+      case 1: DMF_BUF_LAUNCH(64, 128); break;
+      default: DMF_BUF_LAUNCH(64, 64); break;
+    }
+  } else if (a.in_ss == nullptr) {
+    DMF_CONV_LAUNCH(false, -1);
+  } else {
+    switch (a.act_in) {
+      case DMF_ACT_NONE: DMF_CONV_LAUNCH(false, DMF_ACT_NONE); break;
+      case DMF_ACT_RELU: DMF_CONV_LAUNCH(false, DMF_ACT_RELU); break;
+      default: DMF_CONV_LAUNCH(false, DMF_ACT_GELU); break;
+    }
+  }
+#undef DMF_BUF_LAUNCH
+#undef DMF_CONV_LAUNCH
+}
+
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
-  const int epc = dtype == DMF_BF16 ? 8 : 4;
+  DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "%s: bad dtype %d", what, dtype);
+  const int epc = is16(dtype) ? 8 : 4;
   DMF_CHECK_ARG(a.C % epc == 0 && a.ldx % epc == 0, "%s: input channels (%d) and stride (%d) must be multiples of %d",
                 what, a.C, a.ldx, epc);
   DMF_CHECK_ARG(a.Nout % epc == 0 && a.ldy % epc == 0,
@@ -1192,132 +1302,33 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   a.ntiles = cdiv(a.Nout, plan.bn);
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
-  const int es = dtype == DMF_BF16 ? 2 : 4;
+  const int es = is16(dtype) ? 2 : 4;
   const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
-  const dim3 g((unsigned)nblk), b(CTHREADS);
-  const int bk = dtype == DMF_BF16 ? 64 : 32;
-  const bool fastc = a.C % bk == 0 && (a.x2 == nullptr || a.C1 % bk == 0);
-#define DMF_CONV_LAUNCH(TT, DG, INA)                                                            \
-  do {                                                                                          \
-    if (fastc) hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, true>), g, b, lds_total, st, a);  \
-    else hipLaunchKernelGGL((k_conv_igemm<TT, DG, INA, false>), g, b, lds_total, st, a);       \
-  } while (0)
-#define DMF_BUF_LAUNCH(TT, BM, BN)                                                                           \
-  do {                                                                                                       \
-    if (dual) hipLaunchKernelGGL((k_conv_fwd_buf<TT, true, true, BM, BN>), g, b, lds_total, st, a);          \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, BM, BN>), g, b, lds_total, st, a);  \
-    else hipLaunchKernelGGL((k_conv_fwd_buf<TT, true, false, BM, BN>), g, b, lds_total, st, a);              \
-  } while (0)
-  if (plan.stem) {
-    return launch_conv_stem(a, st);
-  } else if (dgrad) {
-    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, true, -1);
-    else DMF_CONV_LAUNCH(float, true, -1);
-  } else if (plan.pp) {
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  if (plan.stem) return launch_conv_stem(a, st, dtype);
+  if (!dgrad && plan.pp) {
     // statistics without bias over whole tiles: the fast epilogue (EPI 5)
     const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
     DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
-    return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st);
-  } else if (plan.ps) {
+    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
+  }
+  if (!dgrad && plan.ps) {
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
-    // statistics without bias over whole tiles: the fast epilogue (EPI 5)
-    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
-    a.dbg = g_ps_dbg;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
-#define DMF_PS(E)                                                                                      \
-  do {                                                                                                 \
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E>), gp, bq, lds_total, st, a);  \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E>), gp, bq, lds_total, st, a);    \
-    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E>), gp, bq, lds_total, st, a);                \
-  } while (0)
-    switch (epi) {
-      case 0: DMF_PS(0); break;
-      case 1: DMF_PS(1); break;
-      case 2: DMF_PS(2); break;
-      case 3: DMF_PS(3); break;
-      case 5: DMF_PS(5); break;
-      default: DMF_PS(4); break;
-    }
-#undef DMF_PS
-  } else if (plan.sq) {
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const dim3 bq(QTHREADS);
-#define DMF_SQ(V)                                                                                      \
-  do {                                                                                                 \
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, V>), g, bq, lds_total, st, a);   \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_sq<false, false, V>), g, bq, lds_total, st, a);     \
-    else hipLaunchKernelGGL((k_conv_fwd_sq<true, false, V>), g, bq, lds_total, st, a);                 \
-  } while (0)
-    switch (g_sq_var) {
-      case 1: DMF_SQ(1); break;
-      case 2: DMF_SQ(2); break;
-      case 3: DMF_SQ(3); break;
-      default: DMF_SQ(0); break;
-    }
-#undef DMF_SQ
-  } else if (plan.wide) {
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const dim3 bw(WTHREADS);
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_wide<true, true>), g, bw, lds_total, st, a);
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_wide<false, false>), g, bw, lds_total, st, a);
-    else hipLaunchKernelGGL((k_conv_fwd_wide<true, false>), g, bw, lds_total, st, a);
-  } else if (plan.buf && a.in_ss != nullptr) {
+    DMF_CHECK_ARG(a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
+  }
+  if (!dgrad && plan.buf && a.in_ss != nullptr) {
     DMF_CHECK_ARG(((uintptr_t)a.in_ss % 16) == 0, "%s: input scale/shift must be 16-byte aligned", what);
     DMF_CHECK_ARG(a.C <= 4096, "%s: input-affine conv over %d channels exceeds the LDS staging", what, a.C);
-    const size_t lds_ina = lds_total + (size_t)a.C * 8;
-    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
-#define DMF_INA_BUF(TT, IA)                                                                                         do {                                                                                                                switch (cfg) {                                                                                                      case 3: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 128, 128, IA>), g, b, lds_ina, st, a); break;       case 2: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 128, 64, IA>), g, b, lds_ina, st, a); break;        case 1: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 64, 128, IA>), g, b, lds_ina, st, a); break;        default: hipLaunchKernelGGL((k_conv_fwd_buf<TT, false, false, 64, 64, IA>), g, b, lds_ina, st, a);             }                                                                                                               } while (0)
-#define DMF_INA_ACT(TT)                                                                        do {                                                                                           switch (a.act_in) {                                                                            case DMF_ACT_NONE: DMF_INA_BUF(TT, DMF_ACT_NONE); break;                                     case DMF_ACT_RELU: DMF_INA_BUF(TT, DMF_ACT_RELU); break;                                     case DMF_ACT_GELU: DMF_INA_BUF(TT, DMF_ACT_GELU); break;                                     default: DMF_CHECK_ARG(false, "%s: unsupported input activation %d", what, a.act_in);     }                                                                                          } while (0)
-    if (dtype == DMF_BF16) DMF_INA_ACT(bf16_t);
-    else DMF_INA_ACT(float);
-#undef DMF_INA_ACT
-#undef DMF_INA_BUF
-  } else if (plan.buf) {
-    const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
-    const bool dual = a.x2 != nullptr;
-    const int cfg = (plan.bm == 128 ? 2 : 0) + (plan.bn == 128 ? 1 : 0);
-    if (dtype == DMF_BF16) {
-      switch (cfg) {
-        case 3: DMF_BUF_LAUNCH(bf16_t, 128, 128); break;
-        case 2: DMF_BUF_LAUNCH(bf16_t, 128, 64); break;
-        case 1: DMF_BUF_LAUNCH(bf16_t, 64, 128); break;
-        default: DMF_BUF_LAUNCH(bf16_t, 64, 64); break;
-      }
-    } else {
-      switch (cfg) {
-        case 3: DMF_BUF_LAUNCH(float, 128, 128); break;
-        case 2: DMF_BUF_LAUNCH(float, 128, 64); break;
-        case 1: DMF_BUF_LAUNCH(float, 64, 128); break;
-        default: DMF_BUF_LAUNCH(float, 64, 64); break;
-      }
-    }
-  } else if (a.in_ss == nullptr) {
-    if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, -1);
-    else DMF_CONV_LAUNCH(float, false, -1);
-  } else {
-    DMF_CHECK_ARG(a.x2 == nullptr, "%s: input affine needs a single source", what);
-    DMF_CHECK_ARG(((uintptr_t)a.in_ss % 16) == 0, "%s: input scale/shift must be 16-byte aligned", what);
-    switch (a.act_in) {
-      case DMF_ACT_NONE:
-        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_NONE); else DMF_CONV_LAUNCH(float, false, DMF_ACT_NONE);
-        break;
-      case DMF_ACT_RELU:
-        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_RELU); else DMF_CONV_LAUNCH(float, false, DMF_ACT_RELU);
-        break;
-      case DMF_ACT_GELU:
-        if (dtype == DMF_BF16) DMF_CONV_LAUNCH(bf16_t, false, DMF_ACT_GELU); else DMF_CONV_LAUNCH(float, false, DMF_ACT_GELU);
-        break;
-      default:
-        DMF_CHECK_ARG(false, "%s: unsupported input activation %d", what, a.act_in);
-    }
   }
-#undef DMF_BUF_LAUNCH
-#undef DMF_CONV_LAUNCH
+  if (!dgrad && a.in_ss != nullptr) {
+    DMF_CHECK_ARG(plan.buf || a.x2 == nullptr, "%s: input affine needs a single source", what);
+    DMF_CHECK_ARG(((uintptr_t)a.in_ss % 16) == 0, "%s: input scale/shift must be 16-byte aligned", what);
+    DMF_CHECK_ARG(a.act_in == DMF_ACT_NONE || a.act_in == DMF_ACT_RELU || a.act_in == DMF_ACT_GELU,
+                  "%s: unsupported input activation %d", what, a.act_in);
+  }
+  DMF_DISPATCH_DTYPE(dtype, T, launch_conv_t<T>(plan, dgrad, a, nblk, lds_total, st));
   DMF_LAUNCH_CHECK(what);
   return 0;
 }
@@ -1363,6 +1374,7 @@ __device__ __forceinline__ float weight_prep_elem(const float* __restrict__ w, l
 constexpr int WPM_SPAN = 4096;
 __device__ __forceinline__ void wprep_store(const dmf_wprep_job& J, long long i, float v) {
   if (J.dtype == DMF_BF16) ((bf16_t*)J.out)[i] = f2bf(v);
+  else if (J.dtype == DMF_F16) ((f16_t*)J.out)[i] = (f16_t)v;
   else ((float*)J.out)[i] = v;
 }
 __global__ void __launch_bounds__(256) k_weight_prep_multi(const dmf_wprep_job* __restrict__ jobs,
@@ -1483,13 +1495,13 @@ static int conv_fwd_common(ConvArgs& a, int dtype, const void* x, int N, int H, 
                            const void* x2, int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride,
                            int pad, int dil, const float* bias, void* y, int Ho, int Wo, int ldy, int act,
                            const float* in_ss, int in_act, const char* what) {
-  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "%s: bad dtype %d", what, dtype);
+  DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "%s: bad dtype %d", what, dtype);
   DMF_CHECK_ARG(stride >= 1 && dil >= 1 && KH >= 1 && KW >= 1, "%s: bad geometry", what);
   DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
                 "%s: output size %dx%d inconsistent with input %dx%d k%d s%d p%d d%d", what, Ho, Wo, H, W, KH,
                 stride, pad, dil);
   a.x = x; a.w = w; a.bias = bias; a.y = y;
-  const int epc = dtype == DMF_BF16 ? 8 : 4;
+  const int epc = is16(dtype) ? 8 : 4;
   DMF_CHECK_ARG(!x2 || (Cin2 > 0 && Cin2 % epc == 0 && ldx2 % epc == 0 && ((uintptr_t)x2 % 16) == 0),
                 "%s: bad second source (C2=%d ld2=%d)", what, Cin2, ldx2);
   a.N = N; a.H = H; a.W = W; a.C = Cin + (x2 ? Cin2 : 0); a.ldx = ldx;
@@ -1554,7 +1566,7 @@ extern "C" int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, 
 extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,
                                 int Cin, int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx,
                                 void* stream) {
-  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_dgrad: bad dtype %d", dtype);
+  DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "dmf_conv2d_dgrad: bad dtype %d", dtype);
   DMF_CHECK_ARG(Ho == (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 && Wo == (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1,
                 "dmf_conv2d_dgrad: geometry mismatch");
   ConvArgs a{};
@@ -1582,12 +1594,8 @@ extern "C" int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Co
   DMF_CHECK_ARG(CinP >= Cin && mode >= 0 && mode <= 2, "dmf_conv_weight_prep: bad args");
   const long long total = (long long)Cout * CinP * KH * KW;
   const int grid = (int)(total < 65536 * 256LL ? cdiv(total, 256) : 65536);
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_weight_prep<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)out, Cout,
-                       Cin, CinP, KH, KW, mode);
-  else
-    hipLaunchKernelGGL(k_weight_prep<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, (float*)out, Cout, Cin,
-                       CinP, KH, KW, mode);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_weight_prep<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, w,
+                                                   (T*)out, Cout, Cin, CinP, KH, KW, mode));
   DMF_LAUNCH_CHECK("dmf_conv_weight_prep");
   return 0;
 }

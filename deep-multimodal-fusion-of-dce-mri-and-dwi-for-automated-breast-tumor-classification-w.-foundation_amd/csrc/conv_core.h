@@ -11,6 +11,7 @@ namespace dmf {
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
+
 struct ConvArgs {
   const void* x;      // A source (FWD: input; DGRAD: dy)
   const void* w;      // B source [Nout][Ktot]
@@ -195,7 +196,7 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int fr) {
 
 // (FM pixel fragments per wave, TBM pixel rows per tile: 8 / 256 for the 256x256 forms, 4 / 128 for
 // the 128x128 two-workgroup form; two pixel-half waves per channel slab in both)
-template <int EPI, int TBN = QBN, int FM = 8, int TBM = QBM>
+template <int EPI, int TBN = QBN, int FM = 8, int TBM = QBM, typename T = bf16_t>
 __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM][4], int lin,
                                             __amdgpu_buffer_rsrc_t ry, float* sred, const float* sbias, int tid,
                                             int wm, int wn, int fr, int fg) {
@@ -234,7 +235,7 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
     }
     uint32_t w8[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) w8[e] = (uint32_t)f2bf(v[2 * e]) | ((uint32_t)f2bf(v[2 * e + 1]) << 16);
+    for (int e = 0; e < 8; ++e) w8[e] = B16<T>::pack(v[2 * e], v[2 * e + 1]);
     const unsigned off = ok ? (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2) : BUF_OOB;
     if (a.dbg & 32) {
       __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 2);
@@ -295,10 +296,10 @@ __device__ __forceinline__ void vm_wait_rt(int n) {
 // 7x7 / stride-2 stem conv (conv_stem.hip): legality, pixels per workgroup (= BN slab rows), launcher
 bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a);
 int conv_stem_m_tile(const ConvArgs& a);
-int launch_conv_stem(ConvArgs& a, hipStream_t st);
+int launch_conv_stem(ConvArgs& a, hipStream_t st, int dtype);
 
 // persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 BN statistics, 1 + act: bias + act)
-int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st);
+int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype);
 int conv_pp_tune(int value);  // dmf_conv_tune key 8
 constexpr int PP_THREADS = 512;
 constexpr int PP_HALF = 128 * 128;  // one half-tile: 128 rows x 128 B

@@ -63,7 +63,7 @@ __device__ __forceinline__ void vm_wait() {
 // tile's first half-tiles are in flight under the finished tile's epilogue (its 16 stores, +2 float64
 // atomics in statistics mode, are then younger than those DMA pieces: the first K-tile after an
 // epilogue waits with 16 more).
-template <bool PADCHK, bool DUAL, int EPI>
+template <bool PADCHK, bool DUAL, int EPI, typename T = bf16_t>
 __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   constexpr int ES = 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -199,8 +199,7 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int j0 = 0; j0 < 2; ++j0)
-          acc[4 * ph + ii][2 * chh + j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              *(const bf16x8_t*)&cv[kk][j0], *(const bf16x8_t*)&pv[kk][ii], acc[4 * ph + ii][2 * chh + j0], 0, 0, 0);
+          acc[4 * ph + ii][2 * chh + j0] = mfma16<T>(cv[kk][j0], pv[kk][ii], acc[4 * ph + ii][2 * chh + j0]);
   };
   // the MFMA segment of phase p: barrier, this wave's fragment reads retired, 16 MFMAs at priority 1, barrier
   auto mfma_segment = [&](int p) {
@@ -221,7 +220,7 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   // store / reduce from the accumulators (ps_epilogue zeroes them), re-stagger
   auto epilogue = [&](int j, bool restagger) {
     if (wm == 0) pp_barrier();
-    ps_epilogue<EPI>(a, acc, tile_lin(j), ry, sred, sbias, tid, wm, wn, fr, fg);
+    ps_epilogue<EPI, QBN, 8, QBM, T>(a, acc, tile_lin(j), ry, sred, sbias, tid, wm, wn, fr, fg);
     __builtin_amdgcn_sched_barrier(0);
     if (restagger && wm == 1) pp_barrier();
   };
@@ -306,7 +305,7 @@ int conv_pp_tune(int value) {
   return 0;
 }
 
-int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st) {
+int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -319,20 +318,26 @@ int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_
   const size_t lds = (size_t)PP_LDS + lds_bias;
   DMF_CHECK_ARG(lds <= 160 * 1024, "conv_pp: %d output channels of bias exceed the LDS staging", a.Nout);
   a.dbg = 0;
-#define DMF_PP(E)                                                                                    \
-  do {                                                                                               \
-    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_pp<true, true, E>), g, b, lds, st, a);      \
-    else if (plain) hipLaunchKernelGGL((k_conv_fwd_pp<false, false, E>), g, b, lds, st, a);         \
-    else hipLaunchKernelGGL((k_conv_fwd_pp<true, false, E>), g, b, lds, st, a);                     \
+#define DMF_PP(E, TT)                                                                                    \
+  do {                                                                                                   \
+    if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_pp<true, true, E, TT>), g, b, lds, st, a);      \
+    else if (plain) hipLaunchKernelGGL((k_conv_fwd_pp<false, false, E, TT>), g, b, lds, st, a);         \
+    else hipLaunchKernelGGL((k_conv_fwd_pp<true, false, E, TT>), g, b, lds, st, a);                     \
   } while (0)
-  switch (epi) {
-    case 0: DMF_PP(0); break;
-    case 1: DMF_PP(1); break;
-    case 2: DMF_PP(2); break;
-    case 3: DMF_PP(3); break;
-    case 5: DMF_PP(5); break;
-    default: DMF_PP(4); break;
-  }
+#define DMF_PP_E(TT)                  \
+  do {                                \
+    switch (epi) {                    \
+      case 0: DMF_PP(0, TT); break;   \
+      case 1: DMF_PP(1, TT); break;   \
+      case 2: DMF_PP(2, TT); break;   \
+      case 3: DMF_PP(3, TT); break;   \
+      case 5: DMF_PP(5, TT); break;   \
+      default: DMF_PP(4, TT); break;  \
+    }                                 \
+  } while (0)
+  if (dtype == DMF_F16) DMF_PP_E(f16_t);
+  else DMF_PP_E(bf16_t);
+#undef DMF_PP_E
 #undef DMF_PP
   DMF_LAUNCH_CHECK("conv_pp");
   return 0;

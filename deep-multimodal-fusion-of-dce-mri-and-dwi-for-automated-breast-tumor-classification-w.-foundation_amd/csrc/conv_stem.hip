@@ -28,6 +28,7 @@
 // pixels are summed in registers across all its rows and added once at the end
 // (float64 arena replicas, or one slab row per workgroup).
 #include <algorithm>
+#include <type_traits>
 
 #include "conv_core.h"
 
@@ -36,8 +37,9 @@ namespace dmf {
 constexpr int STEM_SLOTS = 9;  // 7 rows in use + the next step's 2
 
 // C: padded input channels (8 / 16); STATS: BN statistics epilogue (a.partials)
-template <int C, bool STATS>
+template <int C, bool STATS, bool F16 = false>
 __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plane) {
+  typedef typename std::conditional<F16, f16_t, bf16_t>::type T;  // storage type (bf16 / f16)
   constexpr int NPL = C / 8;               // 16-B channel planes per pixel
   constexpr int CP = 32 / C;               // taps per K-chunk
   constexpr int TG = (7 + CP - 1) / CP;    // K-chunks per filter row
@@ -57,15 +59,14 @@ __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plan
   // this wave's 16 output channels: weights of every K-chunk (row operand), loaded before any DMA
   // is issued ([Cout][7][7][C] bf16; taps past the 7th are zero)
   const int co = wid * 16 + fr;
-  bf16x8_t wf[NCH];
+  uint4 wf[NCH];
   {
     const char* W = (const char*)a.w;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int r = c / TG, g = c % TG;
       const int s = g * CP + (fg * 8) / C, ci = (fg * 8) % C;
-      wf[c] = s < 7 ? *(const bf16x8_t*)(W + ((size_t)((co * 7 + r) * 7 + s) * C + ci) * 2)
-                    : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      wf[c] = s < 7 ? *(const uint4*)(W + ((size_t)((co * 7 + r) * 7 + s) * C + ci) * 2) : make_uint4(0, 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -116,8 +117,8 @@ __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plan
           const int wo = cb * 64 + i * 16 + fr;
           const int p = C == 16 ? 2 * wo + 2 * g + (fg >> 1) : 2 * wo + 4 * g + fg;
           const int pl = C == 16 ? (fg & 1) : 0;
-          const bf16x8_t pv = *(const bf16x8_t*)(smem + rb[r] + pl * pl1 + p * 16);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], pv, acc[i], 0, 0, 0);
+          const uint4 pv = *(const uint4*)(smem + rb[r] + pl * pl1 + p * 16);
+          acc[i] = mfma16<T>(wf[c], pv, acc[i]);
         }
       }
       // lane: pixel wo = cb*64 + 16i + fr, channels 16 wid + 4 fg + 0..3
@@ -125,8 +126,8 @@ __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plan
       for (int i = 0; i < 4; ++i) {
         const int m = (n * a.Ho + ho) * a.Wo + cb * 64 + i * 16 + fr;
         uint32_t w2[2];
-        w2[0] = (uint32_t)f2bf(acc[i][0]) | ((uint32_t)f2bf(acc[i][1]) << 16);
-        w2[1] = (uint32_t)f2bf(acc[i][2]) | ((uint32_t)f2bf(acc[i][3]) << 16);
+        w2[0] = B16<T>::pack(acc[i][0], acc[i][1]);
+        w2[1] = B16<T>::pack(acc[i][2], acc[i][3]);
         const unsigned off = (unsigned)(((size_t)m * a.ldy + wid * 16 + fg * 4) * 2);
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, w2), ry, off, 0, 0);
@@ -170,7 +171,7 @@ static int stem_rows(int N, int Ho) {
 static int stem_plane(int W) { return (((W + 6) * 16 + 1023) / 1024) * 1024; }
 
 bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a) {
-  if (dtype != DMF_BF16 || dgrad || a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.dil != 1) return false;
+  if (!is16(dtype) || dgrad || a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.dil != 1) return false;
   if ((a.C != 8 && a.C != 16) || a.ldx != a.C || a.x2 != nullptr || a.in_ss != nullptr || a.tickets != nullptr)
     return false;
   if (a.Nout != 64 || a.bias != nullptr || a.act != DMF_ACT_NONE || a.ldy % 4 != 0) return false;
@@ -184,19 +185,25 @@ bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a) {
 // pixels per workgroup (the BN statistics slab has one row per workgroup)
 int conv_stem_m_tile(const ConvArgs& a) { return stem_rows(a.N, a.Ho) * a.Wo; }
 
-int launch_conv_stem(ConvArgs& a, hipStream_t st) {
+int launch_conv_stem(ConvArgs& a, hipStream_t st, int dtype) {
   const int rpw = stem_rows(a.N, a.Ho);
   const int plane = stem_plane(a.W);
   const size_t lds = (size_t)STEM_SLOTS * (a.C == 16 ? 2 * plane + 16 : plane);
   const dim3 g((unsigned)(a.N * (a.Ho / rpw))), b(256);
   const bool stats = a.partials != nullptr;
-  if (a.C == 16) {
-    if (stats) hipLaunchKernelGGL((k_conv_stem<16, true>), g, b, lds, st, a, rpw, plane);
-    else hipLaunchKernelGGL((k_conv_stem<16, false>), g, b, lds, st, a, rpw, plane);
-  } else {
-    if (stats) hipLaunchKernelGGL((k_conv_stem<8, true>), g, b, lds, st, a, rpw, plane);
-    else hipLaunchKernelGGL((k_conv_stem<8, false>), g, b, lds, st, a, rpw, plane);
-  }
+#define DMF_STEM(F)                                                                      \
+  do {                                                                                   \
+    if (a.C == 16) {                                                                     \
+      if (stats) hipLaunchKernelGGL((k_conv_stem<16, true, F>), g, b, lds, st, a, rpw, plane);  \
+      else hipLaunchKernelGGL((k_conv_stem<16, false, F>), g, b, lds, st, a, rpw, plane);       \
+    } else {                                                                             \
+      if (stats) hipLaunchKernelGGL((k_conv_stem<8, true, F>), g, b, lds, st, a, rpw, plane);   \
+      else hipLaunchKernelGGL((k_conv_stem<8, false, F>), g, b, lds, st, a, rpw, plane);        \
+    }                                                                                    \
+  } while (0)
+  if (dtype == DMF_F16) DMF_STEM(true);
+  else DMF_STEM(false);
+#undef DMF_STEM
   DMF_LAUNCH_CHECK("conv_stem");
   return 0;
 }

@@ -150,8 +150,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8_w*)&av[i], *(bf16x8_w*)&bv[j], acc[i][j],
-                                                                0, 0, 0);
+            acc[i][j] = mfma16<T>(av[i], bv[j], acc[i][j]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -196,7 +195,7 @@ __device__ __forceinline__ int wtr_off(int row, int ch) {
   return (row << 8) + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
 }
 
-template <int WM, int WN>
+template <int WM, int WN, typename ET = bf16_t>
 __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_wgrad_tr(WgArgs a) {
   constexpr int T = 64 * WM * WN;
   constexpr int BM = 64 * WM, BN = 64 * WN, BK = 64;
@@ -331,7 +330,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<ET>(__builtin_bit_cast(uint4, af[i]), __builtin_bit_cast(uint4, bfr[j]), acc[i][j]);
     }
     if (kt + 1 < nk) lds_store(cur ^ 1);
     __syncthreads();
@@ -363,10 +362,12 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
 // step's 8 pieces per wave issued right after the barrier that frees them.
 // DUAL (channel-concat input): each 128-column tile must lie in one tap of
 // one source (Cin % 128 == 0, C1 % 128 == 0), so the source is wave-uniform.
-template <bool DUAL, int WM, int WN>
+// FMW: 16-row output-channel fragments per wave (4: a 64x64 wave tile; 8: 128x64, the 256x256 tile of
+// 8 waves, half the operand staging per MFMA of the 128x128 / 128x256 forms)
+template <bool DUAL, int WM, int WN, int FMW = 4, typename ET = bf16_t>
 __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_wgrad_dma(WgArgs a) {
   constexpr int NW = WM * WN;
-  constexpr int BM = 64 * WM, BN = 64 * WN, BK = 64, SUB = BK * 256;
+  constexpr int BM = 16 * FMW * WM, BN = 64 * WN, BK = 64, SUB = BK * 256;
   constexpr int SA_N = BM / 128, SB_N = BN / 128, STAGE = (SA_N + SB_N) * SUB;
   constexpr int PA = SA_N * 16 / NW, PB = SB_N * 16 / NW;  // 1 KiB DMA pieces per wave per operand
   static_assert(PA >= 1 && PB >= 1 && PA * NW == SA_N * 16 && PB * NW == SB_N * 16, "piece split");
@@ -449,9 +450,9 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
     }
   };
 
-  f32x4_w acc[4][4];
+  f32x4_w acc[FMW][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FMW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_w{0.f, 0.f, 0.f, 0.f};
 
@@ -467,13 +468,13 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
     const char* SB = SA + SA_N * SUB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_w af[4], bfr[4];
+      bf16x8_w af[FMW], bfr[4];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = kk * 32 + 8 * g + 4 * h + q;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int cl = wm * 64 + i * 16;
+        for (int i = 0; i < FMW; ++i) {
+          const int cl = wm * (16 * FMW) + i * 16;
           const char* pa = SA + (cl >> 7) * SUB + wtr_off(row, ((cl & 127) >> 3) + (p4 >> 1)) + 8 * (p4 & 1);
           const v4s_w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_w*)pa);
 #pragma unroll
@@ -489,21 +490,21 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) k_conv_w
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FMW; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<ET>(__builtin_bit_cast(uint4, af[i]), __builtin_bit_cast(uint4, bfr[j]), acc[i][j]);
     }
   }
   float* slab = a.ws + (size_t)blockIdx.y * a.Cout * a.Ktot;
   const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FMW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wm * 64 + i * 16 + fg * 4 + e;
+        const int co = co0 + wm * (16 * FMW) + i * 16 + fg * 4 + e;
         const int k = k0 + wn * 64 + j * 16 + fr;
         if (co < a.Cout && k < a.Ktot) slab[(size_t)co * a.Ktot + k] = acc[i][j][e];
       }
@@ -917,11 +918,20 @@ static int wgrad_tr_enabled() { return g_wgrad_tr; }
 static int g_wgrad_dma = 1;
 static int wgrad_dma_enabled() { return g_wgrad_dma; }
 static int g_wgrad_wide = 1;
+// key 3: the 256x256 LDS-DMA tile (8 waves of 128x64, one workgroup per CU): 0 off, 1 where legal
+static int g_wgrad_sq = 0;
+// the 256x256 form takes a launch (and sizes its pixel splits for it): bf16, 256-row and -column tiles
+// whole (Cout % 256 == 0, Ktot % 256 == 0); a dual-source input also needs Cin, C1 % 256 == 0 (checked
+// at launch, which otherwise keeps the 128-wide forms with the same split count)
+static bool wgrad_sq_ok(int dtype, int Cout, long long Ktot) {
+  return is16(dtype) && g_wgrad_sq && Cout % 256 == 0 && Ktot % 256 == 0;
+}
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
-  DMF_CHECK_ARG(key >= 0 && key <= 2, "dmf_conv_wgrad_tune: unknown key %d", key);
+  DMF_CHECK_ARG(key >= 0 && key <= 3, "dmf_conv_wgrad_tune: unknown key %d", key);
   if (key == 0) g_wgrad_dma = value != 0;
   else if (key == 1) g_wgrad_wide = value != 0;
+  else if (key == 3) g_wgrad_sq = value != 0;
   else {
     DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_wgrad_tune: transposed-read mode %d", value);
     g_wgrad_tr = value;
@@ -930,10 +940,12 @@ extern "C" int dmf_conv_wgrad_tune(int key, int value) {
 }
 
 extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int KW, long long M) {
-  const long long tiles = (long long)cdiv(Cout, 128) * cdiv((long long)KH * KW * Cin, 128);
+  const bool sq = wgrad_sq_ok(dtype, Cout, (long long)KH * KW * Cin) && wgrad_tr_enabled() && wgrad_dma_enabled();
+  const long long tiles = sq ? (long long)(Cout / 256) * (((long long)KH * KW * Cin) / 256)
+                             : (long long)cdiv(Cout, 128) * cdiv((long long)KH * KW * Cin, 128);
   // transposed-read kernel: ~2 resident blocks per CU, and every split costs
-  // a Cout x K fp32 slab round trip, so aim for one wave of 512 blocks
-  const long long target = (dtype == DMF_BF16 && wgrad_tr_enabled()) ? 512 : 1024;
+  // a Cout x K fp32 slab round trip, so aim for one wave of 512 blocks (256 of the 256x256 form)
+  const long long target = sq ? 256 : (is16(dtype) && wgrad_tr_enabled()) ? 512 : 1024;
   long long want = (target + tiles - 1) / tiles;
   // >= 256 pixels (4 K-steps) per split, and at most 64 MiB of fp32 slabs: a small
   // weight (64x64 1x1: one tile) then runs 128 splits of 4 K-steps instead of 32
@@ -949,14 +961,14 @@ extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int
 }
 
 extern "C" int dmf_conv2d_wgrad_pixel_step(int dtype) {
-  return dtype == DMF_BF16 ? 64 : 32;
+  return is16(dtype) ? 64 : 32;
 }
 
 extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
                                 int Cin2, int ldx2, const void* dy, int Ho, int Wo, int Cout, int lddy, int KH, int KW,
                                 int stride, int pad, int dil, int splits, float* workspace, void* stream) {
-  const int epc = dtype == DMF_BF16 ? 8 : 4;
-  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_conv2d_wgrad: bad dtype");
+  const int epc = is16(dtype) ? 8 : 4;
+  DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "dmf_conv2d_wgrad: bad dtype");
   DMF_CHECK_ARG(Cin % epc == 0 && ldx % epc == 0 && Cout % epc == 0 && lddy % epc == 0,
                 "dmf_conv2d_wgrad: channel counts/strides must be multiples of %d (Cin=%d Cout=%d)", epc, Cin, Cout);
   DMF_CHECK_ARG(splits >= 1 && workspace, "dmf_conv2d_wgrad: bad workspace");
@@ -974,41 +986,52 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
   a.mtiles = cdiv(Cout, 128);
   a.ntiles = cdiv(a.Ktot, 128);
   a.splits = splits;
-  const int bk = dtype == DMF_BF16 ? 64 : 8 * epc;
+  const int bk = is16(dtype) ? 64 : 8 * epc;
   a.pix_per_split = cdiv(cdiv(a.M, splits), bk) * bk;
   dim3 grid(a.mtiles * a.ntiles, splits);
   const size_t lds = 2 * 2 * 128 * 128;
   DMF_CHECK_ARG((uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && (!x2 || (uintptr_t)x2 % 16 == 0),
                 "dmf_conv2d_wgrad: pointers must be 16-byte aligned");
-  if (dtype == DMF_BF16 && wgrad_tr_enabled() == 2 && a.Ktot >= 256) {
-    // 128 x 256 tile, 8 waves: half the operand re-reads per flop
-    a.ntiles = cdiv(a.Ktot, 256);
-    grid = dim3(a.mtiles * a.ntiles, splits);
-    hipLaunchKernelGGL((k_conv_wgrad_tr<2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
-  } else if (dtype == DMF_BF16 && wgrad_tr_enabled() && wgrad_dma_enabled() &&
-             (long long)a.N * a.H * a.W * std::max(a.ldx, x2 ? a.ldx2 : 0) * 2 < (1LL << 31) &&
-             (long long)a.M * a.lddy * 2 < (1LL << 31) && (!x2 || (a.Cin % 128 == 0 && a.C1 % 128 == 0))) {
-    // 128x256 tiles (8 waves, one workgroup per CU, 96 KiB): a third less operand staging per
-    // flop than 128x128 at two workgroups per CU. Measured (tools/wgrad_bench.py): faster on the
-    // 1x1 convs up to K = 1024 (512->2048: 96.9 -> 87.0 us), slower on the 3x3s and K = 2048
-    const bool wide = g_wgrad_wide && a.KH * a.KW == 1 && a.Ktot >= 256 && a.Ktot <= 1024 && a.Cout >= 128 &&
-                      (!x2 || (a.Cin % 256 == 0 && a.C1 % 256 == 0));
-    if (wide) {
+  auto launch16 = [&](auto tag) {
+    using ET = decltype(tag);
+    if (wgrad_tr_enabled() == 2 && a.Ktot >= 256) {
+      // 128 x 256 tile, 8 waves: half the operand re-reads per flop
       a.ntiles = cdiv(a.Ktot, 256);
       grid = dim3(a.mtiles * a.ntiles, splits);
-      if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
-      else hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 4>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
-    } else if (x2) {
-      hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+      hipLaunchKernelGGL((k_conv_wgrad_tr<2, 4, ET>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+    } else if (wgrad_tr_enabled() && wgrad_dma_enabled() &&
+               (long long)a.N * a.H * a.W * std::max(a.ldx, x2 ? a.ldx2 : 0) * 2 < (1LL << 31) &&
+               (long long)a.M * a.lddy * 2 < (1LL << 31) && (!x2 || (a.Cin % 128 == 0 && a.C1 % 128 == 0))) {
+      // 128x256 tiles (8 waves, one workgroup per CU, 96 KiB): a third less operand staging per
+      // flop than 128x128 at two workgroups per CU. Measured (tools/wgrad_bench.py): faster on the
+      // 1x1 convs up to K = 1024 (512->2048: 96.9 -> 87.0 us), slower on the 3x3s and K = 2048
+      const bool wide = g_wgrad_wide && a.KH * a.KW == 1 && a.Ktot >= 256 && a.Ktot <= 1024 && a.Cout >= 128 &&
+                        (!x2 || (a.Cin % 256 == 0 && a.C1 % 256 == 0));
+      if (wgrad_sq_ok(dtype, a.Cout, a.Ktot) && (!x2 || (a.Cin % 256 == 0 && a.C1 % 256 == 0))) {
+        a.mtiles = a.Cout / 256;
+        a.ntiles = a.Ktot / 256;
+        grid = dim3(a.mtiles * a.ntiles, splits);
+        if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 4, 8, ET>), grid, dim3(512), (size_t)2 * 4 * 64 * 256, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 4, 8, ET>), grid, dim3(512), (size_t)2 * 4 * 64 * 256, (hipStream_t)stream, a);
+      } else if (wide) {
+        a.ntiles = cdiv(a.Ktot, 256);
+        grid = dim3(a.mtiles * a.ntiles, splits);
+        if (x2) hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 4, 4, ET>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+        else hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 4, 4, ET>), grid, dim3(512), (size_t)2 * 3 * 64 * 256, (hipStream_t)stream, a);
+      } else if (x2) {
+        hipLaunchKernelGGL((k_conv_wgrad_dma<true, 2, 2, 4, ET>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+      } else {
+        hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 2, 4, ET>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+      }
+    } else if (wgrad_tr_enabled()) {
+      hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2, ET>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
     } else {
-      hipLaunchKernelGGL((k_conv_wgrad_dma<false, 2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(k_conv_wgrad<ET>, grid, dim3(256), lds, (hipStream_t)stream, a);
     }
-  } else if (dtype == DMF_BF16 && wgrad_tr_enabled())
-    hipLaunchKernelGGL((k_conv_wgrad_tr<2, 2>), grid, dim3(256), (size_t)2 * 2 * 64 * 256, (hipStream_t)stream, a);
-  else if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_wgrad<bf16_t>, grid, dim3(256), lds, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(k_conv_wgrad<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
+  };
+  if (dtype == DMF_BF16) launch16(bf16_t{});
+  else if (dtype == DMF_F16) launch16(f16_t{});
+  else hipLaunchKernelGGL(k_conv_wgrad<float>, grid, dim3(256), lds, (hipStream_t)stream, a);
   DMF_LAUNCH_CHECK("dmf_conv2d_wgrad");
   return 0;
 }
@@ -1042,12 +1065,8 @@ extern "C" int dmf_conv_cout1_fwd(int dtype, const void* x, int N, int H, int W,
   const long long M = (long long)N * Ho * Wo;
   if (M == 0) return 0;
   const int grid = (int)((M + 15) / 16);
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cout1<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
-                       Cin, ldx, w, bias, KH, KW, stride, pad, dil, (bf16_t*)y, Ho, Wo, ldy, act);
-  else
-    hipLaunchKernelGGL(k_conv_cout1<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
-                       Cin, ldx, w, bias, KH, KW, stride, pad, dil, (float*)y, Ho, Wo, ldy, act);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cout1<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
+                       Cin, ldx, w, bias, KH, KW, stride, pad, dil, (T*)y, Ho, Wo, ldy, act));
   DMF_LAUNCH_CHECK("dmf_conv_cout1_fwd");
   return 0;
 }
@@ -1060,21 +1079,13 @@ extern "C" int dmf_conv_cout1_dgrad(int dtype, const void* dy, int lddy, const f
   if (total == 0) return 0;
   if (Cin % 8 == 0 && lddx % 8 == 0 && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)w % 16) == 0 && total < (1LL << 31)) {
     const long long t8 = total / 8;
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_conv_cout1_dgrad8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (bf16_t*)dx, lddx);
-    else
-      hipLaunchKernelGGL(k_conv_cout1_dgrad8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (float*)dx, lddx);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cout1_dgrad8<T>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream,
+                         (const T*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (T*)dx, lddx));
     DMF_LAUNCH_CHECK("dmf_conv_cout1_dgrad");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cout1_dgrad<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (bf16_t*)dx, lddx);
-  else
-    hipLaunchKernelGGL(k_conv_cout1_dgrad<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (float*)dx, lddx);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cout1_dgrad<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dy, lddy, w, N, H, W, Cin, KH, KW, stride, pad, dil, Ho, Wo, (T*)dx, lddx));
   DMF_LAUNCH_CHECK("dmf_conv_cout1_dgrad");
   return 0;
 }
@@ -1118,19 +1129,11 @@ static int cout1_wgrad(int dtype, const void* x, int N, int H, int W, int Cin, i
     const int KV = K / 8;
     const int CVt = KV >= 64 ? 64 : (KV >= 32 ? 32 : (KV >= 16 ? 16 : (KV >= 8 ? 8 : (KV >= 4 ? 4 : (KV >= 2 ? 2 : 1)))));
     const dim3 g8(cdiv(KV, CVt), splits);
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_conv_cout1_wgrad8r<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
-                         W, Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, CVt, workspace,
-                         wsb);
-    else
-      hipLaunchKernelGGL(k_conv_cout1_wgrad8r<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
-                         Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, CVt, workspace, wsb);
-  } else if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cout1_wgrad<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H, W,
-                       Cin, ldx, (const bf16_t*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
-  else
-    hipLaunchKernelGGL(k_conv_cout1_wgrad<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
-                       Cin, ldx, (const float*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cout1_wgrad8r<T>, g8, dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H,
+                         W, Cin, ldx, (const T*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, CVt, workspace,
+                         wsb));
+  } else DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cout1_wgrad<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H, W,
+                       Cin, ldx, (const T*)dy, lddy, KH, KW, stride, pad, dil, Ho, Wo, pps, workspace, wsb));
   DMF_LAUNCH_CHECK("dmf_conv_cout1_wgrad");
   if (dw)
     hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(K, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, splits, K, dw,
@@ -1144,12 +1147,8 @@ extern "C" int dmf_conv_cin1_fwd(int dtype, const void* x, int ldx, const float*
                                  long long M, int Cout, int act, void* stream) {
   DMF_CHECK_ARG(x && w && y, "dmf_conv_cin1_fwd: null pointer");
   if (M == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cin1<bf16_t>, dim3(gsz(M * Cout)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, w, bias, (bf16_t*)y, ldy, M, Cout, act);
-  else
-    hipLaunchKernelGGL(k_conv_cin1<float>, dim3(gsz(M * Cout)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
-                       ldx, w, bias, (float*)y, ldy, M, Cout, act);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cin1<T>, dim3(gsz(M * Cout)), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       ldx, w, bias, (T*)y, ldy, M, Cout, act));
   DMF_LAUNCH_CHECK("dmf_conv_cin1_fwd");
   return 0;
 }
@@ -1159,12 +1158,8 @@ extern "C" int dmf_conv_cin1_dgrad(int dtype, const void* dy, int lddy, const fl
   DMF_CHECK_ARG(dy && w && dx, "dmf_conv_cin1_dgrad: null pointer");
   if (M == 0) return 0;
   const int grid = (int)((M + 3) / 4);
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cin1_dgrad<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                       lddy, w, (bf16_t*)dx, lddx, M, Cout);
-  else
-    hipLaunchKernelGGL(k_conv_cin1_dgrad<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
-                       w, (float*)dx, lddx, M, Cout);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cin1_dgrad<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                       lddy, w, (T*)dx, lddx, M, Cout));
   DMF_LAUNCH_CHECK("dmf_conv_cin1_dgrad");
   return 0;
 }
@@ -1177,12 +1172,8 @@ extern "C" int dmf_conv_cin1_wgrad(int dtype, const void* x, int ldx, const void
   DMF_CHECK_ARG(x && dy && workspace && Cout <= 256, "dmf_conv_cin1_wgrad: bad args (Cout<=256)");
   const int tiles = (int)((M + 255) / 256);
   float* wsb = db ? workspace + (size_t)tiles * Cout : nullptr;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_conv_cin1_wgrad<bf16_t>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, (const bf16_t*)dy, lddy, M, Cout, workspace, wsb);
-  else
-    hipLaunchKernelGGL(k_conv_cin1_wgrad<float>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
-                       (const float*)dy, lddy, M, Cout, workspace, wsb);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_conv_cin1_wgrad<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       ldx, (const T*)dy, lddy, M, Cout, workspace, wsb));
   DMF_LAUNCH_CHECK("dmf_conv_cin1_wgrad");
   // reduce tiles: treat [tiles][Cout] as splits x K
   if (dw) hipLaunchKernelGGL(k_sum_splits16, dim3(cdiv(Cout, 64)), dim3(1024), 0, (hipStream_t)stream, workspace, tiles, Cout, dw, 1, 0);

@@ -1021,21 +1021,13 @@ extern "C" int dmf_tokens_fwd(int dtype, const void* x, int ldx, int B, int H, i
   if (C % 8 == 0 && CV <= 64 && 64 % CV == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0 &&
       ((uintptr_t)tokens % 16) == 0 && (long long)B * H * W * ldx < (1LL << 31)) {
     const dim3 g(cdiv((long long)B * Hp * Wp, 4));
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_tokens_fwd8<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, B, H, W, C,
-                         Hp, Wp, tokens);
-    else
-      hipLaunchKernelGGL(k_tokens_fwd8<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, B, H, W, C,
-                         Hp, Wp, tokens);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_tokens_fwd8<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, B, H, W, C,
+                         Hp, Wp, tokens));
     DMF_LAUNCH_CHECK("dmf_tokens_fwd");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_tokens_fwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, B, H, W, C, Hp, Wp, tokens);
-  else
-    hipLaunchKernelGGL(k_tokens_fwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
-                       B, H, W, C, Hp, Wp, tokens);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_tokens_fwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       ldx, B, H, W, C, Hp, Wp, tokens));
   DMF_LAUNCH_CHECK("dmf_tokens_fwd");
   return 0;
 }
@@ -1047,21 +1039,13 @@ extern "C" int dmf_tokens_bwd(int dtype, const float* dtokens, int B, int H, int
   if (C % 8 == 0 && lddx % 8 == 0 && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)dtokens % 16) == 0 &&
       (long long)B * H * W * lddx < (1LL << 31)) {
     const long long t8 = total / 8;
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_tokens_bwd8<bf16_t>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
-                         Hp, Wp, (bf16_t*)dx, lddx, accumulate);
-    else
-      hipLaunchKernelGGL(k_tokens_bwd8<float>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
-                         Hp, Wp, (float*)dx, lddx, accumulate);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_tokens_bwd8<T>, dim3(gsz(t8)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                         Hp, Wp, (T*)dx, lddx, accumulate));
     DMF_LAUNCH_CHECK("dmf_tokens_bwd");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_tokens_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
-                       Hp, Wp, (bf16_t*)dx, lddx, accumulate);
-  else
-    hipLaunchKernelGGL(k_tokens_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
-                       Hp, Wp, (float*)dx, lddx, accumulate);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_tokens_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, dtokens, B, H, W, C,
+                       Hp, Wp, (T*)dx, lddx, accumulate));
   DMF_LAUNCH_CHECK("dmf_tokens_bwd");
   return 0;
 }
@@ -1071,13 +1055,9 @@ extern "C" int dmf_fusion_combine_fwd(int dtype, const void* p_dwi, const void* 
                                       int ldy, void* stream) {
   DMF_CHECK_ARG(p_dwi && p_dce && gates && y, "dmf_fusion_combine_fwd: bad args");
   const long long total = (long long)B * H * W * C;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_combine_fwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, gates, lowres, B, H, W, C, Hp, Wp, (bf16_t*)y,
-                       ldy);
-  else
-    hipLaunchKernelGGL(k_combine_fwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)p_dwi,
-                       (const float*)p_dce, ld, gates, lowres, B, H, W, C, Hp, Wp, (float*)y, ldy);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_combine_fwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)p_dwi, (const T*)p_dce, ld, gates, lowres, B, H, W, C, Hp, Wp, (T*)y,
+                       ldy));
   DMF_LAUNCH_CHECK("dmf_fusion_combine_fwd");
   return 0;
 }
@@ -1092,47 +1072,26 @@ extern "C" int dmf_fusion_combine_bwd(int dtype, const void* dy, int lddy, const
   const bool v8 = C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0 && lddy % 8 == 0 && ld % 8 == 0 &&
                   ((uintptr_t)dy % 16) == 0 && (!dlowres || ((uintptr_t)dlowres % 16) == 0) &&
                   ((uintptr_t)p_dwi % 16) == 0 && ((uintptr_t)p_dce % 16) == 0;
-  if (v8 && dtype == DMF_BF16) {
-    if (dp_dwi || dp_dce)
-      hipLaunchKernelGGL(k_combine_bwd_maps<bf16_t>, dim3(gsz(total)), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
-                         gates, H * W, C, total, (bf16_t*)dp_dwi, (bf16_t*)dp_dce, ldd);
+  if (v8) {
+    DMF_DISPATCH_DTYPE(dtype, T,
+      if (dp_dwi || dp_dce)
+        hipLaunchKernelGGL(k_combine_bwd_maps<T>, dim3(gsz(total)), dim3(256), 0, st_, (const T*)dy, lddy,
+                           gates, H * W, C, total, (T*)dp_dwi, (T*)dp_dce, ldd);
+      if (dgates)
+        hipLaunchKernelGGL(k_combine_bwd_gate8<T>, dim3(B), dim3(1024), 0, st_, (const T*)dy, lddy,
+                           (const T*)p_dwi, (const T*)p_dce, ld, H * W, C, dgates);
+      if (dlowres)
+        hipLaunchKernelGGL(k_combine_bwd_low8w<T>, dim3(cdiv((long long)B * Hp * Wp, 4)), dim3(256), 0, st_,
+                           (const T*)dy, lddy, B, H, W, C, Hp, Wp, dlowres));
+  } else DMF_DISPATCH_DTYPE(dtype, T, if (dp_dwi || dp_dce)
+      hipLaunchKernelGGL(k_combine_bwd_maps<T>, dim3(gsz(total)), dim3(256), 0, st_, (const T*)dy, lddy,
+                         gates, H * W, C, total, (T*)dp_dwi, (T*)dp_dce, ldd);
     if (dgates)
-      hipLaunchKernelGGL(k_combine_bwd_gate8<bf16_t>, dim3(B), dim3(1024), 0, st_, (const bf16_t*)dy, lddy,
-                         (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, H * W, C, dgates);
+      hipLaunchKernelGGL(k_combine_bwd_gate<T>, dim3(B), dim3(256), 0, st_, (const T*)dy, lddy,
+                         (const T*)p_dwi, (const T*)p_dce, ld, H * W, C, dgates);
     if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low8w<bf16_t>, dim3(cdiv((long long)B * Hp * Wp, 4)), dim3(256), 0, st_,
-                         (const bf16_t*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
-  } else if (v8) {
-    if (dp_dwi || dp_dce)
-      hipLaunchKernelGGL(k_combine_bwd_maps<float>, dim3(gsz(total)), dim3(256), 0, st_, (const float*)dy, lddy, gates,
-                         H * W, C, total, (float*)dp_dwi, (float*)dp_dce, ldd);
-    if (dgates)
-      hipLaunchKernelGGL(k_combine_bwd_gate8<float>, dim3(B), dim3(1024), 0, st_, (const float*)dy, lddy,
-                         (const float*)p_dwi, (const float*)p_dce, ld, H * W, C, dgates);
-    if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low8w<float>, dim3(cdiv((long long)B * Hp * Wp, 4)), dim3(256), 0, st_,
-                         (const float*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
-  } else if (dtype == DMF_BF16) {
-    if (dp_dwi || dp_dce)
-      hipLaunchKernelGGL(k_combine_bwd_maps<bf16_t>, dim3(gsz(total)), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
-                         gates, H * W, C, total, (bf16_t*)dp_dwi, (bf16_t*)dp_dce, ldd);
-    if (dgates)
-      hipLaunchKernelGGL(k_combine_bwd_gate<bf16_t>, dim3(B), dim3(256), 0, st_, (const bf16_t*)dy, lddy,
-                         (const bf16_t*)p_dwi, (const bf16_t*)p_dce, ld, H * W, C, dgates);
-    if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low<bf16_t>, dim3(gsz((long long)B * Hp * Wp * C)), dim3(256), 0, st_,
-                         (const bf16_t*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
-  } else {
-    if (dp_dwi || dp_dce)
-      hipLaunchKernelGGL(k_combine_bwd_maps<float>, dim3(gsz(total)), dim3(256), 0, st_, (const float*)dy, lddy, gates,
-                         H * W, C, total, (float*)dp_dwi, (float*)dp_dce, ldd);
-    if (dgates)
-      hipLaunchKernelGGL(k_combine_bwd_gate<float>, dim3(B), dim3(256), 0, st_, (const float*)dy, lddy,
-                         (const float*)p_dwi, (const float*)p_dce, ld, H * W, C, dgates);
-    if (dlowres)
-      hipLaunchKernelGGL(k_combine_bwd_low<float>, dim3(gsz((long long)B * Hp * Wp * C)), dim3(256), 0, st_,
-                         (const float*)dy, lddy, B, H, W, C, Hp, Wp, dlowres);
-  }
+      hipLaunchKernelGGL(k_combine_bwd_low<T>, dim3(gsz((long long)B * Hp * Wp * C)), dim3(256), 0, st_,
+                         (const T*)dy, lddy, B, H, W, C, Hp, Wp, dlowres));
   DMF_LAUNCH_CHECK("dmf_fusion_combine_bwd");
   return 0;
 }

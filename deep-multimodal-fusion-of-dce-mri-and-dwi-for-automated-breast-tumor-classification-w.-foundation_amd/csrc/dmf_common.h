@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <stdarg.h>
 
+#include "../../include/dmf_hip.h"
+
 namespace dmf {
 
 // ---------------------------------------------------------------- errors
@@ -45,6 +47,33 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+typedef _Float16 f16_t;   // IEEE binary16 storage (the "16-mixed" compute dtype)
+
+// 16-bit storage dtypes (8 elements per 16-B chunk, 16-bit MFMA operands)
+__host__ __device__ inline bool is16(int dt) { return dt == DMF_BF16 || dt == DMF_F16; }
+// run the statements with T bound to the storage type of dtype (bf16 / f16 / f32)
+#define DMF_DISPATCH_DTYPE(dtype, T, ...)          \
+  do {                                             \
+    switch (dtype) {                               \
+      case DMF_BF16: {                             \
+        typedef ::dmf::bf16_t T;                   \
+        __VA_ARGS__;                               \
+      } break;                                     \
+      case DMF_F16: {                              \
+        typedef ::dmf::f16_t T;                    \
+        __VA_ARGS__;                               \
+      } break;                                     \
+      default: {                                   \
+        typedef float T;                           \
+        __VA_ARGS__;                               \
+      } break;                                     \
+    }                                              \
+  } while (0)
+
+__device__ __forceinline__ float h2f(uint32_t bits16) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16); }
+// round-to-nearest-even (v_cvt_f16_f32); overflow to +-inf as torch's fp16 autocast
+__device__ __forceinline__ uint32_t f2h(float f) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f); }
+
 template <typename T> struct Cvt;
 template <> struct Cvt<float> {
   __device__ __forceinline__ static float load(float v) { return v; }
@@ -54,7 +83,41 @@ template <> struct Cvt<bf16_t> {
   __device__ __forceinline__ static float load(bf16_t v) { return bf2f(v); }
   __device__ __forceinline__ static bf16_t store(float v) { return f2bf(v); }
 };
+template <> struct Cvt<f16_t> {
+  __device__ __forceinline__ static float load(f16_t v) { return (float)v; }
+  __device__ __forceinline__ static f16_t store(float v) { return (f16_t)v; }
+};
 template <typename T> __device__ __forceinline__ float ld(const T* p) { return Cvt<T>::load(*p); }
+// is T a 16-bit storage type (bf16 / f16: 8 elements per 16-B chunk, 16-bit MFMA operands)
+template <typename T> struct Is16 { static constexpr bool value = sizeof(T) == 2; };
+
+// one 16x16x32 MFMA on 16-B fragments of 16-bit elements of storage type T (bf16 or f16: the two run
+// at the same rate on gfx950), fp32 accumulation
+typedef __attribute__((ext_vector_type(8))) short dmf_s16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 dmf_h16x8;
+typedef __attribute__((ext_vector_type(4))) float dmf_f32x4;
+template <typename T>
+__device__ __forceinline__ dmf_f32x4 mfma16(const uint4& a, const uint4& b, dmf_f32x4 c) {
+  if constexpr (__is_same(T, f16_t))
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(dmf_h16x8, a), __builtin_bit_cast(dmf_h16x8, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dmf_s16x8, a), __builtin_bit_cast(dmf_s16x8, b),
+                                                   c, 0, 0, 0);
+}
+
+// the two 16-bit elements of a 32-bit word (low element first) <-> floats, per storage type
+template <typename T> struct B16;
+template <> struct B16<bf16_t> {
+  __device__ __forceinline__ static float lo(uint32_t w) { return __uint_as_float(w << 16); }
+  __device__ __forceinline__ static float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+  __device__ __forceinline__ static uint32_t pack(float l, float h) { return (uint32_t)f2bf(l) | ((uint32_t)f2bf(h) << 16); }
+};
+template <> struct B16<f16_t> {
+  __device__ __forceinline__ static float lo(uint32_t w) { return h2f(w & 0xffffu); }
+  __device__ __forceinline__ static float hi(uint32_t w) { return h2f(w >> 16); }
+  __device__ __forceinline__ static uint32_t pack(float l, float h) { return f2h(l) | (f2h(h) << 16); }
+};
 template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = Cvt<T>::store(v); }
 
 // 8-element vector access (16 B for bf16, 32 B for f32); p must be aligned
@@ -67,6 +130,15 @@ __device__ __forceinline__ void ld8(const bf16_t* p, float v[8]) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+__device__ __forceinline__ void ld8(const f16_t* p, float v[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = h2f(w[i] & 0xffffu);
+    v[2 * i + 1] = h2f(w[i] >> 16);
+  }
+}
 __device__ __forceinline__ void ld8(const float* p, float v[8]) {
   const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
@@ -76,6 +148,12 @@ __device__ __forceinline__ void st8(bf16_t* p, const float v[8]) {
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void st8(f16_t* p, const float v[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = f2h(v[2 * i]) | (f2h(v[2 * i + 1]) << 16);
   *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
 }
 __device__ __forceinline__ void st8(float* p, const float v[8]) {

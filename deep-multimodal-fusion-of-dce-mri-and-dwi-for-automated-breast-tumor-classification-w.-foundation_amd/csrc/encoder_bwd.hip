@@ -233,33 +233,24 @@ extern "C" int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, i
                            const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C,
                            void* stream) {
   DMF_CHECK_ARG(dz && a && b && wlogit && da && db && dw, "dmf_mix_bwd: bad args");
-  const int es = dtype == DMF_BF16 ? 2 : 4;
+  const int es = is16(dtype) ? 2 : 4;
   if (C % 8 == 0 && lddz % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldd % 8 == 0 && M * std::max(ldd, lddz) < (1LL << 31) &&
       ((uintptr_t)dz | (uintptr_t)a | (uintptr_t)b | (uintptr_t)da | (uintptr_t)db) % (8 * es) == 0) {
     long long g8 = (M * C / 8 + 255) / 256;
     if (g8 > 2048) g8 = 2048;
     if (g8 < 1) g8 = 1;
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_mix_bwd8<bf16_t>, dim3((unsigned)g8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz,
-                         lddz, (const bf16_t*)a, lda, (const bf16_t*)b, ldb, wlogit, (bf16_t*)da, (bf16_t*)db, ldd, dw,
-                         (int)M, C);
-    else
-      hipLaunchKernelGGL(k_mix_bwd8<float>, dim3((unsigned)g8), dim3(256), 0, (hipStream_t)stream, (const float*)dz,
-                         lddz, (const float*)a, lda, (const float*)b, ldb, wlogit, (float*)da, (float*)db, ldd, dw,
-                         (int)M, C);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix_bwd8<T>, dim3((unsigned)g8), dim3(256), 0, (hipStream_t)stream, (const T*)dz,
+                         lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, dw,
+                         (int)M, C));
     DMF_LAUNCH_CHECK("dmf_mix_bwd");
     return 0;
   }
   long long g = (M * C + 255) / 256;
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_mix_bwd<bf16_t>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz,
-                       lddz, (const bf16_t*)a, lda, (const bf16_t*)b, ldb, wlogit, (bf16_t*)da, (bf16_t*)db, ldd, dw,
-                       M, C);
-  else
-    hipLaunchKernelGGL(k_mix_bwd<float>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                       (const float*)a, lda, (const float*)b, ldb, wlogit, (float*)da, (float*)db, ldd, dw, M, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix_bwd<T>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const T*)dz,
+                       lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, dw,
+                       M, C));
   DMF_LAUNCH_CHECK("dmf_mix_bwd");
   return 0;
 }
@@ -280,17 +271,10 @@ extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const vo
   float* S = workspace + (size_t)N * HW * hidden;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(N, cdiv(HW, MA_PIX));
-  if (dtype == DMF_BF16) {
-    hipLaunchKernelGGL(k_mask_attn_bwd1<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, lddo, (const bf16_t*)f,
-                       ldf, (const bf16_t*)m, P, stats, HW, C, (bf16_t*)df, lddf, dhh, S, grads);
-    hipLaunchKernelGGL(k_mask_attn_bwd2<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)m, P, stats, HW, dhh, S,
-                       (bf16_t*)dm, grads);
-  } else {
-    hipLaunchKernelGGL(k_mask_attn_bwd1<float>, grid, dim3(256), 0, s, (const float*)dout, lddo, (const float*)f,
-                       ldf, (const float*)m, P, stats, HW, C, (float*)df, lddf, dhh, S, grads);
-    hipLaunchKernelGGL(k_mask_attn_bwd2<float>, grid, dim3(256), 0, s, (const float*)m, P, stats, HW, dhh, S,
-                       (float*)dm, grads);
-  }
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mask_attn_bwd1<T>, grid, dim3(256), 0, s, (const T*)dout, lddo, (const T*)f,
+                       ldf, (const T*)m, P, stats, HW, C, (T*)df, lddf, dhh, S, grads);
+    hipLaunchKernelGGL(k_mask_attn_bwd2<T>, grid, dim3(256), 0, s, (const T*)m, P, stats, HW, dhh, S,
+                       (T*)dm, grads));
   DMF_LAUNCH_CHECK("dmf_mask_attn_bwd");
   return 0;
 }

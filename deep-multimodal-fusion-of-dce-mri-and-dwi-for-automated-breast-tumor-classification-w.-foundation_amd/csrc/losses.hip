@@ -666,16 +666,10 @@ extern "C" int dmf_soft_dice(int dtype, const void* logits, const float* target,
                              float* sums_ws, float* loss, float* dlogits, void* stream) {
   DMF_CHECK_ARG(logits && target && sums_ws && loss && B > 0 && P > 0, "dmf_soft_dice: bad args");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == DMF_BF16) {
-    hipLaunchKernelGGL((k_dice_sums<bf16_t, float>), dim3(B), dim3(256), 0, s, (const bf16_t*)logits, target, P,
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_dice_sums<T, float>), dim3(B), dim3(256), 0, s, (const T*)logits, target, P,
                        sums_ws);
-    hipLaunchKernelGGL((k_dice_grad<bf16_t, float>), dim3(gsz((long long)B * P)), dim3(256), 0, s,
-                       (const bf16_t*)logits, target, B, P, eps, sums_ws, loss, dlogits);
-  } else {
-    hipLaunchKernelGGL((k_dice_sums<float, float>), dim3(B), dim3(256), 0, s, (const float*)logits, target, P, sums_ws);
-    hipLaunchKernelGGL((k_dice_grad<float, float>), dim3(gsz((long long)B * P)), dim3(256), 0, s, (const float*)logits,
-                       target, B, P, eps, sums_ws, loss, dlogits);
-  }
+    hipLaunchKernelGGL((k_dice_grad<T, float>), dim3(gsz((long long)B * P)), dim3(256), 0, s,
+                       (const T*)logits, target, B, P, eps, sums_ws, loss, dlogits));
   DMF_LAUNCH_CHECK("dmf_soft_dice");
   return 0;
 }
@@ -725,23 +719,13 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
     const int nb = cdiv(S, RECON_RB);
     const dim3 g(B, nb);
     const size_t lds = (size_t)(5 * RECON_NR * S + S) * sizeof(float) + (size_t)S * sizeof(short);
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_recon_stream<bf16_t>, g, dim3(256), lds, (hipStream_t)stream, a, ws);
-    else
-      hipLaunchKernelGGL(k_recon_stream<float>, g, dim3(256), lds, (hipStream_t)stream, a, ws);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_recon_stream<T>, g, dim3(256), lds, (hipStream_t)stream, a, ws));
     hipLaunchKernelGGL(k_recon_finish, dim3(cdiv((long long)nterms * B * h * w, 256) + 1), dim3(256), 0,
                        (hipStream_t)stream, a, ws, nb);
   } else if (S <= RECON_MAXS && h <= S && (RECON_RB * h + S - 1) / S + 2 <= RECON_RB + 2) {
     const dim3 g(B, cdiv(S, RECON_RB));
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_recon_band<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(k_recon_band<float>, g, dim3(256), 0, (hipStream_t)stream, a);
-  } else if (dtype == DMF_BF16) {
-    hipLaunchKernelGGL(k_recon<bf16_t>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
-  } else {
-    hipLaunchKernelGGL(k_recon<float>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a);
-  }
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_recon_band<T>, g, dim3(256), 0, (hipStream_t)stream, a));
+  } else DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_recon<T>, dim3(B * S), dim3(256), 0, (hipStream_t)stream, a));
   DMF_LAUNCH_CHECK("dmf_recon_loss");
   return 0;
 }
@@ -750,14 +734,9 @@ extern "C" int dmf_mimic_loss(int dtype, const void* student, const void* teache
                               long long tstride, int ld, int HW, int C, int npairs, float* loss, void* dstudent,
                               long long dstride, void* stream) {
   DMF_CHECK_ARG(student && teacher && loss && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_mimic<bf16_t>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)student,
-                       (const bf16_t*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
-                       (bf16_t*)dstudent, dstride);
-  else
-    hipLaunchKernelGGL(k_mimic<float>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const float*)student,
-                       (const float*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
-                       (float*)dstudent, dstride);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mimic<T>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const T*)student,
+                       (const T*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
+                       (T*)dstudent, dstride));
   DMF_LAUNCH_CHECK("dmf_mimic_loss");
   return 0;
 }
@@ -775,12 +754,8 @@ extern "C" int dmf_scale_by_cast(int dtype, const float* src, long long M, int C
   DMF_CHECK_ARG(src && scalar && dst, "dmf_scale_by_cast: bad args");
   const long long n = M * C;
   if (n == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_scale_by_cast<bf16_t>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
-                       (bf16_t*)dst, ldd, C);
-  else
-    hipLaunchKernelGGL(k_scale_by_cast<float>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
-                       (float*)dst, ldd, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_scale_by_cast<T>, dim3(gsz(n)), dim3(256), 0, (hipStream_t)stream, src, n, scalar, mul,
+                       (T*)dst, ldd, C));
   DMF_LAUNCH_CHECK("dmf_scale_by_cast");
   return 0;
 }

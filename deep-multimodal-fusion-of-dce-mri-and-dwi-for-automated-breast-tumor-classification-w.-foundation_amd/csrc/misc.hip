@@ -909,18 +909,10 @@ extern "C" int dmf_input_prep(int dtype, const float* x, int N, int C, int H, in
   const long long total = (long long)N * H * W;
   if (total == 0) return 0;
   if (y && Cp % 8 == 0 && a16(y)) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_input_prep8<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
-                         gate, (bf16_t*)y, Cp, chan_mean);
-    else
-      hipLaunchKernelGGL(k_input_prep8<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
-                         gate, (float*)y, Cp, chan_mean);
-  } else if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_input_prep<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
-                       (bf16_t*)y, Cp, chan_mean);
-  else
-    hipLaunchKernelGGL(k_input_prep<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
-                       (float*)y, Cp, chan_mean);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_input_prep8<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
+                         gate, (T*)y, Cp, chan_mean));
+  } else DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_input_prep<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W, gate,
+                       (T*)y, Cp, chan_mean));
   DMF_LAUNCH_CHECK("dmf_input_prep");
   return 0;
 }
@@ -975,12 +967,8 @@ extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b,
     int CVt, groups, S, rpb;
     nhwc_reduce_plan(N, HW, C, CVt, groups, S, rpb);
     const dim3 g8(N, groups, S);
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_nhwc_reduce8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)a, lda, (const bf16_t*)b, ldb,
-                         HW, C, CVt, rpb, out_sq ? 1 : 0, workspace);
-    else
-      hipLaunchKernelGGL(k_nhwc_reduce8<float>, g8, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, HW,
-                         C, CVt, rpb, out_sq ? 1 : 0, workspace);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_nhwc_reduce8<T>, g8, dim3(256), 0, st, (const T*)a, lda, (const T*)b, ldb,
+                         HW, C, CVt, rpb, out_sq ? 1 : 0, workspace));
     const long long nc = (long long)N * C;
     if (!out) {  // stage 1 only: the consumer (dmf_se_mlp) sums the S partial planes itself
       DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
@@ -996,12 +984,8 @@ extern "C" int dmf_nhwc_reduce(int dtype, const void* a, int lda, const void* b,
     const void* bb = pass ? a : b;
     const int ldbb = pass ? lda : ldb;
     float* o = pass ? out_sq : out;
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_nhwc_reduce<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)a, lda, (const bf16_t*)bb,
-                         ldbb, HW, C, scale, o, accumulate);
-    else
-      hipLaunchKernelGGL(k_nhwc_reduce<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)bb, ldbb,
-                         HW, C, scale, o, accumulate);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_nhwc_reduce<T>, grid, dim3(256), 0, st, (const T*)a, lda, (const T*)bb,
+                         ldbb, HW, C, scale, o, accumulate));
   }
   DMF_LAUNCH_CHECK("dmf_nhwc_reduce");
   return 0;
@@ -1013,21 +997,13 @@ extern "C" int dmf_channel_scale(int dtype, const void* x, int ldx, const float*
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, ldy, x, y, gate)) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_channel_scale8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)x, ldx, gate, (bf16_t*)y, ldy, (long long)N, HW, C);
-    else
-      hipLaunchKernelGGL(k_channel_scale8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)x, ldx, gate, (float*)y, ldy, (long long)N, HW, C);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_channel_scale8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const T*)x, ldx, gate, (T*)y, ldy, (long long)N, HW, C));
     DMF_LAUNCH_CHECK("dmf_channel_scale");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_channel_scale<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, gate, (bf16_t*)y, ldy, (long long)N, HW, C);
-  else
-    hipLaunchKernelGGL(k_channel_scale<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
-                       ldx, gate, (float*)y, ldy, (long long)N, HW, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_channel_scale<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       ldx, gate, (T*)y, ldy, (long long)N, HW, C));
   DMF_LAUNCH_CHECK("dmf_channel_scale");
   return 0;
 }
@@ -1037,21 +1013,13 @@ extern "C" int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb
   DMF_CHECK_ARG(a && b && wlogit && z, "dmf_mix: bad args");
   if (M * C == 0) return 0;
   if (v8ok(C, lda, ldb, a, b) && ldz % 8 == 0 && a16(z)) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_mix8<bf16_t>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a,
-                         lda, (const bf16_t*)b, ldb, wlogit, (bf16_t*)z, ldz, M, C);
-    else
-      hipLaunchKernelGGL(k_mix8<float>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
-                         (const float*)b, ldb, wlogit, (float*)z, ldz, M, C);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix8<T>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const T*)a,
+                         lda, (const T*)b, ldb, wlogit, (T*)z, ldz, M, C));
     DMF_LAUNCH_CHECK("dmf_mix");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_mix<bf16_t>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)a, lda,
-                       (const bf16_t*)b, ldb, wlogit, (bf16_t*)z, ldz, M, C);
-  else
-    hipLaunchKernelGGL(k_mix<float>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const float*)a, lda,
-                       (const float*)b, ldb, wlogit, (float*)z, ldz, M, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix<T>, dim3(gsz(M * C)), dim3(256), 0, (hipStream_t)stream, (const T*)a, lda,
+                       (const T*)b, ldb, wlogit, (T*)z, ldz, M, C));
   DMF_LAUNCH_CHECK("dmf_mix");
   return 0;
 }
@@ -1061,12 +1029,8 @@ extern "C" int dmf_gn_apply(int dtype, const void* z, int ldz, const float* mean
   DMF_CHECK_ARG(z && mean && m2 && gamma && beta && y, "dmf_gn_apply: bad args");
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_gn_apply<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)z, ldz,
-                       mean, m2, gamma, beta, eps, (bf16_t*)y, ldy, (long long)N, HW, C);
-  else
-    hipLaunchKernelGGL(k_gn_apply<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)z, ldz,
-                       mean, m2, gamma, beta, eps, (float*)y, ldy, (long long)N, HW, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gn_apply<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)z, ldz,
+                       mean, m2, gamma, beta, eps, (T*)y, ldy, (long long)N, HW, C));
   DMF_LAUNCH_CHECK("dmf_gn_apply");
   return 0;
 }
@@ -1077,26 +1041,15 @@ extern "C" int dmf_gn_bwd(int dtype, const void* dy, int lddy, const void* z, in
   DMF_CHECK_ARG(dy && z && mean && m2 && gamma && s1 && s2 && dz, "dmf_gn_bwd: bad args");
   dim3 grid(N, cdiv(C, 64));
   const long long total = (long long)N * HW * C;
-  if (dtype == DMF_BF16) {
-    if (v8ok(C, lddy, ldz, dy, z))
-      hipLaunchKernelGGL(k_gn_bwd_reduce8<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy, lddy,
-                         (const bf16_t*)z, ldz, mean, m2, eps, HW, C, s1, s2);
+  DMF_DISPATCH_DTYPE(dtype, T, if (v8ok(C, lddy, ldz, dy, z))
+      hipLaunchKernelGGL(k_gn_bwd_reduce8<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dy, lddy,
+                         (const T*)z, ldz, mean, m2, eps, HW, C, s1, s2);
     else
-      hipLaunchKernelGGL(k_gn_bwd_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy, lddy,
-                         (const bf16_t*)z, ldz, mean, m2, eps, HW, C, s1, s2);
-    hipLaunchKernelGGL(k_gn_bwd_apply<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                       lddy, (const bf16_t*)z, ldz, mean, m2, s1, s2, gamma, eps, (bf16_t*)dz, lddz, (long long)N, HW,
-                       C);
-  } else {
-    if (v8ok(C, lddy, ldz, dy, z))
-      hipLaunchKernelGGL(k_gn_bwd_reduce8<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
-                         (const float*)z, ldz, mean, m2, eps, HW, C, s1, s2);
-    else
-      hipLaunchKernelGGL(k_gn_bwd_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
-                         (const float*)z, ldz, mean, m2, eps, HW, C, s1, s2);
-    hipLaunchKernelGGL(k_gn_bwd_apply<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
-                       lddy, (const float*)z, ldz, mean, m2, s1, s2, gamma, eps, (float*)dz, lddz, (long long)N, HW, C);
-  }
+      hipLaunchKernelGGL(k_gn_bwd_reduce<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dy, lddy,
+                         (const T*)z, ldz, mean, m2, eps, HW, C, s1, s2);
+    hipLaunchKernelGGL(k_gn_bwd_apply<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                       lddy, (const T*)z, ldz, mean, m2, s1, s2, gamma, eps, (T*)dz, lddz, (long long)N, HW,
+                       C));
   DMF_LAUNCH_CHECK("dmf_gn_bwd");
   return 0;
 }
@@ -1107,21 +1060,13 @@ extern "C" int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int 
   const long long total = (long long)N * Ho * Wo * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, ldy, x, y)) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_maxpool8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)x, N, H, W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, k, s, p);
-    else
-      hipLaunchKernelGGL(k_maxpool8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)x, N, H, W, C, ldx, (float*)y, Ho, Wo, ldy, k, s, p);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const T*)x, N, H, W, C, ldx, (T*)y, Ho, Wo, ldy, k, s, p));
     DMF_LAUNCH_CHECK("dmf_maxpool2d");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_maxpool<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N, H,
-                       W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, k, s, p);
-  else
-    hipLaunchKernelGGL(k_maxpool<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, H, W,
-                       C, ldx, (float*)y, Ho, Wo, ldy, k, s, p);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H,
+                       W, C, ldx, (T*)y, Ho, Wo, ldy, k, s, p));
   DMF_LAUNCH_CHECK("dmf_maxpool2d");
   return 0;
 }
@@ -1133,12 +1078,8 @@ extern "C" int dmf_maxpool2d_idx(int dtype, const void* x, int N, int H, int W, 
   const long long total = (long long)N * Ho * Wo * C;
   DMF_CHECK_ARG(total < (1LL << 31) && (long long)N * H * W * C < (1LL << 31), "dmf_maxpool2d_idx: too large");
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_maxpool_idx8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)x, N, H, W, C, ldx, (bf16_t*)y, Ho, Wo, ldy, (unsigned char*)idx, k, s, p);
-  else
-    hipLaunchKernelGGL(k_maxpool_idx8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)x, N, H, W, C, ldx, (float*)y, Ho, Wo, ldy, (unsigned char*)idx, k, s, p);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool_idx8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)x, N, H, W, C, ldx, (T*)y, Ho, Wo, ldy, (unsigned char*)idx, k, s, p));
   DMF_LAUNCH_CHECK("dmf_maxpool2d_idx");
   return 0;
 }
@@ -1150,13 +1091,9 @@ extern "C" int dmf_maxpool2d_bwd_idx(int dtype, const void* dy, int N, int H, in
   const long long total = (long long)N * H * W * C;
   DMF_CHECK_ARG(total < (1LL << 31), "dmf_maxpool2d_bwd_idx: too large");
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_maxpool_bwd_idx8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, N, H, W, C, Ho, Wo, lddy, (const unsigned char*)idx, (bf16_t*)dx, lddx, k, s,
-                       p);
-  else
-    hipLaunchKernelGGL(k_maxpool_bwd_idx8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)dy, N, H, W, C, Ho, Wo, lddy, (const unsigned char*)idx, (float*)dx, lddx, k, s, p);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool_bwd_idx8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dy, N, H, W, C, Ho, Wo, lddy, (const unsigned char*)idx, (T*)dx, lddx, k, s,
+                       p));
   DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd_idx");
   return 0;
 }
@@ -1167,21 +1104,13 @@ extern "C" int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, 
   const long long total = (long long)N * H * W * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, lddy, x, dy, dx) && lddx % 8 == 0) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_maxpool_bwd8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)x, N, H, W, C, ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, k, s, p);
-    else
-      hipLaunchKernelGGL(k_maxpool_bwd8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)x, N, H, W, C, ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, k, s, p);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool_bwd8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const T*)x, N, H, W, C, ldx, (const T*)dy, Ho, Wo, lddy, (T*)dx, lddx, k, s, p));
     DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_maxpool_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       N, H, W, C, ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, k, s, p);
-  else
-    hipLaunchKernelGGL(k_maxpool_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N,
-                       H, W, C, ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, k, s, p);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       N, H, W, C, ldx, (const T*)dy, Ho, Wo, lddy, (T*)dx, lddx, k, s, p));
   DMF_LAUNCH_CHECK("dmf_maxpool2d_bwd");
   return 0;
 }
@@ -1192,21 +1121,13 @@ extern "C" int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, 
   const long long total = (long long)N * r * r * H * W * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, 8, x, y)) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_up_nearest8<bf16_t>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const bf16_t*)x, ldx, (bf16_t*)y, N, H, W, C, r);
-    else
-      hipLaunchKernelGGL(k_up_nearest8<float>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
-                         (const float*)x, ldx, (float*)y, N, H, W, C, r);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_up_nearest8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const T*)x, ldx, (T*)y, N, H, W, C, r));
     DMF_LAUNCH_CHECK("dmf_upsample_nearest");
     return 0;
   }
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_up_nearest<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       ldx, (bf16_t*)y, N, H, W, C, r);
-  else
-    hipLaunchKernelGGL(k_up_nearest<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
-                       (float*)y, N, H, W, C, r);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_up_nearest<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x,
+                       ldx, (T*)y, N, H, W, C, r));
   DMF_LAUNCH_CHECK("dmf_upsample_nearest");
   return 0;
 }
@@ -1216,12 +1137,8 @@ extern "C" int dmf_upsample_nearest_bwd(int dtype, const void* dy, void* dx, int
   DMF_CHECK_ARG(dy && dx && r >= 1, "dmf_upsample_nearest_bwd: bad args");
   const long long total = (long long)N * H * W * C;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_up_nearest_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, (bf16_t*)dx, N, H, W, C, r);
-  else
-    hipLaunchKernelGGL(k_up_nearest_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy,
-                       (float*)dx, N, H, W, C, r);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_up_nearest_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dy, (T*)dx, N, H, W, C, r));
   DMF_LAUNCH_CHECK("dmf_upsample_nearest_bwd");
   return 0;
 }
@@ -1231,12 +1148,8 @@ extern "C" int dmf_bilinear(int dtype, const void* x, int N, int Hi, int Wi, int
   DMF_CHECK_ARG(x && y, "dmf_bilinear: bad args");
   const long long total = (long long)N * Ho * Wo * C;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_bilinear<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, N,
-                       Hi, Wi, C, ldx, (bf16_t*)y, Ho, Wo, ldy);
-  else
-    hipLaunchKernelGGL(k_bilinear<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x, N, Hi,
-                       Wi, C, ldx, (float*)y, Ho, Wo, ldy);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bilinear<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, N,
+                       Hi, Wi, C, ldx, (T*)y, Ho, Wo, ldy));
   DMF_LAUNCH_CHECK("dmf_bilinear");
   return 0;
 }
@@ -1246,12 +1159,8 @@ extern "C" int dmf_bilinear_bwd(int dtype, const void* dy, int N, int Ho, int Wo
   DMF_CHECK_ARG(dy && dx, "dmf_bilinear_bwd: bad args");
   const long long total = (long long)N * Hi * Wi * C;
   if (total == 0) return 0;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_bilinear_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                       N, Ho, Wo, C, lddy, (bf16_t*)dx, Hi, Wi, lddx);
-  else
-    hipLaunchKernelGGL(k_bilinear_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const float*)dy, N,
-                       Ho, Wo, C, lddy, (float*)dx, Hi, Wi, lddx);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bilinear_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                       N, Ho, Wo, C, lddy, (T*)dx, Hi, Wi, lddx));
   DMF_LAUNCH_CHECK("dmf_bilinear_bwd");
   return 0;
 }
@@ -1260,26 +1169,18 @@ extern "C" int dmf_col_stats_tiles(long long M) { return (int)((M + 255) / 256);
 
 extern "C" int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream) {
   DMF_CHECK_ARG(x && partials && M > 0 && C > 0, "dmf_col_stats: bad args");
-  const int es = dtype == DMF_BF16 ? 2 : 4;
+  const int es = is16(dtype) ? 2 : 4;
   if (C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % (8 * es)) == 0) {
     const int CVt = std::min(32, C / 8);
     dim3 g8((unsigned)((M + 255) / 256), (unsigned)cdiv(C / 8, CVt));
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_col_stats8<bf16_t>, g8, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, C, CVt,
-                         partials);
-    else
-      hipLaunchKernelGGL(k_col_stats8<float>, g8, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, M, C, CVt,
-                         partials);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_col_stats8<T>, g8, dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, M, C, CVt,
+                         partials));
     DMF_LAUNCH_CHECK("dmf_col_stats");
     return 0;
   }
   dim3 grid((unsigned)((M + 255) / 256), (unsigned)cdiv(C, 64));
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_col_stats<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx, M, C,
-                       partials);
-  else
-    hipLaunchKernelGGL(k_col_stats<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx, M, C,
-                       partials);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_col_stats<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx, M, C,
+                       partials));
   DMF_LAUNCH_CHECK("dmf_col_stats");
   return 0;
 }
@@ -1293,15 +1194,9 @@ extern "C" int dmf_mask_attn_fwd(int dtype, const void* f, int ldf, const void* 
   MaskAttnP P{w1, gn_w, gn_b, w2, b2, gamma, eps, hidden};
   const long long total = (long long)N * HW;
   const int grid = (int)((total + 3) / 4 > 16384 ? 16384 : (total + 3) / 4);
-  if (dtype == DMF_BF16) {
-    hipLaunchKernelGGL(k_mask_stats<bf16_t>, dim3(N), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)m, HW, stats);
-    hipLaunchKernelGGL(k_mask_attn_fwd<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)f, ldf,
-                       (const bf16_t*)m, P, stats, (bf16_t*)out, ldo, (bf16_t*)A_out, (long long)N, HW, C);
-  } else {
-    hipLaunchKernelGGL(k_mask_stats<float>, dim3(N), dim3(256), 0, (hipStream_t)stream, (const float*)m, HW, stats);
-    hipLaunchKernelGGL(k_mask_attn_fwd<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const float*)f, ldf,
-                       (const float*)m, P, stats, (float*)out, ldo, (float*)A_out, (long long)N, HW, C);
-  }
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mask_stats<T>, dim3(N), dim3(256), 0, (hipStream_t)stream, (const T*)m, HW, stats);
+    hipLaunchKernelGGL(k_mask_attn_fwd<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const T*)f, ldf,
+                       (const T*)m, P, stats, (T*)out, ldo, (T*)A_out, (long long)N, HW, C));
   DMF_LAUNCH_CHECK("dmf_mask_attn_fwd");
   return 0;
 }
@@ -1364,12 +1259,8 @@ extern "C" int dmf_adaptive_avgpool2d(int dtype, const void* x, int N, int H, in
                                       int Wo, int ldy, void* stream) {
   DMF_CHECK_ARG(x && y && N > 0 && H > 0 && W > 0 && C > 0 && Ho > 0 && Wo > 0, "dmf_adaptive_avgpool2d: bad args");
   const long long total = (long long)N * Ho * Wo * C;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_adaptive_avgpool<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)x, ldx, (bf16_t*)y, ldy, N, H, W, C, Ho, Wo);
-  else
-    hipLaunchKernelGGL(k_adaptive_avgpool<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)x, ldx, (float*)y, ldy, N, H, W, C, Ho, Wo);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_adaptive_avgpool<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)x, ldx, (T*)y, ldy, N, H, W, C, Ho, Wo));
   DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d");
   return 0;
 }
@@ -1379,12 +1270,8 @@ extern "C" int dmf_adaptive_avgpool2d_bwd(int dtype, const void* dy, int N, int 
   DMF_CHECK_ARG(dy && dx && N > 0 && H > 0 && W > 0 && C > 0 && Ho > 0 && Wo > 0,
                 "dmf_adaptive_avgpool2d_bwd: bad args");
   const long long total = (long long)N * H * W * C;
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_adaptive_avgpool_bwd<bf16_t>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, N, H, W, C, Ho, Wo);
-  else
-    hipLaunchKernelGGL(k_adaptive_avgpool_bwd<float>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)dy, lddy, (float*)dx, lddx, N, H, W, C, Ho, Wo);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_adaptive_avgpool_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dy, lddy, (T*)dx, lddx, N, H, W, C, Ho, Wo));
   DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d_bwd");
   return 0;
 }

@@ -767,34 +767,20 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
 #define DMF_AA8(TT, A)                                                                                          \
   hipLaunchKernelGGL((k_affine_act8<TT, A>), dim3(g8), dim3(256), 0, s, (const TT*)x, ldx, scale_shift,          \
                      (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, (TT*)y, ldy, M, C)
-    if (dtype == DMF_BF16) {
-      switch (act) {
-        case DMF_ACT_RELU: DMF_AA8(bf16_t, DMF_ACT_RELU); break;
-        case DMF_ACT_GELU: DMF_AA8(bf16_t, DMF_ACT_GELU); break;
-        case DMF_ACT_SIGMOID: DMF_AA8(bf16_t, DMF_ACT_SIGMOID); break;
-        default: DMF_AA8(bf16_t, DMF_ACT_NONE);
-      }
-    } else {
-      switch (act) {
-        case DMF_ACT_RELU: DMF_AA8(float, DMF_ACT_RELU); break;
-        case DMF_ACT_GELU: DMF_AA8(float, DMF_ACT_GELU); break;
-        case DMF_ACT_SIGMOID: DMF_AA8(float, DMF_ACT_SIGMOID); break;
-        default: DMF_AA8(float, DMF_ACT_NONE);
-      }
-    }
+    DMF_DISPATCH_DTYPE(dtype, T, switch (act) {
+        case DMF_ACT_RELU: DMF_AA8(T, DMF_ACT_RELU); break;
+        case DMF_ACT_GELU: DMF_AA8(T, DMF_ACT_GELU); break;
+        case DMF_ACT_SIGMOID: DMF_AA8(T, DMF_ACT_SIGMOID); break;
+        default: DMF_AA8(T, DMF_ACT_NONE);
+      });
 #undef DMF_AA8
     DMF_LAUNCH_CHECK("dmf_affine_act");
     return 0;
   }
   const int g = grid_for(M * (C / 4));
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_affine_act<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, ldx,
-                       scale_shift, (const bf16_t*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (bf16_t*)y,
-                       ldy, M, C);
-  else
-    hipLaunchKernelGGL(k_affine_act<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)x, ldx,
-                       scale_shift, (const float*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (float*)y,
-                       ldy, M, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_affine_act<T>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const T*)x, ldx,
+                       scale_shift, (const T*)res, ldr, res_scale_shift, act, dropout_p, rng, site, (T*)y,
+                       ldy, M, C));
   DMF_LAUNCH_CHECK("dmf_affine_act");
   return 0;
 }
@@ -816,7 +802,7 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
                             const void* res, int ldr, const dmf_bn_desc* res_bn, const float* res_scale_shift, int act,
                             float dropout_p, const unsigned long long* rng, int site, void* y, int ldy, long long M,
                             int C, void* stream) {
-  DMF_CHECK_ARG(dtype == DMF_F32 || dtype == DMF_BF16, "dmf_bn_apply: bad dtype %d", dtype);
+  DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "dmf_bn_apply: bad dtype %d", dtype);
   DMF_CHECK_ARG(C > 0 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (!res || ldr % 8 == 0),
                 "dmf_bn_apply: C=%d and strides must be multiples of 8", C);
   DMF_CHECK_ARG(M < (1LL << 31), "dmf_bn_apply: M=%lld too large", M);
@@ -857,8 +843,7 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
       default: DMF_BA_R(TT, DMF_ACT_NONE);                \
     }                                                     \
   } while (0)
-  if (dtype == DMF_BF16) DMF_BA_A(bf16_t);
-  else DMF_BA_A(float);
+  DMF_DISPATCH_DTYPE(dtype, T, DMF_BA_A(T));
 #undef DMF_BA_A
 #undef DMF_BA_R
 #undef DMF_BA
@@ -875,14 +860,9 @@ extern "C" int dmf_act_bwd(int dtype, const void* dy, int lddy, const void* x, i
   DMF_CHECK_ARG(act == DMF_ACT_NONE || x, "dmf_act_bwd: activation backward needs x");
   if (M == 0) return 0;
   const int g = grid_for(M * (C / 4));
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_act_bwd<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy, lddy,
-                       (const bf16_t*)x, ldx, scale_shift, (const bf16_t*)res, ldr, res_scale_shift, act, dropout_p,
-                       rng, site, (bf16_t*)dz, lddz, M, C);
-  else
-    hipLaunchKernelGGL(k_act_bwd<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)dy, lddy,
-                       (const float*)x, ldx, scale_shift, (const float*)res, ldr, res_scale_shift, act, dropout_p,
-                       rng, site, (float*)dz, lddz, M, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_act_bwd<T>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const T*)dy, lddy,
+                       (const T*)x, ldx, scale_shift, (const T*)res, ldr, res_scale_shift, act, dropout_p,
+                       rng, site, (T*)dz, lddz, M, C));
   DMF_LAUNCH_CHECK("dmf_act_bwd");
   return 0;
 }
@@ -898,18 +878,10 @@ extern "C" int dmf_bn_bwd_reduce(int dtype, const void* dz, int lddz, const void
   dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
   if (C % 8 == 0 && lddz % 8 == 0 && (!x || ldx % 8 == 0) &&
       ((uintptr_t)dz | (uintptr_t)(x ? x : dz)) % 16 == 0) {
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_bn_bwd_reduce8<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
-                         (const bf16_t*)x, ldx, save_mean_invstd, M, C, partials);
-    else
-      hipLaunchKernelGGL(k_bn_bwd_reduce8<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                         (const float*)x, ldx, save_mean_invstd, M, C, partials);
-  } else if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_bn_bwd_reduce<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
-                       (const bf16_t*)x, ldx, save_mean_invstd, M, C, partials);
-  else
-    hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                       (const float*)x, ldx, save_mean_invstd, M, C, partials);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_reduce8<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
+                         (const T*)x, ldx, save_mean_invstd, M, C, partials));
+  } else DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_reduce<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
+                       (const T*)x, ldx, save_mean_invstd, M, C, partials));
   DMF_LAUNCH_CHECK("dmf_bn_bwd_reduce");
   return 0;
 }
@@ -936,22 +908,14 @@ extern "C" int dmf_bn_bwd_apply(int dtype, const void* dz, int lddz, const void*
   if (C % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && lddx % 8 == 0 && M * (C / 8) < (1LL << 31) &&
       ((uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx) % 16 == 0) {
     const int g8 = grid_for(M * (C / 8));
-    if (dtype == DMF_BF16)
-      hipLaunchKernelGGL(k_bn_bwd_apply8<bf16_t>, dim3(g8), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz,
-                         lddz, (const bf16_t*)x, ldx, coef, (bf16_t*)dx, lddx, M, C);
-    else
-      hipLaunchKernelGGL(k_bn_bwd_apply8<float>, dim3(g8), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                         (const float*)x, ldx, coef, (float*)dx, lddx, M, C);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply8<T>, dim3(g8), dim3(256), 0, (hipStream_t)stream, (const T*)dz,
+                         lddz, (const T*)x, ldx, coef, (T*)dx, lddx, M, C));
     DMF_LAUNCH_CHECK("dmf_bn_bwd_apply");
     return 0;
   }
   const int g = grid_for(M * C);
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_bn_bwd_apply<bf16_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
-                       (const bf16_t*)x, ldx, coef, (bf16_t*)dx, lddx, M, C);
-  else
-    hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                       (const float*)x, ldx, coef, (float*)dx, lddx, M, C);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply<T>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
+                       (const T*)x, ldx, coef, (T*)dx, lddx, M, C));
   DMF_LAUNCH_CHECK("dmf_bn_bwd_apply");
   return 0;
 }
@@ -1002,14 +966,9 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
   int rows = 256;
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
   const dim3 g((unsigned)cdiv(M, rows), (unsigned)gy);
-  if (dtype == DMF_BF16)
-    hipLaunchKernelGGL(k_bn_bwd_apply_acc<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dz, lddz,
-                       (const bf16_t*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
-                       (bf16_t*)dx, lddx, (int)M, C, rows);
-  else
-    hipLaunchKernelGGL(k_bn_bwd_apply_acc<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)dz, lddz,
-                       (const float*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
-                       (float*)dx, lddx, (int)M, C, rows);
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply_acc<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
+                       (const T*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
+                       (T*)dx, lddx, (int)M, C, rows));
   DMF_LAUNCH_CHECK("dmf_bn_bwd_apply_acc");
   return 0;
 }
@@ -1039,21 +998,12 @@ static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const voi
   dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
   hipStream_t s = (hipStream_t)stream;
 #define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)dy2, lddy2, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
-  if (dtype == DMF_BF16) {
-    switch (act) {
-      case DMF_ACT_RELU: DMF_ABR(bf16_t, DMF_ACT_RELU); break;
-      case DMF_ACT_GELU: DMF_ABR(bf16_t, DMF_ACT_GELU); break;
-      case DMF_ACT_SIGMOID: DMF_ABR(bf16_t, DMF_ACT_SIGMOID); break;
-      default: DMF_ABR(bf16_t, DMF_ACT_NONE);
-    }
-  } else {
-    switch (act) {
-      case DMF_ACT_RELU: DMF_ABR(float, DMF_ACT_RELU); break;
-      case DMF_ACT_GELU: DMF_ABR(float, DMF_ACT_GELU); break;
-      case DMF_ACT_SIGMOID: DMF_ABR(float, DMF_ACT_SIGMOID); break;
-      default: DMF_ABR(float, DMF_ACT_NONE);
-    }
-  }
+  DMF_DISPATCH_DTYPE(dtype, T, switch (act) {
+      case DMF_ACT_RELU: DMF_ABR(T, DMF_ACT_RELU); break;
+      case DMF_ACT_GELU: DMF_ABR(T, DMF_ACT_GELU); break;
+      case DMF_ACT_SIGMOID: DMF_ABR(T, DMF_ACT_SIGMOID); break;
+      default: DMF_ABR(T, DMF_ACT_NONE);
+    });
 #undef DMF_ABR
   DMF_LAUNCH_CHECK("dmf_act_bwd_bn_reduce");
   return 0;

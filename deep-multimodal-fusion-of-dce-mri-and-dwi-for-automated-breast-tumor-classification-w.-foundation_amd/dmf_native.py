@@ -23,7 +23,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DMF_HIP_LIB", os.path.join(_HERE, "libdmf_hip.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dmf_hip.h")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2  # include/dmf_hip.h DMF_F32 / DMF_BF16 / DMF_F16
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3
 # conv kernel bodies (dmf_conv_last_form, include/dmf_hip.h DMF_FORM_*)
 FORMS = {0: "igemm", 1: "buf", 2: "buf_ina", 3: "wide", 4: "sq", 5: "ps", 6: "pp", 7: "stem"}
@@ -146,7 +146,9 @@ def dtype_code(dt):
         return F32
     if dt == torch.bfloat16:
         return BF16
-    raise RuntimeError(f"unsupported dtype {dt} (expected float32 or bfloat16)")
+    if dt == torch.float16:
+        return F16
+    raise RuntimeError(f"unsupported dtype {dt} (expected float32, bfloat16 or float16)")
 
 
 def require_cuda(*tensors):

@@ -21,7 +21,7 @@ import torch
 
 import dmf_native as N
 
-F32, BF16 = N.F32, N.BF16
+F32, BF16, F16 = N.F32, N.BF16, N.F16
 ACT = {"none": N.ACT_NONE, "relu": N.ACT_RELU, "gelu": N.ACT_GELU, "sigmoid": N.ACT_SIGMOID}
 
 
@@ -1357,7 +1357,7 @@ def se_block(x, se_module):
 # ---------------------------------------------------------- input staging
 def channel_pad(c, dtype):
     """Channels padded so the conv engine's 16-byte K chunks align."""
-    m = 8 if dtype == torch.bfloat16 else 4
+    m = 8 if dtype in (torch.bfloat16, torch.float16) else 4
     return ((c + m - 1) // m) * m
 
 
@@ -2454,6 +2454,7 @@ KNOBS = {
     "wgrad_dma": ("wgrad_tune", 0),
     "wgrad_wide": ("wgrad_tune", 1),
     "wgrad_tr": ("wgrad_tune", 2),
+    "wgrad_sq": ("wgrad_tune", 3),
 }
 
 

@@ -445,7 +445,9 @@ def build_medical_backbone(parameters, device, method, in_channels):
     mp = parameters[f"{method}_model_parameters"]
     name = mp["backbone_str"].lower()
     output_stride = 8
-    dtype = mp.get("compute_dtype", torch.bfloat16)
+    import parameters as _PR
+
+    dtype = _PR.compute_dtype_of(parameters, mp)
     if name in ("resnet50d", "resnet50"):
         bb = build_imagenet_backbone(name=name, device=device, in_channels=in_channels, output_stride=output_stride,
                                      use_advanced_adapt=mp["use_advanced_adapt"], skip_adapt=mp["use_input_adapt"],

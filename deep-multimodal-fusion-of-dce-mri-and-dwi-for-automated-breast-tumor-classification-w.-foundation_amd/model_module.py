@@ -18,6 +18,7 @@ import torch.nn as nn
 from torch.nn import init
 
 import dmf_ops as O
+import parameters as PR
 from foundation_model import _DisabledWrapper, _caches
 from transformer_model import TransformerStage
 
@@ -452,7 +453,7 @@ class ModelMaskHeadBackbone(nn.Module):
         self.proj_f2 = Projector(c2, self.proj_dim, dim=self.dim)
         self.proj_r1 = Projector(1, self.proj_dim, dim=self.dim)
         self.proj_r2 = Projector(1, self.proj_dim, dim=self.dim)
-        set_compute_dtype(self, mp.get("compute_dtype", torch.bfloat16))
+        set_compute_dtype(self, PR.compute_dtype_of(P, mp))
 
     # ------------------------------------------------------------- helpers
     def _projector(self, proj, f):
@@ -617,7 +618,7 @@ class FusionModel(nn.Module):
         self.fusion_reconstruct = ReconHead(in_ch=C, recon_ch=self.fusion_recon_ch, upsample=False, dim=self.dim)
         self.classifier = nn.Sequential(nn.AdaptiveAvgPool2d((1, 1)), nn.Flatten(), nn.Linear(C, self.num_classes))
         self.projF = Projector(in_ch=C, proj_dim=self.proj_dim, dim=self.dim)
-        set_compute_dtype(self, fc.get("compute_dtype", torch.bfloat16))
+        set_compute_dtype(self, PR.compute_dtype_of(parameters_dict, fc))
 
     def _proj(self, mod, f):
         f = _to_compute(f, _dt(self))
@@ -690,9 +691,11 @@ def initialize_model(model, requires_grad):
 
 def set_compute_dtype(model, dtype):
     """Select the arithmetic type of every kernel under ``model``:
-    torch.bfloat16 (throughput, fp32 accumulation) or torch.float32 (parity)."""
-    if dtype not in (torch.float32, torch.bfloat16):
-        raise ValueError(f"compute dtype must be float32 or bfloat16, got {dtype}")
+    torch.bfloat16 (throughput, fp32 accumulation), torch.float16 (the
+    reference's "16-mixed" fp16 autocast: IEEE half activations and MFMA
+    operands, fp32 accumulation, norms and losses) or torch.float32 (parity)."""
+    if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        raise ValueError(f"compute dtype must be float32, bfloat16 or float16, got {dtype}")
     for m in model.modules():
         m.compute_dtype = dtype
     return model

@@ -9,6 +9,8 @@ object as ``dwi_model_parameters`` (quirk Q1, :174, :183).
 """
 from __future__ import annotations
 
+import torch
+
 
 def default_parameters():
     P = {}
@@ -86,9 +88,12 @@ def default_parameters():
         "fusion_channels": 128, "dwi_out_channels": mp["channels"][-1], "dce_out_channels": mp["channels"][-1],
         "fusion_recon_ch": 1}
     P["early_stopping_parameters"] = {"metric": "val_roc_auc", "mode": "max", "patience": 90, "min_delta": 1e-4}
-    # :211 is "16-mixed" (autocast + GradScaler). The 16-bit MFMA type here is
-    # bf16; "16-mixed" is honoured too -- the same bf16 compute plus the
-    # GradScaler protocol (dmf_optim.DeviceGradScaler, FusionTrainer).
+    # :211 is "16-mixed" (fp16 autocast + GradScaler; run.py:59-76 keeps it on an
+    # MI355X). Both 16-bit modes are built: "16-mixed" = IEEE fp16 activations
+    # and MFMA operands with the device GradScaler (dmf_optim.DeviceGradScaler,
+    # FusionTrainer), "bf16-mixed" = bf16 (fp32 range, no scaler) -- the
+    # default here, as run.py:59-71 picks on bf16-capable GPUs. compute_dtype_of()
+    # maps the precision to the kernels' compute dtype.
     P["precision"] = "bf16-mixed"
     P["test_mode"] = "tta_mc"                           # :215
     P["mc_passes"] = 10                                 # :216
@@ -125,3 +130,18 @@ def small_parameters(channels=(16, 32, 64), input_size=64, dwi_c=14, dce_c=6, dr
     P["dwi_channel_num"] = dwi_c
     P["dce_channel_num"] = dce_c
     return P
+
+
+PRECISION_DTYPES = {"16-mixed": torch.float16, "16": torch.float16, "bf16-mixed": torch.bfloat16,
+                    "bf16": torch.bfloat16, "32": torch.float32, "32-true": torch.float32}
+
+
+def compute_dtype_of(P, mp=None):
+    """The kernels' compute dtype: an explicit ``compute_dtype`` in the model
+    parameters, else the one Lightning's ``precision`` names (fp16 for
+    "16-mixed", bf16 for "bf16-mixed", fp32 for "32")."""
+    mp = mp if mp is not None else P["dwi_model_parameters"]
+    dt = mp.get("compute_dtype")
+    if dt is not None:
+        return dt
+    return PRECISION_DTYPES.get(str(P.get("precision", "bf16-mixed")), torch.bfloat16)

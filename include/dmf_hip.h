@@ -35,9 +35,10 @@
 extern "C" {
 #endif
 
-#define DMF_ABI_VERSION 1
+#define DMF_ABI_VERSION 2
 
-enum { DMF_F32 = 0, DMF_BF16 = 1 };
+/* compute / storage dtypes: f32, bf16 and IEEE f16 (the reference's "16-mixed" autocast) */
+enum { DMF_F32 = 0, DMF_BF16 = 1, DMF_F16 = 2 };
 enum { DMF_ACT_NONE = 0, DMF_ACT_RELU = 1, DMF_ACT_GELU = 2, DMF_ACT_SIGMOID = 3 };
 
 /* ------------------------------------------------------------- runtime */
@@ -72,7 +73,8 @@ int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
  * bf16 transposed-read kernel on (1, default) / off; key 1 = its 128x256 tile
  * (one workgroup per CU) where K >= 256 on (1, default) / off; key 2 = the
- * transposed-read kernels 1 (default) / 2 (register-staged 128x256) / 0 (off). */
+ * transposed-read kernels 1 (default) / 2 (register-staged 128x256) / 0 (off);
+ * key 3 = the 256x256 LDS-DMA tile where Cout and KH*KW*Cin are multiples of 256. */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */

@@ -737,3 +737,113 @@ def test_conv_ps_stream_forward(case):
     assert err <= 3e-2 * ref.abs().max().item(), err
     assert torch.allclose(bd.running_mean.cpu(), bn.running_mean, rtol=1e-2, atol=1e-3 * raw.abs().max().item())
     assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
+
+
+# the 256x256 LDS-DMA weight-gradient tile (dmf_conv_wgrad_tune key 3, knob "wgrad_sq"): Cout and
+# KH*KW*Cin multiples of 256, its own pixel split count; a dual-source input (the neck's concat)
+SQ_WGRAD_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, dil, Cin2)
+    (8, 256, 32, 32, 256, 3, 1, 2, 2, 0),
+    (9, 512, 32, 32, 512, 1, 1, 0, 1, 0),
+    (16, 2048, 16, 16, 512, 1, 1, 0, 1, 0),
+    (4, 256, 32, 32, 256, 3, 1, 1, 1, 256),
+    (5, 256, 31, 33, 768, 1, 1, 0, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", SQ_WGRAD_CASES)
+def test_conv_wgrad_sq_bf16(case):
+    O.set_knobs(wgrad_sq=1)
+    try:
+        n, ci, h, w, co, k, s, p, d, ci2 = case
+        torch.manual_seed(7)
+        q = lambda t: t.bfloat16().float()  # noqa: E731
+        a = q(torch.randn(n, ci, h, w))
+        b = q(torch.randn(n, ci2, h, w)) if ci2 else None
+        conv = nn.Conv2d(ci + ci2, co, k, stride=s, padding=p, dilation=d, bias=False)
+        wq = q(conv.weight.detach())
+        xin = (torch.cat([a, b], 1) if ci2 else a).double()
+        yr = F.conv2d(xin, wq.double(), None, s, p, d)
+        gy = q(torch.randn(yr.shape))
+        ref_dw = torch.nn.grad.conv2d_weight(xin, wq.shape, gy.double(), s, p, d).float()
+        cd = copy.deepcopy(conv).to(DEV)
+        with torch.no_grad():
+            cd.weight.copy_(wq)
+        _, dw, _ = O._conv_backward(_to_dev(a, torch.bfloat16), cd.weight, None, O.ConvGeom(cd),
+                                    (O.WeightCache(), O.WeightCache()), _to_dev(gy, torch.bfloat16), False, True, False,
+                                    x2=_to_dev(b, torch.bfloat16) if ci2 else None)
+        err = (dw.cpu() - ref_dw).abs().max().item()
+        assert err <= 1e-3 * ref_dw.abs().max().item(), err
+    finally:
+        O.set_knobs(wgrad_sq=0)
+
+
+# the fp16 compute dtype ("16-mixed" = IEEE half activations / MFMA operands, fp32 accumulation): every
+# forward body on its own shape (form asserted from the launch record), BN statistics into the arena,
+# against fp32 on the same half-rounded operands; plus the weight gradient and the stride-1 dgrad
+F16_CASES = [
+    # (N, Cin, H, W, Cout, k, stride, pad, dil, form)
+    (33, 64, 64, 64, 256, 1, 1, 0, 1, "ps"),
+    (34, 2048, 32, 32, 512, 1, 1, 0, 1, "pp"),
+    (64, 256, 32, 32, 256, 3, 1, 2, 2, "pp"),
+    (33, 256, 32, 32, 256, 3, 1, 1, 1, "wide"),
+    (4, 64, 16, 16, 128, 3, 1, 1, 1, "buf"),
+    (4, 16, 256, 256, 64, 7, 2, 3, 1, "stem"),
+    (3, 24, 17, 19, 40, 3, 2, 1, 1, "igemm"),
+]
+
+
+@pytest.mark.parametrize("case", F16_CASES)
+def test_conv_f16_forms_forward_and_bn_stats(case):
+    import dmf_native as N
+
+    n, ci, h, w, co, k, s, p, d, form = case
+    torch.manual_seed(13)
+    conv = nn.Conv2d(ci, co, k, stride=s, padding=p, dilation=d, bias=False)
+    a = torch.rand(n, ci, h, w).half().float() if form == "stem" else torch.randn(n, ci, h, w).half().float()
+    wq = conv.weight.detach().half().float()
+    bn = nn.BatchNorm2d(co)
+    with torch.no_grad():
+        raw = F.conv2d(a, wq, None, s, p, d)  # fp32 accumulation: far inside the half tolerance
+        ref = F.relu(bn(raw))
+    cd, bd = copy.deepcopy(conv).to(DEV), nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        cd.weight.copy_(wq)
+        with O.bn_scope(cd, DEV):
+            y = O.conv_bn_act(_to_dev(a, torch.float16), cd, (O.WeightCache(), O.WeightCache()), bd, "relu")
+    assert y.dtype == torch.float16
+    assert N.FORMS[N.load().dmf_conv_last_form()] == form
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+    assert torch.allclose(bd.running_mean.cpu(), bn.running_mean, rtol=2e-3, atol=2e-4 * raw.abs().max().item())
+    assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=4e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("case", BWD_CASES[:5])
+def test_conv_backward_f16(case):
+    n, ci, h, w, co, k, s, p, d, ci2 = case
+    torch.manual_seed(6)
+    q = lambda t: t.half().float()  # noqa: E731
+    a = q(torch.randn(n, ci, h, w))
+    b = q(torch.randn(n, ci2, h, w)) if ci2 else None
+    conv = nn.Conv2d(ci + ci2, co, k, stride=s, padding=p, dilation=d, bias=False)
+    wq = q(conv.weight.detach())
+    xin = (torch.cat([a, b], 1) if ci2 else a).double().requires_grad_(True)
+    wr = wq.double().requires_grad_(True)
+    yr = F.conv2d(xin, wr, None, s, p, d)
+    gy = q(torch.randn(yr.shape))
+    yr.backward(gy.double())
+    cd = copy.deepcopy(conv).to(DEV)
+    with torch.no_grad():
+        cd.weight.copy_(wq)
+    dx, dw, _ = O._conv_backward(_to_dev(a, torch.float16), cd.weight, None, O.ConvGeom(cd),
+                                 (O.WeightCache(), O.WeightCache()), _to_dev(gy, torch.float16), True, True, False,
+                                 x2=_to_dev(b, torch.float16) if ci2 else None)
+    if ci2:
+        dx = torch.cat([dx[0].float(), dx[1].float()], 1)
+    ref_dx, ref_dw = xin.grad.float(), wr.grad.float()
+    assert dx.dtype in (torch.float16, torch.float32)
+    err_x = (dx.float().cpu() - ref_dx).abs().max().item()
+    assert err_x <= 2e-3 * ref_dx.abs().max().item(), err_x
+    err_w = (dw.cpu() - ref_dw).abs().max().item()
+    assert err_w <= 1e-3 * ref_dw.abs().max().item(), err_w
