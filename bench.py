@@ -60,7 +60,8 @@ def parse():
                          "5: hybrid TransformerStage encoders (transformer_model.py, replaces block3), S=384 unless --size")
     ap.add_argument("--no-extras", action="store_true",
                     help="default run only: skip the mode-B, config-2 and config-5 sub-measurements")
-    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--dtype", choices=["bf16", "fp16", "fp32"], default="bf16",
+                    help="compute dtype; fp16 = precision '16-mixed' (fp16 MFMA operands + dynamic loss scale)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -112,6 +113,8 @@ def build(P, device, dtype, mode, seed=0):
 
     torch.manual_seed(seed)
     P["dwi_model_parameters"]["compute_dtype"] = dtype
+    if dtype == torch.float16:
+        P["precision"] = "16-mixed"  # the reference's default: fp16 with dynamic loss scaling (DeviceGradScaler)
     P["backbone_freeze_on_start"] = mode == "A"
     bb_dwi = FM.build_medical_backbone(P, "cpu", "dwi", P["dwi_channel_num"])
     dwi = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, bb_dwi), True)
@@ -184,6 +187,14 @@ def encoder_forward_probe(trainer, batch, args):
     return out
 
 
+DT_TAG = {torch.bfloat16: "bf16", torch.float16: "f16", torch.float32: "f32"}
+
+
+def mfma_peak(dtype):
+    # the dense fp16 MFMA rate equals bf16's on gfx950
+    return BF16_MFMA_PEAK_TFLOPS if dtype in (torch.bfloat16, torch.float16) else F32_MFMA_PEAK_TFLOPS
+
+
 def wgrad_probe(trainer, batch, dtype):
     """Mode B's dominant kernel family, the MFMA weight gradient
     (k_conv_wgrad_dma / _tr + its split-K reduce): one eager mode-B step
@@ -208,10 +219,10 @@ def wgrad_probe(trainer, batch, dtype):
     wg_only = [dict(r, calls=r["calls"][:1]) for r in recs]
     avg_ms_wg, _ = O.probe_replay(wg_only)
     recs.clear()
-    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    peak = mfma_peak(dtype)
     achieved = flops / n / (avg_ms * 1e-3) / 1e12
     return {"kernel": "conv2d weight gradient (k_conv_wgrad_dma / k_conv_wgrad_tr + k_wgrad_reduce), %s" %
-                      ("bf16" if dtype == torch.bfloat16 else "f32"),
+                      DT_TAG[dtype],
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None,
             "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
@@ -292,12 +303,12 @@ def roofline_probe(trainer, batch, dtype):
                     f.write(json.dumps({"shape": shp, "ms": round(t, 4), "gflop": round(fl / 1e9, 3),
                                         "tflops": round(fl / (t * 1e-3) / 1e12, 1)}) + "\n")
     recs.clear()
-    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    peak = mfma_peak(dtype)
     achieved = flops / (ms * 1e-3) / 1e12
     traffic = pmc_traffic()
     return {
         "kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_pp / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_stem / k_conv_igemm, %s)" %
-                  ("bf16" if dtype == torch.bfloat16 else "f32"),
+                  DT_TAG[dtype],
         "bound": "mfma",
         "achieved": round(achieved, 2),
         "peak": peak,
@@ -441,7 +452,7 @@ def conv_probe(fn, dtype):
     byt = sum(r["bytes"] for r in recs)
     n = len(recs)
     avg_ms, _ = O.probe_replay(recs)
-    peak = BF16_MFMA_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_MFMA_PEAK_TFLOPS
+    peak = mfma_peak(dtype)
     achieved = flops / n / (avg_ms * 1e-3) / 1e12
     recs.clear()
     return {"kernel": "conv2d forward (k_conv_fwd_ps / k_conv_fwd_pp / k_conv_fwd_sq / k_conv_fwd_wide / k_conv_fwd_buf / k_conv_stem / k_conv_igemm)",
@@ -636,7 +647,9 @@ def main():
         return
 
     args.batch = args.batch or 32
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
+    if args.config == 5 and dtype == torch.float16:
+        raise SystemExit("config 5 (TransformerStage token GEMMs) runs bf16 / fp32 only")
     P = PR.default_parameters()
     if args.config == 5:
         # hybrid CNN -> Transformer stage (E=512, depth 6, 4 heads, patch 2;

@@ -918,20 +918,27 @@ static int wgrad_tr_enabled() { return g_wgrad_tr; }
 static int g_wgrad_dma = 1;
 static int wgrad_dma_enabled() { return g_wgrad_dma; }
 static int g_wgrad_wide = 1;
-// key 3: the 256x256 LDS-DMA tile (8 waves of 128x64, one workgroup per CU): 0 off, 1 where legal
-static int g_wgrad_sq = 0;
-// the 256x256 form takes a launch (and sizes its pixel splits for it): bf16, 256-row and -column tiles
-// whole (Cout % 256 == 0, Ktot % 256 == 0); a dual-source input also needs Cin, C1 % 256 == 0 (checked
-// at launch, which otherwise keeps the 128-wide forms with the same split count)
+// key 3: the 256x256 LDS-DMA tile (8 waves of 128x64, one workgroup per CU): 0 off, 1 (default) where
+// legal and the weight has >= 2^18 entries, 2 wherever legal. Measured on the encoder pair's 39 shapes
+// (tools/wgrad_bench.py --sq, profiles/r04e_wgrad_sq.txt): 9.40 -> 7.66 ms per step; the only losers are
+// the small 1x1 weights (256x256, 256x512: 1.5-2 us each, too few 256-wide tiles to fill the chip)
+static int g_wgrad_sq = 1;
+// the 256x256 form takes a launch (and sizes its pixel splits for it): bf16/f16, 256-row and -column
+// tiles whole (Cout % 256 == 0, Ktot % 256 == 0); a dual-source input also needs Cin, C1 % 256 == 0
+// (checked at launch, which otherwise keeps the 128-wide forms with the same split count)
 static bool wgrad_sq_ok(int dtype, int Cout, long long Ktot) {
-  return is16(dtype) && g_wgrad_sq && Cout % 256 == 0 && Ktot % 256 == 0;
+  if (!is16(dtype) || !g_wgrad_sq || Cout % 256 != 0 || Ktot % 256 != 0) return false;
+  return g_wgrad_sq == 2 || (long long)Cout * Ktot >= (1LL << 18);
 }
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
   DMF_CHECK_ARG(key >= 0 && key <= 3, "dmf_conv_wgrad_tune: unknown key %d", key);
   if (key == 0) g_wgrad_dma = value != 0;
   else if (key == 1) g_wgrad_wide = value != 0;
-  else if (key == 3) g_wgrad_sq = value != 0;
+  else if (key == 3) {
+    DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_wgrad_tune: 256x256 tile mode %d", value);
+    g_wgrad_sq = value;
+  }
   else {
     DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_wgrad_tune: transposed-read mode %d", value);
     g_wgrad_tr = value;

@@ -143,7 +143,10 @@ class TransformerStage(nn.Module):
         self.tokens_to_map = TokensToFeatureMap(dim=dim)
 
     def forward(self, x):
+        dt = getattr(self, "compute_dtype", torch.bfloat16)
+        if dt == torch.float16:
+            raise TypeError("TransformerStage: the token GEMM / attention kernels run bf16 or f32; "
+                            "compute dtype float16 (precision '16-mixed') covers the CNN encoders only")
         tokens, hw = self.patch_embed(x)
         tokens = self.transformer(tokens)
-        dt = getattr(self, "compute_dtype", torch.bfloat16)
         return D.tokens_to_map(tokens, hw[0], hw[1], dt)

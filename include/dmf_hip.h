@@ -74,7 +74,8 @@ int dmf_conv_tune(int key, int value);
  * bf16 transposed-read kernel on (1, default) / off; key 1 = its 128x256 tile
  * (one workgroup per CU) where K >= 256 on (1, default) / off; key 2 = the
  * transposed-read kernels 1 (default) / 2 (register-staged 128x256) / 0 (off);
- * key 3 = the 256x256 LDS-DMA tile where Cout and KH*KW*Cin are multiples of 256. */
+ * key 3 = the 256x256 LDS-DMA tile where Cout and KH*KW*Cin are multiples of 256:
+ * 0 off / 1 (default) for weights of >= 2^18 entries / 2 wherever legal. */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */

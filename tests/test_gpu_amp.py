@@ -157,8 +157,9 @@ def test_trainer_16_mixed_reduced_precision_gradients_and_overflow_skip(cdt):
     (lm_a, tr_a, la, init), (lm_b, tr_b, lb, _) = runs[pair[0][0]], runs["16-mixed"]
     assert tr_b.scaler is not None and tr_b.scaler.get_scale() == 2.0 ** 16
     assert lm_b.dwi_model.compute_dtype == pair[1][1]
+    ltol = {"bf16": 2e-3, "fp16": 1e-2}[cdt]  # fp16: the half-rounded forward itself, vs fp32
     for a, b in zip(la, lb):
-        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (la, lb)
+        assert abs(a - b) <= ltol * max(1.0, abs(a)), (la, lb)
     pa = dict(lm_a.named_parameters())
     d_a, d_b = [], []
     for n, p in lm_b.named_parameters():

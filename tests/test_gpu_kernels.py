@@ -739,7 +739,8 @@ def test_conv_ps_stream_forward(case):
     assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
 
 
-# the 256x256 LDS-DMA weight-gradient tile (dmf_conv_wgrad_tune key 3, knob "wgrad_sq"): Cout and
+# the 256x256 LDS-DMA weight-gradient tile (dmf_conv_wgrad_tune key 3, knob "wgrad_sq", default 1 = weights
+# of >= 2^18 entries) forced on (2) and off (0), so both forms stay covered: Cout and
 # KH*KW*Cin multiples of 256, its own pixel split count; a dual-source input (the neck's concat)
 SQ_WGRAD_CASES = [
     # (N, Cin, H, W, Cout, k, stride, pad, dil, Cin2)
@@ -751,9 +752,10 @@ SQ_WGRAD_CASES = [
 ]
 
 
+@pytest.mark.parametrize("sq", [0, 2])  # the 128-wide forms / the 256x256 tile wherever legal
 @pytest.mark.parametrize("case", SQ_WGRAD_CASES)
-def test_conv_wgrad_sq_bf16(case):
-    O.set_knobs(wgrad_sq=1)
+def test_conv_wgrad_sq_bf16(case, sq):
+    O.set_knobs(wgrad_sq=sq)
     try:
         n, ci, h, w, co, k, s, p, d, ci2 = case
         torch.manual_seed(7)
@@ -775,7 +777,7 @@ def test_conv_wgrad_sq_bf16(case):
         err = (dw.cpu() - ref_dw).abs().max().item()
         assert err <= 1e-3 * ref_dw.abs().max().item(), err
     finally:
-        O.set_knobs(wgrad_sq=0)
+        O.set_knobs(wgrad_sq=1)
 
 
 # the fp16 compute dtype ("16-mixed" = IEEE half activations / MFMA operands, fp32 accumulation): every

@@ -254,3 +254,20 @@ def test_knobs_are_set_from_code_only():
         assert getattr(obj, last) is old
     with pytest.raises(ValueError):
         O.set_knobs(no_such_knob=1)
+
+
+def test_precision_16_mixed_maps_to_fp16_and_transformer_refuses_it():
+    """precision "16-mixed" (the reference's default, parameters_generate.py:211)
+    selects fp16 compute for the CNN encoders; the TransformerStage token kernels
+    are bf16/f32 only and say so instead of running a wrong dtype."""
+    import transformer_model as TM
+
+    P = copy.deepcopy(PR.default_parameters())
+    assert PR.compute_dtype_of(P) == torch.bfloat16
+    P["precision"] = "16-mixed"
+    assert PR.compute_dtype_of(P) == torch.float16
+    P["precision"] = "32"
+    assert PR.compute_dtype_of(P) == torch.float32
+    st = MM.set_compute_dtype(TM.TransformerStage(8, 32, depth=1, heads=2), torch.float16)
+    with pytest.raises(TypeError, match="float16"):
+        st(torch.zeros(1, 8, 8, 8))
