@@ -560,6 +560,49 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* __restrict__ 
   }
 }
 
+// The same sum for small weights with many splits (a 64x64 1x1 weight runs ~128-512 splits): one
+// thread per element walked `splits` slabs in a chain of dependent load rounds (4096 weights x 512
+// splits: 28 us). Here SL split lanes per element each sum every SL-th slab (four in flight), then
+// the lanes are added in lane order through LDS (fixed order: deterministic). Block = 256/SL
+// consecutive elements (slab order, coalesced) x SL split lanes.
+template <int SL>
+__global__ void __launch_bounds__(256) k_wgrad_reduce_sl(const float* __restrict__ ws, int splits, int Cout, int Cin,
+                                                         int CinP, int KH, int KW, float* __restrict__ dw,
+                                                         int accumulate) {
+  constexpr int EL = 256 / SL;
+  __shared__ float red[SL][EL + 1];
+  const int el = threadIdx.x % EL, sl = threadIdx.x / EL;
+  const int KK = KH * KW;
+  const int total = Cout * KK * Cin;
+  const long long slab = (long long)Cout * KK * CinP;
+  const int i = blockIdx.x * EL + el;
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int ci = 0, t = 0;
+  if (i < total) {
+    ci = i % Cin;
+    t = i / Cin;
+    const float* src = ws + (long long)t * CinP + ci;
+    int sp = sl;
+    for (; sp + 3 * SL < splits; sp += 4 * SL) {
+      v0 += src[(sp + 0 * SL) * slab];
+      v1 += src[(sp + 1 * SL) * slab];
+      v2 += src[(sp + 2 * SL) * slab];
+      v3 += src[(sp + 3 * SL) * slab];
+    }
+    for (; sp < splits; sp += SL) v0 += src[sp * slab];
+  }
+  red[sl][el] = (v0 + v1) + (v2 + v3);
+  __syncthreads();
+  if (sl == 0 && i < total) {
+    float v = red[0][el];
+#pragma unroll
+    for (int s = 1; s < SL; ++s) v += red[s][el];
+    const int co = t / KK, rs = t - co * KK;
+    float* d = dw + ((long long)co * Cin + ci) * KK + rs;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
 // --------------------------------------------------- single-output-channel
 // y[m] = sum_{r,s,ci} x[n, ho*st-pad+r*dil, wo*st-pad+s*dil, ci] * w[(r,s,ci)] + b
 // one 16-lane group per output pixel
@@ -931,9 +974,13 @@ static bool wgrad_sq_ok(int dtype, int Cout, long long Ktot) {
   return g_wgrad_sq == 2 || (long long)Cout * Ktot >= (1LL << 18);
 }
 
+// key 4: split-lane reducers for many-split sums (k_wgrad_reduce_sl): 0 off, 1 (default) on
+static int g_reduce_sl = 1;
+
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
-  DMF_CHECK_ARG(key >= 0 && key <= 3, "dmf_conv_wgrad_tune: unknown key %d", key);
-  if (key == 0) g_wgrad_dma = value != 0;
+  DMF_CHECK_ARG(key >= 0 && key <= 4, "dmf_conv_wgrad_tune: unknown key %d", key);
+  if (key == 4) g_reduce_sl = value != 0;
+  else if (key == 0) g_wgrad_dma = value != 0;
   else if (key == 1) g_wgrad_wide = value != 0;
   else if (key == 3) {
     DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_wgrad_tune: 256x256 tile mode %d", value);
@@ -1049,6 +1096,18 @@ extern "C" int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int C
   const long long total = (long long)Cout * Cin * KH * KW;
   DMF_CHECK_ARG(total < (1LL << 31) && (long long)Cout * KH * KW * CinP < (1LL << 31),
                 "dmf_conv2d_wgrad_reduce: %lld weights exceed the 32-bit walk", total);
+  if (g_reduce_sl && splits >= 64) {
+    hipLaunchKernelGGL(k_wgrad_reduce_sl<16>, dim3((unsigned)cdiv(total, 16LL)), dim3(256), 0, (hipStream_t)stream,
+                       workspace, splits, Cout, Cin, CinP, KH, KW, dw, accumulate);
+    DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");
+    return 0;
+  }
+  if (g_reduce_sl && splits >= 16) {
+    hipLaunchKernelGGL(k_wgrad_reduce_sl<4>, dim3((unsigned)cdiv(total, 64LL)), dim3(256), 0, (hipStream_t)stream,
+                       workspace, splits, Cout, Cin, CinP, KH, KW, dw, accumulate);
+    DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");
+    return 0;
+  }
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, workspace, splits, Cout, Cin,
                      CinP, KH, KW, dw, accumulate);
   DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");

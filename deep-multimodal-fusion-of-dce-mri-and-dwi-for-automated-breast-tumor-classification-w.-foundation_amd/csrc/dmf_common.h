@@ -161,6 +161,30 @@ __device__ __forceinline__ void st8(float* p, const float v[8]) {
   *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// raw 8-element vectors, so a kernel can put several rows' loads in flight before it converts any
+template <typename T> struct Vec8 { uint4 u; };
+template <> struct Vec8<float> { float4 a, b; };
+template <typename T> __device__ __forceinline__ Vec8<T> ldv8(const T* p) { return Vec8<T>{*(const uint4*)p}; }
+template <> __device__ __forceinline__ Vec8<float> ldv8(const float* p) {
+  return Vec8<float>{*(const float4*)p, *(const float4*)(p + 4)};
+}
+template <typename T> __device__ __forceinline__ Vec8<T> zero8() { return Vec8<T>{make_uint4(0, 0, 0, 0)}; }
+template <> __device__ __forceinline__ Vec8<float> zero8<float>() {
+  return Vec8<float>{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+}
+template <typename T> __device__ __forceinline__ void unpack8(const Vec8<T>& r, float v[8]) {
+  const uint32_t w[4] = {r.u.x, r.u.y, r.u.z, r.u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = B16<T>::lo(w[i]);
+    v[2 * i + 1] = B16<T>::hi(w[i]);
+  }
+}
+template <> __device__ __forceinline__ void unpack8(const Vec8<float>& r, float v[8]) {
+  v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
+  v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+}
+
 // exact (erf) GELU, as torch nn.GELU() default
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));

@@ -522,20 +522,37 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
       ra[e] = ssr ? ssr[c0 + e] : 1.f;
       rb[e] = ssr ? ssr[C + c0 + e] : 0.f;
     }
-    for (int r = rl; r < 256; r += 32) {
-      const long long m = r0 + r;
+    // 8 rows per thread in two batches of 4, every load of a batch issued before any row is
+    // converted: one row at a time left each thread with 2 loads in flight and the kernel
+    // latency-bound at ~2.5 TB/s
+    constexpr int RB = 4;
+#pragma unroll 1
+    for (int jb = 0; jb < 8; jb += RB) {
+      Vec8<T> vg[RB], vg2[RB], vx[RB], vr[RB];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const long long m = r0 + rl + 32 * (jb + j);
+        const bool in = m < M;
+        vg[j] = in ? ldv8(dy + m * lddy + c0) : zero8<T>();
+        if (dy2) vg2[j] = in ? ldv8(dy2 + m * lddy2 + c0) : zero8<T>();
+        vx[j] = in ? ldv8(x + m * ldx + c0) : zero8<T>();
+        if (ACT != DMF_ACT_NONE && res) vr[j] = in ? ldv8(res + m * ldr + c0) : zero8<T>();
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+      const long long m = r0 + rl + 32 * (jb + j);
       if (m >= M) break;
       float g[8], xv[8];
-      ld8(dy + m * lddy + c0, g);
+      unpack8(vg[j], g);
       if (dy2) {
         // a second gradient of the same output (the next block's shortcut), summed here in fp32
         // instead of by a separate add pass
         float g2[8];
-        ld8(dy2 + m * lddy2 + c0, g2);
+        unpack8(vg2[j], g2);
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] += g2[e];
       }
-      ld8(x + m * ldx + c0, xv);
+      unpack8(vx[j], xv);
       if (p > 0.f) {
         bool keep[4];
         dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
@@ -551,7 +568,7 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
         for (int e = 0; e < 8; ++e) z[e] = xv[e] * a[e] + b[e];
         if (res) {
           float rv[8];
-          ld8(res + m * ldr + c0, rv);
+          unpack8(vr[j], rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) z[e] += rv[e] * ra[e] + rb[e];
         }
@@ -563,6 +580,7 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
       for (int e = 0; e < 8; ++e) {
         s[e] += g[e];
         q[e] += g[e] * (xv[e] - mean[e]) * inv[e];
+      }
       }
     }
   }
@@ -656,13 +674,28 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
   }
   const int mbeg = blockIdx.x * rows_per_blk;
   const int mend = min(M, mbeg + rows_per_blk);
-  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
-    float g[8], xv[8];
-    ld8(dz + (size_t)m * lddz + c0, g);
-    ld8(x + (size_t)m * ldx + c0, xv);
+  // four rows' loads in flight per thread before any is converted (as k_act_bwd_bnred8)
+  constexpr int RB = 4;
+  for (int m0 = mbeg + (tid >> 3); m0 < mend; m0 += 32 * RB) {
+    Vec8<T> vg[RB], vx[RB];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
-    st8(dx + (size_t)m * lddx + c0, g);
+    for (int j = 0; j < RB; ++j) {
+      const int m = m0 + 32 * j;
+      const bool in = m < mend;
+      vg[j] = in ? ldv8(dz + (size_t)m * lddz + c0) : zero8<T>();
+      vx[j] = in ? ldv8(x + (size_t)m * ldx + c0) : zero8<T>();
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int m = m0 + 32 * j;
+      if (m >= mend) break;
+      float g[8], xv[8];
+      unpack8(vg[j], g);
+      unpack8(vx[j], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
+      st8(dx + (size_t)m * lddx + c0, g);
+    }
   }
 }
 

@@ -749,6 +749,11 @@ SQ_WGRAD_CASES = [
     (16, 2048, 16, 16, 512, 1, 1, 0, 1, 0),
     (4, 256, 32, 32, 256, 3, 1, 1, 1, 256),
     (5, 256, 31, 33, 768, 1, 1, 0, 1, 0),
+    # small weights, many pixel splits: the split-lane reducers (k_wgrad_reduce_sl<16> at >= 64 splits,
+    # <4> at >= 16)
+    (8, 64, 64, 64, 64, 1, 1, 0, 1, 0),
+    (8, 128, 32, 32, 256, 1, 1, 0, 1, 0),
+    (6, 64, 40, 40, 64, 3, 1, 1, 1, 0),
 ]
 
 

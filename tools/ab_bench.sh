@@ -6,7 +6,7 @@ R=${1:?rounds}; shift
 mkdir -p gpurun_out/ab
 for r in $(seq 1 $R); do
   for n in "$@"; do
-    DMF_HIP_LIB=ab/$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 > gpurun_out/ab/$n.$r.json 2> gpurun_out/ab/$n.$r.err || { echo "bench $n failed"; tail -20 gpurun_out/ab/$n.$r.err; exit 1; }
+    DMF_HIP_LIB=ab/$n.so timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 $AB_ARGS > gpurun_out/ab/$n.$r.json 2> gpurun_out/ab/$n.$r.err || { echo "bench $n failed"; tail -20 gpurun_out/ab/$n.$r.err; exit 1; }
     python - "$n" "$r" <<'PY'
 import json, sys
 n, r = sys.argv[1], sys.argv[2]

@@ -2,6 +2,7 @@
 # Interleaved A/B of knob settings (dmf_ops.KNOBS, passed as bench.py --knob) on the bench's
 # encoder-forward north star and step throughput (same library):
 #   bash tools/ab_env.sh ROUNDS "sgemm_v4=0" "sgemm_v4=1" ...   (a setting may hold several: "a=1,b=0"; "-" = defaults)
+#   AB_ARGS="--mode B" bash tools/ab_env.sh ...                  (extra bench.py arguments for every run)
 set -o pipefail
 R=${1:?rounds}; shift
 mkdir -p gpurun_out/abenv
@@ -11,7 +12,7 @@ for r in $(seq 1 $R); do
     i=$((i + 1))
     K=""
     if [ "$e" != "-" ]; then for kv in ${e//,/ }; do K="$K --knob $kv"; done; fi
-    timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 $K > gpurun_out/abenv/$i.$r.json 2> gpurun_out/abenv/$i.$r.err || { echo "bench $e failed"; tail -20 gpurun_out/abenv/$i.$r.err; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --steps 30 --warmup 5 $AB_ARGS $K > gpurun_out/abenv/$i.$r.json 2> gpurun_out/abenv/$i.$r.err || { echo "bench $e failed"; tail -20 gpurun_out/abenv/$i.$r.err; exit 1; }
     python - "$e" gpurun_out/abenv/$i.$r.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

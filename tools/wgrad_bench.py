@@ -72,7 +72,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--sq", action="store_true", help="A/B the 256x256 form against the default")
+    ap.add_argument("--reduce", action="store_true",
+                    help="time dmf_conv2d_wgrad_reduce alone, split-lane reducers off / on (key 4)")
     a = ap.parse_args()
+    if a.reduce:
+        return reduce_ab(a)
     cnt = collections.Counter(tuple(json.loads(l)["shape"]) for l in open(a.src))
     shapes = [s for s in sorted(cnt, key=lambda s: -cnt[s] * s[0] * s[1] * s[2] * s[3] * s[4] * s[5] ** 2 / s[6] ** 2)
               if s[3] >= 8 and s[4] >= 8]
@@ -112,6 +116,34 @@ def main():
     tune((1, 1, 0))
     print("weighted totals (ms per step, one encoder pair's forward shapes): " +
           "  ".join(f"{v} {t:.3f}" for v, t in zip(variants, tot)))
+
+
+def reduce_ab(a):
+    cnt = collections.Counter(tuple(json.loads(l)["shape"]) for l in open(a.src))
+    shapes = [s for s in cnt if s[3] >= 8 and s[4] >= 8]
+    tot = [0.0, 0.0]
+    for i, shape in enumerate(shapes):
+        launch, reduce, _ = setup(shape)
+        launch()
+        outs, times = [], [[], []]
+        for v in (0, 1):
+            N.call("dmf_conv_wgrad_tune", 4, v)
+            outs.append(reduce())
+        for _ in range(a.rounds):
+            for v in (0, 1):
+                N.call("dmf_conv_wgrad_tune", 4, v)
+                times[v].append(timed(reduce, a.reps))
+        med = [statistics.median(t) for t in times]
+        for v in (0, 1):
+            tot[v] += med[v] * cnt[shape]
+        n, h, w, ci, co, k, st, dl = shape
+        ho = (h + 2 * (k // 2) * dl - dl * (k - 1) - 1) // st + 1
+        splits = N.load().dmf_conv2d_wgrad_splits(N.BF16, co, ci, k, k, n * ho * ho)
+        close = ((outs[0] - outs[1]).abs().max() <= 1e-5 * outs[0].abs().max()).item()
+        print(f"{i:2d} {str(shape):38s} x{cnt[shape]:2d} splits {splits:4d} weights {co * ci * k * k:8d}  "
+              f"one-lane {med[0] * 1e3:6.1f} us  split-lane {med[1] * 1e3:6.1f} us  close={close}", flush=True)
+    N.call("dmf_conv_wgrad_tune", 4, 1)
+    print(f"weighted totals (ms per step): one-lane {tot[0]:.3f}  split-lane {tot[1]:.3f}")
 
 
 if __name__ == "__main__":
