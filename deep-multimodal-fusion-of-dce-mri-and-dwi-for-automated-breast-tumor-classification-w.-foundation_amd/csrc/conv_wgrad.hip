@@ -1096,13 +1096,16 @@ extern "C" int dmf_conv2d_wgrad_reduce(const float* workspace, int splits, int C
   const long long total = (long long)Cout * Cin * KH * KW;
   DMF_CHECK_ARG(total < (1LL << 31) && (long long)Cout * KH * KW * CinP < (1LL << 31),
                 "dmf_conv2d_wgrad_reduce: %lld weights exceed the 32-bit walk", total);
-  if (g_reduce_sl && splits >= 64) {
+  // split-lane forms where they measured faster (tools/wgrad_bench.py --reduce, profiles/r04i_wgrad_reduce.txt):
+  // small weights with many splits (4096 x 512 splits: 18.6 -> 5.5 us); above ~48K weights at >= 64 splits
+  // the 64-B segments per slab row lose to the one-lane walk (262144 x 64: 13.8 -> 24.9 us)
+  if (g_reduce_sl && splits >= 64 && total <= 49152) {
     hipLaunchKernelGGL(k_wgrad_reduce_sl<16>, dim3((unsigned)cdiv(total, 16LL)), dim3(256), 0, (hipStream_t)stream,
                        workspace, splits, Cout, Cin, CinP, KH, KW, dw, accumulate);
     DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");
     return 0;
   }
-  if (g_reduce_sl && splits >= 16) {
+  if (g_reduce_sl && splits >= 24 && splits < 64 && total <= (1LL << 20)) {
     hipLaunchKernelGGL(k_wgrad_reduce_sl<4>, dim3((unsigned)cdiv(total, 64LL)), dim3(256), 0, (hipStream_t)stream,
                        workspace, splits, Cout, Cin, CinP, KH, KW, dw, accumulate);
     DMF_LAUNCH_CHECK("dmf_conv2d_wgrad_reduce");

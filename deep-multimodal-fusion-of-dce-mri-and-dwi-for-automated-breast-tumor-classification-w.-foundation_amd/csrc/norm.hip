@@ -243,7 +243,8 @@ __device__ __forceinline__ void bn_src_affine(const BnApplySrc& s, int c, int C,
 }
 
 // y = drop(act(x*sa + ba [+ res*sr + br | + res])). Block = 64 channels
-// (blockIdx.y) x rows_per_blk pixels (blockIdx.x); 256 threads = 8 16-B
+// (blockIdx.x, fastest, so the resident blocks stream whole rows) x rows_per_blk pixels (blockIdx.y);
+// 256 threads = 8 16-B
 // channel chunks x 32 rows; the block's 64 (scale, shift) pairs are
 // finalized once into LDS. Dropout elements are indexed m*C + c exactly as
 // k_affine_act8 / k_act_bwd, so backward regenerates the same masks.
@@ -254,8 +255,8 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
                                                    int M, int C, int rows_per_blk) {
   __shared__ float sa[2][64], sr[2][64];
   const int tid = threadIdx.x;
-  const int cg = blockIdx.y * 64;
-  const bool first = blockIdx.x == 0;
+  const int cg = blockIdx.x * 64;
+  const bool first = blockIdx.y == 0;
   if (tid < 64) {
     const int c = cg + tid;
     float sc = 1.f, sh = 0.f;
@@ -269,7 +270,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
     sr[0][tid - 64] = sc;
     sr[1][tid - 64] = sh;
   }
-  if (first && blockIdx.y == 0 && tid == 0) {
+  if (first && blockIdx.x == 0 && tid == 0) {
     if (A.acc && A.fin.nbt) *A.fin.nbt += 1;
     if (RES == 2 && R.acc && R.fin.nbt) *R.fin.nbt += 1;
   }
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
     }
   }
   const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int mbeg = blockIdx.x * rows_per_blk;
+  const int mbeg = blockIdx.y * rows_per_blk;
   const int mend = min(M, mbeg + rows_per_blk);
   for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
     float v[8];
@@ -505,8 +506,8 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
                                                         double* __restrict__ acc, int replicas) {
   __shared__ float red[32][65 * 2];
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c0 = blockIdx.y * 64 + cl * 8;
-  const long long r0 = (long long)blockIdx.x * 256;
+  const int c0 = blockIdx.x * 64 + cl * 8;
+  const long long r0 = (long long)blockIdx.y * 256;
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   float s[8], q[8];
 #pragma unroll
@@ -595,10 +596,10 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
     float t = 0.f;
 #pragma unroll 8
     for (int r = 0; r < 32; ++r) t += red[r][c * 2 + w];
-    const int cg = blockIdx.y * 64 + c;
+    const int cg = blockIdx.x * 64 + c;
     if (cg < C) {
-      if (acc) unsafeAtomicAdd(acc + ((size_t)(blockIdx.x % (unsigned)replicas) * C + cg) * 2 + w, (double)t);
-      else part[((size_t)blockIdx.x * C + cg) * 2 + w] = t;
+      if (acc) unsafeAtomicAdd(acc + ((size_t)(blockIdx.y % (unsigned)replicas) * C + cg) * 2 + w, (double)t);
+      else part[((size_t)blockIdx.y * C + cg) * 2 + w] = t;
     }
   }
 }
@@ -622,7 +623,7 @@ __global__ void k_bn_bwd_apply8(const T* __restrict__ dz, int lddz, const T* __r
 }
 
 // BN backward apply with the finalize folded in (dmf_bn_bwd_apply_acc): block =
-// 64 channels (blockIdx.y) x rows_per_blk pixels; its 64 (A, Cc, B) come from the
+// 64 channels (blockIdx.x) x rows_per_blk pixels (blockIdx.y); its 64 (A, Cc, B) come from the
 // column sums accumulated by dmf_act_bwd_bn_reduce_acc into [replicas][C][2]
 // doubles (summed in a fixed order, the arithmetic of k_bn_bwd_finalize_wide);
 // the blockIdx.x == 0 blocks also add dgamma / dbeta. dx = A*dz + Cc*x + B.
@@ -635,7 +636,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
                                                           int rows_per_blk) {
   __shared__ float sco[3][64];
   const int tid = threadIdx.x;
-  const int cg = blockIdx.y * 64;
+  const int cg = blockIdx.x * 64;
   if (tid < 64) {
     const int c = cg + tid;
     float A = 0.f, Cc = 0.f, B = 0.f;
@@ -645,7 +646,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
         s += acc[((size_t)r * C + c) * 2];
         q += acc[((size_t)r * C + c) * 2 + 1];
       }
-      if (blockIdx.x == 0) {
+      if (blockIdx.y == 0) {
         if (dbeta) dbeta[c] += (float)s;
         if (dgamma) dgamma[c] += (float)q;
       }
@@ -672,30 +673,15 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
     c8[k] = sco[1][cl + k];
     b8[k] = sco[2][cl + k];
   }
-  const int mbeg = blockIdx.x * rows_per_blk;
+  const int mbeg = blockIdx.y * rows_per_blk;
   const int mend = min(M, mbeg + rows_per_blk);
-  // four rows' loads in flight per thread before any is converted (as k_act_bwd_bnred8)
-  constexpr int RB = 4;
-  for (int m0 = mbeg + (tid >> 3); m0 < mend; m0 += 32 * RB) {
-    Vec8<T> vg[RB], vx[RB];
+  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
+    float g[8], xv[8];
+    ld8(dz + (size_t)m * lddz + c0, g);
+    ld8(x + (size_t)m * ldx + c0, xv);
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int m = m0 + 32 * j;
-      const bool in = m < mend;
-      vg[j] = in ? ldv8(dz + (size_t)m * lddz + c0) : zero8<T>();
-      vx[j] = in ? ldv8(x + (size_t)m * ldx + c0) : zero8<T>();
-    }
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int m = m0 + 32 * j;
-      if (m >= mend) break;
-      float g[8], xv[8];
-      unpack8(vg[j], g);
-      unpack8(vx[j], xv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
-      st8(dx + (size_t)m * lddx + c0, g);
-    }
+    for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
+    st8(dx + (size_t)m * lddx + c0, g);
   }
 }
 
@@ -855,7 +841,7 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
   // ~8 row iterations per thread, but at least ~1024 blocks in flight
   int rows = 256;
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
-  const dim3 g((unsigned)cdiv(M, rows), (unsigned)gy);
+  const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
   const int resk = res == nullptr ? 0 : ((res_bn || res_scale_shift) ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
 #define DMF_BA(TT, AC, RK)                                                                                     \
@@ -998,7 +984,7 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
   const int gy = cdiv(C, 64);
   int rows = 256;
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
-  const dim3 g((unsigned)cdiv(M, rows), (unsigned)gy);
+  const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply_acc<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
                        (const T*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
                        (T*)dx, lddx, (int)M, C, rows));
@@ -1027,8 +1013,8 @@ static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const voi
     return dmf_bn_bwd_reduce(dtype, dz, lddz, x, ldx, save_mean_invstd, M, C, partials, stream);
   }
   const long long tiles = (M + 255) / 256;
-  DMF_CHECK_ARG(tiles < 65536LL * 32768LL, "dmf_act_bwd_bn_reduce: too many rows");
-  dim3 grid((unsigned)tiles, (unsigned)cdiv(C, 64));
+  DMF_CHECK_ARG(tiles < 65536LL, "dmf_act_bwd_bn_reduce: too many rows");
+  dim3 grid((unsigned)cdiv(C, 64), (unsigned)tiles);  // channel groups fastest: resident blocks cover whole rows
   hipStream_t s = (hipStream_t)stream;
 #define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)dy2, lddy2, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
   DMF_DISPATCH_DTYPE(dtype, T, switch (act) {
