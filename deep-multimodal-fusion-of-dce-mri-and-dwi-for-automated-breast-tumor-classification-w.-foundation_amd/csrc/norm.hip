@@ -494,8 +494,10 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dz, int lddz, const T* __re
 // (k_bn_bwd_reduce would re-read dz and x). Block = 32 row lanes x 8 channel
 // lanes of 8 channels (64 channels), 16-B accesses; x is the BN input (the
 // raw conv output), z = x*ssa + shift (+ residual) recomputed for act'.
-template <typename T, int ACT>
-__global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy, int lddy,
+// F: which optional operands the instance handles (bit 0 residual, bit 1 second gradient, bit 2 dropout),
+// so the common plain-ReLU instance holds no registers for the others (occupancy: ~180 VGPRs for all)
+template <typename T, int ACT, int F>
+__global__ void __launch_bounds__(256, (F & 5) ? 1 : 4) k_act_bwd_bnred8(const T* __restrict__ dy, int lddy,
                                                         const T* __restrict__ dy2, int lddy2, const T* __restrict__ x,
                                                         int ldx, const float* __restrict__ ssa,
                                                         const T* __restrict__ res, int ldr,
@@ -504,29 +506,36 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
                                                         const float* __restrict__ save, T* __restrict__ dz, int lddz,
                                                         long long M, int C, float* __restrict__ part,
                                                         double* __restrict__ acc, int replicas) {
+  constexpr bool HR = (F & 1) && ACT != DMF_ACT_NONE, HD = F & 2, HP = F & 4;
   __shared__ float red[32][65 * 2];
+  __shared__ __attribute__((aligned(16))) float rss[2][64];  // the residual's BN scale / shift (HR): read per row
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.x * 64 + cl * 8;
   const long long r0 = (long long)blockIdx.y * 256;
-  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const float sc = HP && p > 0.f ? 1.f / (1.f - p) : 1.f;
   float s[8], q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if constexpr (HR) {
+    if (threadIdx.x < 128) {
+      const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+      rss[w][threadIdx.x & 63] = c < C && ssr ? ssr[w * C + c] : (w == 0 ? 1.f : 0.f);
+    }
+    __syncthreads();
+  }
   if (c0 < C) {
-    float mean[8], inv[8], a[8], b[8], ra[8], rb[8];
+    float mean[8], inv[8], a[8], b[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       mean[e] = save[c0 + e];
       inv[e] = save[C + c0 + e];
       a[e] = ssa[c0 + e];
       b[e] = ssa[C + c0 + e];
-      ra[e] = ssr ? ssr[c0 + e] : 1.f;
-      rb[e] = ssr ? ssr[C + c0 + e] : 0.f;
     }
     // 8 rows per thread in two batches of 4, every load of a batch issued before any row is
     // converted: one row at a time left each thread with 2 loads in flight and the kernel
     // latency-bound at ~2.5 TB/s
-    constexpr int RB = 4;
+    constexpr int RB = (HR || HD) ? 2 : 4;  // rows per batch: keep the 3- and 4-operand forms near 128 VGPRs
 #pragma unroll 1
     for (int jb = 0; jb < 8; jb += RB) {
       Vec8<T> vg[RB], vg2[RB], vx[RB], vr[RB];
@@ -535,9 +544,9 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
         const long long m = r0 + rl + 32 * (jb + j);
         const bool in = m < M;
         vg[j] = in ? ldv8(dy + m * lddy + c0) : zero8<T>();
-        if (dy2) vg2[j] = in ? ldv8(dy2 + m * lddy2 + c0) : zero8<T>();
+        if constexpr (HD) vg2[j] = in && dy2 ? ldv8(dy2 + m * lddy2 + c0) : zero8<T>();
         vx[j] = in ? ldv8(x + m * ldx + c0) : zero8<T>();
-        if (ACT != DMF_ACT_NONE && res) vr[j] = in ? ldv8(res + m * ldr + c0) : zero8<T>();
+        if constexpr (HR) vr[j] = in && res ? ldv8(res + m * ldr + c0) : zero8<T>();
       }
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
@@ -545,7 +554,7 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
       if (m >= M) break;
       float g[8], xv[8];
       unpack8(vg[j], g);
-      if (dy2) {
+      if constexpr (HD) {
         // a second gradient of the same output (the next block's shortcut), summed here in fp32
         // instead of by a separate add pass
         float g2[8];
@@ -554,7 +563,7 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
         for (int e = 0; e < 8; ++e) g[e] += g2[e];
       }
       unpack8(vx[j], xv);
-      if (p > 0.f) {
+      if (HP && p > 0.f) {
         bool keep[4];
         dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
@@ -567,9 +576,13 @@ __global__ void __launch_bounds__(256) k_act_bwd_bnred8(const T* __restrict__ dy
         float z[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] = xv[e] * a[e] + b[e];
-        if (res) {
+        if constexpr (HR) {
           float rv[8];
           unpack8(vr[j], rv);
+          const float4 ra0 = *(const float4*)&rss[0][cl * 8], ra1 = *(const float4*)&rss[0][cl * 8 + 4];
+          const float4 rb0 = *(const float4*)&rss[1][cl * 8], rb1 = *(const float4*)&rss[1][cl * 8 + 4];
+          const float ra[8] = {ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w};
+          const float rb[8] = {rb0.x, rb0.y, rb0.z, rb0.w, rb1.x, rb1.y, rb1.z, rb1.w};
 #pragma unroll
           for (int e = 0; e < 8; ++e) z[e] += rv[e] * ra[e] + rb[e];
         }
@@ -1016,13 +1029,28 @@ static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const voi
   DMF_CHECK_ARG(tiles < 65536LL, "dmf_act_bwd_bn_reduce: too many rows");
   dim3 grid((unsigned)cdiv(C, 64), (unsigned)tiles);  // channel groups fastest: resident blocks cover whole rows
   hipStream_t s = (hipStream_t)stream;
-#define DMF_ABR(TT, A)                                                                                           hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)dy2, lddy2, (const TT*)x, ldx,                      scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, site, save_mean_invstd,                      (TT*)dz, lddz, M, C, partials, acc, replicas)
+  // residual / second-gradient / dropout specialisations (k_act_bwd_bnred8's F); any dropout takes
+  // the all-operands instance
+  const int F = dropout_p > 0.f ? 7 : ((res && act != DMF_ACT_NONE) ? 1 : 0) | (dy2 ? 2 : 0);
+#define DMF_ABR(TT, A, FF)                                                                                   \
+  hipLaunchKernelGGL((k_act_bwd_bnred8<TT, A, FF>), grid, dim3(256), 0, s, (const TT*)dy, lddy, (const TT*)dy2, \
+                     lddy2, (const TT*)x, ldx, scale_shift, (const TT*)res, ldr, res_scale_shift, dropout_p, rng, \
+                     site, save_mean_invstd, (TT*)dz, lddz, M, C, partials, acc, replicas)
+#define DMF_ABR_F(TT, A)                 \
+  switch (F) {                           \
+    case 0: DMF_ABR(TT, A, 0); break;    \
+    case 1: DMF_ABR(TT, A, 1); break;    \
+    case 2: DMF_ABR(TT, A, 2); break;    \
+    case 3: DMF_ABR(TT, A, 3); break;    \
+    default: DMF_ABR(TT, A, 7); break;   \
+  }
   DMF_DISPATCH_DTYPE(dtype, T, switch (act) {
-      case DMF_ACT_RELU: DMF_ABR(T, DMF_ACT_RELU); break;
-      case DMF_ACT_GELU: DMF_ABR(T, DMF_ACT_GELU); break;
-      case DMF_ACT_SIGMOID: DMF_ABR(T, DMF_ACT_SIGMOID); break;
-      default: DMF_ABR(T, DMF_ACT_NONE);
+      case DMF_ACT_RELU: DMF_ABR_F(T, DMF_ACT_RELU); break;
+      case DMF_ACT_GELU: DMF_ABR_F(T, DMF_ACT_GELU); break;
+      case DMF_ACT_SIGMOID: DMF_ABR(T, DMF_ACT_SIGMOID, 7); break;
+      default: DMF_ABR(T, DMF_ACT_NONE, 7);
     });
+#undef DMF_ABR_F
 #undef DMF_ABR
   DMF_LAUNCH_CHECK("dmf_act_bwd_bn_reduce");
   return 0;

@@ -75,7 +75,14 @@ def main():
                        acc.data_ptr(), 8, st())
             return f
 
-        rows = [("copy (1R+1W)", copy, 2), ("torch add (2R+1W)", add, 3), ("bn_bwd_apply_acc (2R+1W)", apply, 3),
+        part = torch.empty((M + 255) // 256 * C * 2, dtype=torch.float32, device=dev)
+
+        def actbwd_slab():
+            N.call("dmf_act_bwd_bn_reduce", N.BF16, t[0].data_ptr(), C, None, 0, t[1].data_ptr(), C, ss.data_ptr(),
+                   None, 0, None, N.ACT_RELU, 0.0, None, 0, save.data_ptr(), t[2].data_ptr(), C, M, C,
+                   part.data_ptr(), st())
+
+        rows = [("copy (1R+1W)", copy, 2), ("act_bwd_bnred slab partials (2R+1W)", actbwd_slab, 3), ("torch add (2R+1W)", add, 3), ("bn_bwd_apply_acc (2R+1W)", apply, 3),
                 ("act_bwd_bnred (2R+1W)", actbwd(), 3), ("act_bwd_bnred +res (3R+1W)", actbwd(True), 4),
                 ("act_bwd_bnred +res+dy2 (4R+1W)", actbwd(True, True), 5)]
         for name, fn, passes in rows:
