@@ -854,3 +854,38 @@ def test_conv_backward_f16(case):
     assert err_x <= 2e-3 * ref_dx.abs().max().item(), err_x
     err_w = (dw.cpu() - ref_dw).abs().max().item()
     assert err_w <= 1e-3 * ref_dw.abs().max().item(), err_w
+
+
+# fp32 GEMM (dmf_sgemm, 64x64 tiles with the ordered split-K reduce where the workspace is given): every
+# transpose, alpha, an accumulating beta, bias and activation, against float64 torch on the same operands
+SGEMM_CASES = [
+    # (tA, tB, M, N, K, beta, bias, act)
+    (0, 1, 512, 128, 128, 0.0, True, "none"),
+    (0, 0, 512, 128, 384, 0.0, False, "relu"),
+    (1, 0, 384, 128, 512, 1.0, False, "none"),
+    (1, 1, 70, 45, 600, 0.5, True, "gelu"),
+    (0, 1, 32, 4, 512, 0.0, True, "none"),
+    (0, 0, 33, 129, 1100, 0.0, False, "sigmoid"),
+    (0, 1, 2048, 512, 256, 0.0, True, "none"),
+]
+
+
+@pytest.mark.parametrize("case", SGEMM_CASES)
+def test_sgemm_forms(case):
+    tA, tB, M, N_, K, beta, with_bias, act = case
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn((K, M) if tA else (M, K), generator=g)
+    B = torch.randn((N_, K) if tB else (K, N_), generator=g)
+    C0 = torch.randn(M, N_, generator=g)
+    bias = torch.randn(N_, generator=g) if with_bias else None
+    ref = 0.75 * ((A.t() if tA else A).double() @ (B.t() if tB else B).double()) + beta * C0.double()
+    if bias is not None:
+        ref = ref + bias.double()
+    ref = {"none": ref, "relu": torch.relu(ref), "gelu": F.gelu(ref), "sigmoid": torch.sigmoid(ref)}[act]
+    Ad, Bd, Cd = A.to(DEV), B.to(DEV), C0.clone().to(DEV)
+    bd = bias.to(DEV) if bias is not None else None
+    O._sgemm(tA, tB, M, N_, K, 0.75, Ad.data_ptr(), Ad.shape[1], Bd.data_ptr(), Bd.shape[1], beta, Cd.data_ptr(),
+             N_, O._p(bd), O.ACT[act], O._stream())
+    torch.cuda.synchronize()
+    err = (Cd.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * max(1.0, ref.abs().max().item()) * (K / 128) ** 0.5, err
