@@ -520,3 +520,51 @@ def test_patch_embed_fp8_matches_quantised_reference():
     xr2 = x.float().detach().requires_grad_(True)
     torch.nn.functional.conv2d(xr2, conv.weight.detach(), None, stride=p).backward(g.float())
     assert (xd.grad.float() - xr2.grad).abs().max().item() <= 3e-2 * xr2.grad.abs().max().item()
+
+
+# token-linear shapes through the bf16 GEMM (128x128 tiles) with every forward epilogue -- bias, gelu +
+# aux, LayerScale + f32 residual -- M tails, against float64 on the bf16-rounded operands
+NT_CASES = [
+    # (M, N, K, out dtype, epilogue)
+    (1030, 512, 512, torch.bfloat16, "bias"),
+    (4608, 1536, 512, torch.bfloat16, "bias"),
+    (700, 384, 2048, torch.float32, "scale_res"),
+    (520, 256, 128, torch.bfloat16, "gelu_aux"),
+]
+
+
+@pytest.mark.parametrize("case", NT_CASES)
+def test_gemm_token_linear_epilogues(case):
+    M, Nn, K, odt, epi = case
+    g = torch.Generator().manual_seed(M + K)
+    A, W, bias = torch.randn(M, K, generator=g), torch.randn(Nn, K, generator=g) * 0.1, torch.randn(Nn, generator=g)
+    res, gam = torch.randn(M, Nn, generator=g), torch.rand(Nn, generator=g)
+    Ad, Wd = A.to(DEV, torch.bfloat16), W.to(DEV, torch.bfloat16)
+    pre = _bf(A).double() @ _bf(W).double().t() + bias.double()
+    C = torch.empty((M, Nn), dtype=odt, device=DEV)
+    aux = torch.empty((M, Nn), dtype=torch.bfloat16, device=DEV) if epi == "gelu_aux" else None
+    kw = dict(bias=bias.to(DEV))
+    if epi == "scale_res":
+        kw.update(colscale=gam.to(DEV), res=res.to(DEV))
+    if epi == "gelu_aux":
+        kw.update(act="gelu", aux=aux)
+    D.gemm(C, Ad, Wd, M, Nn, K, lda=K, ldb=K, ldc=Nn, **kw)
+    ref = {"bias": pre, "scale_res": res.double() + pre * gam.double(), "gelu_aux": F.gelu(pre)}[epi]
+    _close(C, ref, 1e-2, "token linear")
+    if epi == "gelu_aux":
+        _close(aux, pre, 1e-2, "aux")
+
+
+def test_gemm_attention_scores_head_slices():
+    """Q K^T over head slices of packed qkv rows (batch strides, b_off), n = 200 (tails in both tiles)"""
+    b, h, n, d = 2, 4, 200, 128
+    e = h * d
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(b, n, 3 * e, generator=g)
+    qd = qkv.to(DEV, torch.bfloat16)
+    S = torch.empty((b, h, n, n), device=DEV)
+    D.gemm(S, qd, qd, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, h), sa=(n * 3 * e, d), sb=(n * 3 * e, d),
+           sc=(h * n * n, n * n), b_off=e, alpha=0.125)
+    q = _bf(qkv[..., :e]).double().view(b, n, h, d).transpose(1, 2)
+    k = _bf(qkv[..., e:2 * e]).double().view(b, n, h, d).transpose(1, 2)
+    _close(S, 0.125 * (q @ k.transpose(-1, -2)), 1e-3, "QK^T")

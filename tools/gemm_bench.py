@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Token-GEMM microbench (config 5 shapes: 32 volumes x 576 tokens, E = 512,
+4 heads): the linears and Q K^T through dmf_gemm_bf16, HIP events over a
+hipGraph of R launches.
+
+    python tools/gemm_bench.py [--reps 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "deep-multimodal-fusion-of-dce-mri-and-dwi-for-automated-breast-tumor-classification-w.-foundation_amd")]
+
+import torch  # noqa: E402
+
+import dmf_tokens as D  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dev = "cuda"
+    r, e, hid, b, h, n = 32 * 576, 512, 2048, 32, 4, 576
+    d = e // h
+    bf = dict(dtype=torch.bfloat16, device=dev)
+    x = torch.randn(r, e, **bf)
+    hbuf = torch.randn(r, hid, **bf)
+    qkv = torch.randn(r, 3 * e, **bf)
+    cases = {
+        "qkv  (18432x1536x512)": lambda: D.gemm(torch.empty((r, 3 * e), **bf) if False else out_qkv, x, wq, r, 3 * e, e,
+                                                 lda=e, ldb=e, ldc=3 * e, bias=bq),
+        "fc1  (18432x2048x512) gelu": lambda: D.gemm(out_h, x, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=b1, act="gelu"),
+        "fc2  (18432x512x2048) f32": lambda: D.gemm(out_f, hbuf, w2, r, e, hid, lda=hid, ldb=hid, ldc=e, bias=bp),
+        "proj (18432x512x512) f32": lambda: D.gemm(out_f, x, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=bp),
+        "QK^T (576x576x128 x128)": lambda: D.gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, h),
+                                                  sa=(n * 3 * e, d), sb=(n * 3 * e, d), sc=(h * n * n, n * n), b_off=e),
+    }
+    wq, w1, w2, wp = (torch.randn(3 * e, e, **bf), torch.randn(hid, e, **bf), torch.randn(e, hid, **bf),
+                      torch.randn(e, e, **bf))
+    bq, b1, bp = torch.randn(3 * e, device=dev), torch.randn(hid, device=dev), torch.randn(e, device=dev)
+    out_qkv, out_h = torch.empty((r, 3 * e), **bf), torch.empty((r, hid), **bf)
+    out_f = torch.empty((r, e), dtype=torch.float32, device=dev)
+    S = torch.empty((b, h, n, n), dtype=torch.float32, device=dev)
+    flops = {"qkv": 2 * r * 3 * e * e, "fc1": 2 * r * hid * e, "fc2": 2 * r * e * hid, "proj": 2 * r * e * e,
+             "QK^T": 2 * b * h * n * n * d}
+    for name, fn in cases.items():
+        us = timed(fn, a.reps)
+        fl = flops[name.split()[0]]
+        print(f"{name:30s} {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
