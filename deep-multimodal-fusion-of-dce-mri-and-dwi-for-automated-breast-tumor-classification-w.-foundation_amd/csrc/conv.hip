@@ -1440,7 +1440,6 @@ extern "C" int dmf_conv_m_tile(void) { return CBM; }
 
 extern "C" int dmf_conv_last_form(void) { return g_last_form; }
 
-int sgemm_tune_v4(int v4);   // dense.hip
 
 extern "C" int dmf_conv_tune(int key, int value) {
   switch (key) {
@@ -1454,7 +1453,6 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 8: return conv_pp_tune(value != 0);
     case 10: g_stem_enable = value != 0; return 0;
     case 11: g_fast_epi = value != 0; return 0;
-    case 13: return sgemm_tune_v4(value);
     case 14: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: wide min tiles %d", value); g_wide_min_tiles = value; return 0;
     case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);

@@ -41,11 +41,9 @@ __device__ __forceinline__ float actf(int act, float z) {
 // partial tile into ws[z][M][N] and k_sgemm_reduce sums the splits in a
 // fixed order and applies alpha, bias and act (deterministic).
 // BK = K rows staged per barrier (16; a 64-deep form measured neutral on the
-// mode-A step, interleaved A/B 3108 vs 3100 vol/s, and was removed)
-// V4: each thread owns 4 consecutive rows x 4 consecutive columns, so its A and B fragments are two
-// 16-B LDS reads per k (the strided 4 x 4 mapping issued 8 scalar reads); V4 = false keeps the
-// strided form (A/B, dmf_conv_tune key 13)
-template <int BK, bool V4>
+// mode-A step, interleaved A/B 3108 vs 3100 vol/s, and was removed; so was a 4x4
+// vector micro-tile with two 16-B LDS reads per k: 3114 vs 3108, round 4)
+template <int BK>
 __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int K, int kchunk, float alpha,
                                                const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                int ldb, float beta, float* __restrict__ C, int ldc,
@@ -90,16 +88,10 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
 #pragma unroll
     for (int kk = 0; kk < BK; ++kk) {
       float a[4], b[4];
-      if constexpr (V4) {
-        const float4 av = *(const float4*)&As[kk][ty * 4], bv = *(const float4*)&Bs[kk][tx * 4];
-        a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-        b[0] = bv.x; b[1] = bv.y; b[2] = bv.z; b[3] = bv.w;
-      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
-      }
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx + 16 * j];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -110,7 +102,7 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int m = V4 ? m0 + ty * 4 + i : m0 + ty + 16 * i, n = V4 ? n0 + tx * 4 + j : n0 + tx + 16 * j;
+      const int m = m0 + ty + 16 * i, n = n0 + tx + 16 * j;
       if (m < M && n < N) {
         if (split) {
           ws[((size_t)blockIdx.z * M + m) * N + n] = acc[i][j];
@@ -889,11 +881,6 @@ static int sgemm_splits(int M, int N, int K) {
   return std::max(1, cdiv(K, kchunk));
 }
 
-static bool g_sgemm_v4 = false;  // vector 4 x 4 micro-tile (dmf_conv_tune key 13)
-int sgemm_tune_v4(int v4) {
-  g_sgemm_v4 = v4 != 0;
-  return 0;
-}
 
 extern "C" int dmf_sgemm_ws_size(int M, int N, int K) {
   const int S = sgemm_splits(M, N, K);
@@ -911,12 +898,8 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);
   S = S > 1 ? cdiv(K, kchunk) : 1;
   dim3 grid(cdiv(N, 64), cdiv(M, 64), S);
-  if (g_sgemm_v4)
-    hipLaunchKernelGGL((k_sgemm<16, true>), grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda,
-                       B, ldb, beta, C, ldc, bias, act, workspace);
-  else
-    hipLaunchKernelGGL((k_sgemm<16, false>), grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda,
-                       B, ldb, beta, C, ldc, bias, act, workspace);
+  hipLaunchKernelGGL((k_sgemm<16>), grid, dim3(256), 0, st, transA, transB, M, N, K, kchunk, alpha, A, lda, B, ldb,
+                     beta, C, ldc, bias, act, workspace);
   if (S > 1)
     hipLaunchKernelGGL(k_sgemm_reduce, dim3(gsz((long long)M * N)), dim3(256), 0, st, S, M, N, alpha, workspace, beta,
                        C, ldc, bias, act);

@@ -2448,7 +2448,6 @@ KNOBS = {
     "conv_pp_persist": ("tune", 8),
     "conv_stem": ("tune", 10),
     "conv_fast_epi": ("tune", 11),
-    "sgemm_v4": ("tune", 13),
     "conv_wide_min_tiles": ("tune", 14),
     "conv_sq_min_tiles": ("tune", 15),
     "wgrad_dma": ("wgrad_tune", 0),

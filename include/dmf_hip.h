@@ -66,8 +66,8 @@ int dmf_conv_last_form(void);
  * 1 = its scheduling variant 0..3; 2 = forced tile; 3 = statistics accumulation
  * mode; 4 = persistent 256x256 form on / off; 6 = benchmark-only skip bits of the
  * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
- * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 13 = fp32 GEMM 4x4 vector
- * micro-tile; 14 / 15 = tiles a launch needs for the 256x128 / 256x256 forms.
+ * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 14 / 15 = tiles a launch
+ * needs for the 256x128 / 256x256 forms.
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the

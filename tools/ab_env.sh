@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of knob settings (dmf_ops.KNOBS, passed as bench.py --knob) on the bench's
 # encoder-forward north star and step throughput (same library):
-#   bash tools/ab_env.sh ROUNDS "sgemm_v4=0" "sgemm_v4=1" ...   (a setting may hold several: "a=1,b=0"; "-" = defaults)
+#   bash tools/ab_env.sh ROUNDS "wgrad_sq=0" "wgrad_sq=1" ...   (a setting may hold several: "a=1,b=0"; "-" = defaults)
 #   AB_ARGS="--mode B" bash tools/ab_env.sh ...                  (extra bench.py arguments for every run)
 set -o pipefail
 R=${1:?rounds}; shift
