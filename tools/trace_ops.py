@@ -37,6 +37,10 @@ class Tracer(TorchDispatchMode):
                 if ("foundation_amd" in fr.filename or "bench.py" in fr.filename) and "dmf_native" not in fr.filename:
                     site = f"{os.path.basename(fr.filename)}:{fr.lineno}"
                     break
+            if site == "?":
+                shp = [tuple(a.shape) for a in args if isinstance(a, torch.Tensor)][:2]
+                dts = [str(a.dtype).replace("torch.", "") for a in args if isinstance(a, torch.Tensor)][:1]
+                site = f"? {shp} {dts}"
             self.counts[(base, site)] += 1
         return func(*args, **(kwargs or {}))
 
