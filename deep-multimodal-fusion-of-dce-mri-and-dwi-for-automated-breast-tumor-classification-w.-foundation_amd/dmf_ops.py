@@ -2455,6 +2455,7 @@ KNOBS = {
     "wgrad_tr": ("wgrad_tune", 2),
     "wgrad_sq": ("wgrad_tune", 3),
     "wgrad_reduce_sl": ("wgrad_tune", 4),
+    "wgrad_fill": ("wgrad_tune", 5),
 }
 
 
