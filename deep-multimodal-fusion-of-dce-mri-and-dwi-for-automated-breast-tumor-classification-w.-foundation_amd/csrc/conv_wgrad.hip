@@ -976,8 +976,11 @@ static bool wgrad_sq_ok(int dtype, int Cout, long long Ktot) {
 
 // key 4: split-lane reducers for many-split sums (k_wgrad_reduce_sl): 0 off, 1 (default) on
 static int g_reduce_sl = 1;
-// key 5: the block count the pixel splits aim for, in percent of one chip-filling wave (default 100)
-static int g_wgrad_fill = 100;
+// key 5: the block count the pixel splits aim for, in percent of one chip-filling wave. Default 50:
+// a weight gradient runs beside the other encoder's backward (and its own dX chain), and a launch
+// sized to fill the chip alone holds CUs those need -- mode B, interleaved A/B: 20 % 944, 30 % 992,
+// 40 % 1010, 50 % 1011-1015, 65 % 1010, 100 % 988, 200 % 975 vol/s
+static int g_wgrad_fill = 50;
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
   DMF_CHECK_ARG(key >= 0 && key <= 5, "dmf_conv_wgrad_tune: unknown key %d", key);
@@ -1005,7 +1008,7 @@ extern "C" int dmf_conv2d_wgrad_splits(int dtype, int Cout, int Cin, int KH, int
   // transposed-read kernel: ~2 resident blocks per CU, and every split costs
   // a Cout x K fp32 slab round trip, so aim for one wave of 512 blocks (256 of the 256x256 form)
   long long target = sq ? 256 : (is16(dtype) && wgrad_tr_enabled()) ? 512 : 1024;
-  if (g_wgrad_fill != 100) target = std::max(1LL, target * g_wgrad_fill / 100);
+  target = std::max(1LL, target * g_wgrad_fill / 100);
   long long want = (target + tiles - 1) / tiles;
   // >= 256 pixels (4 K-steps) per split, and at most 64 MiB of fp32 slabs: a small
   // weight (64x64 1x1: one tile) then runs 128 splits of 4 K-steps instead of 32
