@@ -82,14 +82,17 @@ def main():
                    None, 0, None, N.ACT_RELU, 0.0, None, 0, save.data_ptr(), t[2].data_ptr(), C, M, C,
                    part.data_ptr(), st())
 
-        def affine(act):
+        rng = O.RNG.snapshot(dev)
+
+        def affine(act, p=0.0):
             def f():
-                N.call("dmf_affine_act", N.BF16, t[0].data_ptr(), C, ss.data_ptr(), None, 0, None, act, 0.0, None, 0,
-                       t[2].data_ptr(), C, M, C, st())
+                N.call("dmf_affine_act", N.BF16, t[0].data_ptr(), C, ss.data_ptr(), None, 0, None, act, p,
+                       rng.data_ptr() if p > 0 else None, 1, t[2].data_ptr(), C, M, C, st())
             return f
 
         rows = [("copy (1R+1W)", copy, 2), ("affine + relu (1R+1W)", affine(N.ACT_RELU), 2),
                 ("affine + gelu (1R+1W)", affine(N.ACT_GELU), 2),
+                ("affine + gelu + dropout 0.4 (1R+1W)", affine(N.ACT_GELU, 0.4), 2),
                 ("act_bwd_bnred slab partials (2R+1W)", actbwd_slab, 3), ("torch add (2R+1W)", add, 3), ("bn_bwd_apply_acc (2R+1W)", apply, 3),
                 ("act_bwd_bnred (2R+1W)", actbwd(), 3), ("act_bwd_bnred +res (3R+1W)", actbwd(True), 4),
                 ("act_bwd_bnred +res+dy2 (4R+1W)", actbwd(True, True), 5)]
