@@ -271,3 +271,23 @@ def test_precision_16_mixed_maps_to_fp16_and_transformer_refuses_it():
     st = MM.set_compute_dtype(TM.TransformerStage(8, 32, depth=1, heads=2), torch.float16)
     with pytest.raises(TypeError, match="float16"):
         st(torch.zeros(1, 8, 8, 8))
+
+
+def test_bench_dtype_options_and_peaks():
+    """bench.py --dtype: bf16 (default), fp16 ("16-mixed": fp16 MFMA at the bf16 rate, device loss
+    scaling) and fp32 (the exact f32 MFMA peak), each priced against its own dense MFMA peak; the
+    fp16 build selects precision "16-mixed"."""
+    import sys
+
+    import bench
+
+    argv = sys.argv
+    try:
+        for dt in ("bf16", "fp16", "fp32"):
+            sys.argv = ["bench.py", "--dtype", dt]
+            assert bench.parse().dtype == dt
+    finally:
+        sys.argv = argv
+    assert bench.mfma_peak(torch.bfloat16) == bench.mfma_peak(torch.float16) == bench.BF16_MFMA_PEAK_TFLOPS
+    assert bench.mfma_peak(torch.float32) == bench.F32_MFMA_PEAK_TFLOPS
+    assert bench.DT_TAG[torch.float16] == "f16"
