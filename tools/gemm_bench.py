@@ -46,8 +46,7 @@ def main():
     hbuf = torch.randn(r, hid, **bf)
     qkv = torch.randn(r, 3 * e, **bf)
     cases = {
-        "qkv  (18432x1536x512)": lambda: D.gemm(torch.empty((r, 3 * e), **bf) if False else out_qkv, x, wq, r, 3 * e, e,
-                                                 lda=e, ldb=e, ldc=3 * e, bias=bq),
+        "qkv  (18432x1536x512)": lambda: D.gemm(out_qkv, x, wq, r, 3 * e, e, lda=e, ldb=e, ldc=3 * e, bias=bq),
         "fc1  (18432x2048x512) gelu": lambda: D.gemm(out_h, x, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=b1, act="gelu"),
         "fc2  (18432x512x2048) f32": lambda: D.gemm(out_f, hbuf, w2, r, e, hid, lda=hid, ldb=hid, ldc=e, bias=bp),
         "proj (18432x512x512) f32": lambda: D.gemm(out_f, x, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=bp),
