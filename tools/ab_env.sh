@@ -16,7 +16,7 @@ for r in $(seq 1 $R); do
     python - "$e" gpurun_out/abenv/$i.$r.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(f"{sys.argv[1]:28s} {d['value']:8.1f} vol/s  {d['ms_per_step']:7.3f} ms/step  enc fwd {d['encoder_forward']['ms']:6.3f} ms", flush=True)
+print(f"{sys.argv[1]:28s} {d['value']:8.1f} vol/s  {d['ms_per_step']:7.3f} ms/step  enc fwd {d.get('encoder_forward', {}).get('ms', float('nan')):6.3f} ms", flush=True)
 PY
   done
 done
