@@ -1388,11 +1388,21 @@ __global__ void __launch_bounds__(256) k_weight_prep_multi(const dmf_wprep_job* 
   if (J.mode == 0) {
     const int total = J.Cout * taps * J.CinP;
     const int end = min(total, unit + WPM_SPAN);
-    for (int i = unit + tid; i < end; i += 256) {
+    // all of a thread's loads issued before the first store: a rolled loop waits out one
+    // global-load latency per element
+    constexpr int PER = WPM_SPAN / 256;
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = unit + tid + k * 256;
       const int row = i / J.CinP, ci = i - row * J.CinP;  // row = co * taps + (r, s)
       const int co = row / taps, rs = row - co * taps;
-      const float v = ci < J.Cin ? J.w[((size_t)co * J.Cin + ci) * taps + rs] : 0.f;
-      wprep_store(J, i, v);
+      v[k] = (i < end && ci < J.Cin) ? J.w[((size_t)co * J.Cin + ci) * taps + rs] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = unit + tid + k * 256;
+      if (i < end) wprep_store(J, i, v[k]);
     }
     return;
   }
@@ -1410,13 +1420,21 @@ __global__ void __launch_bounds__(256) k_weight_prep_multi(const dmf_wprep_job* 
       const int rr = J.mode == 2 ? J.KH - 1 - r : r, ss = J.mode == 2 ? J.KW - 1 - s : s;
       if (ci < J.Cin) src = (ci * J.KH + rr) * J.KW + ss;
     }
-    for (int c = ty; c < 64; c += 4) {
-      const int co = co0 + c;
-      tile[tx][c] = (src >= 0 && co < J.Cout) ? J.w[(size_t)co * J.Cin * taps + src] : 0.f;
+    // constant trip counts, unrolled: the 16 loads (and stores) of a thread in flight together
+    const size_t rowlen = (size_t)J.Cin * taps;
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int co = co0 + ty + 4 * q;
+      v[q] = (src >= 0 && co < J.Cout) ? J.w[(size_t)co * rowlen + src] : 0.f;
     }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tile[tx][ty + 4 * q] = v[q];
   }
   __syncthreads();
-  for (int kk = ty; kk < 64; kk += 4) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int kk = ty + 4 * q;
     const int k = k0 + kk, co = co0 + tx;
     if (k < K && co < J.Cout) wprep_store(J, (size_t)k * J.Cout + co, tile[kk][tx]);
   }
