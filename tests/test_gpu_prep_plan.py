@@ -7,7 +7,9 @@ mapping, same rounding); (2) three bf16 training steps with the plan follow
 the unplanned steps (losses within 1e-3 relative; the BN statistics' float64
 atomics make runs differ in the last bits, so not bit for bit); (3) the per-conv
 launches disappear from the planned steps; (4) a weight changed in place by
-torch after the batched launch is re-prepared (version check)."""
+torch after the batched launch is re-prepared (version check); (5) the
+batched kernel against torch-written layouts over odd shapes, every mode and
+dtype in one launch."""
 import copy
 
 import pytest
@@ -128,3 +130,43 @@ def test_prep_plan_version_check():
     assert torch.equal(got, ref)
     assert got.data_ptr() == e.out.data_ptr()  # re-prepared into the planned buffer
     O.PREP.invalidate()
+
+
+# (Cout, Cin, CinP, KH, KW): partial 64x64 tiles on both sides, channel padding, 1x1 / 3x3 / 7x7, and a
+# weight longer than one WPREP_SPAN run
+WPREP_SHAPES = [(3, 5, 8, 7, 7), (70, 17, 24, 3, 3), (130, 64, 64, 1, 1), (64, 130, 136, 3, 3), (256, 96, 96, 3, 3)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_weight_prep_multi_layouts_vs_torch(dtype):
+    """dmf_conv_weight_prep_multi against the layouts written out with torch:
+    mode 0 [Cout][KH][KW][CinP], mode 1 [CinP][KH][KW][Cout], mode 2 the same
+    with the taps flipped (the data-gradient filter); padded channels zero.
+    Every shape and mode in ONE launch, as PrepPlan builds it; bit-exact."""
+    import ctypes
+    g = torch.Generator().manual_seed(5)
+    cases, jobs, blk = [], [], []
+    for co, ci, cinp, kh, kw in WPREP_SHAPES:
+        w = torch.randn(co, ci, kh, kw, generator=g).to(DEV)
+        wp = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cinp - ci))
+        for mode in range(3):
+            if mode == 0:
+                ref = wp.permute(0, 2, 3, 1)
+            else:
+                ref = (wp.flip(2, 3) if mode == 2 else wp).permute(1, 2, 3, 0)
+            out = torch.full((ref.numel(),), float("nan"), device=DEV).to(dtype)
+            j = len(jobs)
+            jobs.append(O._WPrepJob(w.data_ptr(), out.data_ptr(), N.dtype_code(dtype), co, ci, cinp, kh, kw, mode, 0))
+            if mode == 0:
+                blk.extend((j << 40) | s for s in range(0, co * cinp * kh * kw, O.WPREP_SPAN))
+            else:
+                blk.extend((j << 40) | t for t in range(-(-cinp * kh * kw // 64) * -(-co // 64)))
+            cases.append((w, out, ref.to(dtype).contiguous().reshape(-1), (co, ci, cinp, kh, kw, mode)))
+    arr = (O._WPrepJob * len(jobs))(*jobs)
+    jt = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(DEV)
+    bt = torch.tensor(blk, dtype=torch.int64, device=DEV)
+    assert ctypes.sizeof(O._WPrepJob) * len(jobs) == jt.numel()
+    N.call("dmf_conv_weight_prep_multi", jt.data_ptr(), bt.data_ptr(), len(blk), O._stream())
+    torch.cuda.synchronize()
+    for _, out, ref, what in cases:
+        assert torch.equal(out, ref), what
