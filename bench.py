@@ -606,8 +606,8 @@ GFLOP_PER_VOL = {"A": 155.0, "B": 458.0}
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if os.environ.get("DMF_BENCH_SHARE_GPU") != "1" and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+        # the parent never touches HIP (no device query either): each rank checks its own cuda:<rank>
+        assert not torch.cuda.is_initialized(), "bench.py parent initialised HIP before spawning ranks"
         sys.exit(spawn_ranks(args.gpus))
     rank, local_rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), \
         int(os.environ.get("WORLD_SIZE", 1))
@@ -615,7 +615,15 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} rank(s)", file=sys.stderr)
     # one process per GPU over RCCL ("nccl"). DMF_DIST_BACKEND=gloo with
     # DMF_BENCH_SHARE_GPU=1 rehearses the multi-rank control flow on a 1-GPU box.
-    dev_idx = local_rank % torch.cuda.device_count() if os.environ.get("DMF_BENCH_SHARE_GPU") == "1" else local_rank
+    ndev = torch.cuda.device_count()
+    if os.environ.get("DMF_BENCH_SHARE_GPU") == "1" and ndev > 0:
+        dev_idx = local_rank % ndev
+    else:
+        dev_idx = local_rank
+        if dev_idx >= ndev:
+            print(f"bench.py rank {rank}: cuda:{dev_idx} is not visible ({ndev} GPU(s)); "
+                  f"--gpus {args.gpus} needs one GPU per rank", file=sys.stderr, flush=True)
+            sys.exit(3)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(dev_idx)

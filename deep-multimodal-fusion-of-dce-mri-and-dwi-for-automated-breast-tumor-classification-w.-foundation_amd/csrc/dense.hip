@@ -236,10 +236,46 @@ __global__ void k_layernorm(const float* __restrict__ x, int R, int E, const flo
   if (lane == 0 && save) { save[2 * r] = mean; save[2 * r + 1] = rs; }
 }
 
-__global__ void k_layernorm_bwd(const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ save,
-                                int R, int E, const float* __restrict__ g, float* __restrict__ dx, float* dg,
-                                float* db) {
+// Blocks [0, nrb): one wave per row, dx. Blocks [nrb, ...): 64 columns each,
+// dgamma / dbeta (+)= column sums over all rows in a fixed order (4 row lanes
+// strided by 4, combined in LDS lane 0..3) -- deterministic, no atomics, one
+// launch (nn.LayerNorm's backward reduces dgamma / dbeta in a fixed order,
+// reference model_module.py:799-818).
+__global__ void __launch_bounds__(256) k_layernorm_bwd(const float* __restrict__ dy, const float* __restrict__ x,
+                                                       const float* __restrict__ save, int R, int E,
+                                                       const float* __restrict__ g, float* __restrict__ dx, float* dg,
+                                                       float* db, int nrb) {
   const int lane = threadIdx.x & 63;
+  if ((int)blockIdx.x >= nrb) {
+    __shared__ float red[2][4][64];
+    const int c = ((int)blockIdx.x - nrb) * 64 + lane, rl = threadIdx.x >> 6;
+    float ag[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < E) {
+      int r = rl;
+      for (; r + 12 < R; r += 16) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int rr = r + 4 * u;
+          const float d = dy[(size_t)rr * E + c];
+          ag[u] += d * ((x[(size_t)rr * E + c] - save[2 * rr]) * save[2 * rr + 1]);
+          ab[u] += d;
+        }
+      }
+      for (; r < R; r += 4) {
+        const float d = dy[(size_t)r * E + c];
+        ag[0] += d * ((x[(size_t)r * E + c] - save[2 * r]) * save[2 * r + 1]);
+        ab[0] += d;
+      }
+    }
+    red[0][rl][lane] = (ag[0] + ag[1]) + (ag[2] + ag[3]);
+    red[1][rl][lane] = (ab[0] + ab[1]) + (ab[2] + ab[3]);
+    __syncthreads();
+    if (rl == 0 && c < E) {
+      if (dg) dg[c] += ((red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]));
+      if (db) db[c] += ((red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]));
+    }
+    return;
+  }
   const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (r >= R) return;
   const float mean = save[2 * r], rs = save[2 * r + 1];
@@ -251,8 +287,6 @@ __global__ void k_layernorm_bwd(const float* __restrict__ dy, const float* __res
     const float gd = pd[i] * g[i];
     s1 += gd;
     s2 += gd * xh;
-    if (dg) atomicAdd(dg + i, pd[i] * xh);
-    if (db) atomicAdd(db + i, pd[i]);
   }
   s1 = wave_sum(s1) / E;
   s2 = wave_sum(s2) / E;
@@ -267,7 +301,7 @@ __global__ void k_layernorm_bwd(const float* __restrict__ dy, const float* __res
 // requires Nq,Nk <= 64, D <= 128.
 __global__ void k_attn_fwd(const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
                            const float* __restrict__ v, int ldv, int Nq, int Nk, int H, int D, float scale,
-                           float* __restrict__ o, int ldo, float* __restrict__ probs, float* __restrict__ avgw) {
+                           float* __restrict__ o, int ldo, float* __restrict__ probs) {
   __shared__ float Ks[64][129], Vs[64][129], Ps[64][65];
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const float* qb = q + (size_t)b * Nq * ldq + h * D;
@@ -300,7 +334,6 @@ __global__ void k_attn_fwd(const float* __restrict__ q, int ldq, const float* __
   for (int t = threadIdx.x; t < Nq * Nk; t += blockDim.x) {
     const int i = t / Nk, j = t % Nk;
     if (probs) probs[(((size_t)b * H + h) * Nq + i) * Nk + j] = Ps[i][j];
-    if (avgw) atomicAdd(avgw + ((size_t)b * Nq + i) * Nk + j, Ps[i][j] / H);
   }
   for (int t = threadIdx.x; t < Nq * D; t += blockDim.x) {
     const int i = t / D, d = t % D;
@@ -308,6 +341,17 @@ __global__ void k_attn_fwd(const float* __restrict__ q, int ldq, const float* __
     for (int j = 0; j < Nk; ++j) s += Ps[i][j] * Vs[j][d];
     o[((size_t)b * Nq + i) * ldo + h * D + d] = s;
   }
+}
+
+// head-averaged attention weights (nn.MultiheadAttention average_attn_weights:
+// the mean over heads of the probabilities), summed in head order
+__global__ void k_head_mean(const float* __restrict__ probs, int B, int H, int NN, float* __restrict__ avgw) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * NN) return;
+  const int b = t / NN, e = t - b * NN;
+  float s = 0.f;
+  for (int h = 0; h < H; ++h) s += probs[((size_t)b * H + h) * NN + e];
+  avgw[t] = s / (float)H;
 }
 
 __global__ void k_attn_bwd(const float* __restrict__ q, int ldq, const float* __restrict__ k, int ldk,
@@ -719,36 +763,60 @@ __global__ void k_gate_fwd(const float* __restrict__ pa, const float* __restrict
   }
 }
 
-// dz = softmax backward; dW (+)=, db (+)=, dpa/dpb/dca/dcb written (nullable)
+// dz = softmax backward; dW (+)=, db (+)=, dpa/dpb/dca/dcb written (nullable).
+// Blocks [0, B): one item each, the input gradients. Blocks [B, ...): 256
+// weight columns each, dW / db summed over the items in item order
+// (deterministic, no atomics; nn.Linear's backward, reference
+// model_module.py:745-780).
+__device__ __forceinline__ void gate_dz(const float* g, const float* dg, int n, float& dz0, float& dz1) {
+  const float g0 = g[2 * n], g1 = g[2 * n + 1];
+  const float s = dg[2 * n] * g0 + dg[2 * n + 1] * g1;
+  dz0 = g0 * (dg[2 * n] - s);
+  dz1 = g1 * (dg[2 * n + 1] - s);
+}
+
 __global__ void k_gate_bwd(const float* __restrict__ pa, const float* __restrict__ pb, const float* __restrict__ ca,
                            const float* __restrict__ cb, int C, const float* __restrict__ Wt,
                            const float* __restrict__ g, const float* __restrict__ dg, float* dW, float* db,
                            float* __restrict__ dpa, float* __restrict__ dpb, float* __restrict__ dca,
-                           float* __restrict__ dcb) {
-  const int n = blockIdx.x;
+                           float* __restrict__ dcb, int B) {
   const int In = 2 * C + (ca ? 2 : 0);
-  const float g0 = g[2 * n], g1 = g[2 * n + 1];
-  const float s = dg[2 * n] * g0 + dg[2 * n + 1] * g1;
-  const float dz0 = g0 * (dg[2 * n] - s), dz1 = g1 * (dg[2 * n + 1] - s);
-  for (int i = threadIdx.x; i < In; i += blockDim.x) {
-    float x;
-    if (i < C) x = pa[n * C + i];
-    else if (i < 2 * C) x = pb[n * C + i - C];
-    else if (i == 2 * C) x = ca[n];
-    else x = cb[n];
-    if (dW) {
-      atomicAdd(dW + i, dz0 * x);
-      atomicAdd(dW + In + i, dz1 * x);
+  if ((int)blockIdx.x >= B) {
+    const int i = ((int)blockIdx.x - B) * blockDim.x + threadIdx.x;
+    if (i < In && dW) {
+      float a0 = 0.f, a1 = 0.f;
+      for (int n = 0; n < B; ++n) {
+        float dz0, dz1;
+        gate_dz(g, dg, n, dz0, dz1);
+        const float x = i < C ? pa[n * C + i] : (i < 2 * C ? pb[n * C + i - C] : (i == 2 * C ? ca[n] : cb[n]));
+        a0 += dz0 * x;
+        a1 += dz1 * x;
+      }
+      dW[i] += a0;
+      dW[In + i] += a1;
     }
+    if (i == 0 && db) {
+      float b0 = 0.f, b1 = 0.f;
+      for (int n = 0; n < B; ++n) {
+        float dz0, dz1;
+        gate_dz(g, dg, n, dz0, dz1);
+        b0 += dz0;
+        b1 += dz1;
+      }
+      db[0] += b0;
+      db[1] += b1;
+    }
+    return;
+  }
+  const int n = blockIdx.x;
+  float dz0, dz1;
+  gate_dz(g, dg, n, dz0, dz1);
+  for (int i = threadIdx.x; i < In; i += blockDim.x) {
     const float dx = dz0 * Wt[i] + dz1 * Wt[In + i];
     if (i < C) { if (dpa) dpa[n * C + i] = dx; }
     else if (i < 2 * C) { if (dpb) dpb[n * C + i - C] = dx; }
     else if (i == 2 * C) { if (dca) dca[n] = dx; }
     else { if (dcb) dcb[n] = dx; }
-  }
-  if (threadIdx.x == 0 && db) {
-    atomicAdd(db, dz0);
-    atomicAdd(db + 1, dz1);
   }
 }
 
@@ -966,9 +1034,10 @@ extern "C" int dmf_layernorm_fwd(const float* x, int R, int E, const float* gamm
 
 extern "C" int dmf_layernorm_bwd(const float* dy, const float* x, const float* save, int R, int E, const float* gamma,
                                  float* dx, float* dgamma, float* dbeta, void* stream) {
-  DMF_CHECK_ARG(dy && x && save && gamma && dx, "dmf_layernorm_bwd: bad args");
-  hipLaunchKernelGGL(k_layernorm_bwd, dim3(cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, dy, x, save, R, E, gamma,
-                     dx, dgamma, dbeta);
+  DMF_CHECK_ARG(dy && x && save && gamma && dx && R > 0 && E > 0, "dmf_layernorm_bwd: bad args");
+  const int nrb = cdiv(R, 4), ncb = (dgamma || dbeta) ? cdiv(E, 64) : 0;
+  hipLaunchKernelGGL(k_layernorm_bwd, dim3(nrb + ncb), dim3(256), 0, (hipStream_t)stream, dy, x, save, R, E, gamma,
+                     dx, dgamma, dbeta, nrb);
   DMF_LAUNCH_CHECK("dmf_layernorm_bwd");
   return 0;
 }
@@ -978,8 +1047,12 @@ extern "C" int dmf_attn_fwd(const float* q, int ldq, const float* k, int ldk, co
                             void* stream) {
   DMF_CHECK_ARG(q && k && v && out && Nq <= 64 && Nk <= 64 && D <= 128,
                 "dmf_attn_fwd: short-sequence kernel needs Nq,Nk<=64, D<=128 (got %d,%d,%d)", Nq, Nk, D);
+  DMF_CHECK_ARG(!avg_weights || probs, "dmf_attn_fwd: avg_weights needs the probs buffer");
   hipLaunchKernelGGL(k_attn_fwd, dim3(B * H), dim3(256), 0, (hipStream_t)stream, q, ldq, k, ldk, v, ldv, Nq, Nk, H, D,
-                     scale, out, ldo, probs, avg_weights);
+                     scale, out, ldo, probs);
+  if (avg_weights)
+    hipLaunchKernelGGL(k_head_mean, dim3(cdiv((long long)B * Nq * Nk, 256)), dim3(256), 0, (hipStream_t)stream, probs,
+                       B, H, Nq * Nk, avg_weights);
   DMF_LAUNCH_CHECK("dmf_attn_fwd");
   return 0;
 }
@@ -1094,8 +1167,10 @@ extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const floa
                             float* db, float* dpv_dwi, float* dpv_dce, float* dconf_dwi, float* dconf_dce,
                             void* stream) {
   DMF_CHECK_ARG(pv_dwi && pv_dce && W && gates && dgates, "dmf_gate_bwd: bad args");
-  hipLaunchKernelGGL(k_gate_bwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pv_dwi, pv_dce, conf_dwi, conf_dce, C, W,
-                     gates, dgates, dW, db, dpv_dwi, dpv_dce, dconf_dwi, dconf_dce);
+  const int In = 2 * C + (conf_dwi ? 2 : 0);
+  const int ncb = (dW || db) ? cdiv(In, 256) : 0;
+  hipLaunchKernelGGL(k_gate_bwd, dim3(B + ncb), dim3(256), 0, (hipStream_t)stream, pv_dwi, pv_dce, conf_dwi, conf_dce,
+                     C, W, gates, dgates, dW, db, dpv_dwi, dpv_dce, dconf_dwi, dconf_dce, B);
   DMF_LAUNCH_CHECK("dmf_gate_bwd");
   return 0;
 }

@@ -14,7 +14,7 @@ namespace dmf {
 template <typename T>
 __global__ void k_mix_bwd(const T* __restrict__ dz, int lddz, const T* __restrict__ a, int lda,
                           const T* __restrict__ b, int ldb, const float* __restrict__ wlogit, T* __restrict__ da,
-                          T* __restrict__ db, int ldd, float* __restrict__ dw, long long M, int C) {
+                          T* __restrict__ db, int ldd, float* __restrict__ part, long long M, int C) {
   __shared__ float red[16];
   const float al = 1.f / (1.f + __expf(-wlogit[0]));
   float acc = 0.f;
@@ -30,7 +30,7 @@ __global__ void k_mix_bwd(const T* __restrict__ dz, int lddz, const T* __restric
     acc += g * (av - bv);
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) atomicAdd(dw, acc * al * (1.f - al));
+  if (threadIdx.x == 0) part[blockIdx.x] = acc * al * (1.f - al);
 }
 
 // 8-channel vector form (16-B accesses, 32-bit index math): the scalar form's
@@ -39,7 +39,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_mix_bwd8(const T* __restrict__ dz, int lddz, const T* __restrict__ a,
                                                   int lda, const T* __restrict__ b, int ldb,
                                                   const float* __restrict__ wlogit, T* __restrict__ da,
-                                                  T* __restrict__ db, int ldd, float* __restrict__ dw, int M, int C) {
+                                                  T* __restrict__ db, int ldd, float* __restrict__ part, int M, int C) {
   __shared__ float red[16];
   const float al = 1.f / (1.f + __expf(-wlogit[0]));
   const int CV = C >> 3;
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) k_mix_bwd8(const T* __restrict__ dz, int 
     st8(db + (size_t)m * ldd + cv * 8, o2);
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) atomicAdd(dw, acc * al * (1.f - al));
+  if (threadIdx.x == 0) part[blockIdx.x] = acc * al * (1.f - al);
 }
 
 struct MaskAttnB {
@@ -94,7 +94,7 @@ template <typename T>
 __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* __restrict__ f, int ldf,
                                  const T* __restrict__ m, MaskAttnB P, const float* __restrict__ stats, int HW, int C,
                                  T* __restrict__ df, int lddf, float* __restrict__ dhh, float* __restrict__ S,
-                                 float* __restrict__ grads) {
+                                 float* __restrict__ slab) {
   __shared__ float sacc[4][64];  // per-wave accumulators for lanes < hid: [gn_w, gn_b, w2] + [db2, dgamma, S1, S2]
   __shared__ float sw[4][8];
   const int n = blockIdx.x;
@@ -155,20 +155,22 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
       a_s2 += dh * hh;
     }
   }
-  // reduce over the 4 waves
+  // reduce over the 4 waves into this block's slab row (grads layout; summed over the rows in
+  // row order after pass 2: deterministic, no atomics)
+  float* row = slab + ((size_t)n * gridDim.y + blockIdx.y) * (4 * P.hid + 2);
   a_s1 = wave_sum(a_s1);
   a_s2 = wave_sum(a_s2);
   sacc[wid][lane] = a_gw;
   __syncthreads();
-  if (wid == 0 && lane < P.hid) atomicAdd(grads + P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  if (wid == 0 && lane < P.hid) row[P.hid + lane] = (sacc[0][lane] + sacc[1][lane]) + (sacc[2][lane] + sacc[3][lane]);
   __syncthreads();
   sacc[wid][lane] = a_gb;
   __syncthreads();
-  if (wid == 0 && lane < P.hid) atomicAdd(grads + 2 * P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  if (wid == 0 && lane < P.hid) row[2 * P.hid + lane] = (sacc[0][lane] + sacc[1][lane]) + (sacc[2][lane] + sacc[3][lane]);
   __syncthreads();
   sacc[wid][lane] = a_w2;
   __syncthreads();
-  if (wid == 0 && lane < P.hid) atomicAdd(grads + 3 * P.hid + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  if (wid == 0 && lane < P.hid) row[3 * P.hid + lane] = (sacc[0][lane] + sacc[1][lane]) + (sacc[2][lane] + sacc[3][lane]);
   if (lane == 0) {
     sw[wid][0] = a_db2;
     sw[wid][1] = a_dgam;
@@ -180,8 +182,8 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
     float t[4] = {0.f, 0.f, 0.f, 0.f};
     for (int w = 0; w < 4; ++w)
       for (int k = 0; k < 4; ++k) t[k] += sw[w][k];
-    atomicAdd(grads + 4 * P.hid, t[0]);
-    atomicAdd(grads + 4 * P.hid + 1, t[1]);
+    row[4 * P.hid] = t[0];
+    row[4 * P.hid + 1] = t[1];
     S[2 * ((size_t)n * gridDim.y + blockIdx.y)] = t[2];
     S[2 * ((size_t)n * gridDim.y + blockIdx.y) + 1] = t[3];
   }
@@ -191,7 +193,7 @@ __global__ void k_mask_attn_bwd1(const T* __restrict__ dout, int lddo, const T* 
 template <typename T>
 __global__ void k_mask_attn_bwd2(const T* __restrict__ m, MaskAttnB P, const float* __restrict__ stats, int HW,
                                  const float* __restrict__ dhh, const float* __restrict__ S, T* __restrict__ dm,
-                                 float* __restrict__ grads) {
+                                 float* __restrict__ slab) {
   __shared__ float sacc[4][64];
   const int n = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -222,7 +224,9 @@ __global__ void k_mask_attn_bwd2(const T* __restrict__ m, MaskAttnB P, const flo
   }
   sacc[wid][lane] = a_w1;
   __syncthreads();
-  if (wid == 0 && lane < P.hid) atomicAdd(grads + lane, sacc[0][lane] + sacc[1][lane] + sacc[2][lane] + sacc[3][lane]);
+  if (wid == 0 && lane < P.hid)
+    slab[((size_t)n * gridDim.y + blockIdx.y) * (4 * P.hid + 2) + lane] =
+        (sacc[0][lane] + sacc[1][lane]) + (sacc[2][lane] + sacc[3][lane]);
 }
 
 }  // namespace dmf
@@ -231,8 +235,8 @@ using namespace dmf;
 
 extern "C" int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, const void* b, int ldb,
                            const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C,
-                           void* stream) {
-  DMF_CHECK_ARG(dz && a && b && wlogit && da && db && dw, "dmf_mix_bwd: bad args");
+                           float* ws, void* stream) {
+  DMF_CHECK_ARG(dz && a && b && wlogit && da && db && dw && ws && M > 0 && C > 0, "dmf_mix_bwd: bad args");
   const int es = is16(dtype) ? 2 : 4;
   if (C % 8 == 0 && lddz % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldd % 8 == 0 && M * std::max(ldd, lddz) < (1LL << 31) &&
       ((uintptr_t)dz | (uintptr_t)a | (uintptr_t)b | (uintptr_t)da | (uintptr_t)db) % (8 * es) == 0) {
@@ -240,23 +244,24 @@ extern "C" int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, i
     if (g8 > 2048) g8 = 2048;
     if (g8 < 1) g8 = 1;
     DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix_bwd8<T>, dim3((unsigned)g8), dim3(256), 0, (hipStream_t)stream, (const T*)dz,
-                         lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, dw,
+                         lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, ws,
                          (int)M, C));
     DMF_LAUNCH_CHECK("dmf_mix_bwd");
-    return 0;
+    return dmf_colsum_f32(ws, 1, (int)g8, 1, dw, 1, stream);  // dw += the block partials in block order
   }
   long long g = (M * C + 255) / 256;
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix_bwd<T>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (const T*)dz,
-                       lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, dw,
+                       lddz, (const T*)a, lda, (const T*)b, ldb, wlogit, (T*)da, (T*)db, ldd, ws,
                        M, C));
   DMF_LAUNCH_CHECK("dmf_mix_bwd");
-  return 0;
+  return dmf_colsum_f32(ws, 1, (int)g, 1, dw, 1, stream);
 }
 
 extern "C" int dmf_mask_attn_bwd_ws_size(int N, int HW, int hidden) {
-  return (int)((long long)N * HW * hidden + 2LL * N * cdiv(HW, MA_PIX));
+  const long long rows = (long long)N * cdiv(HW, MA_PIX);
+  return (int)((long long)N * HW * hidden + 2LL * rows + rows * (4LL * hidden + 2));
 }
 
 extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int ldf, const void* m, int N,
@@ -268,13 +273,16 @@ extern "C" int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const vo
                 "dmf_mask_attn_bwd: bad args");
   MaskAttnB P{w1, gn_w, gn_b, w2, b2, gamma, eps, hidden};
   float* dhh = workspace;
+  const int rows = N * cdiv(HW, MA_PIX);
   float* S = workspace + (size_t)N * HW * hidden;
+  float* slab = S + 2 * (size_t)rows;  // [rows][4 * hidden + 2] per-block parameter-gradient partials
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(N, cdiv(HW, MA_PIX));
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mask_attn_bwd1<T>, grid, dim3(256), 0, s, (const T*)dout, lddo, (const T*)f,
-                       ldf, (const T*)m, P, stats, HW, C, (T*)df, lddf, dhh, S, grads);
+                       ldf, (const T*)m, P, stats, HW, C, (T*)df, lddf, dhh, S, slab);
     hipLaunchKernelGGL(k_mask_attn_bwd2<T>, grid, dim3(256), 0, s, (const T*)m, P, stats, HW, dhh, S,
-                       (T*)dm, grads));
+                       (T*)dm, slab));
   DMF_LAUNCH_CHECK("dmf_mask_attn_bwd");
-  return 0;
+  // grads (+)= the slab's column sums in row order
+  return dmf_colsum_f32(slab, 4 * hidden + 2, rows, 4 * hidden + 2, grads, 1, stream);
 }

@@ -7,7 +7,8 @@
 //   aux[m][n] = IT(t)                                    (optional: pre-activation kept for backward)
 //   forward epilogue : t = dropout(act(t))
 //   gradient epilogue: t = dropout_mask(t) * act'(pre[m][n])   (when `pre` is given)
-//   t *= colscale[n]; t += res[m][n]; C[m][n] = t; dbias[n] += t (column sums, atomics)
+//   t *= colscale[n]; t += res[m][n]; C[m][n] = t; dbias[n] += t (column sums: per-tile slab rows, then
+//   an ordered sum over the tiles)
 //   op(A)[m][k] = TA ? A[k*lda + m] : A[m*lda + k]
 //   op(B)[k][n] = TB ? B[k*ldb + n] : B[n*ldb + k]      ("NT": weights [N][K])
 //   batch z = z1*H + z2 (blockIdx.z), element offsets z1*s1 + z2*s2 per operand
@@ -54,6 +55,7 @@ struct GemmArgs {
   const unsigned long long* rng;
   int site;
   float* dbias;              // column sums of the final t (accumulated) or null
+  float* dbias_ws;           // [M tiles][N] per-tile column sums (dbias: summed in tile order after the launch)
 };
 
 constexpr int GBM = 128, GBN = 128, GTHREADS = 256;   // k per step: 128 bytes of IT
@@ -267,7 +269,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, float* Cs, int 
     default: gemm_epilogue_act<IT, OutT, BM, BN, NTH, DMF_ACT_NONE>(g, Cs, tid, m0, n0, z, csum); break;
   }
   if (g.dbias) {
-    // threads sharing a chunk column: tid % CPR; reduce through LDS, one atomic per column
+    // threads sharing a chunk column: tid % CPR; reduce through LDS into this M tile's slab row
+    // (dbias = the slab's column sums in tile order, after the launch: deterministic)
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < EPC; ++e) Cs[tid * EPC + e] = csum[e];
@@ -276,7 +279,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, float* Cs, int 
       const int c = tid, cc = c / EPC, ce = c % EPC;
       float s = 0.f;
       for (int t = cc; t < NTH; t += CPR) s += Cs[t * EPC + ce];
-      if (n0 + c < g.N) atomicAdd(g.dbias + n0 + c, s);
+      if (n0 + c < g.N) g.dbias_ws[(size_t)(m0 / BM) * g.N + n0 + c] = s;
     }
   }
 }
@@ -490,7 +493,7 @@ static int gemm_launch(const char* name, int out_dtype, int ta, int tb, int M, i
                        long long sB2, void* C, int ldc, long long sC1, long long sC2, int batch1, int batch2,
                        const float* bias, int act, const float* colscale, const float* res, int ldr, void* aux,
                        int ldaux, const void* pre, int ldpre, float dropout_p, const unsigned long long* rng,
-                       int site, float* dbias, void* stream) {
+                       int site, float* dbias, float* dbias_ws, void* stream) {
   constexpr int ie = 16 / sizeof(IT);  // operand elements per 16 bytes
   DMF_CHECK_ARG(out_dtype == DMF_F32 || out_dtype == DMF_BF16, "%s: bad out dtype %d", name, out_dtype);
   DMF_CHECK_ARG(M > 0 && N > 0 && K > 0 && batch1 > 0 && batch2 > 0, "%s: empty problem", name);
@@ -509,9 +512,11 @@ static int gemm_launch(const char* name, int out_dtype, int ta, int tb, int M, i
   DMF_CHECK_ARG(!aux || (ldaux % 4 == 0 && ((uintptr_t)aux % (4 * sizeof(IT))) == 0),
                 "%s: aux rows must hold whole, aligned groups of 4", name);
   DMF_CHECK_ARG(dropout_p <= 0.f || (rng && dropout_p < 1.f), "%s: dropout needs rng state and p < 1", name);
+  DMF_CHECK_ARG(!dbias || (dbias_ws && batch1 * batch2 == 1), "%s: dbias needs an unbatched problem and its "
+                "workspace (cdiv(M, 128) * N floats)", name);
   GemmArgs g{A, B, C, bias, M, N, K, lda, ldb, ldc, batch2,
              sA1, sA2, sB1, sB2, sC1, sC2, alpha, act, cdiv(N, GBN), colscale, res, ldr, aux, ldaux,
-             pre, ldpre, dropout_p, rng, site, dbias};
+             pre, ldpre, dropout_p, rng, site, dbias, dbias_ws};
   const dim3 grid((unsigned)(cdiv(M, GBM) * g.ntiles), 1, (unsigned)(batch1 * batch2));
   DMF_CHECK_ARG((long long)cdiv(M, GBM) * g.ntiles < (1LL << 31) && batch1 * batch2 < 65536, "%s: grid too large",
                 name);
@@ -531,6 +536,7 @@ static int gemm_launch(const char* name, int out_dtype, int ta, int tb, int M, i
   }
 #undef DMF_G
   DMF_LAUNCH_CHECK(name);
+  if (dbias) return dmf_colsum_f32(dbias_ws, N, cdiv(M, GBM), N, dbias, 1, stream);
   return 0;
 }
 
@@ -539,10 +545,10 @@ extern "C" int dmf_gemm_bf16(int out_dtype, int ta, int tb, int M, int N, int K,
                              void* C, int ldc, long long sC1, long long sC2, int batch1, int batch2,
                              const float* bias, int act, const float* colscale, const float* res, int ldr, void* aux,
                              int ldaux, const void* pre, int ldpre, float dropout_p,
-                             const unsigned long long* rng, int site, float* dbias, void* stream) {
+                             const unsigned long long* rng, int site, float* dbias, float* dbias_ws, void* stream) {
   return gemm_launch<bf16_t>("dmf_gemm_bf16", out_dtype, ta, tb, M, N, K, alpha, A, lda, sA1, sA2, B, ldb, sB1, sB2,
                              C, ldc, sC1, sC2, batch1, batch2, bias, act, colscale, res, ldr, aux, ldaux, pre, ldpre,
-                             dropout_p, rng, site, dbias, stream);
+                             dropout_p, rng, site, dbias, dbias_ws, stream);
 }
 
 extern "C" int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda,
@@ -550,10 +556,10 @@ extern "C" int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, 
                             void* C, int ldc, long long sC1, long long sC2, int batch1, int batch2,
                             const float* bias, int act, const float* colscale, const float* res, int ldr, float* aux,
                             int ldaux, const float* pre, int ldpre, float dropout_p,
-                            const unsigned long long* rng, int site, float* dbias, void* stream) {
+                            const unsigned long long* rng, int site, float* dbias, float* dbias_ws, void* stream) {
   return gemm_launch<float>("dmf_gemm_f32", out_dtype, ta, tb, M, N, K, alpha, A, lda, sA1, sA2, B, ldb, sB1, sB2,
                             C, ldc, sC1, sC2, batch1, batch2, bias, act, colscale, res, ldr, aux, ldaux, pre, ldpre,
-                            dropout_p, rng, site, dbias, stream);
+                            dropout_p, rng, site, dbias, dbias_ws, stream);
 }
 
 template <typename PT>

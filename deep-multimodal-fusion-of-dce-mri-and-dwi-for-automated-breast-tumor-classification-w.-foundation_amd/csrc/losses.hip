@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(256) k_recon_finish(ReconArgs a, const float* 
 template <typename T>
 __global__ void k_mimic(const T* __restrict__ sbase, const T* __restrict__ tbase, long long sstride,
                         long long tstride, int ldm, int HW, int C, int npairs, float eps_norm, float eps_clamp,
-                        float* __restrict__ loss, T* __restrict__ dstudent, long long dstride) {
+                        float* __restrict__ part, T* __restrict__ dstudent, long long dstride) {
   // block per (pair, channel)
   __shared__ float red[16];
   const int pr = blockIdx.x / C, c = blockIdx.x % C;
@@ -535,7 +535,7 @@ __global__ void k_mimic(const T* __restrict__ sbase, const T* __restrict__ tbase
   const float ns = fmaxf(sqrtf(ss), eps_norm), nt = fmaxf(sqrtf(tt), eps_norm);
   const float cos = st_ / (ns * nt);
   const float lo = -1.f + eps_clamp, hi = 1.f - eps_clamp;
-  if (threadIdx.x == 0) atomicAdd(loss, (1.f - fminf(fmaxf(cos, lo), hi)) / (float)(C * npairs));
+  if (threadIdx.x == 0) part[blockIdx.x] = (1.f - fminf(fmaxf(cos, lo), hi)) / (float)(C * npairs);
   if (dstudent) {
     const bool pass = cos >= lo && cos <= hi;
     const float scale = -1.f / (float)(C * npairs);
@@ -732,13 +732,13 @@ extern "C" int dmf_recon_loss(int dtype, int nterms, const void* r0, const void*
 
 extern "C" int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long long sstride,
                               long long tstride, int ld, int HW, int C, int npairs, float* loss, void* dstudent,
-                              long long dstride, void* stream) {
-  DMF_CHECK_ARG(student && teacher && loss && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
+                              long long dstride, float* ws, void* stream) {
+  DMF_CHECK_ARG(student && teacher && loss && ws && npairs >= 1 && C > 0 && HW > 0, "dmf_mimic_loss: bad args");
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mimic<T>, dim3(npairs * C), dim3(256), 0, (hipStream_t)stream, (const T*)student,
-                       (const T*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, loss,
+                       (const T*)teacher, sstride, tstride, ld, HW, C, npairs, 1e-12f, 1e-6f, ws,
                        (T*)dstudent, dstride));
   DMF_LAUNCH_CHECK("dmf_mimic_loss");
-  return 0;
+  return dmf_colsum_f32(ws, 1, npairs * C, 1, loss, 1, stream);  // the terms in (pair, channel) order
 }
 
 extern "C" int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream) {

@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(256) k_ln_fwd(const TX* __restrict__ x, int ld
   if (lane == 0 && save) { save[2 * r] = mean; save[2 * r + 1] = rs; }
 }
 
-// block-reduce per-lane column partials acc[j] (4 waves) and add them to out[] atomically
+// block-reduce per-lane column partials acc[j] (4 waves) into this block's slab row (the
+// launcher then sums the slab rows in block order: deterministic, no atomics)
 __device__ __forceinline__ void tk_col_flush(float* red, const float4 (&acc)[TK_JMAX], int nj, float* out) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int E = nj * 256;
@@ -79,19 +80,18 @@ __device__ __forceinline__ void tk_col_flush(float* red, const float4 (&acc)[TK_
     if (j < nj) *(float4*)(red + wid * E + j * 256 + lane * 4) = acc[j];
   __syncthreads();
   for (int c = threadIdx.x; c < E; c += 256) {
-    const float s = red[c] + red[E + c] + red[2 * E + c] + red[3 * E + c];
-    atomicAdd(out + c, s);
+    out[c] = (red[c] + red[E + c]) + (red[2 * E + c] + red[3 * E + c]);
   }
   __syncthreads();
 }
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) (+ dres);
-// dgamma += sum dy*xhat, dbeta += sum dy (column reductions, one atomic per column per block)
+// dgamma += sum dy*xhat, dbeta += sum dy (column reductions: one slab row per block, slab0 / slab1)
 template <typename TX>
 __global__ void __launch_bounds__(256) k_ln_bwd(const float* __restrict__ dy, const TX* __restrict__ x, int ldx,
                                                 const float* __restrict__ save, long long R, int E,
                                                 const float* __restrict__ g, const float* dres, float* dx,
-                                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                float* __restrict__ slab0, float* __restrict__ slab1) {
   extern __shared__ float red[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nj = E >> 8;
@@ -133,8 +133,8 @@ __global__ void __launch_bounds__(256) k_ln_bwd(const float* __restrict__ dy, co
         *(float4*)(dx + r * E + c) = o;
       }
   }
-  if (dgamma) tk_col_flush(red, ag, nj, dgamma);
-  if (dbeta) tk_col_flush(red, ab, nj, dbeta);
+  if (slab0) tk_col_flush(red, ag, nj, slab0 + (size_t)blockIdx.x * E);
+  if (slab1) tk_col_flush(red, ab, nj, slab1 + (size_t)blockIdx.x * E);
 }
 
 // Branch backward of out = res + drop(y) * gamma, given gout = d out (f32):
@@ -144,8 +144,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ gout, const T* __restrict__ yaux,
                                                     long long R, int E, const float* __restrict__ gamma, float p,
                                                     const unsigned long long* rng, int site,
-                                                    T* __restrict__ dy, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbias) {
+                                                    T* __restrict__ dy, float* __restrict__ slab0,
+                                                    float* __restrict__ slab1) {
   extern __shared__ float red[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nj = E >> 8;
@@ -180,11 +180,12 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
         tk_st4(dy + r * E + c, make_float4(d0, d1, d2, d3));
       }
   }
-  if (dgamma) tk_col_flush(red, ag, nj, dgamma);
-  if (dbias) tk_col_flush(red, ab, nj, dbias);
+  if (slab0) tk_col_flush(red, ag, nj, slab0 + (size_t)blockIdx.x * E);
+  if (slab1) tk_col_flush(red, ab, nj, slab1 + (size_t)blockIdx.x * E);
 }
 
-// out[c] += sum_r X[r][c] (bf16 X, C % 8 == 0); block = 256 column chunks of 8 x 64 rows
+// slab[r / 64][c] = sum over the 64-row band of X[r][c] (bf16 X, C % 8 == 0); block = 256 column
+// chunks of 8 x 64 rows; the launcher sums the bands in order
 __device__ __forceinline__ void tk_ld8(const bf16_t* p, float* v) { ld8(p, v); }
 __device__ __forceinline__ void tk_ld8(const float* p, float* v) {
   const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
@@ -205,7 +206,7 @@ __global__ void __launch_bounds__(256) k_tok_colsum(const T* __restrict__ X, int
     for (int e = 0; e < 8; ++e) s[e] += v[e];
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) atomicAdd(out + c + e, s[e]);
+  for (int e = 0; e < 8; ++e) out[(size_t)blockIdx.y * C + c + e] = s[e];
 }
 
 __global__ void __launch_bounds__(256) k_cast_bf16(const float* __restrict__ x, long long n, bf16_t* __restrict__ y) {
@@ -259,68 +260,90 @@ extern "C" int dmf_tok_layernorm_fwd(int x_dtype, const void* x, int ldx, long l
   return 0;
 }
 
+extern "C" long long dmf_tok_bwd_ws_floats(long long R, int E) {
+  return 2 * ((R + TK_ROWS - 1) / TK_ROWS) * (long long)E;
+}
+
+// the two column-sum slabs -> out0 / out1 (accumulated), rows in block order
+static int tk_slab_sums(const float* ws, long long nblk, int E, float* out0, float* out1, void* stream) {
+  DMF_CHECK_ARG(nblk < (1LL << 31), "token backward: too many row blocks");
+  if (out0 && dmf_colsum_f32(ws, E, (int)nblk, E, out0, 1, stream)) return -2;
+  if (out1 && dmf_colsum_f32(ws + nblk * E, E, (int)nblk, E, out1, 1, stream)) return -2;
+  return 0;
+}
+
 extern "C" int dmf_tok_layernorm_bwd(const float* dy, int x_dtype, const void* x, int ldx, const float* save,
                                      long long R, int E, const float* gamma, const float* dres, float* dx,
-                                     float* dgamma, float* dbeta, void* stream) {
-  DMF_CHECK_ARG(dy && x && save && gamma && dx && R >= 0, "dmf_tok_layernorm_bwd: bad args");
+                                     float* dgamma, float* dbeta, float* ws, void* stream) {
+  DMF_CHECK_ARG(dy && x && save && gamma && dx && R >= 0 && (ws || !(dgamma || dbeta)),
+                "dmf_tok_layernorm_bwd: bad args");
   DMF_CHECK_ARG(tk_width_ok(E) && ldx % 4 == 0, "dmf_tok_layernorm_bwd: E (%d) must be a multiple of 256, <= %d", E,
                 256 * TK_JMAX);
   DMF_CHECK_ARG(x_dtype == DMF_F32 || x_dtype == DMF_BF16, "dmf_tok_layernorm_bwd: bad dtype");
   if (R == 0) return 0;
-  const dim3 grid((unsigned)((R + TK_ROWS - 1) / TK_ROWS)), blk(256);
+  const long long nblk = (R + TK_ROWS - 1) / TK_ROWS;
+  const dim3 grid((unsigned)nblk), blk(256);
+  float* s0 = dgamma ? ws : nullptr;
+  float* s1 = dbeta ? ws + nblk * E : nullptr;
   if (x_dtype == DMF_F32)
     hipLaunchKernelGGL(k_ln_bwd<float>, grid, blk, 4 * E * sizeof(float), (hipStream_t)stream, dy, (const float*)x,
-                       ldx, save, R, E, gamma, dres, dx, dgamma, dbeta);
+                       ldx, save, R, E, gamma, dres, dx, s0, s1);
   else
     hipLaunchKernelGGL(k_ln_bwd<bf16_t>, grid, blk, 4 * E * sizeof(float), (hipStream_t)stream, dy,
-                       (const bf16_t*)x, ldx, save, R, E, gamma, dres, dx, dgamma, dbeta);
+                       (const bf16_t*)x, ldx, save, R, E, gamma, dres, dx, s0, s1);
   DMF_LAUNCH_CHECK("dmf_tok_layernorm_bwd");
-  return 0;
+  return tk_slab_sums(ws, nblk, E, dgamma, dbeta, stream);
 }
 
 template <typename T>
 static int lsdrop_launch(const char* name, const float* gout, const void* yaux, long long R, int E,
                          const float* gamma, float dropout_p, const unsigned long long* rng, int site, void* dy,
-                         float* dgamma, float* dbias, void* stream) {
-  DMF_CHECK_ARG(gout && yaux && gamma && dy && R >= 0, "%s: bad args", name);
+                         float* dgamma, float* dbias, float* ws, void* stream) {
+  DMF_CHECK_ARG(gout && yaux && gamma && dy && R >= 0 && (ws || !(dgamma || dbias)), "%s: bad args", name);
   DMF_CHECK_ARG(tk_width_ok(E), "%s: E (%d) must be a multiple of 256, <= %d", name, E, 256 * TK_JMAX);
   DMF_CHECK_ARG(dropout_p <= 0.f || (rng && dropout_p < 1.f), "%s: dropout needs rng, p < 1", name);
   if (R == 0) return 0;
-  hipLaunchKernelGGL(k_lsdrop_bwd<T>, dim3((unsigned)((R + TK_ROWS - 1) / TK_ROWS)), dim3(256),
+  const long long nblk = (R + TK_ROWS - 1) / TK_ROWS;
+  hipLaunchKernelGGL(k_lsdrop_bwd<T>, dim3((unsigned)nblk), dim3(256),
                      4 * E * sizeof(float), (hipStream_t)stream, gout, (const T*)yaux, R, E, gamma, dropout_p, rng,
-                     site, (T*)dy, dgamma, dbias);
+                     site, (T*)dy, dgamma ? ws : nullptr, dbias ? ws + nblk * E : nullptr);
   DMF_LAUNCH_CHECK(name);
-  return 0;
+  return tk_slab_sums(ws, nblk, E, dgamma, dbias, stream);
 }
 
 extern "C" int dmf_tok_scale_dropout_bwd(const float* gout, const void* yaux, long long R, int E, const float* gamma,
                                          float dropout_p, const unsigned long long* rng, int site, void* dy,
-                                         float* dgamma, float* dbias, void* stream) {
+                                         float* dgamma, float* dbias, float* ws, void* stream) {
   return lsdrop_launch<bf16_t>("dmf_tok_scale_dropout_bwd", gout, yaux, R, E, gamma, dropout_p, rng, site, dy, dgamma,
-                               dbias, stream);
+                               dbias, ws, stream);
 }
 
 extern "C" int dmf_tok_scale_dropout_bwd_f32(const float* gout, const float* yaux, long long R, int E,
                                              const float* gamma, float dropout_p, const unsigned long long* rng,
-                                             int site, float* dy, float* dgamma, float* dbias, void* stream) {
+                                             int site, float* dy, float* dgamma, float* dbias, float* ws,
+                                             void* stream) {
   return lsdrop_launch<float>("dmf_tok_scale_dropout_bwd_f32", gout, yaux, R, E, gamma, dropout_p, rng, site, dy,
-                              dgamma, dbias, stream);
+                              dgamma, dbias, ws, stream);
 }
 
 template <typename T>
-static int colsum_launch(const char* name, const void* X, int ldx, long long R, int C, float* out, void* stream) {
-  DMF_CHECK_ARG(X && out && R >= 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X % 16) == 0,
+static int colsum_launch(const char* name, const void* X, int ldx, long long R, int C, float* out, float* ws,
+                         void* stream) {
+  DMF_CHECK_ARG(X && out && ws && R >= 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X % 16) == 0,
                 "%s: bad args (C=%d ldx=%d)", name, C, ldx);
   if (R == 0 || C == 0) return 0;
   DMF_CHECK_ARG((R + 63) / 64 < 65536, "%s: too many rows", name);
-  hipLaunchKernelGGL(k_tok_colsum<T>, dim3((unsigned)cdiv(C / 8, 256), (unsigned)((R + 63) / 64)), dim3(256), 0,
-                     (hipStream_t)stream, (const T*)X, ldx, R, C, out);
+  const int bands = (int)((R + 63) / 64);
+  hipLaunchKernelGGL(k_tok_colsum<T>, dim3((unsigned)cdiv(C / 8, 256), (unsigned)bands), dim3(256), 0,
+                     (hipStream_t)stream, (const T*)X, ldx, R, C, ws);
   DMF_LAUNCH_CHECK(name);
-  return 0;
+  return dmf_colsum_f32(ws, C, bands, C, out, 1, stream);  // the 64-row bands in order
 }
 
-extern "C" int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, void* stream) {
-  return colsum_launch<bf16_t>("dmf_colsum_bf16", X, ldx, R, C, out, stream);
+extern "C" long long dmf_colsum_bf16_ws_floats(long long R, int C) { return ((R + 63) / 64) * (long long)C; }
+
+extern "C" int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, float* ws, void* stream) {
+  return colsum_launch<bf16_t>("dmf_colsum_bf16", X, ldx, R, C, out, ws, stream);
 }
 
 extern "C" int dmf_cast_bf16(const float* x, long long n, void* y, void* stream) {

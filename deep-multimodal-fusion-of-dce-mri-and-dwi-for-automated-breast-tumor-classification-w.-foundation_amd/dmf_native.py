@@ -67,13 +67,25 @@ def _signatures():
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     sigs = {}
-    for m in re.finditer(r"\b(?:int|const char\*)\s+(dmf_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
-        name, params = m.group(1), m.group(2).strip()
+    for m in re.finditer(r"\b(int|long long|const char\*)\s+(dmf_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        ret, name, params = m.group(1), m.group(2), m.group(3).strip()
+        if ret == "long long":
+            _RESTYPES[name] = L
         if params in ("", "void"):
             sigs[name] = []
         else:
             sigs[name] = [_ctype_of(p) for p in params.split(",")]
     return sigs
+
+
+def _header_constants():
+    """Integer ``#define DMF_*`` constants of include/dmf_hip.h (workspace sizes and the like)."""
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    return {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define\s+(DMF_[A-Z0-9_]+)\s+(0x[0-9a-fA-F]+|\d+)\s", src)}
+
+
+globals().update(_header_constants())
 
 
 def declared_symbols():

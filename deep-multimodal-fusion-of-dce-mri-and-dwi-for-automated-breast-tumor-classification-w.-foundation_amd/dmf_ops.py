@@ -1507,9 +1507,10 @@ class _GNMixFn(torch.autograd.Function):
             da = empty_nhwc(n, c, h, w, z.dtype, dev)
             db_ = empty_nhwc(n, c, h, w, z.dtype, dev)
             dw = torch.zeros(1, dtype=torch.float32, device=dev)
+            ws = torch.empty(N.DMF_MIX_BWD_WS, dtype=torch.float32, device=dev)
             N.call("dmf_mix_bwd", dt(z), dz.data_ptr(), nhwc(dz)[4], a.data_ptr(), nhwc(a)[4], b.data_ptr(),
                    nhwc(b)[4], wlogit.data_ptr(), da.data_ptr(), db_.data_ptr(), nhwc(da)[4], dw.data_ptr(),
-                   n * h * w, c, _stream())
+                   n * h * w, c, ws.data_ptr(), _stream())
             dw = dw.view_as(wlogit)
         return da, db_, dw, dgamma, dbeta, None
 
@@ -1804,7 +1805,7 @@ class _AttnCoreFn(torch.autograd.Function):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         o = torch.empty((b, nq, e), dtype=torch.float32, device=q.device)
         probs = torch.empty((b, heads, nq, nk), dtype=torch.float32, device=q.device)
-        avgw = torch.zeros((b, nq, nk), dtype=torch.float32, device=q.device)
+        avgw = torch.empty((b, nq, nk), dtype=torch.float32, device=q.device)
         N.call("dmf_attn_fwd", q.data_ptr(), e, k.data_ptr(), e, v.data_ptr(), e, b, nq, nk, heads, d, scale,
                o.data_ptr(), e, probs.data_ptr(), avgw.data_ptr(), _stream())
         ctx.save_for_backward(q, k, v, probs)
@@ -1894,7 +1895,7 @@ class _CrossAttnFn(torch.autograd.Function):
         scale = d ** -0.5
         o = torch.empty((b, nq, e), dtype=torch.float32, device=qf.device)
         probs = torch.empty((b, heads, nq, nk), dtype=torch.float32, device=qf.device)
-        avgw = torch.zeros((b, nq, nk), dtype=torch.float32, device=qf.device)
+        avgw = torch.empty((b, nq, nk), dtype=torch.float32, device=qf.device)
         N.call("dmf_attn_fwd", qf.data_ptr(), w3, kvf.data_ptr() + 4 * e, w3, kvf.data_ptr() + 8 * e, w3, b, nq, nk,
                heads, d, scale, o.data_ptr(), e, probs.data_ptr(), avgw.data_ptr(), _stream())
         ctx.save_for_backward(qf, kvf, probs)
@@ -2208,8 +2209,9 @@ class _MimicFn(torch.autograd.Function):
         ds = None
         if s.requires_grad:
             ds = torch.zeros_like(s)
+        ws = torch.empty(npairs * c, dtype=torch.float32, device=s.device)
         N.call("dmf_mimic_loss", dt(s), s.data_ptr(), t.data_ptr(), sstride, tstride, ld, hw, c, npairs,
-               loss.data_ptr(), _p(ds), sstride, _stream())
+               loss.data_ptr(), _p(ds), sstride, ws.data_ptr(), _stream())
         ctx.save_for_backward(ds)
         return loss
 

@@ -56,7 +56,10 @@ def gemm(out, a, b, M, Nn, K, ta=0, tb=0, lda=None, ldb=None, ldc=None, batch=(1
             O._p(aux), int(aux.stride(0)) if aux is not None else 0,
             O._p(pre), int(pre.stride(0)) if pre is not None else 0,
             float(dropout_p), O._p(rng), int(site), O._p(dbias))
-    N.call(fn, *args, _s())
+    # dbias: per-128-row-tile column sums, summed in tile order by the launcher (deterministic)
+    dbias_ws = torch.empty(((int(M) + 127) // 128) * int(Nn), dtype=torch.float32, device=out.device) \
+        if dbias is not None else None
+    N.call(fn, *args, O._p(dbias_ws), _s())
     probe = O.PROBE["tok_gemm"]
     if probe is not None and res is None and dbias is None:
         # (an epilogue that reads res / accumulates dbias changes state on a replay: not probed)
@@ -90,11 +93,16 @@ def ln_fwd(x2d, gamma, beta, eps, out_dtype):
     return y, save
 
 
+def _tok_ws(r, e, dev):
+    """Workspace of the token backward's ordered column sums (dmf_tok_bwd_ws_floats)."""
+    return torch.empty(N.load().dmf_tok_bwd_ws_floats(r, e), dtype=torch.float32, device=dev)
+
+
 def ln_bwd(dy, x2d, save, gamma, dres, dgamma, dbeta):
     r, e = x2d.shape
     dx = dres if dres is not None else torch.empty((r, e), dtype=torch.float32, device=dy.device)
     N.call("dmf_tok_layernorm_bwd", dy.data_ptr(), O.dt(x2d), x2d.data_ptr(), x2d.stride(0), save.data_ptr(), r, e,
-           gamma.data_ptr(), O._p(dres), dx.data_ptr(), O._p(dgamma), O._p(dbeta), _s())
+           gamma.data_ptr(), O._p(dres), dx.data_ptr(), O._p(dgamma), O._p(dbeta), (ws := _tok_ws(r, e, dy.device)).data_ptr(), _s())
     return dx
 
 
@@ -258,7 +266,8 @@ def _attn_bwd(dout, a, saved, wq, wp, b, n, heads, p_attn, p_proj, rng, s_attn, 
     dqkvw, dqkvb, dprojw, dprojb, dgamma = grads
     dy = torch.empty((r, e), **bf)
     N.call("dmf_tok_scale_dropout_bwd" + _sfx(cdt), dout.data_ptr(), y.data_ptr(), r, e, gamma.data_ptr(),
-           float(p_proj), O._p(rng), int(s_proj), dy.data_ptr(), O._p(dgamma), dprojb.data_ptr(), _s())
+           float(p_proj), O._p(rng), int(s_proj), dy.data_ptr(), O._p(dgamma), dprojb.data_ptr(), (ws := _tok_ws(r, e, dev)).data_ptr(),
+           _s())
     gemm(dprojw, dy, o, e, e, r, ta=1, tb=1, lda=e, ldb=e, ldc=e)
     do = gemm(torch.empty((r, e), **bf), dy, wp, r, e, e, tb=1, lda=e, ldb=e, ldc=e)
     del dy
@@ -282,7 +291,8 @@ def _attn_bwd(dout, a, saved, wq, wp, b, n, heads, p_attn, p_proj, rng, s_attn, 
     gemm(dqkvw, dqkv, a, 3 * e, e, r, ta=1, tb=1, lda=3 * e, ldb=e, ldc=e)
     if dqkvb is not None:
         if cdt == torch.bfloat16:
-            N.call("dmf_colsum_bf16", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), _s())
+            ws = torch.empty(N.load().dmf_colsum_bf16_ws_floats(r, 3 * e), dtype=torch.float32, device=dev)
+            N.call("dmf_colsum_bf16", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), ws.data_ptr(), _s())
         else:
             N.call("dmf_colsum_f32", dqkv.data_ptr(), 3 * e, r, 3 * e, dqkvb.data_ptr(), 1, _s())
     return gemm(torch.empty((r, e), **f32), dqkv, wq, r, e, 3 * e, tb=1, lda=3 * e, ldb=e, ldc=e)
@@ -312,7 +322,7 @@ def _mlp_bwd(dout, a, saved, w1, w2, p, rng, s1, s2, gamma, grads):
     dfc1w, dfc1b, dfc2w, dfc2b, dgamma = grads
     dy = torch.empty((r, e), **bf)
     N.call("dmf_tok_scale_dropout_bwd" + _sfx(cdt), dout.data_ptr(), y.data_ptr(), r, e, gamma.data_ptr(), float(p),
-           O._p(rng), int(s2), dy.data_ptr(), O._p(dgamma), dfc2b.data_ptr(), _s())
+           O._p(rng), int(s2), dy.data_ptr(), O._p(dgamma), dfc2b.data_ptr(), (ws := _tok_ws(r, e, dev)).data_ptr(), _s())
     gemm(dfc2w, dy, h, e, hid, r, ta=1, tb=1, lda=e, ldb=hid, ldc=hid)
     dpre = gemm(torch.empty((r, hid), **bf), dy, w2, r, hid, e, tb=1, lda=e, ldb=hid, ldc=hid, act="gelu",
                 pre=hpre, dropout_p=p, rng=rng, site=s1, dbias=dfc1b)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DMF_ABI_VERSION 2
+#define DMF_ABI_VERSION 3
 
 /* compute / storage dtypes: f32, bf16 and IEEE f16 (the reference's "16-mixed" autocast) */
 enum { DMF_F32 = 0, DMF_BF16 = 1, DMF_F16 = 2 };
@@ -329,8 +329,11 @@ int dmf_mask_attn_bwd(int dtype, const void* dout, int lddo, const void* f, int 
                       int C, const float* w1, const float* gn_w, const float* gn_b, const float* w2, const float* b2,
                       const float* gamma, int hidden, float eps, const float* stats, void* df, int lddf, void* dm,
                       float* workspace, float* grads, void* stream);
+/* dw (accumulated) = the per-block partials in ws (>= DMF_MIX_BWD_WS floats) summed in block order */
+#define DMF_MIX_BWD_WS 4096
 int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, const void* b, int ldb,
-                const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C, void* stream);
+                const float* wlogit, void* da, void* db, int ldd, float* dw, long long M, int C, float* ws,
+                void* stream);
 
 /* ------------------------------------------- cross-modal fusion op (fp32)
  * FusionModel.forward (model_module.py:919-1000): GatingAttention
@@ -363,7 +366,7 @@ int dmf_layernorm_fwd(const float* x, int R, int E, const float* gamma, const fl
                       float* save, void* stream);
 int dmf_layernorm_bwd(const float* dy, const float* x, const float* save, int R, int E, const float* gamma,
                       float* dx, float* dgamma, float* dbeta, void* stream);
-/* avg_weights must be zeroed by the caller (heads accumulate into it) */
+/* avg_weights (nullable, needs probs): the mean over heads of probs, summed in head order */
 int dmf_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, int B, int Nq, int Nk,
                  int H, int D, float scale, float* out, int ldo, float* probs, float* avg_weights, void* stream);
 int dmf_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* probs,
@@ -406,9 +409,11 @@ int dmf_recon_loss(int dtype, int nterms, const void* r0, const void* r1, const 
  * gradients written, not accumulated); 0 = not applicable: pass ws = NULL with zeroed
  * sums / gradients (atomic one-pass forms) */
 int dmf_recon_ws_floats(int nterms, int B, int h, int w, int S);
-/* loss must be zeroed by the caller (pairs/channels accumulate) */
+/* loss (accumulated) += the per-(pair, channel) terms, written to ws (npairs * C floats) and
+ * summed in a fixed order (deterministic) */
 int dmf_mimic_loss(int dtype, const void* student, const void* teacher, long long sstride, long long tstride, int ld,
-                   int HW, int C, int npairs, float* loss, void* dstudent, long long dstride, void* stream);
+                   int HW, int C, int npairs, float* loss, void* dstudent, long long dstride, float* ws,
+                   void* stream);
 int dmf_scale_by(const float* src, long long n, const float* scalar, float mul, float* dst, void* stream);
 int dmf_scale_by_cast(int dtype, const float* src, long long M, int C, const float* scalar, float mul, void* dst,
                       int ldd, void* stream);
@@ -440,12 +445,15 @@ int dmf_batch_accuracy(const float* logits, const long long* labels, int B, int 
  *   pre == NULL: t = dropout(act(t), p)         (forward; Philox index z*M*N + m*N + n at `site`)
  *   pre != NULL: t = dropout_mask(t) * act'(pre[m][n])   (gradient of that forward)
  *   t *= colscale[n]; t += res[m][n] (f32, unbatched; may alias C); C = t; dbias[n] += t
+ *   (dbias: unbatched only; per-128-row-tile column sums into dbias_ws [cdiv(M,128)][N],
+ *   then summed in tile order -- deterministic)
  * A, B bf16; C f32 or bf16 (out_dtype). */
 int dmf_gemm_bf16(int out_dtype, int ta, int tb, int M, int N, int K, float alpha, const void* A, int lda,
                   long long sA1, long long sA2, const void* B, int ldb, long long sB1, long long sB2, void* C,
                   int ldc, long long sC1, long long sC2, int batch1, int batch2, const float* bias, int act,
                   const float* colscale, const float* res, int ldr, void* aux, int ldaux, const void* pre, int ldpre,
-                  float dropout_p, const unsigned long long* rng, int site, float* dbias, void* stream);
+                  float dropout_p, const unsigned long long* rng, int site, float* dbias, float* dbias_ws,
+                  void* stream);
 /* the same GEMM with f32 A, B, aux and pre on the 16x16x4 f32 MFMA (exact
  * f32 products): the fp32 parity mode of the transformer stage
  * (set_compute_dtype(float32)); K, lda, ldb multiples of 4. */
@@ -453,7 +461,8 @@ int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha
                  long long sA1, long long sA2, const float* B, int ldb, long long sB1, long long sB2, void* C,
                  int ldc, long long sC1, long long sC2, int batch1, int batch2, const float* bias, int act,
                  const float* colscale, const float* res, int ldr, float* aux, int ldaux, const float* pre, int ldpre,
-                 float dropout_p, const unsigned long long* rng, int site, float* dbias, void* stream);
+                 float dropout_p, const unsigned long long* rng, int site, float* dbias, float* dbias_ws,
+                  void* stream);
 /* attention probabilities (transformer_model.py:104-110): per row of L f32
  * scores, probs = softmax(scale * s) (bf16, kept for backward) and
  * probs_dropped = dropout(probs, p) (bf16, the P operand of P v); Philox
@@ -478,20 +487,27 @@ int dmf_softmax_dropout_bwd_f32(const float* probs, int ldp, const float* dprobs
  * E % 256 == 0 and E <= 1024. LayerNorm: y bf16, save = (mean, rstd) per row. */
 int dmf_tok_layernorm_fwd(int x_dtype, const void* x, int ldx, long long R, int E, const float* gamma,
                           const float* beta, float eps, int y_dtype, void* y, int ldy, float* save, void* stream);
-/* dx (f32) = LN'(dy) (+ dres; dx may alias dres); dgamma/dbeta accumulated (nullable) */
+/* workspace floats of the token backward column sums (dmf_tok_layernorm_bwd,
+ * dmf_tok_scale_dropout_bwd*): one slab row per 32-row block and sum, summed in
+ * block order (deterministic) */
+long long dmf_tok_bwd_ws_floats(long long R, int E);
+/* dx (f32) = LN'(dy) (+ dres; dx may alias dres); dgamma/dbeta accumulated (nullable; ws needed with either) */
 int dmf_tok_layernorm_bwd(const float* dy, int x_dtype, const void* x, int ldx, const float* save, long long R,
                           int E, const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta,
-                          void* stream);
+                          float* ws, void* stream);
 /* backward of out = res + dropout(y) * gamma: dy (bf16) = mask * gamma * gout,
  * dgamma += sum gout * dropout(y), dbias += sum dy (accumulated, nullable) */
 int dmf_tok_scale_dropout_bwd(const float* gout, const void* yaux, long long R, int E, const float* gamma,
                               float dropout_p, const unsigned long long* rng, int site, void* dy, float* dgamma,
-                              float* dbias, void* stream);
+                              float* dbias, float* ws, void* stream);
 /* f32 yaux / dy (parity mode) */
 int dmf_tok_scale_dropout_bwd_f32(const float* gout, const float* yaux, long long R, int E, const float* gamma,
                                   float dropout_p, const unsigned long long* rng, int site, float* dy, float* dgamma,
-                                  float* dbias, void* stream);
-int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, void* stream);
+                                  float* dbias, float* ws, void* stream);
+/* out (accumulated) += column sums of bf16 X [R][ldx]: 64-row band sums into ws
+ * (dmf_colsum_bf16_ws_floats), then the bands in order */
+long long dmf_colsum_bf16_ws_floats(long long R, int C);
+int dmf_colsum_bf16(const void* X, int ldx, long long R, int C, float* out, float* ws, void* stream);
 int dmf_cast_bf16(const float* x, long long n, void* y, void* stream);
 int dmf_cast_f32(const void* x, long long n, float* y, void* stream);
 /* keep[i] (0/1) of element i at dropout site `site` -- the mask every fused

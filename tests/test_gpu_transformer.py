@@ -241,8 +241,9 @@ def test_token_layernorm_and_scale_dropout():
     ydev = yb.to(DEV, torch.bfloat16)
     dyo = torch.empty((R, E), dtype=torch.bfloat16, device=DEV)
     dgam, dbias = torch.zeros(E, device=DEV), torch.zeros(E, device=DEV)
+    ws = torch.empty(N.load().dmf_tok_bwd_ws_floats(R, E), dtype=torch.float32, device=DEV)
     N.call("dmf_tok_scale_dropout_bwd", dy.to(DEV).data_ptr(), ydev.data_ptr(), R, E, gam.to(DEV).data_ptr(), p,
-           rng.data_ptr(), site, dyo.data_ptr(), dgam.data_ptr(), dbias.data_ptr(), N.stream_ptr())
+           rng.data_ptr(), site, dyo.data_ptr(), dgam.data_ptr(), dbias.data_ptr(), ws.data_ptr(), N.stream_ptr())
     _close(dyo, dy * mk * gam, 1e-2, "branch dy")
     _close(dgam, (dy * mk * _bf(yb)).sum(0), 1e-3, "dgamma")
     _close(dbias, (dy * mk * gam).sum(0), 1e-3, "dbias")

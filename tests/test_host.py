@@ -3,6 +3,7 @@ structure / state-dict names (drop-in checkpoints), optimizer grouping and
 gradual unfreeze, class weights, first-conv adaptation, checkpoint key
 mapping, epoch metrics, rank sampling. No kernel is launched."""
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -291,3 +292,23 @@ def test_bench_dtype_options_and_peaks():
     assert bench.mfma_peak(torch.bfloat16) == bench.mfma_peak(torch.float16) == bench.BF16_MFMA_PEAK_TFLOPS
     assert bench.mfma_peak(torch.float32) == bench.F32_MFMA_PEAK_TFLOPS
     assert bench.DT_TAG[torch.float16] == "f16"
+
+
+def test_bench_gpus_2_parent_spawns_without_hip():
+    """VERDICT r04 item 3, on the CPU host: ``bench.py --gpus 2`` with no launcher
+    spawns two ranks from a parent that never initialises HIP (it asserts so
+    before spawning); with no GPU here every rank reports its missing device and
+    the parent returns non-zero without a result line."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "DMF_BENCH_SHARE_GPU")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # (no GPU in this container anyway)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-extras",
+                        "--no-cpu-baseline"], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "rank 0: cuda:0 is not visible" in r.stderr or "rank 1: cuda:1 is not visible" in r.stderr, r.stderr[-2000:]
+    assert "initialised HIP" not in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
