@@ -568,18 +568,23 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
 // that retires the current tile (vmcnt(0): only it is in flight) and frees
 // the other stage. Requires Nout % 256 == 0 plus the wide form's conditions.
 
-// VAR bit 0: waves 4-7 at static priority 1; bit 1: s_setprio around each MFMA group
-template <bool PADCHK, bool DUAL, int VAR, typename T = bf16_t>
-__global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
+// VAR bit 0: waves 4-7 at static priority 1; bit 1: s_setprio around each MFMA group.
+// WM_ x WN_ waves: 2 x 4 (8 waves, 128x64 each, two per SIMD) or 2 x 2 (4 waves, ONE per SIMD,
+// 128x128 each: 8x8 fragments = 256 accumulator registers in the AGPR half of the 512-entry file,
+// 2/3 of the LDS fragment reads per MFMA of the 8-wave split, 16 LDS-DMA pieces per wave per K-step;
+// DESIGN.md section 9.1)
+template <bool PADCHK, bool DUAL, int VAR, typename T = bf16_t, int WM_ = QWM, int WN_ = QWN>
+__global__ void __launch_bounds__(64 * WM_ * WN_, 1) k_conv_fwd_sq(ConvArgs a) {
   constexpr int ES = 2, EPC = 8, BK = 64;
-  constexpr int NW = QTHREADS / 64;
-  constexpr int NA = QBM / 8 / NW;  // A row-groups (8 rows) per wave: 4
-  constexpr int NB = QBN / 8 / NW;  // B row-groups per wave: 4
-  constexpr int FM = QBM / (16 * QWM), FN = QBN / (16 * QWN);
+  constexpr int NW = WM_ * WN_;
+  constexpr int NA = QBM / 8 / NW;  // A row-groups (8 rows) per wave: 4 (8 waves) / 8 (4 waves)
+  constexpr int NB = QBN / 8 / NW;  // B row-groups per wave
+  constexpr int FM = QBM / (16 * WM_), FN = QBN / (16 * WN_);
+  constexpr int PPK = (NA + NB) / 2;  // DMA pieces per k-half
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / QWN, wn = wid % QWN;
+  const int wm = wid / WN_, wn = wid % WN_;
   if constexpr (VAR & 1) {
     if (wid >= 4) __builtin_amdgcn_s_setprio(1);
   }
@@ -674,17 +679,23 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
       uint4 av[FM], bv[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int col = wn * (QBN / QWN) + j * 16 + fr;
+        const int col = wn * (QBN / WN_) + j * 16 + fr;
         bv[j] = *(const uint4*)(Bs + col * 128 + ((ch ^ (col & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int row = wm * (QBM / QWM) + i * 16 + fr;
+        const int row = wm * (QBM / WM_) + i * 16 + fr;
         av[i] = *(const uint4*)(As + row * 128 + ((ch ^ (row & 7)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if (more && (i & 1) == 0) piece(kk * 4 + (i >> 1));
+        if constexpr (PPK >= FM) {
+          if (more)
+#pragma unroll
+            for (int q = 0; q < PPK / FM; ++q) piece(kk * PPK + i * (PPK / FM) + q);
+        } else {
+          if (more && i % (FM / PPK) == 0) piece(kk * PPK + i / (FM / PPK));
+        }
         if constexpr ((VAR & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
@@ -694,7 +705,7 @@ __global__ void __launch_bounds__(QTHREADS, 1) k_conv_fwd_sq(ConvArgs a) {
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  conv_epilogue<T, QBM, QBN, QWM, QWN>(a, acc, smem, tid, mt, nt, m0, n0);
+  conv_epilogue<T, QBM, QBN, WM_, WN_>(a, acc, smem, tid, mt, nt, m0, n0);
 }
 
 // ------------------------------- forward, persistent LDS-DMA square form (bf16)
@@ -757,7 +768,15 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
   // bias (heads / projections with bias) staged once: the epilogue must issue no vmem load
   // (a compiler-visible load would be waited for behind the in-flight DMA)
   float* sbias = sred + 2 * TBN * 2;
-  if (a.bias) {
+  if constexpr (EPI == 8 || EPI == 11) {
+    // the known BatchNorm(s) of the affine epilogue: [scale | shift (+ the shortcut's shift) | shortcut scale]
+    for (int i = tid; i < a.Nout; i += NTH) {
+      sbias[i] = a.out_ss[i];
+      sbias[a.Nout + i] = a.out_ss[a.Nout + i] + (EPI == 11 ? a.res_ss[a.Nout + i] : 0.f);
+      if (EPI == 11) sbias[2 * a.Nout + i] = a.res_ss[i];
+    }
+    __syncthreads();
+  } else if (a.bias) {
     for (int i = tid; i < a.Nout; i += NTH) sbias[i] = a.bias[i];
     __syncthreads();
   }
@@ -1060,6 +1079,8 @@ static int g_stem_enable = 1;
 static int g_fast_epi = 1;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
+// 16 = k_conv_fwd_sq with 4 waves of 128x128 (one per SIMD) instead of 8 of 128x64: 0 off (default) / 1 on
+static int g_sq_w4 = 0;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
 // 3 buf 128x64, 4 buf 64x64, 5 wide 256x128, 6 square 256x256 (only where legal)
 static int g_force = 0;
@@ -1199,8 +1220,11 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
   if constexpr (sizeof(T) == 2) {
     if (plan.ps) {
       const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
-      // statistics without bias over whole tiles: the fast epilogue (EPI 5)
-      const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
+      // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
+      // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
+      const int epi = a.out_ss != nullptr ? (a.res_ss != nullptr ? 11 : 8)
+                      : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
+                                              : 1 + a.act;
       a.dbg = g_ps_dbg;
 #define DMF_PS(E)                                                                                                \
   do {                                                                                                           \
@@ -1208,7 +1232,14 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
     else if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a); \
     else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);        \
   } while (0)
+#define DMF_PS_AFF(E)                                                                                            \
+  do {                                                                                                           \
+    if (plain) hipLaunchKernelGGL((k_conv_fwd_ps<false, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a); \
+    else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);        \
+  } while (0)
       switch (epi) {
+        case 8: DMF_PS_AFF(8); break;
+        case 11: DMF_PS_AFF(11); break;
         case 0: DMF_PS(0); break;
         case 1: DMF_PS(1); break;
         case 2: DMF_PS(2); break;
@@ -1217,10 +1248,18 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
         default: DMF_PS(4); break;
       }
 #undef DMF_PS
+#undef DMF_PS_AFF
       return;
     }
     if (plan.sq) {
       const dim3 bq(QTHREADS);
+      if (g_sq_w4) {
+        const dim3 b4(256);
+        if (dual) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, 0, T, 2, 2>), g, b4, lds_total, st, a);
+        else if (plain) hipLaunchKernelGGL((k_conv_fwd_sq<false, false, 0, T, 2, 2>), g, b4, lds_total, st, a);
+        else hipLaunchKernelGGL((k_conv_fwd_sq<true, false, 0, T, 2, 2>), g, b4, lds_total, st, a);
+        return;
+      }
 #define DMF_SQ(V)                                                                                         \
   do {                                                                                                    \
     if (dual) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, V, T>), g, bq, lds_total, st, a);             \
@@ -1303,7 +1342,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = is16(dtype) ? 2 : 4;
-  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.bias ? (size_t)a.Nout * 4 : 0)
+  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.out_ss ? (a.res_ss ? 3 : 2) * (size_t)a.Nout * 4
+                                                     : a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
   if (plan.stem) return launch_conv_stem(a, st, dtype);
@@ -1314,6 +1354,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
+  DMF_CHECK_ARG(a.out_ss == nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
+                "%s: the affine epilogue needs the persistent 1x1 form (no bias, one source, a shortcut)", what);
   if (!dgrad && plan.ps) {
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     DMF_CHECK_ARG(a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
@@ -1473,6 +1515,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 11: g_fast_epi = value != 0; return 0;
     case 14: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: wide min tiles %d", value); g_wide_min_tiles = value; return 0;
     case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
+    case 16: g_sq_w4 = value != 0; return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1577,6 +1620,40 @@ extern "C" int dmf_conv2d_fwd_bn(int dtype, const void* x, int N, int H, int W, 
   a.fin = BnFin{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, 1,
                 scale_shift, save_mean_invstd};
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_bn");
+}
+
+// the ps plan (and so the affine epilogue) for a 1x1 conv of this shape
+static ConvArgs affine_args(int dtype, int N, int H, int W, int Cin, int ldx, int Cout, int stride) {
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = ldx; a.C1 = Cin;
+  a.Nout = Cout; a.KH = 1; a.KW = 1; a.stride = stride; a.pad = 0; a.dil = 1; a.Ktot = Cin;
+  a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1; a.M = N * a.Ho * a.Wo; a.ldy = Cout;
+  (void)dtype;
+  return a;
+}
+
+extern "C" int dmf_conv2d_fwd_affine_ok(int dtype, int N, int H, int W, int Cin, int Cout, int stride) {
+  if (!is16(dtype) || stride < 1) return 0;
+  ConvArgs a = affine_args(dtype, N, H, W, Cin, Cin, Cout, stride);
+  // (staged scale, shift and the shortcut's scale: 3 x Cout floats beside the ring)
+  return conv_plan(dtype, false, a).ps && (size_t)PS_LDS + (size_t)3 * Cout * 4 <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                                     int Cout, int stride, void* y, int Ho, int Wo, int ldy, const float* scale_shift,
+                                     const void* res, int ldr, const float* res_scale_shift, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, 1, 1, stride, 0, 1, nullptr, y, Ho,
+                           Wo, ldy, DMF_ACT_RELU, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_affine");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && scale_shift && res && ldr % 8 == 0 && ((uintptr_t)res % 16) == 0 &&
+                    ((long long)a.M * ldr * 2 < (1LL << 31)),
+                "dmf_conv2d_fwd_affine: needs a 16-bit dtype, scale_shift and an aligned shortcut");
+  a.out_ss = scale_shift;
+  a.res = res;
+  a.ldr = ldr;
+  a.res_ss = res_scale_shift;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_affine");
 }
 
 extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,

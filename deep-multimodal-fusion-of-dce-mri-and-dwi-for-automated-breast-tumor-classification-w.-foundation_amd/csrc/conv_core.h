@@ -47,6 +47,13 @@ struct ConvArgs {
   // DMA (the loop then computes on stale LDS), bit 2 the epilogue, bit 3 its
   // stores, bit 4 its statistics; bit 5 makes the stores non-temporal (dmf_conv_tune key 6 only)
   int dbg;
+  // affine epilogue of k_conv_fwd_ps (EPI 8 / 11, dmf_conv2d_fwd_affine): the BatchNorm already known,
+  // y = relu(acc * out_ss[n] + out_ss[Nout + n] + r), r = res (EPI 8) or res * res_ss[n] + res_ss[Nout + n]
+  // (EPI 11, the shortcut's own BatchNorm): conv -> BN -> + shortcut -> ReLU written once
+  const float* out_ss;
+  const void* res;
+  int ldr;
+  const float* res_ss;
 };
 
 template <int ACT>
@@ -205,11 +212,35 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   const int m0 = mt * TBM, n0 = nt * TBN;
   const int cl = wn * 64 + fg * 8;  // this lane's channels: n0 + cl .. +7 and n0 + cl + 32 .. +39
   // EPI 0: BN statistics; EPI 5: the same for a launch without bias whose M is a multiple of the tile
-  // height (every row in range: no bias adds, no row masks -- half the VALU of EPI 0)
+  // height (every row in range: no bias adds, no row masks -- half the VALU of EPI 0);
+  // EPI 8 / 11: affine (+ plain / BN'd residual) + ReLU with the statistics known (sbias holds them
+  // staged, see below)
   constexpr bool stats = EPI == 0 || EPI == 5, fast = EPI == 5;
-  float bsv[16];
+  constexpr bool aff = EPI == 8 || EPI == 11, rbn = EPI == 11;
+  // staged [scale | shift (+ the residual's shift) | residual scale] x Nout (k_conv_fwd_ps)
+  float bsv[16], shv[16], rsv[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) bsv[e] = (!fast && a.bias) ? sbias[n0 + ps_chan(wn, fg, e)] : 0.f;
+  for (int e = 0; e < 16; ++e) {
+    const int n = n0 + ps_chan(wn, fg, e);
+    bsv[e] = aff ? sbias[n] : ((!fast && a.bias) ? sbias[n] : 0.f);
+    shv[e] = aff ? sbias[a.Nout + n] : 0.f;
+    rsv[e] = rbn ? sbias[2 * a.Nout + n] : 1.f;
+  }
+  const __amdgpu_buffer_rsrc_t rres =
+      __builtin_amdgcn_make_buffer_rsrc(aff ? const_cast<void*>(a.res) : a.y, 0,
+                                        (int)((long long)a.M * (aff ? a.ldr : a.ldy) * (int)sizeof(T)), BUF_FLAGS_EP);
+  // affine epilogue: every fragment's shortcut loads in flight together (one exposed latency per tile)
+  v4u_t rsd[aff ? FM : 1][2];
+  if constexpr (aff) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
+      const bool ok = m < a.M;
+      const unsigned ro = ok ? (unsigned)(((size_t)m * a.ldr + n0 + cl) * sizeof(T)) : BUF_OOB;
+      rsd[i][0] = __builtin_bit_cast(v4u_t, __builtin_amdgcn_raw_buffer_load_b128(rres, ro, 0, 0));
+      rsd[i][1] = __builtin_bit_cast(v4u_t, __builtin_amdgcn_raw_buffer_load_b128(rres, ok ? ro + 64 : BUF_OOB, 0, 0));
+    }
+  }
   float s[16], q[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
@@ -221,7 +252,21 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = fast ? acc[i][j][r] : acc[i][j][r] + bsv[j * 4 + r];
+      for (int r = 0; r < 4; ++r)
+        v[j * 4 + r] = fast ? acc[i][j][r] : (aff ? __builtin_fmaf(acc[i][j][r], bsv[j * 4 + r], shv[j * 4 + r])
+                                                  : acc[i][j][r] + bsv[j * 4 + r]);
+    if constexpr (aff) {
+      // the shortcut: 16 channels of pixel m (two 16-B loads issued for every fragment up front),
+      // plain or through its own BatchNorm
+      const v4u_t r0 = rsd[i][0], r1 = rsd[i][1];
+      const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float lo = B16<T>::lo(rw[k]), hi = B16<T>::hi(rw[k]);
+        v[2 * k] = fmaxf(rbn ? __builtin_fmaf(lo, rsv[2 * k], v[2 * k]) : v[2 * k] + lo, 0.f);
+        v[2 * k + 1] = fmaxf(rbn ? __builtin_fmaf(hi, rsv[2 * k + 1], v[2 * k + 1]) : v[2 * k + 1] + hi, 0.f);
+      }
+    }
     if (fast) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] += v[e]; q[e] = __builtin_fmaf(v[e], v[e], q[e]); }

@@ -158,19 +158,34 @@ __global__ void __launch_bounds__(256, 2) k_gemm_fp8(const uint8_t* __restrict__
     if (kt + 1 < nk) lstore(smem + ((kt + 1) & 1) * F8STAGE);
     __syncthreads();
   }
-  // epilogue: D[4*fg + e][fr] of each 16x16 fragment
+  // epilogue: D[4*fg + e][fr] of each 16x16 fragment, scaled and packed into a bf16 LDS image of the
+  // tile, then written as whole 16-B row chunks (a lane's fragment values are one column of 4 rows:
+  // stored straight, every wave instruction was 64 two-byte pieces scattered over 16 rows)
+  constexpr int CST = F8BN + 8;  // bf16 elements per LDS row (16 B pad)
+  bf16_t* Cs = (bf16_t*)smem;
+  float rsc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * 64 + i * 16 + fg * 4 + e;
+      rsc[i][e] = m < M ? as[m] : 0.f;
+    }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + fr;
-    if (n >= N) continue;
-    const float sb = bs[n], bb = bias ? bias[n] : 0.f;
+    const int cl = wn * 64 + j * 16 + fr, n = n0 + cl;
+    const float sb = n < N ? bs[n] : 0.f, bb = (bias && n < N) ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm * 64 + i * 16 + fg * 4 + e;
-        if (m < M) Cm[(size_t)m * ldc + n] = f2bf(acc[i][j][e] * as[m] * sb + bb);
-      }
+      for (int e = 0; e < 4; ++e)
+        Cs[(wm * 64 + i * 16 + fg * 4 + e) * CST + cl] = f2bf(acc[i][j][e] * rsc[i][e] * sb + bb);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < F8BM * (F8BN / 8); idx += 256) {
+    const int row = idx / (F8BN / 8), ch = idx - row * (F8BN / 8);
+    const int m = m0 + row, n = n0 + ch * 8;
+    if (m < M && n < N) *(uint4*)(Cm + (size_t)m * ldc + n) = *(const uint4*)(Cs + row * CST + ch * 8);
   }
 }
 
@@ -206,6 +221,8 @@ extern "C" int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const f
   DMF_CHECK_ARG(A && B && C && a_scale && b_scale && M > 0 && N > 0 && K > 0, "dmf_gemm_fp8: bad args");
   DMF_CHECK_ARG(K % 16 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
                 "dmf_gemm_fp8: K (%d) and row strides must be multiples of 16 bytes", K);
+  DMF_CHECK_ARG(N % 8 == 0 && ldc % 8 == 0 && ((uintptr_t)C % 16) == 0,
+                "dmf_gemm_fp8: N (%d) and ldc must be multiples of 8, C 16-byte aligned (16-B row stores)", N);
   const int ntiles = cdiv(N, F8BN);
   const long long blocks = (long long)cdiv(M, F8BM) * ntiles;
   DMF_CHECK_ARG(blocks < (1LL << 31), "dmf_gemm_fp8: grid too large");

@@ -59,7 +59,8 @@ def gemm(out, a, b, M, Nn, K, ta=0, tb=0, lda=None, ldb=None, ldc=None, batch=(1
     # dbias: per-128-row-tile column sums, summed in tile order by the launcher (deterministic)
     dbias_ws = torch.empty(((int(M) + 127) // 128) * int(Nn), dtype=torch.float32, device=out.device) \
         if dbias is not None else None
-    N.call(fn, *args, O._p(dbias_ws), _s())
+    args = args + (O._p(dbias_ws),)
+    N.call(fn, *args, _s())
     probe = O.PROBE["tok_gemm"]
     if probe is not None and res is None and dbias is None:
         # (an epilogue that reads res / accumulates dbias changes state on a replay: not probed)
