@@ -166,6 +166,32 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       }
     }
   }
+  if (a.gbar) {
+    // grid-barrier BatchNorm apply (dmf_conv2d_fwd_bn_act, one resident block per tile): every block's
+    // statistics are in the arena after the barrier; the tile's (scale, shift) pairs replace the consumed
+    // statistics scratch, then BN + activation on the accumulators
+    if (a.dbg & 64) __syncthreads();  // (timing only, dmf_conv_tune key 17)
+    else gbar_sync(a.gbar, tid);
+    if (tid < BN) {
+      const int col = n0 + tid;
+      const float2 v = (a.dbg & 128) ? make_float2(1.f, 0.f)
+                       : col < a.Nout ? gbar_bn_channel(a, col, mt == 0) : make_float2(0.f, 0.f);
+      red[tid] = v.x;
+      red[BN + tid] = v.y;
+    }
+    if (mt == 0 && nt == 0 && tid == 0 && a.fin.nbt) *a.fin.nbt += 1;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int lc = wn * (BN / WNW) + j * 16 + fr;
+      const float sc = red[lc], sh = red[BN + lc];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_fmaf(acc[i][j][r], sc, sh);
+      apply_act_col(a.act, acc, j);
+    }
+  }
   __syncthreads();
   // stage C tile through LDS: [128 rows][128 + pad] of T
   constexpr int CPAD = 16 / sizeof(T);
@@ -744,7 +770,9 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
   constexpr int NB = TBN / 8 / NW;  // weight row-groups per wave: 4
   constexpr int FM = TBM / (16 * TWM), FN = TBN / (16 * TWN);  // 8 (256x256) or 4 (128x128) pixel x 4 channel fragments
   static_assert(NA == 4 && NB == 4 && FN == 4, "k_conv_fwd_ps geometry");
-  constexpr int EPI_VM = 2 * FM;  // an epilogue's stores per wave (+2 float64 atomics, pixel-half 0, stat_acc)
+  // an epilogue's stores per wave (+2 float64 atomics, pixel-half 0, stat_acc); the statistics-only
+  // epilogue (12) stores nothing, so nothing younger than the in-flight DMA may be waited out
+  constexpr int EPI_VM = EPI == 12 ? 0 : 2 * FM;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1081,6 +1109,9 @@ static int g_fast_epi = 1;
 static int g_sq_enable = 1, g_sq_var = 1;
 // 16 = k_conv_fwd_sq with 4 waves of 128x128 (one per SIMD) instead of 8 of 128x64: 0 off (default) / 1 on
 static int g_sq_w4 = 0;
+// 17 = timing bits of the grid-barrier BatchNorm apply (tools/gbar_bench.py only; outputs are wrong with
+// either set): 64 skips the barrier, 128 the arena reads
+static int g_gbar_dbg = 0;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
 // 3 buf 128x64, 4 buf 64x64, 5 wide 256x128, 6 square 256x256 (only where legal)
 static int g_force = 0;
@@ -1223,6 +1254,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
       // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
       // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
       const int epi = a.out_ss != nullptr ? (a.res_ss != nullptr ? 11 : 8)
+                      : a.y == nullptr ? 12
                       : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
                                               : 1 + a.act;
       a.dbg = g_ps_dbg;
@@ -1238,6 +1270,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
     else hipLaunchKernelGGL((k_conv_fwd_ps<true, false, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);        \
   } while (0)
       switch (epi) {
+        case 12: DMF_PS_AFF(12); break;
         case 8: DMF_PS_AFF(8); break;
         case 11: DMF_PS_AFF(11); break;
         case 0: DMF_PS(0); break;
@@ -1349,13 +1382,21 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   if (plan.stem) return launch_conv_stem(a, st, dtype);
   if (!dgrad && plan.pp) {
     // statistics without bias over whole tiles: the fast epilogue (EPI 5)
-    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0) : 1 + a.act;
-    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
+    // (the grid-barrier BatchNorm apply: EPI 13)
+    const int epi = a.gbar != nullptr ? 13
+                    : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
+                                            : 1 + a.act;
+    DMF_CHECK_ARG(((epi >= 0 && epi <= 5) || epi == 13) && a.act >= 0 && a.act <= 3, "%s: activation %d", what,
+                  a.act);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
   DMF_CHECK_ARG(a.out_ss == nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
                 "%s: the affine epilogue needs the persistent 1x1 form (no bias, one source, a shortcut)", what);
+  DMF_CHECK_ARG(a.y != nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.M % QBM == 0 &&
+                                   a.stat_acc >= 1),
+                "%s: a statistics-only pass needs the persistent 1x1 form, whole 256-row tiles, no bias and an arena",
+                what);
   if (!dgrad && plan.ps) {
     DMF_CHECK_ARG(lds_total <= 160 * 1024, "%s: %d output channels of bias exceed the LDS staging", what, a.Nout);
     DMF_CHECK_ARG(a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
@@ -1516,6 +1557,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 14: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: wide min tiles %d", value); g_wide_min_tiles = value; return 0;
     case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
     case 16: g_sq_w4 = value != 0; return 0;
+    case 17: g_gbar_dbg = value & (64 | 128); return 0;
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1635,8 +1677,23 @@ static ConvArgs affine_args(int dtype, int N, int H, int W, int Cin, int ldx, in
 extern "C" int dmf_conv2d_fwd_affine_ok(int dtype, int N, int H, int W, int Cin, int Cout, int stride) {
   if (!is16(dtype) || stride < 1) return 0;
   ConvArgs a = affine_args(dtype, N, H, W, Cin, Cin, Cout, stride);
-  // (staged scale, shift and the shortcut's scale: 3 x Cout floats beside the ring)
-  return conv_plan(dtype, false, a).ps && (size_t)PS_LDS + (size_t)3 * Cout * 4 <= 160 * 1024 ? 1 : 0;
+  // (staged scale, shift and the shortcut's scale: 3 x Cout floats beside the ring; whole 256-row tiles for
+  // the statistics-only first pass)
+  return conv_plan(dtype, false, a).ps && a.M % QBM == 0 && (size_t)PS_LDS + (size_t)3 * Cout * 4 <= 160 * 1024
+             ? 1 : 0;
+}
+
+extern "C" int dmf_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                                    int Cout, int stride, int Ho, int Wo, double* bn_acc, int replicas, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, 1, 1, stride, 0, 1, nullptr, nullptr,
+                           Ho, Wo, Cout, DMF_ACT_NONE, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_stats");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && bn_acc && ((uintptr_t)bn_acc % 8) == 0 && replicas >= 1 && replicas <= 64,
+                "dmf_conv2d_fwd_stats: needs a 16-bit dtype and a float64 arena slice");
+  a.partials = (float*)bn_acc;
+  a.stat_acc = replicas;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_stats");
 }
 
 extern "C" int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
@@ -1654,6 +1711,60 @@ extern "C" int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int
   a.ldr = ldr;
   a.res_ss = res_scale_shift;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_affine");
+}
+
+// The grid-barrier BatchNorm apply needs one output tile per block and every block resident: the
+// ping-pong 256x256 form (one 512-thread block per CU, whole tiles, no bias: EPI 13's statistics) or the
+// 256x128 wide form (one 512-thread block per CU; conv_epilogue), at no more tiles than CUs.
+static bool gbar_plan_ok(const ConvPlan& p, const ConvArgs& a) {
+  const long long tiles = (long long)cdiv(a.M, p.bm) * cdiv(a.Nout, p.bn);
+  if (tiles > cu_count()) return false;
+  if (p.pp) return a.bias == nullptr && a.M % QBM == 0;
+  return p.wide && !p.sq && !p.ps && !p.stem;
+}
+
+extern "C" int dmf_conv2d_fwd_bn_act_ok(int dtype, int N, int H, int W, int Cin, int Cin2, int Cout, int KH, int KW,
+                                        int stride, int pad, int dil, int has_bias) {
+  if (!is16(dtype) || stride < 1 || dil < 1 || KH < 1 || KW < 1) return 0;
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = Cin + Cin2; a.ldx = Cin; a.C1 = Cin; a.ldx2 = Cin2;
+  a.x2 = Cin2 > 0 ? (const void*)&a : nullptr;  // (only its presence matters to the plan)
+  a.bias = has_bias ? (const float*)&a : nullptr;
+  a.Nout = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil; a.Ktot = KH * KW * a.C;
+  a.Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  a.Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  a.M = N * a.Ho * a.Wo; a.ldy = Cout;
+  if (a.M <= 0 || a.C % 8 || Cout % 8) return 0;
+  return gbar_plan_ok(conv_plan(dtype, false, a), a) ? 1 : 0;
+}
+
+extern "C" int dmf_conv2d_fwd_bn_act(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
+                                     int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad,
+                                     int dil, const float* bias, void* y, int Ho, int Wo, int ldy, int act,
+                                     double* bn_acc, int replicas, unsigned* gbar, const float* gamma,
+                                     const float* beta, float* running_mean, float* running_var,
+                                     long long* num_batches_tracked, float momentum, float eps, double count,
+                                     double unbias_count, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, x2, Cin2, ldx2, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                           Ho, Wo, ldy, act, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_bn_act");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && bn_acc && ((uintptr_t)bn_acc % 16) == 0 && replicas >= 1 &&
+                    replicas <= GBAR_MAX_REPLICAS && gbar &&
+                    ((uintptr_t)gbar % 4) == 0 && count > 0 &&
+                    (act == DMF_ACT_NONE || act == DMF_ACT_RELU || act == DMF_ACT_GELU),
+                "dmf_conv2d_fwd_bn_act: needs a 16-bit dtype, a float64 arena slice, the barrier words and "
+                "activation none / relu / gelu");
+  a.partials = (float*)bn_acc;
+  a.stat_acc = replicas;
+  a.gbar = gbar;
+  a.dbg = g_gbar_dbg;
+  a.fin = BnFin{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, 1,
+                nullptr, nullptr};
+  DMF_CHECK_ARG(gbar_plan_ok(conv_plan(dtype, false, a), a),
+                "dmf_conv2d_fwd_bn_act: this shape does not run one resident block per output tile "
+                "(dmf_conv2d_fwd_bn_act_ok)");
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_bn_act");
 }
 
 extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,

@@ -782,6 +782,20 @@ extern "C" int dmf_bn_finalize(const float* partials, int ntiles, int C, double 
   return 0;
 }
 
+extern "C" int dmf_bn_finalize_acc(const double* acc, int replicas, int C, double count, double unbias_count,
+                                   const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                   long long* num_batches_tracked, float momentum, float eps, float* scale_shift,
+                                   float* save_mean_invstd, void* stream) {
+  DMF_CHECK_ARG(acc && replicas >= 1 && replicas <= 64 && C > 0 && count > 0 && scale_shift,
+                "dmf_bn_finalize_acc: bad args");
+  BnFin f{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, 1,
+          scale_shift, save_mean_invstd};
+  hipLaunchKernelGGL(k_bn_finalize<double>, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, acc, replicas, C,
+                     f);
+  DMF_LAUNCH_CHECK("dmf_bn_finalize_acc");
+  return 0;
+}
+
 extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
                               const float* res_scale_shift, int act, float dropout_p,
                               const unsigned long long* rng, int site, void* y, int ldy, long long M, int C,

@@ -276,18 +276,21 @@ def needs_grad(*ts):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
-def _conv_launch(fn, args, keep, x, n, h, w, cxt, co, kh, kw, g, ho, wo):
+def _conv_launch(fn, args, keep, x, n, h, w, cxt, co, kh, kw, g, ho, wo, y_maps=1):
     """One MFMA conv-forward C-ABI call (``args`` without the trailing stream).
     With bench.py's probe armed, the call is also recorded -- entry point,
     arguments, the tensors they point into (kept alive) and the algorithmic
-    flops/bytes -- so the probe can replay the same launches GPU-only."""
+    flops/bytes -- so the probe can replay the same launches GPU-only.
+    y_maps: output-sized maps moved (2 for an output written beside a read
+    shortcut; 0 marks a statistics-only pass, whose conv is recomputed by
+    the writing pass: its time counts, its flops and bytes do not)."""
     N.call(fn, *args, _stream())
     probe = PROBE["conv_fwd"]
     if probe is not None:
         es = x.element_size()
         k_tot = kh * kw * cxt
-        flops = 2.0 * n * ho * wo * co * k_tot
-        byts = es * (n * h * w * cxt + co * k_tot + n * ho * wo * co)
+        flops = 2.0 * n * ho * wo * co * k_tot if y_maps else 0.0
+        byts = es * (n * h * w * cxt + co * k_tot + y_maps * n * ho * wo * co) if y_maps else 0.0
         probe.append({"fn": fn, "args": args, "keep": keep, "flops": flops, "bytes": byts,
                       "shape": (n, h, w, cxt, co, kh, g.stride, g.dil),
                       "form": N.FORMS.get(N.load().dmf_conv_last_form(), "?")})
@@ -1024,6 +1027,10 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
     p = float(dropout_p)
     if p > 0 and rng is None:
         raise RuntimeError("dropout requested without an rng snapshot")
+    if _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
+        return _conv_bn_two_pass(x, conv, caches, bn, res, skip)
+    if _gbar_ok(x, conv, bn, act, p, res, skip, x2, in_ss):
+        return _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult)
     if skip is not None:
         xr, conv_r, caches_r, bn_r = skip
         gr = ConvGeom(conv_r)
@@ -1078,6 +1085,154 @@ def conv_bn_stats(x, conv, caches, bn, in_ss=None, in_act="none", x2=None, unbia
         y, ss, _, _ = _conv_bn_forward(x, conv.weight, conv.bias, g, caches, bn, unbias_mult, x2=x2, in_ss=in_ss,
                                        in_act=in_act)
     return y, ss
+
+
+# Two-pass BatchNorm fusion of a forward-only Bottleneck conv3 (1x1 conv -> BN -> + shortcut -> ReLU):
+# pass 1 runs the conv for the batch statistics alone (dmf_conv2d_fwd_stats: nothing written), pass 2
+# recomputes it and writes relu(bn(y) + shortcut) once (dmf_conv2d_fwd_affine). The raw output's write
+# and the apply pass's read + write become a second K loop over the (L2-resident) operands; in eval
+# mode the scale/shift is known up front and only pass 2 runs. Knob "two_pass_bn" = False restores the
+# conv + dmf_bn_apply form.
+TWO_PASS_BN = True
+# measured (profiles/r05g_two_pass_split.txt): the recompute pays for the saved write + apply pass up to
+# K = 256 (layer1-3 conv3s); at K = 512 (layer4, 512 -> 2048) the second K loop costs what it saves
+TWO_PASS_MAX_K = 256
+
+
+def _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
+    if not (TWO_PASS_BN and x2 is None and in_ss is None and conv.bias is None and p == 0 and act == "relu"
+            and unbias_mult == 1 and (res is None) != (skip is None)):
+        return False
+    if (x.dtype not in (torch.bfloat16, torch.float16) or conv.groups != 1 or tuple(conv.kernel_size) != (1, 1)
+            or conv.in_channels > TWO_PASS_MAX_K
+            or conv.padding[0] != 0 or conv.dilation[0] != 1 or conv.stride[0] != conv.stride[1]):
+        return False
+    if needs_grad(x, conv.weight, bn.weight, bn.bias, res):
+        return False
+    n, c, h, w, _ = nhwc(x)
+    if c != conv.in_channels:
+        return False
+    ho, wo = ConvGeom(conv).out_hw(h, w)
+    if skip is not None:
+        xr, conv_r, _, bn_r = skip
+        if (needs_grad(xr, conv_r.weight, bn_r.weight, bn_r.bias) or conv_r.bias is not None
+                or not _is_mfma_conv(conv_r.weight, ConvGeom(conv_r)) or conv_r.out_channels % 8):
+            return False
+    elif nhwc(res)[:4] != (n, conv.out_channels, ho, wo) or not _bn_apply_ok(res):
+        return False
+    return bool(N.load().dmf_conv2d_fwd_affine_ok(dt(x), n, h, w, c, conv.out_channels, conv.stride[0]))
+
+
+# Grid-barrier BatchNorm apply of a forward-only conv -> BN (batch statistics) -> act with no shortcut
+# (dmf_conv2d_fwd_bn_act): the conv's epilogue accumulates the statistics, meets the other blocks at a
+# grid-wide barrier and writes act(bn(y)) once -- no raw output, no dmf_bn_apply pass. Every block of the
+# launch is resident (one tile per block, dmf_conv2d_fwd_bn_act_ok) and spins once, so a second such
+# kernel spinning beside it on another stream could hold CUs the first still needs: it runs only outside a
+# concurrent region (CONCURRENT: raised by train_fusion._encode's two-stream fork and by branch()).
+# Measured and left OFF (knob "grid_barrier_bn"; profiles/r05g_grid_barrier_bench.txt, _enc_ab.txt): the
+# barrier itself costs 7-11 us per launch (the guide's barrier-counter row: 7.4), about what the apply pass
+# it removes costs (8-14 us), and the 3x3 ping-pong form spills under the epilogue's registers (512->512
+# dilated: 160 -> 216 us); it also needs the encoders on one stream, and the serial forward is 9.89 ms
+# against 8.47 ms for the two-stream one (10.55 ms serial with the barrier).
+GRID_BARRIER_BN = False
+CONCURRENT = [0]
+
+
+def _gbar_site(bn, dev):
+    """The barrier words of one BatchNorm2d's launch site (zero at first use, self-resetting; kept out of
+    the state_dict)."""
+    st = bn.__dict__.get("_dmf_gbar")
+    if st is None or st.device != dev:
+        st = torch.zeros(4, dtype=torch.int32, device=dev)
+        bn.__dict__["_dmf_gbar"] = st
+    return st
+
+
+def _gbar_ok(x, conv, bn, act, p, res, skip, x2, in_ss):
+    if not (GRID_BARRIER_BN and CONCURRENT[0] == 0 and res is None and skip is None and in_ss is None and p == 0
+            and act in ("relu", "gelu", "none") and (bn.training or bn.running_mean is None) and x.is_cuda
+            and x.dtype in (torch.bfloat16, torch.float16) and conv.groups == 1
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            and conv.dilation[0] == conv.dilation[1]):
+        return False
+    if needs_grad(x, x2, conv.weight, conv.bias, bn.weight, bn.bias):
+        return False
+    n, c, h, w, _ = nhwc(x)
+    c2 = nhwc(x2)[1] if x2 is not None else 0
+    if c + c2 != conv.in_channels:
+        return False
+    g = ConvGeom(conv)
+    return bool(N.load().dmf_conv2d_fwd_bn_act_ok(dt(x), n, h, w, c, c2, conv.out_channels, g.kh, g.kw, g.stride,
+                                                  g.pad, g.dil, 0 if conv.bias is None else 1))
+
+
+def _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult):
+    g = ConvGeom(conv)
+    n, cx, h, wd, ldx = nhwc(x)
+    cx2, ldx2 = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
+    co = conv.out_channels
+    ho, wo = g.out_hw(h, wd)
+    m = n * ho * wo
+    dev = x.device
+    track = bn.track_running_stats and bn.running_mean is not None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    with torch.no_grad():
+        wk = caches[0].get(conv.weight, x.dtype, cx + cx2, 0)
+        acc = _bn_acc(co, dev)
+        gb = _gbar_site(bn, dev)
+        y = empty_nhwc(n, co, ho, wo, x.dtype, dev)
+        _conv_launch("dmf_conv2d_fwd_bn_act",
+                     (dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, g.kh, g.kw,
+                      g.stride, g.pad, g.dil, _p(conv.bias), y.data_ptr(), ho, wo, nhwc(y)[4], ACT[act],
+                      acc.data_ptr(), BN_ACC_REPLICAS, gb.data_ptr(), _p(bn.weight), _p(bn.bias),
+                      _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
+                      _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), float(m),
+                      float(m * unbias_mult) if unbias_mult != 1 else 0.0),
+                     (x, x2, wk, conv.bias, y, acc, gb, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                      bn.num_batches_tracked), x, n, h, wd, cx + cx2, co, g.kh, g.kw, g, ho, wo)
+    return y
+
+
+def _finalize_acc(d, c):
+    """dmf_bn_finalize_acc of a deferred BatchNorm descriptor (_bn_desc): scale_shift / save_mean_invstd
+    (+ the running statistics) from its float64 arena slice."""
+    N.call("dmf_bn_finalize_acc", d.acc, d.replicas, c, d.count, d.unbias_count, d.gamma, d.beta, d.running_mean,
+           d.running_var, d.num_batches_tracked, d.momentum, d.eps, d.scale_shift, d.save_mean_invstd, _stream())
+
+
+def _conv_bn_two_pass(x, conv, caches, bn, res, skip):
+    g = ConvGeom(conv)
+    n, cx, h, wd, ldx = nhwc(x)
+    co = conv.out_channels
+    ho, wo = g.out_hw(h, wd)
+    m = n * ho * wo
+    dev = x.device
+    dtc = dt(x)
+    with torch.no_grad():
+        wk = caches[0].get(conv.weight, x.dtype, cx, 0)
+        if bn.training or bn.running_mean is None:
+            acc = _bn_acc(co, dev)
+            ss = torch.empty(2 * co, dtype=torch.float32, device=dev)
+            save = torch.empty(2 * co, dtype=torch.float32, device=dev)
+            _conv_launch("dmf_conv2d_fwd_stats",
+                         (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, ho, wo, acc.data_ptr(),
+                          BN_ACC_REPLICAS), (x, wk, acc), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=0)
+            _finalize_acc(_bn_desc(bn, acc, m, 0.0, ss, save), co)
+        else:
+            ss, _ = _bn_finalize(None, m, bn)
+        ss_r = None
+        if skip is not None:
+            xr, conv_r, caches_r, bn_r = skip
+            res, ss_r, _, desc_r = _conv_bn_forward(xr, conv_r.weight, None, ConvGeom(conv_r), caches_r, bn_r,
+                                                    defer=True)
+            if desc_r is not None:
+                _finalize_acc(desc_r, co)
+        out = empty_nhwc(n, co, ho, wo, x.dtype, dev)
+        _conv_launch("dmf_conv2d_fwd_affine",
+                     (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, out.data_ptr(), ho, wo,
+                      nhwc(out)[4], ss.data_ptr(), res.data_ptr(), nhwc(res)[4], _p(ss_r)),
+                     (x, wk, out, ss, res, ss_r), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=2)
+    return out
 
 
 # ============================================================ elementwise
@@ -2292,11 +2447,14 @@ def branch(owner, name, fn, *inputs):
         return out, (lambda: out)
     side = side_stream(owner, name, dev)
     side.wait_stream(main)
+    CONCURRENT[0] += 1  # until the join: no grid-barrier launch on either stream
     with torch.cuda.stream(side):
         record_tree(list(inputs), side)
         out = fn()
 
     def join():
+        if keep:
+            CONCURRENT[0] -= 1
         main.wait_stream(side)
         record_tree(out, main)
         del keep[:]
@@ -2439,6 +2597,8 @@ KNOBS = {
     "shortcut_handoff": ("dmf_ops", "SHORTCUT_HANDOFF"),
     "linear_sink": ("dmf_ops", "LINEAR_SINK"),
     "se_fused": ("dmf_ops", "SE_FUSED"),
+    "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
+    "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),
     "parallel_dead": ("model_module", "PARALLEL_DEAD"),
     "device_loss": ("train_fusion", "DEVICE_LOSS"),
@@ -2452,6 +2612,7 @@ KNOBS = {
     "conv_fast_epi": ("tune", 11),
     "conv_wide_min_tiles": ("tune", 14),
     "conv_sq_min_tiles": ("tune", 15),
+    "conv_sq_w4": ("tune", 16),
     "wgrad_dma": ("wgrad_tune", 0),
     "wgrad_wide": ("wgrad_tune", 1),
     "wgrad_tr": ("wgrad_tune", 2),

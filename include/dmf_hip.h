@@ -123,6 +123,41 @@ int dmf_conv2d_fwd_acc(int dtype, const void* x, int N, int H, int W, int Cin, i
                        int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
                        const float* bias, void* y, int Ho, int Wo, int ldy, double* bn_acc, int replicas,
                        const float* in_scale_shift, int in_act, void* stream);
+/* Two-pass conv -> BatchNorm2d (batch statistics) -> + shortcut -> ReLU of a 1x1 conv that the forward
+ * never differentiates (frozen encoders, mode A: timm Bottleneck conv3 / bn3 / residual / act3,
+ * foundation_model.py:260-267): the first pass accumulates the BN statistics into an arena slice
+ * WITHOUT writing the conv output (dmf_conv2d_fwd_stats; finalized by dmf_bn_finalize_acc), the
+ * second recomputes the conv and writes relu(y * scale_shift + shortcut) once (dmf_conv2d_fwd_affine;
+ * res_scale_shift nullable: the shortcut's own BatchNorm, a projection shortcut's raw conv output).
+ * Replaces the raw conv output's write and the separate BN-apply pass (its read of the raw output) by
+ * a second K loop. dmf_conv2d_fwd_affine_ok: 1 when a 1x1 conv of this shape runs the persistent
+ * 256x256 form both passes need (16-bit dtype, Cout % 256 == 0, N*Ho*Wo % 256 == 0). */
+int dmf_conv2d_fwd_affine_ok(int dtype, int N, int H, int W, int Cin, int Cout, int stride);
+int dmf_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                         int stride, int Ho, int Wo, double* bn_acc, int replicas, void* stream);
+int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                          int stride, void* y, int Ho, int Wo, int ldy, const float* scale_shift, const void* res,
+                          int ldr, const float* res_scale_shift, void* stream);
+/* conv -> BatchNorm2d (batch statistics) -> act in ONE launch, for a forward that is never
+ * differentiated (frozen encoders, mode A: timm Bottleneck conv1 / conv2, the necks; the apply
+ * passes of foundation_model.py:260-267 and model_module.py:401-476). The epilogue adds the
+ * statistics into bn_acc [replicas][Cout][2] (zeroed by the caller), every block meets the others at
+ * a grid-wide barrier, then finalizes its tile's channels from bn_acc (the running statistics and
+ * num_batches_tracked move once, as dmf_bn_finalize with count / unbias_count) and writes
+ * act(conv * scale + shift) -- no raw conv output, no apply pass. Legal only where every block of the
+ * launch is resident and owns one output tile: dmf_conv2d_fwd_bn_act_ok (the 256x256 ping-pong form
+ * without bias over whole tiles, or the 256x128 wide form, at <= one tile per CU). gbar: three
+ * counters of this BatchNorm's launch site, zero on the first call (the launches self-reset them).
+ * A grid that is not fully resident within ~2 s traps instead of hanging. act: DMF_ACT_NONE / RELU /
+ * GELU. */
+int dmf_conv2d_fwd_bn_act_ok(int dtype, int N, int H, int W, int Cin, int Cin2, int Cout, int KH, int KW, int stride,
+                             int pad, int dil, int has_bias);
+int dmf_conv2d_fwd_bn_act(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
+                          int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                          const float* bias, void* y, int Ho, int Wo, int ldy, int act, double* bn_acc, int replicas,
+                          unsigned* gbar, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, long long* num_batches_tracked, float momentum, float eps,
+                          double count, double unbias_count, void* stream);
 int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
@@ -217,6 +252,11 @@ int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc* bn, const
                  const void* res, int ldr, const dmf_bn_desc* res_bn, const float* res_scale_shift, int act,
                  float dropout_p, const unsigned long long* rng, int site, void* y, int ldy, long long M, int C,
                  void* stream);
+/* finalize (as dmf_bn_finalize, training mode) of batch statistics accumulated into an arena slice
+ * [replicas][C][2] (dmf_conv2d_fwd_acc / dmf_conv2d_fwd_stats) */
+int dmf_bn_finalize_acc(const double* acc, int replicas, int C, double count, double unbias_count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, long long* num_batches_tracked,
+                        float momentum, float eps, float* scale_shift, float* save_mean_invstd, void* stream);
 int dmf_affine_act(int dtype, const void* x, int ldx, const float* scale_shift, const void* res, int ldr,
                    const float* res_scale_shift, int act, float dropout_p, const unsigned long long* rng, int site,
                    void* y, int ldy, long long M, int C, void* stream);

@@ -5,6 +5,9 @@ variants, in one process (cdna_hip_programming.md 5.4 rule 24): each variant
 gets its own captured graph; rounds x variants, median ms per variant.
 
     python tools/enc_fwd_ab.py --tunes "7:0;7:1" [--rounds 4] [--reps 10]
+
+A variant entry is KEY:VAL (dmf_conv_tune) or name=VAL (dmf_ops.set_knobs),
+e.g. --tunes "two_pass_bn=1;two_pass_bn=0".
 """
 import argparse
 import json
@@ -20,6 +23,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 import dmf_native as N  # noqa: E402
+import dmf_ops as O  # noqa: E402
 import parameters as PR  # noqa: E402
 
 
@@ -29,7 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
-    variants = [[tuple(int(t) for t in kv.split(":")) for kv in grp.split(",") if kv] for grp in a.tunes.split(";")]
+    variants = [[kv for kv in grp.split(",") if kv] for grp in a.tunes.split(";")]
     dev = torch.device("cuda", 0)
     P = PR.default_parameters()
     lm = bench.build(P, dev, torch.bfloat16, "A", seed=0)
@@ -41,8 +45,13 @@ def main():
 
     graphs = []
     for var in variants:
-        for k, v in var:
-            N.call("dmf_conv_tune", k, v)
+        for kv in var:
+            if "=" in kv:
+                k, v = kv.split("=")
+                O.set_knobs(**{k: int(v)})
+            else:
+                k, v = (int(t) for t in kv.split(":"))
+                N.call("dmf_conv_tune", k, v)
         g, _ = bench._graph(fwd)  # kernels are chosen at capture: the graph keeps this variant
         graphs.append(g)
     times = [[] for _ in variants]

@@ -5,7 +5,7 @@ bf16, captured once as a hipGraph and replayed --reps times. Run it under
 `rocprofv3 --kernel-trace --stats` for a per-kernel split of one forward
 (divide the totals by --reps); prints the HIP-event time per forward.
 
-    python tools/enc_fwd_prof.py [--reps 20] [--batch 32] [--serial]
+    python tools/enc_fwd_prof.py [--reps 20] [--batch 32] [--serial] [--knob name=VAL ...]
 """
 import argparse
 import json
@@ -28,10 +28,14 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--serial", action="store_true", help="one stream (no DCE side stream)")
+    ap.add_argument("--knob", action="append", default=[], help="dmf_ops.set_knobs name=VAL")
     a = ap.parse_args()
+    import dmf_ops as O
+    for kv in a.knob:
+        k, v = kv.split("=")
+        O.set_knobs(**{k: int(v)})
     if a.serial:
-        import train_fusion as TF
-        TF.PARALLEL_ENCODERS = False
+        O.set_knobs(parallel_encoders=0)
     dev = torch.device("cuda", 0)
     P = PR.default_parameters()
     P["dwi_model_parameters"]["input_size"] = a.size
