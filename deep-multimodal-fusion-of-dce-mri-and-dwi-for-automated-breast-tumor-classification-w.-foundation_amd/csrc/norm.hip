@@ -868,6 +868,8 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
   // ~8 row iterations per thread, but at least ~1024 blocks in flight
   int rows = 256;
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
+  // (gridDim.y <= 65535: beyond 16.7 M rows each block walks more rows)
+  if (cdiv(M, rows) > 65535) rows = (int)(cdiv(cdiv(M, 65535), 32) * 32);
   const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
   const int resk = res == nullptr ? 0 : ((res_bn || res_scale_shift) ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
@@ -1011,6 +1013,7 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
   const int gy = cdiv(C, 64);
   int rows = 256;
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
+  if (cdiv(M, rows) > 65535) rows = (int)(cdiv(cdiv(M, 65535), 32) * 32);  // (gridDim.y <= 65535)
   const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply_acc<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
                        (const T*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
@@ -1028,6 +1031,9 @@ static int act_bwd_bn_reduce_impl(int dtype, const void* dy, int lddy, const voi
   DMF_CHECK_ARG(dy && x && scale_shift && save_mean_invstd && dz && (partials || acc) && M > 0 && C > 0,
                 "dmf_act_bwd_bn_reduce: bad args");
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_act_bwd_bn_reduce: dropout needs rng state");
+  // (the vector kernel's residual term is compiled in per specialisation: a shortcut BatchNorm without
+  // its shortcut would add the shift alone)
+  DMF_CHECK_ARG(!res_scale_shift || res, "dmf_act_bwd_bn_reduce: res_scale_shift needs res");
   const bool vec8 = C % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddz % 8 == 0 && (!res || ldr % 8 == 0) &&
                     (!dy2 || lddy2 % 8 == 0) &&
                     ((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dz | (uintptr_t)(res ? res : dz) |

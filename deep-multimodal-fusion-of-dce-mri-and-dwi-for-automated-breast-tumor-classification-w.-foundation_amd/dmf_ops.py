@@ -911,6 +911,11 @@ class _ConvBNActFn(torch.autograd.Function):
                    float(p), _p(rng), site, out.data_ptr(), nhwc(out)[4], m, c, _stream())
         ctx.save_for_backward(x, x2, w, b, y, ss, save, res, xr, wr, yr, ss_r, save_r, rng)
         ctx.spec = spec
+        # the shortcut producer's autograd node: the backward hands the shortcut gradient over only when
+        # the engine will run that node in this pass (not when torch.autograd.grad(..., inputs=...) or a
+        # partial backward prunes it)
+        sc_t = xr if xr is not None else res
+        ctx.handoff_node = sc_t.grad_fn if (_handoff is not None and sc_t is not None) else None
         # the backward's BN column sums: a zeroed slice of this forward's statistics arena
         # (dmf_act_bwd_bn_reduce_acc / dmf_bn_bwd_apply_acc: no finalize launch)
         # (training-mode BN only: the arena is zeroed at the forward's start when a BN trains)
@@ -965,6 +970,9 @@ class _ConvBNActFn(torch.autograd.Function):
                    lddz, m, c, part.data_ptr(), _stream())
             dy = _bn_backward(dz, y, save, bn, dgamma, dbeta, training=bn.training, part=part)
         need_dx = need[0] or (x2 is not None and need[1])
+        if handoff is not None and (ctx.handoff_node is None
+                                    or not torch._C._will_engine_execute_node(ctx.handoff_node)):
+            handoff = None  # the producer's backward is not in this pass: autograd carries the gradient
         dx, dw, db = _conv_backward(x, w, b, g, caches, dy, need_dx, need[2], b is not None and need[3], x2=x2,
                                     gate_holder=ctx.gate_holder, dw_sink=True)
         dx2 = None

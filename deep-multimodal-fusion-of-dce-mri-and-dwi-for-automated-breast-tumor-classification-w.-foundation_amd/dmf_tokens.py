@@ -200,14 +200,19 @@ class _TokensToMapFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, t, h, w, dtype):
         b, n, e = t.shape
-        o = cast_bf16(t) if dtype == torch.bfloat16 else t.contiguous().clone()
+        if dtype == torch.bfloat16:
+            o = cast_bf16(t)
+        elif dtype == torch.float16:
+            o = t.contiguous().to(torch.float16)
+        else:
+            o = t.contiguous().clone()
         return o.view(b, h, w, e).permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dm):
         b, e, h, w = dm.shape
         d = dm.permute(0, 2, 3, 1).contiguous()
-        d = cast_f32(d) if d.dtype == torch.bfloat16 else d
+        d = cast_f32(d) if d.dtype == torch.bfloat16 else d.float()
         return d.view(b, h * w, e), None, None, None
 
 
@@ -448,6 +453,14 @@ def _check_tokens(what, x, e, head_dim=8):
         raise ValueError(f"{what}: expected tokens [B, N, {e}], got {tuple(x.shape)}")
     if x.shape[1] % 8:
         raise ValueError(f"{what}: token count {x.shape[1]} must be a multiple of 8")
+
+
+def token_dtype(dt):
+    """The token kernels' arithmetic type for a model compute dtype: the GEMM / attention / LayerNorm token
+    kernels run bf16 or f32, so under the reference's "16-mixed" (fp16 CNN encoders) the token stages run
+    bf16 -- the other 16-bit mixed-precision type, fp32 accumulation either way -- and cast at their
+    boundaries (TransformerStage / the ViT backbone under "16-mixed")."""
+    return torch.bfloat16 if dt == torch.float16 else dt
 
 
 def _check_dtype(what, dtype):

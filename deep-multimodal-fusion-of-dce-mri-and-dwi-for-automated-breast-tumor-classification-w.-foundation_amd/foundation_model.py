@@ -304,7 +304,9 @@ class VisionTransformerFeatures(nn.Module):
             t = torch.nn.functional.pad(t, (0, 0, 0, npad - n))
         feats = []
         for i, blk in enumerate(m.blocks):
-            t = D.transformer_block(t, blk, None, blk._sites, dt, n_valid=n, gammas=(self._ones, self._ones))
+            # (the token kernels run bf16 under "16-mixed": D.token_dtype; the maps leave in dt)
+            t = D.transformer_block(t, blk, None, blk._sites, D.token_dtype(dt), n_valid=n,
+                                    gammas=(self._ones, self._ones))
             f = t[:, 1:n].reshape(b, gh, gw, e).to(dt)                        # prefix token dropped
             feats.append(O.as_nhwc(f.permute(0, 3, 1, 2)))
             if on_feature is not None:

@@ -49,7 +49,7 @@ class PatchEmbed(nn.Module):
     use_fp8 = False
 
     def forward(self, x):
-        dt = getattr(self, "compute_dtype", torch.bfloat16)
+        dt = D.token_dtype(getattr(self, "compute_dtype", torch.bfloat16))
         x = O.as_nhwc(x.to(dt))
         if self.use_fp8 and dt == torch.bfloat16:
             y = D.patch_embed_fp8(x, self.proj, _caches(self.proj))
@@ -87,7 +87,7 @@ class MultiHeadSelfAttention(nn.Module):
 
     def forward(self, x):
         rng = _rng_if(x, self.attn_drop, self.proj_drop)
-        return D.multihead_self_attention(x, self, rng, getattr(self, "compute_dtype", torch.bfloat16))
+        return D.multihead_self_attention(x, self, rng, D.token_dtype(getattr(self, "compute_dtype", torch.bfloat16)))
 
 
 class MLP(nn.Module):
@@ -102,7 +102,7 @@ class MLP(nn.Module):
 
     def forward(self, x):
         rng = _rng_if(x, self.drop)
-        return D.mlp(x, self, rng, getattr(self, "compute_dtype", torch.bfloat16))
+        return D.mlp(x, self, rng, D.token_dtype(getattr(self, "compute_dtype", torch.bfloat16)))
 
 
 class TransformerBlock(nn.Module):
@@ -119,7 +119,8 @@ class TransformerBlock(nn.Module):
 
     def forward(self, x):
         rng = _rng_if(x, self.attn.attn_drop, self.attn.proj_drop, self.mlp.drop)
-        return D.transformer_block(x.float(), self, rng, self._sites, getattr(self, "compute_dtype", torch.bfloat16))
+        return D.transformer_block(x.float(), self, rng, self._sites,
+                                   D.token_dtype(getattr(self, "compute_dtype", torch.bfloat16)))
 
 
 class TransformerEncoder(nn.Module):
@@ -143,10 +144,9 @@ class TransformerStage(nn.Module):
         self.tokens_to_map = TokensToFeatureMap(dim=dim)
 
     def forward(self, x):
+        # under "16-mixed" the CNN around the stage runs fp16 and the stage bf16 (D.token_dtype): the map
+        # leaves in the dtype it came in
         dt = getattr(self, "compute_dtype", torch.bfloat16)
-        if dt == torch.float16:
-            raise TypeError("TransformerStage: the token GEMM / attention kernels run bf16 or f32; "
-                            "compute dtype float16 (precision '16-mixed') covers the CNN encoders only")
         tokens, hw = self.patch_embed(x)
         tokens = self.transformer(tokens)
         return D.tokens_to_map(tokens, hw[0], hw[1], dt)

@@ -21,11 +21,13 @@ import parameters as PR
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A file-store rendezvous (unique path per call): no TCP port to race for when several
+    multi-process tests (or pytest-xdist workers) start at once. The workers' MASTER_PORT is unused."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="dmf_gloo_", suffix=".store")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _models(seed=0):
@@ -64,8 +66,7 @@ def _local_grads(P, dwi, dce, fm, batch):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         torch.set_num_threads(2)
         from dmf_dp import allgather_rows, allreduce_mean_, rank_strided_indices
@@ -100,7 +101,7 @@ def test_two_rank_bucket_allreduce_matches_ddp_mean():
     bucket, allp, alll, auc = q.get(timeout=500)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+        assert p.exitcode == 0, f"worker exit code {p.exitcode}"
 
     # single-process reference of the same semantics: mean of per-shard grads
     from dmf_dp import rank_strided_indices
@@ -126,8 +127,7 @@ def test_two_rank_bucket_allreduce_matches_ddp_mean():
 
 
 def _fit_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         from dmf_fit import allgather_valid_rows, allreduce_sum, shard
         import metrics as MT
@@ -167,7 +167,7 @@ def test_epoch_driver_shards_and_gathers_every_volume_once():
     items0, allp, ally, cnt, auc, auc_single = q.get(timeout=250)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+        assert p.exitcode == 0, f"worker exit code {p.exitcode}"
     assert len(items0) == 4 and cnt == 11 and allp.shape == (11, 4)
     assert sorted(ally.tolist()) == sorted((torch.arange(11) % 4).tolist())
     assert auc == pytest.approx(auc_single, abs=1e-12)
@@ -198,8 +198,7 @@ def _val_data(n):
 
 
 def _validate_worker(rank, world, port, n, bs, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         from dmf_fit import FusionFit
 
@@ -233,7 +232,7 @@ def test_validate_skips_padding_only_batch():
     val_loss, auc, n_val = q.get(timeout=250)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+        assert p.exitcode == 0, f"worker exit code {p.exitcode}"
     x, y = _val_data(n)
     logits = x.flatten(1)[:, :4] * 3.0
     assert n_val == n

@@ -68,3 +68,37 @@ def test_shortcut_handoff_matches_autograd_add(arena):
     for a, b in zip(got, ref):
         scale = b.abs().max().item()
         assert (a - b).abs().max().item() <= 1e-5 * max(scale, 1e-6), (a - b).abs().max().item()
+
+
+def test_handoff_skipped_when_the_producer_is_pruned():
+    """torch.autograd.grad(..., inputs=[h]) runs only the nodes between the loss and h: the shortcut
+    producers of both blocks are pruned, so each consumer must hand its shortcut gradient to autograd
+    (torch._C._will_engine_execute_node) instead of parking it for a backward that never runs -- nothing
+    is left in GRAD_STASH, and the gradient at h equals the hand-off-free run's."""
+    torch.manual_seed(6)
+    m = Chain().to(DEV).train()
+    ca = m.caches
+    x = torch.randn(4, 16, 24, 24, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    gout = torch.randn(4, 128, 24, 24, device=DEV)
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+
+    def run(handoff):
+        m.load_state_dict(state)
+        O.SHORTCUT_HANDOFF = handoff
+        try:
+            y = O.conv_bn_act(x, m.c0, ca["c0"], m.b0, "relu")
+            h = O.conv_bn_act(y, m.c1, ca["c1"], m.b1, "relu")
+            y = O.conv_bn_act(h, m.c2, ca["c2"], m.b2, "relu", res=y)
+            h = O.conv_bn_act(y, m.c3, ca["c3"], m.b3, "relu")
+            out = O.conv_bn_act(h, m.c4, ca["c4"], m.b4, "relu", skip=(y, m.cd, ca["cd"], m.bd))
+            (g,) = torch.autograd.grad((out.float() * gout).sum(), inputs=[h])
+            torch.cuda.synchronize()
+            return g
+        finally:
+            O.SHORTCUT_HANDOFF = True
+
+    ref = run(False)
+    got = run(True)
+    assert not O.GRAD_STASH, "a shortcut gradient was parked for a pruned producer"
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 1e-5 * max(scale, 1e-6)

@@ -475,6 +475,34 @@ def test_hybrid_encoder_forward_backward():
             _close(prm.grad, gr[name].grad, 1e-3, name)
 
 
+def test_hybrid_encoder_under_16_mixed():
+    """precision "16-mixed" (fp16 compute): the CNN encoder runs fp16 and the hybrid
+    TransformerStage bf16 (dmf_tokens.token_dtype), casting at its boundaries -- the forward and backward
+    run (they used to raise) and the logits stay within the 16-bit tolerance of the f32 parity run."""
+    P = PR.small_parameters(channels=(16, 32, 64), input_size=64, dropout=0.0, use_backbone=False)
+    mp = P["dwi_model_parameters"]
+    mp["use_hybrid_transformer"] = True
+    mp["transformer_embed_dim"] = 256
+    mp["transformer_depth"] = 2
+    mp["transformer_heads"] = 4
+    mp["mask_stage"] = "f2"
+    torch.manual_seed(9)
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", copy.deepcopy(P), None), True)
+    e32 = copy.deepcopy(enc)
+    MM.set_compute_dtype(enc, torch.float16)
+    MM.set_compute_dtype(e32, torch.float32)
+    enc, e32 = enc.to(DEV).eval(), e32.to(DEV).eval()
+    g = torch.Generator().manual_seed(10)
+    x = (0.5 + torch.randn(2, 14, 64, 64, generator=g) / 6).clamp(0, 1).to(DEV)
+    lo, aux, _ = enc(x)
+    l32, aux32, _ = e32(x)
+    assert aux["raw_feats"][2].dtype == torch.float16
+    _close(lo, l32, 3e-2, "logits fp16 vs f32")
+    (aux["raw_feats"][2].float().square().mean()).backward()
+    grads = [p.grad for n, p in enc.named_parameters() if n.startswith("transformer.") and p.grad is not None]
+    assert grads and all(torch.isfinite(g_).all() for g_ in grads)
+
+
 def test_patch_embed_fp8_matches_quantised_reference():
     """Config 5's fp8 patch-embed (PatchEmbed.proj, transformer_model.py:17-22,
     on e4m3 MFMA): the quantiser must produce OCP e4m3fn bytes identical to

@@ -103,3 +103,23 @@ def test_vit_bf16_config_shape():
     print(f"ViT bf16 S=256: block-map rel L2 {max(errs):.2e} (max over 12), logits max abs "
           f"{(lo.float().cpu() - rlo).abs().max().item():.2e}")
     assert max(errs) < 3e-2
+
+
+def test_vit_under_16_mixed():
+    """precision "16-mixed" (fp16 compute): the ViT's patch conv and feature maps run fp16,
+    its transformer blocks bf16 (dmf_tokens.token_dtype); forward + backward run (they used to raise in
+    the token kernels' dtype check) and the block maps stay within the 16-bit tolerance of the oracle."""
+    enc, ref = _pair(64, seed=3, dtype=torch.float16)
+    enc.train()
+    ref.train()
+    x = torch.rand(2, 14, 64, 64)
+    feats = enc.backbone_adapter.backbone(x.to(DEV))
+    with torch.no_grad():
+        rfeats = ref.backbone_adapter.backbone(x)
+    assert all(f.dtype == torch.float16 for f in feats)
+    errs = [_rel(a, b) for a, b in zip(feats, rfeats)]
+    assert max(errs) < 3e-2, errs
+    lo, aux, _ = enc(x.to(DEV))
+    (lo.float().square().mean() + aux["raw_feats"][2].float().square().mean()).backward()
+    grads = [p.grad for n, p in enc.named_parameters() if ".model." in n and p.grad is not None]
+    assert len(grads) > 100 and all(torch.isfinite(g).all() for g in grads)

@@ -257,11 +257,12 @@ def test_knobs_are_set_from_code_only():
         O.set_knobs(no_such_knob=1)
 
 
-def test_precision_16_mixed_maps_to_fp16_and_transformer_refuses_it():
+def test_precision_16_mixed_maps_to_fp16_and_token_stages_to_bf16():
     """precision "16-mixed" (the reference's default, parameters_generate.py:211)
-    selects fp16 compute for the CNN encoders; the TransformerStage token kernels
-    are bf16/f32 only and say so instead of running a wrong dtype."""
-    import transformer_model as TM
+    selects fp16 compute for the CNN encoders; the token kernels (TransformerStage,
+    the ViT blocks) run bf16 under it (dmf_tokens.token_dtype) --
+    tests/test_gpu_transformer.py / test_gpu_vit.py run both on the GPU."""
+    import dmf_tokens as D
 
     P = copy.deepcopy(PR.default_parameters())
     assert PR.compute_dtype_of(P) == torch.bfloat16
@@ -269,9 +270,9 @@ def test_precision_16_mixed_maps_to_fp16_and_transformer_refuses_it():
     assert PR.compute_dtype_of(P) == torch.float16
     P["precision"] = "32"
     assert PR.compute_dtype_of(P) == torch.float32
-    st = MM.set_compute_dtype(TM.TransformerStage(8, 32, depth=1, heads=2), torch.float16)
-    with pytest.raises(TypeError, match="float16"):
-        st(torch.zeros(1, 8, 8, 8))
+    assert D.token_dtype(torch.float16) == torch.bfloat16
+    assert D.token_dtype(torch.bfloat16) == torch.bfloat16
+    assert D.token_dtype(torch.float32) == torch.float32
 
 
 def test_bench_dtype_options_and_peaks():
