@@ -61,6 +61,41 @@ def main():
     S = torch.empty((b, h, n, n), dtype=torch.float32, device=dev)
     flops = {"qkv": 2 * r * 3 * e * e, "fc1": 2 * r * hid * e, "fc2": 2 * r * e * hid, "proj": 2 * r * e * e,
              "QK^T": 2 * b * h * n * n * d}
+    # the same linears on the conv engine (a 1x1 conv over [r, e] rows viewed as NHWC (32, e, 24, 24)):
+    # persistent 256x256 tiles, register epilogue (bias + act, bf16 out)
+    import dmf_ops as O
+
+    def conv_case(w, bias, k_in, act):
+        conv = torch.nn.Conv2d(k_in, w.shape[0], 1).to(dev)
+        with torch.no_grad():
+            conv.weight.copy_(w.float()[:, :, None, None])
+            conv.bias.copy_(bias)
+        conv.requires_grad_(False)
+        xin = (x if k_in == e else hbuf).view(b, 24, 24, k_in).permute(0, 3, 1, 2)
+        caches = (O.WeightCache(), O.WeightCache())
+
+        def run():
+            with torch.no_grad():
+                y, _ = O._conv_forward_raw(xin, conv.weight, conv.bias, O.ConvGeom(conv), caches, False, act)
+            return y
+        return run
+    cases["qkv  conv-engine"] = conv_case(wq, bq, e, "none")
+    cases["fc1  conv-engine gelu"] = conv_case(w1, b1, e, "gelu")
+    cases["fc2  conv-engine (bf16 out)"] = conv_case(w2, bp, hid, "none")
+    cases["proj conv-engine (bf16 out)"] = conv_case(wp, bp, e, "none")
+    sm_p = torch.empty((b, h, n, n), **bf)
+
+    def softmax():
+        import dmf_native as N
+        N.call("dmf_softmax_dropout", S.data_ptr(), n, b * h * n, n, n, float(d ** -0.5), 0.0, None, 0,
+               sm_p.data_ptr(), sm_p.data_ptr(), n, O._stream())
+    cases["softmax (128 x 576 rows)"] = softmax
+    o = torch.empty((r, e), **bf)
+    cases["PV   (576x128x576 x128)"] = lambda: D.gemm(o, sm_p, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e,
+                                                        batch=(b, h), sa=(h * n * n, n * n), sb=(n * 3 * e, d),
+                                                        sc=(n * e, d), b_off=2 * e)
+    flops["softmax"] = 1.0
+    flops["PV"] = 2 * b * h * n * n * d
     for name, fn in cases.items():
         us = timed(fn, a.reps)
         fl = flops[name.split()[0]]
