@@ -244,7 +244,9 @@ def gemm_probes(trainer, batch):
     import dmf_ops as O
 
     fam = {"fp8_gemm": ("e4m3 patch-embed GEMM (k_gemm_fp8, v_mfma_f32_16x16x32_fp8_fp8)", FP8_MFMA_PEAK_TFLOPS),
-           "tok_gemm": ("token GEMMs (k_gemm_bf16: qkv, QK^T, PV, proj, fc1, fc2)", BF16_MFMA_PEAK_TFLOPS)}
+           "tok_gemm": ("token GEMMs of the frozen encoders' blocks: qkv on the conv engine's persistent 1x1 form, "
+                        "QK^T + PV inside the fused attention (dmf_flash_attn_fwd), fc1 on k_gemm_bf16 (its dropout); "
+                        "proj / fc2 (f32 residual epilogues) not probed", BF16_MFMA_PEAK_TFLOPS)}
     recs = {k: [] for k in fam}
     for k in fam:
         O.PROBE[k] = recs[k]

@@ -2607,6 +2607,7 @@ KNOBS = {
     "se_fused": ("dmf_ops", "SE_FUSED"),
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
+    "token_fwd_fused": ("dmf_tokens", "FWD_FUSED"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),
     "parallel_dead": ("model_module", "PARALLEL_DEAD"),
     "device_loss": ("train_fusion", "DEVICE_LOSS"),

@@ -383,6 +383,113 @@ class _BlockFn(torch.autograd.Function):
                 dfc1w, dfc1b, dfc2w, dfc2b, dg1, dg2)
 
 
+# ------------------------------------------------ forward-only block (no autograd graph)
+# A block whose parameters and input need no gradient (frozen encoders, mode A) skips everything a
+# backward would read: the pre-activation / branch copies (aux), the undropped probabilities; the
+# attention core is one fused launch (dmf_flash_attn_fwd: no [b*h, n, n] scores or probabilities in
+# HBM) for head dim 128, and the qkv linear runs on the conv engine's persistent 1x1 form (register
+# epilogue; tools/gemm_bench.py: 18432x1536x512 63.6 -> 41.4 us). fc1 follows it when no dropout
+# follows the GELU (the conv epilogue has none). Knob "token_fwd_fused" = False keeps the training
+# path's kernels.
+FWD_FUSED = True
+_FA_HEAD_DIM = 128
+
+
+class _Geom1x1:
+    stride, padding, dilation, kernel_size = (1, 1), (0, 0), (1, 1), (1, 1)
+
+
+_G1 = O.ConvGeom(_Geom1x1)
+
+
+def _linear_conv(x2d, lin, b, n, act="none"):
+    """act(x W^T + bias) of [b*n, K] bf16 token rows as a 1x1 conv over the NHWC view (b, K, n, 1): the
+    conv engine's forms with their bias + activation epilogue, bf16 out (forward only). Its launches are
+    recorded in the token-GEMM probe family."""
+    r, k = x2d.shape
+    nout = lin.weight.shape[0]
+    caches = lin.__dict__.get("_dmf_conv_caches")
+    if caches is None:
+        caches = lin.__dict__["_dmf_conv_caches"] = (O.WeightCache(), O.WeightCache())
+    x4 = x2d.view(b, n, 1, k).permute(0, 3, 1, 2)
+    saved = O.PROBE["conv_fwd"]
+    O.PROBE["conv_fwd"] = O.PROBE["tok_gemm"]
+    try:
+        y, _ = O._conv_forward_raw(x4, lin.weight.view(nout, k, 1, 1), lin.bias, _G1, caches, False, act)
+    finally:
+        O.PROBE["conv_fwd"] = saved
+    return y.permute(0, 2, 3, 1).reshape(r, nout)
+
+
+def _linear_conv_ok(x2d, lin, n):
+    r, k = x2d.shape
+    return (x2d.dtype == torch.bfloat16 and x2d.is_contiguous() and k % 64 == 0 and lin.weight.shape[0] % 8 == 0
+            and r % n == 0 and x2d.data_ptr() % 16 == 0)
+
+
+def flash_attention(qkv, b, n, nv, e, heads, p_attn, rng, site):
+    """o [b*n, e] bf16 = dropout(softmax(q k^T / sqrt(d))) v per head from the packed qkv rows (one launch)."""
+    o = torch.empty((b * n, e), dtype=torch.bfloat16, device=qkv.device)
+    d = e // heads
+    args = (qkv.data_ptr(), qkv.stride(0), b, n, int(nv), e, heads, float(d ** -0.5), float(p_attn), O._p(rng),
+            int(site), o.data_ptr(), e)
+    N.call("dmf_flash_attn_fwd", *args, _s())
+    probe = O.PROBE["tok_gemm"]
+    if probe is not None:
+        probe.append({"fn": "dmf_flash_attn_fwd", "args": args, "keep": (qkv, o, rng),
+                      "flops": 2.0 * 2.0 * b * heads * n * n * d,
+                      "bytes": 2.0 * (b * n * 3 * e + b * n * e), "shape": ("flash", b, n, e, heads)})
+    return o
+
+
+def _block_fwd_nograd(x, blk, rng, cfg, g1, g2):
+    heads, eps1, eps2, p_attn, p_proj, p_mlp, sites, cdt, nv = cfg
+    s_attn, s_proj, s_m1, s_m2 = sites
+    at, ml = blk.attn, blk.mlp
+    b, n, e = x.shape
+    d = e // heads
+    bf = dict(dtype=cdt, device=x.device)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    x2d = x.contiguous().view(b * n, e)
+    wp, w2 = _wcast(cdt, at.proj.weight, ml.fc2.weight)
+    r = b * n
+    # attention branch: x1 = x + drop(proj(attn(ln1(x)))) * g1
+    ln1, _ = ln_fwd(x2d, blk.norm1.weight, blk.norm1.bias, eps1, cdt)
+    if _linear_conv_ok(ln1, at.qkv, n):
+        qkv = _linear_conv(ln1, at.qkv, b, n)
+    else:
+        (wq,) = _wcast(cdt, at.qkv.weight)
+        qkv = gemm(torch.empty((r, 3 * e), **bf), ln1, wq, r, 3 * e, e, lda=e, ldb=e, ldc=3 * e, bias=at.qkv.bias)
+    if d == _FA_HEAD_DIM and cdt == torch.bfloat16:
+        o = flash_attention(qkv, b, n, nv or n, e, heads, p_attn, rng, s_attn)
+    else:
+        S = torch.empty((b, heads, n, n), **f32)
+        gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * 3 * e, d),
+             sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
+        P = torch.empty((b, heads, n, n), **bf)
+        N.call("dmf_softmax_dropout" + _sfx(cdt), S.data_ptr(), n, b * heads * n, n, int(nv or n),
+               float(d ** -0.5), float(p_attn), O._p(rng), int(s_attn), P.data_ptr(), P.data_ptr(), n, _s())
+        del S
+        o = gemm(torch.empty((r, e), **bf), P, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads),
+                 sa=(heads * n * n, n * n), sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
+    del qkv
+    x1 = gemm(torch.empty((r, e), **f32), o, wp, r, e, e, lda=e, ldb=e, ldc=e, bias=at.proj.bias, colscale=g1,
+              res=x2d, dropout_p=p_proj, rng=rng, site=s_proj)
+    del o
+    # MLP branch: x2 = x1 + drop(fc2(drop(gelu(fc1(ln2(x1)))))) * g2
+    ln2, _ = ln_fwd(x1, blk.norm2.weight, blk.norm2.bias, eps2, cdt)
+    hid = ml.fc1.weight.shape[0]
+    if p_mlp == 0.0 and _linear_conv_ok(ln2, ml.fc1, n):
+        h = _linear_conv(ln2, ml.fc1, b, n, act="gelu")
+    else:
+        (w1,) = _wcast(cdt, ml.fc1.weight)
+        h = gemm(torch.empty((r, hid), **bf), ln2, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=ml.fc1.bias,
+                 act="gelu", dropout_p=p_mlp, rng=rng, site=s_m1)
+    x2 = gemm(torch.empty((r, e), **f32), h, w2, r, e, hid, lda=hid, ldb=hid, ldc=e, bias=ml.fc2.bias, colscale=g2,
+              res=x1, dropout_p=p_mlp, rng=rng, site=s_m2)
+    return x2.view(b, n, e)
+
+
 def _branch_input(x, cdt):
     b, n, e = x.shape
     x2d = x.reshape(b * n, e)
@@ -515,6 +622,9 @@ def transformer_block(x, blk, rng, sites, dtype=torch.bfloat16, n_valid=None, ga
     cfg = (at.num_heads, blk.norm1.eps, blk.norm2.eps, p_attn, p_proj, p_mlp, tuple(sites), dtype, n_valid)
     g1 = blk.gamma1 if gammas is None else gammas[0]
     g2 = blk.gamma2 if gammas is None else gammas[1]
+    if FWD_FUSED and dtype == torch.bfloat16 and not O.needs_grad(x, *blk.parameters(), g1, g2):
+        with torch.no_grad():
+            return _block_fwd_nograd(x, blk, rng, cfg, g1, g2)
     return _BlockFn.apply(x, cfg, rng, blk.norm1.weight, blk.norm1.bias, at.qkv.weight, at.qkv.bias, at.proj.weight,
                           at.proj.bias, blk.norm2.weight, blk.norm2.bias, ml.fc1.weight, ml.fc1.bias,
                           ml.fc2.weight, ml.fc2.bias, g1, g2)

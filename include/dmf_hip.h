@@ -67,7 +67,8 @@ int dmf_conv_last_form(void);
  * mode; 4 = persistent 256x256 form on / off; 6 = benchmark-only skip bits of the
  * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
  * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 14 / 15 = tiles a launch
- * needs for the 256x128 / 256x256 forms.
+ * needs for the 256x128 / 256x256 forms; 16 = 4-wave square tile; 17 = timing-only
+ * bits of dmf_conv2d_fwd_bn_act (64 skip the barrier, 128 the arena reads).
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
@@ -508,6 +509,15 @@ int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha
  * probs_dropped = dropout(probs, p) (bf16, the P operand of P v); Philox
  * element index row*L + col at dropout site `site`. Columns >= Lv are key
  * padding (token counts rounded up to the GEMM granule): probability 0. */
+/* Fused attention forward for a block that builds no autograd graph (frozen encoders, mode A;
+ * transformer_model.py:100-116): o = dropout(softmax(q k^T * scale)) v per (batch item, head) from the
+ * packed qkv rows [batch*n][ldq] (q | k | v, E columns each, head h at columns h*128), bf16, fp32
+ * accumulation; keys >= nv are padding; the dropout mask is dmf_softmax_dropout's (element index
+ * ((b*heads + h)*n + query)*n + key, Philox site `site`), the row sum keeps the pre-dropout
+ * probabilities. o [batch*n][ldo] bf16, head h at columns h*128. Head dim 128 only (E = 128*heads);
+ * the scores and probabilities never reach HBM (csrc/attn.hip). */
+int dmf_flash_attn_fwd(const void* qkv, int ldq, int batch, int n, int nv, int E, int heads, float scale,
+                       float dropout_p, const unsigned long long* rng, int site, void* o, int ldo, void* stream);
 int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, int Lv, float scale, float dropout_p,
                         const unsigned long long* rng, int site, void* probs, void* probs_dropped, int ldp,
                         void* stream);

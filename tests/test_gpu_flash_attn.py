@@ -1,0 +1,113 @@
+"""GPU: the fused attention forward (dmf_flash_attn_fwd, csrc/attn.hip) of a
+block that builds no autograd graph (transformer_model.py:100-116): against a
+float64 restatement of softmax(q k^T / sqrt(d)) v with key padding, against the
+unfused path it replaces (QK^T GEMM -> k_softmax_drop -> PV GEMM) with the same
+Philox dropout masks, and the whole forward-only TransformerBlock
+(dmf_tokens._block_fwd_nograd: the conv-engine qkv linear, the fused attention,
+no backward copies) against the autograd block's forward."""
+import copy
+
+import pytest
+import torch
+
+import dmf_native as N
+import dmf_ops as O
+import dmf_tokens as D
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _qkv(b, n, e, seed=0):
+    torch.manual_seed(seed)
+    return (torch.randn(b * n, 3 * e, device=DEV) * 1.5).bfloat16()
+
+
+def _ref64(qkv, b, n, nv, e, heads):
+    d = e // heads
+    x = qkv.double().view(b, n, 3, heads, d)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    s = q @ k.transpose(-1, -2) * d ** -0.5
+    s[..., nv:] = float("-inf")
+    return (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(b * n, e)
+
+
+@pytest.mark.parametrize("b,n,nv,heads", [(2, 576, 576, 4), (3, 264, 257, 4), (1, 100, 100, 2), (2, 64, 40, 6)])
+def test_flash_attention_vs_float64(b, n, nv, heads):
+    e = 128 * heads
+    qkv = _qkv(b, n, e)
+    o = D.flash_attention(qkv, b, n, nv, e, heads, 0.0, None, 0)
+    torch.cuda.synchronize()
+    ref = _ref64(qkv, b, n, nv, e, heads)
+    err = (o.double() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+def _unfused(qkv, b, n, nv, e, heads, p, rng, site):
+    d = e // heads
+    S = torch.empty((b, heads, n, n), dtype=torch.float32, device=DEV)
+    D.gemm(S, qkv, qkv, n, n, d, lda=3 * e, ldb=3 * e, ldc=n, batch=(b, heads), sa=(n * 3 * e, d),
+           sb=(n * 3 * e, d), sc=(heads * n * n, n * n), b_off=e)
+    P = torch.empty((b, heads, n, n), dtype=torch.bfloat16, device=DEV)
+    Pd = torch.empty_like(P)
+    N.call("dmf_softmax_dropout", S.data_ptr(), n, b * heads * n, n, nv, float(d ** -0.5), float(p), O._p(rng),
+           site, P.data_ptr(), Pd.data_ptr(), n, O._stream())
+    o = torch.empty((b * n, e), dtype=torch.bfloat16, device=DEV)
+    D.gemm(o, Pd, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e, batch=(b, heads), sa=(heads * n * n, n * n),
+           sb=(n * 3 * e, d), sc=(n * e, d), b_off=2 * e)
+    return o
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_matches_unfused_with_dropout(p):
+    """Same Philox masks (element ((b*h + head)*n + query)*n + key) as k_softmax_drop: the outputs
+    agree to the bf16 rounding of the probabilities."""
+    b, n, nv, heads, e = 4, 576, 570, 4, 512
+    qkv = _qkv(b, n, e, seed=1)
+    rng = torch.tensor([0x1234_5678_9ABC, 77], dtype=torch.int64, device=DEV)
+    o1 = D.flash_attention(qkv, b, n, nv, e, heads, p, rng, 5)
+    o2 = _unfused(qkv, b, n, nv, e, heads, p, rng, 5)
+    torch.cuda.synchronize()
+    scale = o2.float().abs().max().item()
+    err = (o1.float() - o2.float()).abs().max().item()
+    assert err <= 1.5e-2 * scale, (err, scale)
+    if p > 0:
+        # a different site draws different masks: the outputs must move well past that bound
+        o3 = D.flash_attention(qkv, b, n, nv, e, heads, p, rng, 6)
+        assert (o3.float() - o2.float()).abs().max().item() > 5e-2 * scale
+
+
+def test_forward_only_block_matches_autograd_forward():
+    """dmf_tokens.transformer_block with no grad (the conv-engine qkv, the fused attention, no backward
+    copies) against the same block's autograd forward (train mode: dropout on, same rng snapshot)."""
+    import transformer_model as TM
+
+    torch.manual_seed(3)
+    blk = TM.TransformerBlock(512, heads=4).to(DEV).train()
+    with torch.no_grad():
+        blk.gamma1.fill_(0.5)
+        blk.gamma2.fill_(0.7)
+    x = torch.randn(4, 576, 512, device=DEV)
+    rng = O.RNG.snapshot(torch.device(DEV))
+    with torch.no_grad():
+        y_fused = D.transformer_block(x, blk, rng, blk._sites, torch.bfloat16)
+    prev = D.FWD_FUSED
+    D.FWD_FUSED = False
+    try:
+        with torch.no_grad():
+            y_ref = D.transformer_block(x, blk, rng, blk._sites, torch.bfloat16)
+    finally:
+        D.FWD_FUSED = prev
+    torch.cuda.synchronize()
+    d = (y_fused - y_ref).abs().max().item()
+    assert d <= 2e-2 * y_ref.abs().max().item(), d
+    # and the path really is the fused one
+    recs = []
+    O.PROBE["tok_gemm"] = recs
+    try:
+        with torch.no_grad():
+            D.transformer_block(x, blk, rng, blk._sites, torch.bfloat16)
+    finally:
+        O.PROBE["tok_gemm"] = None
+    names = [r["fn"] for r in recs]
+    assert "dmf_flash_attn_fwd" in names and any(n.startswith("dmf_conv2d") for n in names), names

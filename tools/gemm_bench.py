@@ -94,6 +94,10 @@ def main():
     cases["PV   (576x128x576 x128)"] = lambda: D.gemm(o, sm_p, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e,
                                                         batch=(b, h), sa=(h * n * n, n * n), sb=(n * 3 * e, d),
                                                         sc=(n * e, d), b_off=2 * e)
+    cases["flash QK^T.softmax.PV (fused)"] = lambda: D.flash_attention(qkv, b, n, n, e, h, 0.0, None, 0)
+    cases["flash + dropout 0.1"] = lambda: D.flash_attention(qkv, b, n, n, e, h, 0.1, rng, 3)
+    rng = O.RNG.snapshot(torch.device(dev))
+    flops["flash"] = 2 * flops["QK^T"]
     flops["softmax"] = 1.0
     flops["PV"] = 2 * b * h * n * n * d
     for name, fn in cases.items():
