@@ -658,8 +658,6 @@ def main():
 
     args.batch = args.batch or 32
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
-    if args.config == 5 and dtype == torch.float16:
-        raise SystemExit("config 5 (TransformerStage token GEMMs) runs bf16 / fp32 only")
     P = PR.default_parameters()
     if args.config == 5:
         # hybrid CNN -> Transformer stage (E=512, depth 6, 4 heads, patch 2;

@@ -518,6 +518,10 @@ int dmf_gemm_f32(int out_dtype, int ta, int tb, int M, int N, int K, float alpha
  * the scores and probabilities never reach HBM (csrc/attn.hip). */
 int dmf_flash_attn_fwd(const void* qkv, int ldq, int batch, int n, int nv, int E, int heads, float scale,
                        float dropout_p, const unsigned long long* rng, int site, void* o, int ldo, void* stream);
+/* dmf_flash_attn_fwd variant (A/B only): 1 = 64 queries per block, 64-key tiles, one tile in flight;
+ * 2 (default) = 128 queries per block, 64-key tiles, one in flight; 3 = 128 queries, 32-key tiles,
+ * two in flight */
+int dmf_flash_attn_tune(int var);
 int dmf_softmax_dropout(const float* S, int lds, long long rows, int L, int Lv, float scale, float dropout_p,
                         const unsigned long long* rng, int site, void* probs, void* probs_dropped, int ldp,
                         void* stream);

@@ -37,6 +37,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated case-name prefixes")
     a = ap.parse_args()
     dev = "cuda"
     r, e, hid, b, h, n = 32 * 576, 512, 2048, 32, 4, 576
@@ -94,13 +95,24 @@ def main():
     cases["PV   (576x128x576 x128)"] = lambda: D.gemm(o, sm_p, qkv, n, d, n, tb=1, lda=n, ldb=3 * e, ldc=e,
                                                         batch=(b, h), sa=(h * n * n, n * n), sb=(n * 3 * e, d),
                                                         sc=(n * e, d), b_off=2 * e)
-    cases["flash QK^T.softmax.PV (fused)"] = lambda: D.flash_attention(qkv, b, n, n, e, h, 0.0, None, 0)
-    cases["flash + dropout 0.1"] = lambda: D.flash_attention(qkv, b, n, n, e, h, 0.1, rng, 3)
+    import dmf_native as N
+
+    def flash(nq, p):
+        def run():
+            N.call("dmf_flash_attn_tune", nq)
+            D.flash_attention(qkv, b, n, n, e, h, p, rng if p > 0 else None, 3)
+        return run
+    for var in (1, 2, 3):
+        cases[f"flash QK^T.softmax.PV var={var}"] = flash(var, 0.0)
+        cases[f"flash + dropout 0.1 var={var}"] = flash(var, 0.1)
     rng = O.RNG.snapshot(torch.device(dev))
     flops["flash"] = 2 * flops["QK^T"]
     flops["softmax"] = 1.0
     flops["PV"] = 2 * b * h * n * n * d
+    only = [c for c in a.only.split(",") if c]
     for name, fn in cases.items():
+        if only and not any(name.startswith(o) for o in only):
+            continue
         us = timed(fn, a.reps)
         fl = flops[name.split()[0]]
         print(f"{name:30s} {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)", flush=True)
