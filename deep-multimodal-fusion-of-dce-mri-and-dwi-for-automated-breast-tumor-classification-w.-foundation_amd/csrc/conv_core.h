@@ -121,12 +121,6 @@ __host__ __device__ constexpr int conv_lds_main(int esize, int bm = CBM, int bn 
 }
 constexpr int CONV_LDS_EXTRA = 64 + CTHREADS * 2 * 8;  // flag + reducer doubles
 
-// bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
-// an XCD; give each XCD a contiguous range of logical tiles.
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  const int q = nblk / 8, r = nblk % 8, xcd = b % 8, loc = b / 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-}
 
 constexpr int BUF_FLAGS_EP = 0x00020000;  // buffer descriptor word 3 (as BUF_FLAGS below)
 

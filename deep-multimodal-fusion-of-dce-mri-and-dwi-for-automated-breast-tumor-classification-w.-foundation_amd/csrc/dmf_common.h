@@ -313,6 +313,13 @@ __device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// bijective XCD-aware remap of a linear block id (T1): blocks b and b+8 share
+// an XCD; give each XCD a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, xcd = b % 8, loc = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
 // ------------------------------------------------ raw buffer loads / LDS-DMA
 // Out-of-range lanes (tile edges, zero padding) get an offset past the buffer
 // and read zeros from the range check: no branches, no 64-bit address math.

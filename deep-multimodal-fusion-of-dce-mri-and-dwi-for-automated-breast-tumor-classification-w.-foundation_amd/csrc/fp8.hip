@@ -189,9 +189,151 @@ __global__ void __launch_bounds__(256, 2) k_gemm_fp8(const uint8_t* __restrict__
   }
 }
 
+// The same product on the block-scaled MFMA: v_mfma_scale_f32_16x16x128_f8f6f4 with e4m3 operands
+// and unit E8M0 block scales (127 = 2^0) is the plain e4m3 dot product at twice the clock rate of
+// the non-scaled form (MI355X_MICROARCH.md, MFMA table); the per-row / per-channel scales stay in
+// the epilogue. Tile (16*FM) x 256 with 4 waves of (16*FM) x 64 (one wave per SIMD, FM x 4
+// fragments, one MFMA per fragment per 128-B K-step). FM = 9 puts configuration 5's 18432 x 512
+// patch-embed GEMM on exactly 256 workgroups (the 128x128 form ran 576 = 1.125 rounds of two per
+// CU). A and B rows go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into a 3-stage ring,
+// two K-steps in flight, the conv engine's source-side XOR swizzle (k_conv_fwd_wide); rows past
+// M / N and K-chunks past K read zeros from the buffer range check. A lane's 32 K-bytes are the
+// two 16-B chunks 2*(lane>>4), +1 of its row, for A and B alike (the sum over K is the same for
+// any K order shared by both operands).
+typedef __attribute__((ext_vector_type(8))) int f8_v8i;
+constexpr int F8S_BN = 256, F8S_NST = 3;
+__host__ __device__ constexpr int f8s_stage(int fm) { return (16 * fm + F8S_BN) * 128; }
+__host__ __device__ constexpr int f8s_lds(int fm) {
+  return F8S_NST * f8s_stage(fm) > 16 * fm * (F8S_BN + 8) * 2 ? F8S_NST * f8s_stage(fm) : 16 * fm * (F8S_BN + 8) * 2;
+}
+
+template <int FM>
+__global__ void __launch_bounds__(256, 1) k_gemm_fp8_dma(const uint8_t* __restrict__ A, int lda,
+                                                         const float* __restrict__ as, const uint8_t* __restrict__ B,
+                                                         int ldb, const float* __restrict__ bs,
+                                                         const float* __restrict__ bias, bf16_t* __restrict__ Cm,
+                                                         int ldc, int M, int N, int K, int ntiles) {
+  constexpr int TBM = 16 * FM, GA = TBM / 8, G = GA + F8S_BN / 8, NGW = (G + 3) / 4;
+  constexpr int STAGE = f8s_stage(FM);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lin / ntiles, nt = lin % ntiles;
+  const int m0 = mt * TBM, n0 = nt * F8S_BN;
+  const int lr = lane >> 3, lc = (lane & 7) ^ lr;
+  const unsigned lds0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  const v4i_t ra = buf_rsrc(A, (long long)M * lda), rb = buf_rsrc(B, (long long)N * ldb);
+
+  // this wave's 8-row groups g = wid + 4t: A rows m0 + 8g + lr for g < GA, B rows n0 + 8(g - GA) + lr
+  const int ng = (G - wid + 3) / 4;
+  unsigned vo[NGW];
+#pragma unroll
+  for (int t = 0; t < NGW; ++t) {
+    const int g = wid + 4 * t;
+    if (g < GA) {
+      const int r = m0 + 8 * g + lr;
+      vo[t] = r < M ? (unsigned)(r * lda + lc * 16) : BUF_OOB;
+    } else {
+      const int r = n0 + 8 * (g - GA) + lr;
+      vo[t] = r < N ? (unsigned)(r * ldb + lc * 16) : BUF_OOB;
+    }
+  }
+  const int nk = (K + 127) / 128;
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * 128;
+    const bool kok = k0 + lc * 16 < K;
+#pragma unroll
+    for (int t = 0; t < NGW; ++t) {
+      if (t < ng) {
+        const int g = wid + 4 * t;
+        dma16(g < GA ? ra : rb, kok ? vo[t] : BUF_OOB, (unsigned)k0, lds0 + stage * STAGE + g * 1024);
+      }
+    }
+  };
+
+  f8_f32x4 acc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f8_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int c0 = ((2 * fg) ^ (fr & 7)) * 16, c1 = ((2 * fg + 1) ^ (fr & 7)) * 16;
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire this wave's DMA of K-step kt (kt+1's stay in flight), then the barrier publishes every
+    // wave's part and orders the refill of stage (kt+2)%3 after all reads of kt-1 (see k_conv_fwd_wide)
+    if (kt + 1 < nk) {
+      if (ng == NGW) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NGW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NGW - 1) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (kt + 2 < nk) issue(kt + 2, st == 0 ? 2 : st - 1);
+    const char* S = smem + st * STAGE;
+    f8_v8i bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const char* p = S + (TBM + wid * 64 + j * 16 + fr) * 128;
+      const int4 lo = *(const int4*)(p + c0), hi = *(const int4*)(p + c1);
+      bv[j] = f8_v8i{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const char* p = S + (i * 16 + fr) * 128;
+      const int4 lo = *(const int4*)(p + c0), hi = *(const int4*)(p + c1);
+      const f8_v8i av = f8_v8i{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+    }
+    st = st == 2 ? 0 : st + 1;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // epilogue as k_gemm_fp8: scales + bias into a bf16 LDS image, then 16-B row stores
+  constexpr int CST = F8S_BN + 8;
+  bf16_t* Cs = (bf16_t*)smem;
+  float rsc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + i * 16 + fg * 4 + e;
+      rsc[i][e] = m < M ? as[m] : 0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wid * 64 + j * 16 + fr, n = n0 + cl;
+    const float sb = n < N ? bs[n] : 0.f, bb = (bias && n < N) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(i * 16 + fg * 4 + e) * CST + cl] = f2bf(acc[i][j][e] * rsc[i][e] * sb + bb);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < TBM * (F8S_BN / 8); idx += 256) {
+    const int row = idx / (F8S_BN / 8), ch = idx - row * (F8S_BN / 8);
+    const int m = m0 + row, n = n0 + ch * 8;
+    if (m < M && n < N) *(uint4*)(Cm + (size_t)m * ldc + n) = *(const uint4*)(Cs + row * CST + ch * 8);
+  }
+}
+
+// 0: the 128x128 non-scaled form; 1 (default): the block-scaled 144x256 LDS-DMA form where it applies
+static int g_fp8_var = 1, g_fp8_last = -1;
+
 }  // namespace dmf
 
 using namespace dmf;
+
+extern "C" int dmf_gemm_fp8_tune(int var) {
+  DMF_CHECK_ARG(var == 0 || var == 1, "dmf_gemm_fp8_tune: var %d (0 or 1)", var);
+  g_fp8_var = var;
+  return 0;
+}
+extern "C" int dmf_gemm_fp8_last_form(void) { return g_fp8_last; }
 
 extern "C" int dmf_patch_quant_fp8(const void* x, int N, int H, int W, int C, int ldx, int P, void* q, int ldq,
                                    float* row_scale, void* stream) {
@@ -223,6 +365,17 @@ extern "C" int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const f
                 "dmf_gemm_fp8: K (%d) and row strides must be multiples of 16 bytes", K);
   DMF_CHECK_ARG(N % 8 == 0 && ldc % 8 == 0 && ((uintptr_t)C % 16) == 0,
                 "dmf_gemm_fp8: N (%d) and ldc must be multiples of 8, C 16-byte aligned (16-B row stores)", N);
+  // block-scaled form: 32-bit buffer offsets; at least one chip-filling round of its tiles
+  if (g_fp8_var == 1 && N >= F8S_BN && (long long)M * lda < (1LL << 31) && (long long)N * ldb < (1LL << 31) &&
+      (long long)cdiv(M, 144) * cdiv(N, F8S_BN) >= 256) {
+    const int nt = cdiv(N, F8S_BN);
+    hipLaunchKernelGGL(k_gemm_fp8_dma<9>, dim3((unsigned)(cdiv(M, 144) * nt)), dim3(256), (size_t)f8s_lds(9),
+                       (hipStream_t)stream, (const uint8_t*)A, lda, a_scale, (const uint8_t*)B, ldb, b_scale, bias,
+                       (bf16_t*)C, ldc, M, N, K, nt);
+    DMF_LAUNCH_CHECK("dmf_gemm_fp8");
+    g_fp8_last = 1;
+    return 0;
+  }
   const int ntiles = cdiv(N, F8BN);
   const long long blocks = (long long)cdiv(M, F8BM) * ntiles;
   DMF_CHECK_ARG(blocks < (1LL << 31), "dmf_gemm_fp8: grid too large");
@@ -230,5 +383,6 @@ extern "C" int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const f
                      (const uint8_t*)A, lda, a_scale, (const uint8_t*)B, ldb, b_scale, bias, (bf16_t*)C, ldc, M, N, K,
                      ntiles);
   DMF_LAUNCH_CHECK("dmf_gemm_fp8");
+  g_fp8_last = 0;
   return 0;
 }

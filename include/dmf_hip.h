@@ -577,12 +577,20 @@ int dmf_dropout_keep_mask(const unsigned long long* rng, int site, long long n, 
  * dmf_weight_quant_fp8: torch weight [E][C][P][P] fp32 -> q [E][P*P*C] e4m3,
  *   col_scale[e] = amax_e / 448.
  * dmf_gemm_fp8: C (bf16) [M][ldc] = a_scale[m] * b_scale[n] * A[m].B[n] + bias[n]
- *   (A [M][lda], B [N][ldb], K-contiguous e4m3; K, lda, ldb multiples of 16). */
+ *   (A [M][lda], B [N][ldb], K-contiguous e4m3; K, lda, ldb multiples of 16).
+ *   Where N >= 256 and the 144x256 tiles fill the chip: the block-scaled
+ *   v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales, twice the non-scaled rate),
+ *   LDS-DMA staged; otherwise the 128x128 non-scaled form.
+ * dmf_gemm_fp8_tune: 1 (default) allows the block-scaled form, 0 forces the
+ *   128x128 form (A/B runs). dmf_gemm_fp8_last_form: the form of the last
+ *   launch (0 / 1; -1 before any). */
 int dmf_patch_quant_fp8(const void* x, int N, int H, int W, int C, int ldx, int P, void* q, int ldq,
                         float* row_scale, void* stream);
 int dmf_weight_quant_fp8(const float* w, int E, int C, int P, void* q, float* col_scale, void* stream);
 int dmf_gemm_fp8(int M, int N, int K, const void* A, int lda, const float* a_scale, const void* B, int ldb,
                  const float* b_scale, const float* bias, void* C, int ldc, void* stream);
+int dmf_gemm_fp8_tune(int var);
+int dmf_gemm_fp8_last_form(void);
 
 /* ------------------------------------------------------------ data path
  *  fp32 NCHW-contiguous planes [N*C][HW].

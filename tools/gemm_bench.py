@@ -105,6 +105,22 @@ def main():
     for var in (1, 2, 3):
         cases[f"flash QK^T.softmax.PV var={var}"] = flash(var, 0.0)
         cases[f"flash + dropout 0.1 var={var}"] = flash(var, 0.1)
+    # the fp8 patch-embed GEMM (18432 x 512 x 1024, e4m3) in both forms
+    kp = 1024
+    qa = (torch.randn(r, kp, device=dev) * 100).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    qb = (torch.randn(e, kp, device=dev) * 100).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    ra_, rb_ = torch.rand(r, device=dev), torch.rand(e, device=dev)
+    y8 = torch.empty((r, e), **bf)
+
+    def fp8(var):
+        def run():
+            N.call("dmf_gemm_fp8_tune", var)
+            N.call("dmf_gemm_fp8", r, e, kp, qa.data_ptr(), kp, ra_.data_ptr(), qb.data_ptr(), kp, rb_.data_ptr(),
+                   bp.data_ptr(), y8.data_ptr(), e, O._stream())
+        return run
+    cases["fp8  (18432x512x1024) 128x128"] = fp8(0)
+    cases["fp8  (18432x512x1024) scaled 144x256"] = fp8(1)
+    flops["fp8"] = 2 * r * e * kp
     rng = O.RNG.snapshot(torch.device(dev))
     flops["flash"] = 2 * flops["QK^T"]
     flops["softmax"] = 1.0
@@ -116,6 +132,7 @@ def main():
         us = timed(fn, a.reps)
         fl = flops[name.split()[0]]
         print(f"{name:30s} {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)", flush=True)
+    N.call("dmf_gemm_fp8_tune", 1)
 
 
 if __name__ == "__main__":
