@@ -221,10 +221,14 @@ def wgrad_probe(trainer, batch, dtype):
     recs.clear()
     peak = mfma_peak(dtype)
     achieved = flops / n / (avg_ms * 1e-3) / 1e12
+    traffic = pmc_traffic("wgrad")
     return {"kernel": "conv2d weight gradient (k_conv_wgrad_dma / k_conv_wgrad_tr + k_wgrad_reduce), %s" %
                       DT_TAG[dtype],
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
+            "frac": round(achieved / peak, 4),
+            "traffic": traffic["traffic_mb_per_launch"] if traffic else None,
+            "traffic_unit": "MB per weight-gradient + split-reduce pair (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, " +
+                            (traffic["source"] if traffic else "no PMC summary") + ")",
             "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
             "avg_wgrad_kernel_us": round(avg_ms_wg * 1e3, 2),
             "avg_reduce_us": round((avg_ms - avg_ms_wg) * 1e3, 2),
@@ -243,7 +247,9 @@ def gemm_probes(trainer, batch):
     (as roofline_probe); each family against its own dense MFMA peak."""
     import dmf_ops as O
 
-    fam = {"fp8_gemm": ("e4m3 patch-embed GEMM (k_gemm_fp8, v_mfma_f32_16x16x32_fp8_fp8)", FP8_MFMA_PEAK_TFLOPS),
+    fam = {"fp8_gemm": ("e4m3 patch-embed GEMM (k_gemm_fp8_dma: 144x256 tiles, v_mfma_scale_f32_16x16x128_f8f6f4 "
+                        "with unit scales; k_gemm_fp8 128x128 where those tiles do not fill the chip)",
+                        FP8_MFMA_PEAK_TFLOPS),
            "tok_gemm": ("token GEMMs of the frozen encoders' blocks: qkv on the conv engine's persistent 1x1 form, "
                         "QK^T + PV inside the fused attention (dmf_flash_attn_fwd), fc1 on k_gemm_bf16 (its dropout); "
                         "proj / fc2 (f32 residual epilogues) not probed", BF16_MFMA_PEAK_TFLOPS)}
@@ -327,12 +333,13 @@ def roofline_probe(trainer, batch, dtype):
     }
 
 
-def pmc_traffic():
-    """HBM bytes per conv-forward launch from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from two
-    rocprofv3 --pmc passes of this bench on an MI355X)."""
+def pmc_traffic(family=""):
+    """HBM bytes per launch of a kernel family from the newest committed PMC
+    summary (profiles/*_pmc_traffic.json for the conv forward,
+    *_pmc_traffic_<family>.json for others; written by tools/pmc_traffic.py from
+    two rocprofv3 --pmc passes of this bench on an MI355X)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic%s.json" % ("_" + family if family else ""))))
     if not files:
         return None
     with open(files[-1]) as f:

@@ -288,8 +288,10 @@ __device__ __forceinline__ void philox(uint32_t key0, uint32_t key1, uint32_t c0
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
-    const uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    // one v_mad_u64_u32 per product instead of v_mul_hi_u32 + v_mul_lo_u32 (both quarter rate)
+    const uint64_t p0 = (uint64_t)M0 * c0, p1 = (uint64_t)M1 * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     const uint32_t n0 = hi1 ^ c1 ^ key0, n2 = hi0 ^ c3 ^ key1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     key0 += W0; key1 += W1;

@@ -25,15 +25,19 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--match", default=r"k_conv_fwd_ps|k_conv_fwd_pp|k_conv_fwd_sq|k_conv_fwd_wide|k_conv_fwd_buf|k_conv_stem|k_conv_igemm<unsigned short, false")
     ap.add_argument("--json", default="")
+    ap.add_argument("--count", default="", help="launches = dispatches matching this regex (default: every "
+                    "matched dispatch); e.g. the weight-gradient kernel of a wgrad + split-reduce pair")
     a = ap.parse_args()
     fe = load(f"{a.dir}/FETCH_SIZE/run_counter_collection.csv")
     wr = load(f"{a.dir}/WRITE_SIZE/run_counter_collection.csv")
     rx = re.compile(a.match)
     f_k = [v for _, n, v in fe if rx.search(n)]
     w_k = [v for _, n, v in wr if rx.search(n)]
-    n = min(len(f_k), len(w_k))
-    fetch = 2.0 * sum(f_k[:n]) * 1024 / n
-    write = sum(w_k[:n]) * 1024 / n
+    if len(f_k) != len(w_k):
+        raise SystemExit(f"the two passes matched {len(f_k)} / {len(w_k)} dispatches")
+    n = len([1 for _, nm, _ in fe if rx.search(nm) and re.search(a.count, nm)]) if a.count else len(f_k)
+    fetch = 2.0 * sum(f_k) * 1024 / n
+    write = sum(w_k) * 1024 / n
     print(f"launches {n}: fetch {fetch / 1e6:.2f} MB (x2 corrected), write {write / 1e6:.2f} MB, "
           f"traffic {(fetch + write) / 1e6:.2f} MB per launch")
     if a.json:
