@@ -798,11 +798,15 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
   float* sbias = sred + 2 * TBN * 2;
   if constexpr (EPI == 8 || EPI == 11) {
     // the known BatchNorm(s) of the affine epilogue: [scale | shift (+ the shortcut's shift) | shortcut scale]
+    // (aff_acc: the BatchNorm finalized here from the float64 arena, dmf_conv2d_fwd_affine_acc; block 0
+    // also moves the running statistics)
     for (int i = tid; i < a.Nout; i += NTH) {
-      sbias[i] = a.out_ss[i];
-      sbias[a.Nout + i] = a.out_ss[a.Nout + i] + (EPI == 11 ? a.res_ss[a.Nout + i] : 0.f);
+      const float2 ss = a.aff_acc ? gbar_bn_channel(a, i, blockIdx.x == 0) : make_float2(a.out_ss[i], a.out_ss[a.Nout + i]);
+      sbias[i] = ss.x;
+      sbias[a.Nout + i] = ss.y + (EPI == 11 ? a.res_ss[a.Nout + i] : 0.f);
       if (EPI == 11) sbias[2 * a.Nout + i] = a.res_ss[i];
     }
+    if (a.aff_acc && blockIdx.x == 0 && tid == 0 && a.fin.nbt) *a.fin.nbt += 1;
     __syncthreads();
   } else if (a.bias) {
     for (int i = tid; i < a.Nout; i += NTH) sbias[i] = a.bias[i];
@@ -887,7 +891,8 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
     // wave's part and orders the refill of the other stage after every wave's reads of the previous
     // step. After an epilogue its 16 stores (+2 atomics) are younger: leave them in flight.
     if (epi) {
-      if ((a.stat_acc > 0 || a.stat_acc == -1) && wm == 0)
+      // (EPI 8 / 11 with aff_acc carry an arena in stat_acc but issue no statistics atomics)
+      if ((EPI == 0 || EPI == 5 || EPI == 12) && (a.stat_acc > 0 || a.stat_acc == -1) && wm == 0)
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(EPI_VM + 2) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(EPI_VM) : "memory");
       epi = false;
@@ -1253,7 +1258,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
       const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
       // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
       // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
-      const int epi = a.out_ss != nullptr ? (a.res_ss != nullptr ? 11 : 8)
+      const int epi = (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
                       : a.y == nullptr ? 12
                       : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
                                               : 1 + a.act;
@@ -1375,7 +1380,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = is16(dtype) ? 2 : 4;
-  const size_t lds_total = plan.ps ? (size_t)PS_LDS + (a.out_ss ? (a.res_ss ? 3 : 2) * (size_t)a.Nout * 4
+  const size_t lds_total = plan.ps ? (size_t)PS_LDS + ((a.out_ss || a.aff_acc) ? (a.res_ss ? 3 : 2) * (size_t)a.Nout * 4
                                                      : a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
@@ -1391,7 +1396,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
-  DMF_CHECK_ARG(a.out_ss == nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
+  DMF_CHECK_ARG((a.out_ss == nullptr && !a.aff_acc) || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
                 "%s: the affine epilogue needs the persistent 1x1 form (no bias, one source, a shortcut)", what);
   DMF_CHECK_ARG(a.y != nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.M % QBM == 0 &&
                                    a.stat_acc >= 1),
@@ -1711,6 +1716,30 @@ extern "C" int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int
   a.ldr = ldr;
   a.res_ss = res_scale_shift;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_affine");
+}
+
+extern "C" int dmf_conv2d_fwd_affine_acc(int dtype, const void* x, int N, int H, int W, int Cin, int ldx,
+                                         const void* w, int Cout, int stride, void* y, int Ho, int Wo, int ldy,
+                                         const dmf_bn_desc* bn, const void* res, int ldr,
+                                         const float* res_scale_shift, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, 1, 1, stride, 0, 1, nullptr, y, Ho,
+                           Wo, ldy, DMF_ACT_RELU, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_affine_acc");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && bn && bn->acc && ((uintptr_t)bn->acc % 16) == 0 && bn->replicas >= 1 &&
+                    bn->replicas <= GBAR_MAX_REPLICAS && bn->count > 0.0 && res && ldr % 8 == 0 &&
+                    ((uintptr_t)res % 16) == 0 && ((long long)a.M * ldr * 2 < (1LL << 31)),
+                "dmf_conv2d_fwd_affine_acc: needs a 16-bit dtype, a float64 arena of <= %d replicas and an aligned "
+                "shortcut", GBAR_MAX_REPLICAS);
+  a.aff_acc = 1;
+  a.partials = (float*)const_cast<double*>(bn->acc);
+  a.stat_acc = bn->replicas;
+  a.fin = BnFin{bn->gamma, bn->beta, bn->running_mean, bn->running_var, bn->num_batches_tracked, bn->momentum,
+                bn->eps, bn->count, bn->unbias_count, 1, nullptr, nullptr};
+  a.res = res;
+  a.ldr = ldr;
+  a.res_ss = res_scale_shift;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_affine_acc");
 }
 
 // The grid-barrier BatchNorm apply needs one output tile per block and every block resident: the

@@ -54,6 +54,10 @@ struct ConvArgs {
   const void* res;
   int ldr;
   const float* res_ss;
+  // aff_acc: EPI 8 / 11 take the BatchNorm's scale / shift from the float64 arena (partials, stat_acc
+  // replicas, fin) when they stage them, instead of from out_ss (dmf_conv2d_fwd_affine_acc: the
+  // finalize launch between the two passes folded in); block 0 also moves the running statistics
+  int aff_acc;
   // grid-barrier BatchNorm apply (dmf_conv2d_fwd_bn_act; k_conv_fwd_pp EPI 13, conv_epilogue of
   // k_conv_fwd_wide): [counter 0, counter 1, generation] of this BatchNorm's launch site, or null
   unsigned* gbar;

@@ -335,12 +335,14 @@ __device__ __forceinline__ v4i_t buf_rsrc(const void* p, long long bytes) {
 // One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc+voff(+soff) to LDS
 // [lds, lds + 1 KiB). Inline asm so the compiler neither tracks it (it would
 // drain vmcnt(0) before every ds_read it cannot disambiguate) nor reorders it
-// across LDS accesses; m0 is saved and restored.
+// across LDS accesses; m0 is saved and restored. lds and soff are wave-uniform by contract; the
+// readfirstlane keeps them in SGPRs where the compiler cannot prove it (a no-op on SGPR values).
 __device__ __forceinline__ void dma16(v4i_t rsrc, unsigned voff, unsigned soff, unsigned lds) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+               : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds)),
+                 "s"(__builtin_amdgcn_readfirstlane(soff))
                : "memory");
 }
 

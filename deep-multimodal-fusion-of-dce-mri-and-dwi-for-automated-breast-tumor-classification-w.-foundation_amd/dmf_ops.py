@@ -1105,6 +1105,9 @@ TWO_PASS_BN = True
 # measured (profiles/r05g_two_pass_split.txt): the recompute pays for the saved write + apply pass up to
 # K = 256 (layer1-3 conv3s); at K = 512 (layer4, 512 -> 2048) the second K loop costs what it saves
 TWO_PASS_MAX_K = 256
+# the finalize between the passes folded into pass 2's staging (dmf_conv2d_fwd_affine_acc); knob
+# "two_pass_fold" = False keeps the dmf_bn_finalize_acc launch
+TWO_PASS_FOLD = True
 
 
 def _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
@@ -1218,6 +1221,7 @@ def _conv_bn_two_pass(x, conv, caches, bn, res, skip):
     dtc = dt(x)
     with torch.no_grad():
         wk = caches[0].get(conv.weight, x.dtype, cx, 0)
+        desc = None
         if bn.training or bn.running_mean is None:
             acc = _bn_acc(co, dev)
             ss = torch.empty(2 * co, dtype=torch.float32, device=dev)
@@ -1225,7 +1229,10 @@ def _conv_bn_two_pass(x, conv, caches, bn, res, skip):
             _conv_launch("dmf_conv2d_fwd_stats",
                          (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, ho, wo, acc.data_ptr(),
                           BN_ACC_REPLICAS), (x, wk, acc), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=0)
-            _finalize_acc(_bn_desc(bn, acc, m, 0.0, ss, save), co)
+            desc = _bn_desc(bn, acc, m, 0.0, ss, save)
+            if not TWO_PASS_FOLD:
+                _finalize_acc(desc, co)
+                desc = None
         else:
             ss, _ = _bn_finalize(None, m, bn)
         ss_r = None
@@ -1236,10 +1243,16 @@ def _conv_bn_two_pass(x, conv, caches, bn, res, skip):
             if desc_r is not None:
                 _finalize_acc(desc_r, co)
         out = empty_nhwc(n, co, ho, wo, x.dtype, dev)
-        _conv_launch("dmf_conv2d_fwd_affine",
-                     (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, out.data_ptr(), ho, wo,
-                      nhwc(out)[4], ss.data_ptr(), res.data_ptr(), nhwc(res)[4], _p(ss_r)),
-                     (x, wk, out, ss, res, ss_r), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=2)
+        if desc is not None:
+            _conv_launch("dmf_conv2d_fwd_affine_acc",
+                         (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, out.data_ptr(), ho, wo,
+                          nhwc(out)[4], ctypes.byref(desc), res.data_ptr(), nhwc(res)[4], _p(ss_r)),
+                         (x, wk, out, desc, res, ss_r), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=2)
+        else:
+            _conv_launch("dmf_conv2d_fwd_affine",
+                         (dtc, x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), co, g.stride, out.data_ptr(), ho, wo,
+                          nhwc(out)[4], ss.data_ptr(), res.data_ptr(), nhwc(res)[4], _p(ss_r)),
+                         (x, wk, out, ss, res, ss_r), x, n, h, wd, cx, co, 1, 1, g, ho, wo, y_maps=2)
     return out
 
 
@@ -2606,6 +2619,7 @@ KNOBS = {
     "linear_sink": ("dmf_ops", "LINEAR_SINK"),
     "se_fused": ("dmf_ops", "SE_FUSED"),
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
+    "two_pass_fold": ("dmf_ops", "TWO_PASS_FOLD"),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
     "token_fwd_fused": ("dmf_tokens", "FWD_FUSED"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),

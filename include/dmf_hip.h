@@ -243,6 +243,13 @@ typedef struct dmf_bn_desc {
   float eps;
   int replicas;                 /* of acc (dmf_conv2d_fwd_acc) */
 } dmf_bn_desc;
+/* dmf_conv2d_fwd_affine with the BatchNorm finalized inside the launch: every block reads the
+ * (sum, sum^2) replicas of bn->acc (<= 8) for the channels it stages and block 0 moves the running
+ * statistics and num_batches_tracked (bn->scale_shift / save_mean_invstd are not written): the
+ * dmf_bn_finalize_acc launch between the two passes of the two-pass conv3 folded in. */
+int dmf_conv2d_fwd_affine_acc(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                              int Cout, int stride, void* y, int Ho, int Wo, int ldy, const dmf_bn_desc* bn,
+                              const void* res, int ldr, const float* res_scale_shift, void* stream);
 /* y = drop(act(x*a + [res*r | res])) with a = finalize(bn) when bn is given
  * (else scale_shift, else identity) and r likewise from res_bn /
  * res_scale_shift (residual optional). One launch replaces

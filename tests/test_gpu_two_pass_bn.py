@@ -1,5 +1,6 @@
 """GPU: the two-pass BatchNorm fusion of a forward-only Bottleneck conv3
-(dmf_conv2d_fwd_stats -> dmf_bn_finalize_acc -> dmf_conv2d_fwd_affine) against
+(dmf_conv2d_fwd_stats -> dmf_bn_finalize_acc -> dmf_conv2d_fwd_affine, or with the finalize folded
+into the second pass: dmf_conv2d_fwd_affine_acc) against
 a float64 CPU restatement of conv -> BN(batch statistics) -> + shortcut -> ReLU
 (foundation_model.py Bottleneck.forward, the reference's timm Bottleneck), and
 against the conv + dmf_bn_apply form it replaces (knob two_pass_bn off):
@@ -79,17 +80,23 @@ def _ref(x, xr, mods, training):
     return (z + r).relu(), stats
 
 
-def _run(x, xr, mods, two_pass):
+def _run(x, xr, mods, two_pass, fold=True, finalizes=None):
     dm = [copy.deepcopy(m).to(DEV) for m in mods]
     calls = []
-    orig = O._conv_bn_two_pass
+    orig, orig_fin = O._conv_bn_two_pass, O._finalize_acc
 
     def counted(*a, **k):
         calls.append(1)
         return orig(*a, **k)
 
-    O.set_knobs(two_pass_bn=two_pass)
+    def counted_fin(*a, **k):
+        if finalizes is not None:
+            finalizes.append(1)
+        return orig_fin(*a, **k)
+
+    O.set_knobs(two_pass_bn=two_pass, two_pass_fold=fold)
     O._conv_bn_two_pass = counted
+    O._finalize_acc = counted_fin
     try:
         with torch.no_grad():
             xd, xrd = _to_dev(x), _to_dev(xr)
@@ -101,8 +108,8 @@ def _run(x, xr, mods, two_pass):
                 y = O.conv_bn_act(xd, dm[0], c, dm[1], "relu", res=xrd)
         torch.cuda.synchronize()
     finally:
-        O._conv_bn_two_pass = orig
-        O.set_knobs(two_pass_bn=True)
+        O._conv_bn_two_pass, O._finalize_acc = orig, orig_fin
+        O.set_knobs(two_pass_bn=True, two_pass_fold=True)
     return y.float().cpu(), dm, len(calls)
 
 
@@ -111,18 +118,24 @@ def _run(x, xr, mods, two_pass):
 SHAPES = [(16, 256, 32, 32, 1024, 0, 1), (32, 128, 64, 64, 512, 256, 2), (32, 64, 64, 64, 256, 64, 1)]
 
 
+# fold: the BatchNorm finalize between the passes folded into pass 2 (dmf_conv2d_fwd_affine_acc) or the
+# separate dmf_bn_finalize_acc launch + dmf_conv2d_fwd_affine
+@pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("training", [True, False])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_two_pass_conv3(shape, training):
+def test_two_pass_conv3(shape, training, fold):
     proj = shape[5] > 0
     x, xr, mods = _case(shape, proj, training)
     dev_ok = N.load().dmf_conv2d_fwd_affine_ok(N.BF16, shape[0], shape[2] // shape[6], shape[3] // shape[6],
                                                shape[1], shape[4], 1)
     assert dev_ok, "test shape must take the persistent plan"
     ref, stats = _ref(x, xr, mods, training)
-    y2, dm2, n2 = _run(x, xr, mods, True)
+    fins = []
+    y2, dm2, n2 = _run(x, xr, mods, True, fold=fold, finalizes=fins)
     y1, dm1, n1 = _run(x, xr, mods, False)
     assert (n2, n1) == (1, 0)
+    # the main BatchNorm's finalize launch only without the fold; a projection shortcut's BN keeps its own
+    assert len(fins) == (int(not fold) + int(proj) if training else 0), fins
     scale = ref.abs().max().item()
     e2 = (y2.double() - ref).abs().max().item() / scale
     e1 = (y1.double() - ref).abs().max().item() / scale

@@ -111,15 +111,47 @@ def fusion(a):
     o_hip, order, h1 = record(fm, a.depth)
     o_ref, _, h2 = record(fr, a.depth)
     o_amp, _, h3 = record(mods[2], a.depth)
+    # the classifier head (AdaptiveAvgPool -> Flatten -> Linear): its pooled input and the logits; the HIP
+    # model calls it functionally (O.gap + O.linear), so O.linear is wrapped for the head's weight
+    import dmf_ops as O
+    orig_linear = O.linear
+
+    def linear(x, w, b=None, *args, **kw):
+        y = orig_linear(x, w, b, *args, **kw)
+        if w is fm.classifier[2].weight:
+            o_hip.setdefault("classifier.pooled", x.detach().float().cpu())
+            o_hip.setdefault("classifier.logits", y.detach().float().cpu())
+        return y
+    O.linear = linear
+    order += ["classifier.pooled", "classifier.logits"]
+    # the oracle calls F.linear on the head's weight (oracle/model.py FusionModel.forward)
+    import torch.nn.functional as F
+    orig_f_linear = F.linear
+    heads = {id(fr.classifier[2].weight): o_ref, id(mods[2].classifier[2].weight): o_amp}
+
+    def f_linear(x, w, b=None):
+        y = orig_f_linear(x, w, b)
+        d = heads.get(id(w))
+        if d is not None:
+            d.setdefault("classifier.pooled", x.detach().float())
+            d.setdefault("classifier.logits", y.detach().float())
+        return y
+    F.linear = f_linear
     with torch.no_grad():
         lm._shared_step(bd, "train", return_preds=True)
         torch.cuda.synchronize()
         OL.fusion_shared_step(dwi_r, dce_r, fr, bt, P, cw, epoch=0)
         with torch.autocast("cpu", dtype=torch.bfloat16):
             OL.fusion_shared_step(mods[0], mods[1], mods[2], bt, P, cw, epoch=0)
+    O.linear = orig_linear
+    F.linear = orig_f_linear
     for h in h1 + h2 + h3:
         h.remove()
     report(order, o_hip, o_ref, o_amp)
+    for k in ("classifier.pooled", "classifier.logits"):
+        print(k, "hip", o_hip[k].flatten()[:8].tolist())
+        print(k, "ref", o_ref[k].flatten()[:8].tolist())
+        print(k, "amp", o_amp[k].flatten()[:8].tolist())
 
 
 def report(order, o_hip, o_ref, o_amp):
