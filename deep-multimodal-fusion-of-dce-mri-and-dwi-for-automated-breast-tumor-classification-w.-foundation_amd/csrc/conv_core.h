@@ -91,8 +91,17 @@ __device__ __forceinline__ void apply_act_arr(int act, float (&v)[N]) {
       for (int e = 0; e < N; ++e) v[e] = fmaxf(v[e], 0.f);
       break;
     case DMF_ACT_GELU:
+      if constexpr (N % 2 == 0) {
 #pragma unroll
-      for (int e = 0; e < N; ++e) v[e] = gelu_f(v[e]);
+        for (int e = 0; e < N; e += 2) {
+          const dmf_f2 g = gelu_f2(dmf_f2{v[e], v[e + 1]});
+          v[e] = g.x;
+          v[e + 1] = g.y;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) v[e] = gelu_f(v[e]);
+      }
       break;
     case DMF_ACT_SIGMOID:
 #pragma unroll
@@ -357,6 +366,13 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
       const float w = ok ? 1.f : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
+    } else if constexpr (EPI - 1 == DMF_ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const dmf_f2 g = gelu_f2(dmf_f2{v[e], v[e + 1]});
+        v[e] = g.x;
+        v[e + 1] = g.y;
+      }
     } else if constexpr (EPI > 1 && EPI < 5) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = apply_act<(EPI < 5 ? EPI - 1 : 0)>(v[e]);

@@ -201,6 +201,24 @@ __device__ __forceinline__ float erf_gelu(float x) {
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erf_gelu(x * 0.70710678118654752440f));
 }
+// the same on two values with the packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per
+// instruction; the reciprocal and exponential stay scalar): ~12 instead of ~20 VALU instructions per value
+typedef float dmf_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dmf_f2 gelu_f2(dmf_f2 x) {
+  const dmf_f2 z = x * 0.70710678118654752440f;
+  const dmf_f2 az = __builtin_elementwise_abs(z);
+  const dmf_f2 d = __builtin_elementwise_fma(az, (dmf_f2)0.3275911f, (dmf_f2)1.0f);
+  const dmf_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  dmf_f2 p = __builtin_elementwise_fma((dmf_f2)1.061405429f, t, (dmf_f2)-1.453152027f);
+  p = __builtin_elementwise_fma(p, t, (dmf_f2)1.421413741f);
+  p = __builtin_elementwise_fma(p, t, (dmf_f2)-0.284496736f);
+  p = __builtin_elementwise_fma(p, t, (dmf_f2)0.254829592f) * t;
+  const dmf_f2 q = -az * az;
+  const dmf_f2 e = {__expf(q.x), __expf(q.y)};
+  const dmf_f2 r = (dmf_f2)1.0f - p * e;
+  const dmf_f2 erf = {copysignf(r.x, z.x), copysignf(r.y, z.y)};
+  return 0.5f * x * ((dmf_f2)1.0f + erf);
+}
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float cdf = 0.5f * (1.0f + erf_gelu(x * 0.70710678118654752440f));
   const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);

@@ -301,11 +301,19 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += RES == 2 ? r[k] * rs8[k] + rh8[k] : r[k];
     }
+    if constexpr (ACT == DMF_ACT_GELU) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
-      else if (ACT == DMF_ACT_GELU) v[k] = gelu_f(v[k]);
-      else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+      for (int k = 0; k < 8; k += 2) {
+        const dmf_f2 g = gelu_f2(dmf_f2{v[k], v[k + 1]});
+        v[k] = g.x;
+        v[k + 1] = g.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
+        else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+      }
     }
     if (p > 0.f) {
       bool keep[4];

@@ -2620,6 +2620,7 @@ KNOBS = {
     "se_fused": ("dmf_ops", "SE_FUSED"),
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
     "two_pass_fold": ("dmf_ops", "TWO_PASS_FOLD"),
+    "wgrad_xcd": ("wgrad_tune", 6),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
     "token_fwd_fused": ("dmf_tokens", "FWD_FUSED"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),

@@ -78,7 +78,8 @@ int dmf_conv_tune(int key, int value);
  * key 3 = the 256x256 LDS-DMA tile where Cout and KH*KW*Cin are multiples of 256:
  * 0 off / 1 (default) for weights of >= 2^18 entries / 2 wherever legal;
  * key 4 = split-lane reducers of dmf_conv2d_wgrad_reduce at >= 16 splits on (1) / off;
- * key 5 = blocks the pixel splits aim for, percent of one chip-filling wave (10..400, default 50). */
+ * key 5 = blocks the pixel splits aim for, percent of one chip-filling wave (10..400, default 50);
+ * key 6 = split-major block order per XCD (the tiles of one pixel split share one L2) on (1) / off (0). */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */
