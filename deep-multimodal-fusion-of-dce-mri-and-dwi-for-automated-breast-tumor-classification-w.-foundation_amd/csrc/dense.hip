@@ -924,6 +924,103 @@ __global__ void __launch_bounds__(256) k_dense_rows(const float* __restrict__ in
   }
 }
 
+// The whole excitation in ONE workgroup for the small SEs of the path (N <= 64 rows, C and mid multiples
+// of 4, both layers' activations in LDS): squeeze sum -> fc1 + GELU -> fc2 + sigmoid with 16 waves of
+// 16 x 16 output tiles on the exact fp32 MFMA (v_mfma_f32_16x16x4f32). K runs in 16-wide steps whose
+// lanes load float4 slices of the activation row (LDS) and of the weight row (global, 64 contiguous
+// bytes per row per step): lane group q takes k = 16 s + 4 q + e in MFMA e of step s, the same order for
+// both operands. The three launches (partial-plane sum, two dense-row passes, ~30 us with their gaps
+// on the step's serial tail) become one of a few microseconds.
+typedef __attribute__((ext_vector_type(4))) float se_f32x4;
+constexpr int SE1_THREADS = 1024;
+constexpr int SE1_PF = 4;  // K-steps whose weight loads a wave issues together
+
+// One layer act(X W^T + b) over 16 x 16 output tiles, X [N][K] in LDS (row stride K), W [J][K] global.
+// With fewer tiles than waves each tile's K-steps are split over P waves (P a power of two): every wave
+// is busy and its weight loads are a few steps long, not a chain of K/16 dependent L2 round trips; the
+// P partial tiles meet in LDS (`red`, 16 x 256 floats) and are summed in a fixed order.
+template <int ACT>
+__device__ __forceinline__ void se_layer(const float* X, int N, int K, const float* __restrict__ W,
+                                         const float* __restrict__ b, int J, float* pre, float* out_g, float* out_l,
+                                         float* red, int tid) {
+  constexpr int NWV = SE1_THREADS / 64;
+  const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, q = lane >> 4;
+  const int tn = (N + 15) / 16, T = tn * ((J + 15) / 16), S = (K + 15) / 16;
+  int P = 1;
+  while (P * 2 * T <= NWV && P * 2 <= S) P *= 2;
+  const int G = NWV / P;  // tiles per round
+  for (int base = 0; base < T; base += G) {
+    const int t = base + wv / P, p = wv % P;
+    se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (t < T) {
+      const int n = (t % tn) * 16 + fr, j = (t / tn) * 16 + fr;
+      const int s0 = p * S / P, s1 = (p + 1) * S / P;
+      // the weight slices of up to SE1_PF K-steps in flight together (one L2 round trip per chunk)
+      for (int c0 = s0; c0 < s1; c0 += SE1_PF) {
+        float4 wb[SE1_PF];
+#pragma unroll
+        for (int i = 0; i < SE1_PF; ++i) {
+          const int k = (c0 + i) * 16 + 4 * q;  // K % 4 == 0: a float4 is wholly in or out
+          wb[i] = (c0 + i < s1 && k < K && j < J) ? *(const float4*)(W + (size_t)j * K + k)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < SE1_PF; ++i) {
+          if (c0 + i >= s1) break;
+          const int k = (c0 + i) * 16 + 4 * q;
+          const float4 a = (k < K && n < N) ? *(const float4*)(X + n * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wb[i].x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wb[i].y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wb[i].z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wb[i].w, acc, 0, 0, 0);
+        }
+      }
+    }
+    *(float4*)(red + wv * 256 + lane * 4) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    // D[row 4q + r][col fr] of each tile: output row n0 + 4q + r, column j0 + fr
+    for (int i = tid; i < G * 256; i += SE1_THREADS) {
+      const int tl = i >> 8, e = i & 255, tt = base + tl;
+      if (tt >= T) continue;
+      float v = 0.f;
+      for (int pp = 0; pp < P; ++pp) v += red[(tl * P + pp) * 256 + e];
+      const int ln = e >> 2, r = e & 3;
+      const int nr = (tt % tn) * 16 + 4 * (ln >> 4) + r, jc = (tt / tn) * 16 + (ln & 15);
+      if (nr >= N || jc >= J) continue;
+      const float z = v + (b ? b[jc] : 0.f);
+      if (pre) pre[(size_t)nr * J + jc] = z;
+      const float o = ACT == DMF_ACT_GELU ? gelu_f(z) : sigmoid_f(z);
+      out_g[(size_t)nr * J + jc] = o;
+      if (out_l) out_l[nr * J + jc] = o;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(SE1_THREADS) k_se_mlp1(const float* __restrict__ ws, int S, int N, int C, float scale,
+                                                         const float* __restrict__ w1, const float* __restrict__ b1,
+                                                         int mid, const float* __restrict__ w2,
+                                                         const float* __restrict__ b2, float* __restrict__ pooled,
+                                                         float* __restrict__ hpre, float* __restrict__ hact,
+                                                         float* __restrict__ gate) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* red = sm;                  // [16 waves][256]
+  float* xs = sm + 16 * 256;        // [N][C]
+  float* hs = xs + N * C;           // [N][mid]
+  const int tid = threadIdx.x;
+  const int NC = N * C;
+  for (int i = tid; i < NC; i += SE1_THREADS) {
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += ws[(size_t)z * NC + i];
+    v *= scale;
+    xs[i] = v;
+    if (pooled) pooled[i] = v;
+  }
+  __syncthreads();
+  se_layer<DMF_ACT_GELU>(xs, N, C, w1, b1, mid, hpre, hact, hs, red, tid);
+  se_layer<DMF_ACT_SIGMOID>(hs, N, mid, w2, b2, C, nullptr, gate, nullptr, red, tid);
+}
+
 // pooled[n][c] = scale * sum_z ws[z][n][c] (the squeeze's stage-1 partial planes)
 __global__ void k_sum_planes(const float* __restrict__ ws, int S, long long NC, float scale, float* __restrict__ out) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < NC; i += (long long)gridDim.x * blockDim.x) {
@@ -1175,6 +1272,13 @@ extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const floa
   return 0;
 }
 
+// 1 (default): the one-workgroup excitation (k_se_mlp1) where it fits; 0: the three-launch form
+static int g_se_one_launch = 1;
+extern "C" int dmf_se_mlp_tune(int one_launch) {
+  g_se_one_launch = one_launch != 0;
+  return 0;
+}
+
 extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1,
                           int mid, const float* w2, const float* b2, float* pooled, float* hpre, float* hact,
                           float* gate, void* stream) {
@@ -1185,6 +1289,18 @@ extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, con
                 "dmf_se_mlp: weights and vectors must be 16-B aligned");
   DMF_CHECK_ARG(pooled || (S == 1 && scale == 1.f), "dmf_se_mlp: a split / scaled squeeze needs `pooled`");
   hipStream_t st = (hipStream_t)stream;
+  const size_t lds1 = (size_t)N * (C + mid) * 4 + 16 * 256 * 4;
+  // (one CU runs both layers on the fp32 MFMA, 2*N*C*mid FMAs each: it wins up to the C = 128 SEs --
+  // 11.8 vs 26.0 us at N = 32, C = 128 -- and ties at C = 256, tools/se_bench.py)
+  if (g_se_one_launch && N <= 64 && C % 4 == 0 && mid % 4 == 0 && lds1 <= 96 * 1024 &&
+      (long long)N * C * mid <= 32LL * 128 * 64 &&
+      (!pooled || pooled != ws || S == 1)) {
+    // (pooled == ws with S == 1: the squeeze read and its write touch the same element in one thread)
+    hipLaunchKernelGGL(k_se_mlp1, dim3(1), dim3(SE1_THREADS), lds1, st, ws, S, N, C, scale, w1, b1, mid, w2, b2,
+                       pooled, hpre, hact, gate);
+    DMF_LAUNCH_CHECK("dmf_se_mlp");
+    return 0;
+  }
   const float* x = ws;
   if (pooled && (S > 1 || scale != 1.f || pooled != ws)) {
     const long long nc = (long long)N * C;

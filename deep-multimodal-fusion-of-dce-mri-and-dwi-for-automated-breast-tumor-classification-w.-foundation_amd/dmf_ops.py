@@ -2609,7 +2609,8 @@ def probe_replay(recs, reps=3):
 # environment: an A/B tool or a test sets them from code (set_knobs; bench.py
 # --knob NAME=VALUE). Each is listed with its test in DESIGN.md "Knobs".
 # name -> (module, attribute) for Python switches, ("tune", key) / ("wgrad_tune", key)
-# for the library's run-time tunables (dmf_conv_tune / dmf_conv_wgrad_tune).
+# for the library's run-time tunables (dmf_conv_tune / dmf_conv_wgrad_tune), ("call", entry point) for
+# the one-argument tunables (dmf_se_mlp_tune, dmf_gemm_fp8_tune).
 KNOBS = {
     "prep_plan": ("dmf_ops", "PREP.enabled"),
     "dgrad_as_fwd": ("dmf_ops", "DGRAD_AS_FWD"),
@@ -2621,6 +2622,8 @@ KNOBS = {
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
     "two_pass_fold": ("dmf_ops", "TWO_PASS_FOLD"),
     "wgrad_xcd": ("wgrad_tune", 6),
+    "se_one_launch": ("call", "dmf_se_mlp_tune"),
+    "fp8_gemm_scaled": ("call", "dmf_gemm_fp8_tune"),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
     "token_fwd_fused": ("dmf_tokens", "FWD_FUSED"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),
@@ -2658,6 +2661,8 @@ def set_knobs(**kw):
             N.call("dmf_conv_tune", attr, int(value))
         elif where == "wgrad_tune":
             N.call("dmf_conv_wgrad_tune", attr, int(value))
+        elif where == "call":
+            N.call(attr, int(value))
         else:
             obj = importlib.import_module(where)
             *path, last = attr.split(".")
