@@ -648,7 +648,7 @@ def test_col_stats_partials(shape, dtype):
 @pytest.mark.parametrize("case", [(4, 128, 16, 16, 3, 1, 1), (5, 64, 12, 12, 1, 1, 0), (3, 12, 9, 7, 3, 1, 1),
                                   (2, 16, 10, 10, 3, 2, 1)])
 def test_conv_cout1_backward(case, dtype):
-    """1-output-channel convs (mask / recon heads): input gradient (8-channel
+    """1-output-channel convs (mask / recon heads): the forward, the input gradient (8-channel
     vector form), weight and bias gradients (pixel-lane partials + the 16-lane
     split sum) against torch fp32."""
     n, ci, h, w, k, s, p = case
@@ -663,6 +663,10 @@ def test_conv_cout1_backward(case, dtype):
     cd.zero_grad(set_to_none=True)
     xd = _to_dev(x, dtype).requires_grad_(True)
     y = O.conv2d(xd, cd, (O.WeightCache(), O.WeightCache()))
+    # forward: the 8-channel vector kernel (Cin % 8 == 0: 16 or 8 lanes per pixel) or the scalar one
+    yt = yr.detach().abs().max().item()
+    torch.testing.assert_close(y.detach().float().cpu(), yr.detach(), rtol=2e-4 if dtype == torch.float32 else 1e-2,
+                               atol=(1e-5 if dtype == torch.float32 else 1e-2) * yt)
     y.backward(_to_dev(gy, dtype))
     rt = 2e-4 if dtype == torch.float32 else 2e-2
     gx = xr.grad.abs().max().item()
