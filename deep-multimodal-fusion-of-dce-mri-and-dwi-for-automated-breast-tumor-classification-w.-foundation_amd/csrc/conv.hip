@@ -1255,7 +1255,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
   }
   if constexpr (sizeof(T) == 2) {
     if (plan.ps) {
-      const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
+      const dim3 gp((unsigned)std::min<long long>(nblk, conv_persist_blocks(cu_count()))), bq(QTHREADS);
       // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
       // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
       const int epi = (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
@@ -1563,6 +1563,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
     case 16: g_sq_w4 = value != 0; return 0;
     case 17: g_gbar_dbg = value & (64 | 128); return 0;
+    case 18: DMF_CHECK_ARG(value >= 0, "dmf_conv_tune: persistent grid cap %d", value); return conv_persist_cap(value);
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }

@@ -513,6 +513,9 @@ int launch_conv_stem(ConvArgs& a, hipStream_t st, int dtype);
 // persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 / 5 BN statistics, 1 + act: bias + act,
 // 13 grid-barrier BatchNorm apply)
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype);
+// persistent-grid cap (dmf_conv_tune key 18): set / blocks for a device of ncu CUs
+int conv_persist_cap(int value);
+int conv_persist_blocks(int ncu);
 int conv_pp_tune(int value);  // dmf_conv_tune key 8
 constexpr int PP_THREADS = 512;
 constexpr int PP_HALF = 128 * 128;  // one half-tile: 128 rows x 128 B

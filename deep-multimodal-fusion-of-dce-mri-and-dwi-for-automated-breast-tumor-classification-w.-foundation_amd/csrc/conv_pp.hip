@@ -311,6 +311,15 @@ int conv_pp_tune(int value) {
   return 0;
 }
 
+// dmf_conv_tune key 18: blocks of a persistent launch (k_conv_fwd_ps / k_conv_fwd_pp), 0 = one per CU;
+// a two-stream region may cap it (dmf_ops.CONC_PERSIST) so the other stream keeps CUs
+static int g_persist_cap = 0;
+int conv_persist_cap(int value) {
+  g_persist_cap = value;
+  return 0;
+}
+int conv_persist_blocks(int ncu) { return g_persist_cap > 0 && g_persist_cap < ncu ? g_persist_cap : ncu; }
+
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype) {
   static int ncu = 0;
   if (!ncu) {
@@ -320,7 +329,9 @@ int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_
     if (ncu <= 0) ncu = 256;
   }
   const int ntile = a.mtiles * a.ntiles;
-  const dim3 g((unsigned)(g_pp_persist ? std::min(ntile, ncu) : ntile)), b(PP_THREADS);
+  // (the grid-barrier form needs one tile per block: never capped)
+  const int pcap = a.gbar ? ncu : conv_persist_blocks(ncu);
+  const dim3 g((unsigned)(g_pp_persist ? std::min(ntile, pcap) : ntile)), b(PP_THREADS);
   const size_t lds = (size_t)PP_LDS + lds_bias;
   DMF_CHECK_ARG(lds <= 160 * 1024, "conv_pp: %d output channels of bias exceed the LDS staging", a.Nout);
   if (!a.gbar) a.dbg = 0;  // (dmf_conv2d_fwd_bn_act's timing bits pass through)

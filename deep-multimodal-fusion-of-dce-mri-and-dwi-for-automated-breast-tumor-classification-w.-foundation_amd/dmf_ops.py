@@ -1147,6 +1147,25 @@ def _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
 # against 8.47 ms for the two-stream one (10.55 ms serial with the barrier).
 GRID_BARRIER_BN = False
 CONCURRENT = [0]
+# dmf_conv_tune values set through set_knobs (key -> value), so a region can restore what it changes
+TUNE_VALUES = {}
+# CONC_MIN_TILES > 0: inside the two-encoder fork (train_fusion._encode) the 256x256 and 256x128 forward
+# tiles take launches from this many tiles (half the CUs at 128: the other encoder's stream fills the
+# rest) instead of the chip-filling 256 (dmf_conv_tune keys 14 / 15); single-stream runs keep 256.
+# Knob "conc_min_tiles" (0 = off).
+CONC_MIN_TILES = 128
+# CONC_PERSIST > 0: the persistent 1x1 / ping-pong forms run this many blocks inside the fork instead of
+# one per CU (dmf_conv_tune key 18). Knob "conc_persist" (0 = off).
+CONC_PERSIST = 0
+
+
+def concurrent_tiles(enter):
+    """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES, CONC_PERSIST)."""
+    if CONC_MIN_TILES > 0:
+        for key in (14, 15):
+            N.call("dmf_conv_tune", key, CONC_MIN_TILES if enter else TUNE_VALUES.get(key, 256))
+    if CONC_PERSIST > 0:
+        N.call("dmf_conv_tune", 18, CONC_PERSIST if enter else TUNE_VALUES.get(18, 0))
 
 
 def _gbar_site(bn, dev):
@@ -2622,6 +2641,8 @@ KNOBS = {
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
     "two_pass_fold": ("dmf_ops", "TWO_PASS_FOLD"),
     "wgrad_xcd": ("wgrad_tune", 6),
+    "conc_min_tiles": ("dmf_ops", "CONC_MIN_TILES"),
+    "conc_persist": ("dmf_ops", "CONC_PERSIST"),
     "se_one_launch": ("call", "dmf_se_mlp_tune"),
     "fp8_gemm_scaled": ("call", "dmf_gemm_fp8_tune"),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
@@ -2659,6 +2680,7 @@ def set_knobs(**kw):
         where, attr = KNOBS[name]
         if where == "tune":
             N.call("dmf_conv_tune", attr, int(value))
+            TUNE_VALUES[attr] = int(value)
         elif where == "wgrad_tune":
             N.call("dmf_conv_wgrad_tune", attr, int(value))
         elif where == "call":
@@ -2668,4 +2690,8 @@ def set_knobs(**kw):
             *path, last = attr.split(".")
             for p in path:
                 obj = getattr(obj, p)
-            setattr(obj, last, bool(int(value)) if isinstance(value, (str, int)) else value)
+            cur = getattr(obj, last)
+            if isinstance(cur, bool) or not isinstance(cur, int):
+                setattr(obj, last, bool(int(value)) if isinstance(value, (str, int)) else value)
+            else:
+                setattr(obj, last, int(value))

@@ -126,6 +126,7 @@ class LightningFusionModel(nn.Module):
         prev = O.RNG_CURRENT[0]
         O.ORIGIN_STREAM[0] = main
         O.CONCURRENT[0] += 1  # the two encoders overlap: no grid-barrier launches (dmf_ops.GRID_BARRIER_BN)
+        O.concurrent_tiles(True)
         try:
             O.RNG_CURRENT[0] = snap_dwi
             out_dwi = self.dwi_model(dwi_inputs)
@@ -137,6 +138,7 @@ class LightningFusionModel(nn.Module):
             O.RNG_CURRENT[0] = prev
             O.ORIGIN_STREAM[0] = None
             O.CONCURRENT[0] -= 1
+            O.concurrent_tiles(False)
         main.wait_stream(side)
         O.record_tree(out_dce, main)
         return out_dwi, out_dce

@@ -68,7 +68,8 @@ int dmf_conv_last_form(void);
  * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
  * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 14 / 15 = tiles a launch
  * needs for the 256x128 / 256x256 forms; 16 = 4-wave square tile; 17 = timing-only
- * bits of dmf_conv2d_fwd_bn_act (64 skip the barrier, 128 the arena reads).
+ * bits of dmf_conv2d_fwd_bn_act (64 skip the barrier, 128 the arena reads); 18 = blocks of a persistent
+ * launch (0 = one per CU; a two-stream region may cap it).
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the

@@ -248,11 +248,11 @@ def test_knobs_are_set_from_code_only():
         for p in path:
             obj = getattr(obj, p)
         old = getattr(obj, last)
-        assert isinstance(old, bool), name
+        assert isinstance(old, (bool, int)), name
         O.set_knobs(**{name: "0"})
-        assert getattr(obj, last) is False
+        assert getattr(obj, last) == 0 and type(getattr(obj, last)) is type(old), name
         O.set_knobs(**{name: int(old)})
-        assert getattr(obj, last) is old
+        assert getattr(obj, last) == old and type(getattr(obj, last)) is type(old), name
     with pytest.raises(ValueError):
         O.set_knobs(no_such_knob=1)
 
