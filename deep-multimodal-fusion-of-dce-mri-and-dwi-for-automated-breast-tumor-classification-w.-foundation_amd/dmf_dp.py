@@ -233,13 +233,22 @@ class FusionTrainer:
         self.opt.zero_grad(set_to_none=False)
         loss = self.lm.training_step(batch)
         bwd = self.scaler.backward if self.scaler is not None else (lambda t: t.backward())
-        if self.overlap:
-            self._begin_backward()
-            bwd(loss)
-            self._end_backward()
-        else:
-            bwd(loss)
         import dmf_ops as O
+
+        # both encoders differentiate (mode B): their backwards run on two streams
+        two = all(any(p.requires_grad for p in m.parameters()) for m in (self.lm.dwi_model, self.lm.dce_model))
+        if two:
+            O.concurrent_tiles(True, bwd=True)
+        try:
+            if self.overlap:
+                self._begin_backward()
+                bwd(loss)
+                self._end_backward()
+            else:
+                bwd(loss)
+        finally:
+            if two:
+                O.concurrent_tiles(False, bwd=True)
 
         if O.GRAD_STASH:
             # a full backward consumes every shortcut-gradient hand-off (dmf_ops.conv_bn_act)

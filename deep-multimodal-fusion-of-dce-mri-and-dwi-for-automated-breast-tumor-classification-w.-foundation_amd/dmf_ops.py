@@ -1159,11 +1159,21 @@ CONC_MIN_TILES = 128
 CONC_PERSIST = 0
 
 
-def concurrent_tiles(enter):
-    """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES, CONC_PERSIST)."""
-    if CONC_MIN_TILES > 0:
+# CONC_BWD_MIN_TILES > 0: the same threshold for the dgrad launches (forward tiles) of a training backward
+# whose two encoders both differentiate (mode B: autograd replays each encoder's backward on its own
+# stream). Knob "conc_bwd_min_tiles" (0 = off).
+CONC_BWD_MIN_TILES = 128
+
+
+def concurrent_tiles(enter, bwd=False):
+    """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES, CONC_PERSIST;
+    bwd: CONC_BWD_MIN_TILES for a two-encoder backward)."""
+    mt = CONC_BWD_MIN_TILES if bwd else CONC_MIN_TILES
+    if mt > 0:
         for key in (14, 15):
-            N.call("dmf_conv_tune", key, CONC_MIN_TILES if enter else TUNE_VALUES.get(key, 256))
+            N.call("dmf_conv_tune", key, mt if enter else TUNE_VALUES.get(key, 256))
+    if bwd:
+        return
     if CONC_PERSIST > 0:
         N.call("dmf_conv_tune", 18, CONC_PERSIST if enter else TUNE_VALUES.get(18, 0))
 
@@ -2643,6 +2653,7 @@ KNOBS = {
     "wgrad_xcd": ("wgrad_tune", 6),
     "conc_min_tiles": ("dmf_ops", "CONC_MIN_TILES"),
     "conc_persist": ("dmf_ops", "CONC_PERSIST"),
+    "conc_bwd_min_tiles": ("dmf_ops", "CONC_BWD_MIN_TILES"),
     "se_one_launch": ("call", "dmf_se_mlp_tune"),
     "fp8_gemm_scaled": ("call", "dmf_gemm_fp8_tune"),
     "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
