@@ -96,6 +96,8 @@ __global__ void __launch_bounds__(FA_THREADS, 2)
     drow[j] = ((unsigned long long)bh * n + (unsigned)qrow[j]) * (unsigned long long)n;
   }
   const float ks_drop = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
+  // the Philox (seed, offset) read once (the K loop's barriers would reload them per mask)
+  const unsigned long long rseed = dp > 0.f ? rng[0] : 0ull, roff = dp > 0.f ? rng[1] : 0ull;
   const int q = (lane >> 2) & 3, p4 = lane & 3;
   const int nkt = (nv + KT - 1) / KT;
 #pragma unroll
@@ -164,7 +166,7 @@ __global__ void __launch_bounds__(FA_THREADS, 2)
         }
         if (dp > 0.f) {
           bool keep[4];
-          dropout_keep4(rng, site, drow[j] + (unsigned long long)(kb0 + 16 * f), dp, keep);
+          dropout_keep4v(rseed, roff, site, drow[j] + (unsigned long long)(kb0 + 16 * f), dp, keep);
 #pragma unroll
           for (int r = 0; r < 4; ++r) p[r] = keep[r] ? p[r] * ks_drop : 0.f;
         }

@@ -320,6 +320,17 @@ __device__ __forceinline__ void philox(uint32_t key0, uint32_t key1, uint32_t c0
 // Bernoulli(1-p) keep flags of elements e..e+3 (e % 4 == 0) of dropout site
 // `site`: Philox on (seed, offset) read from device memory (graph replays
 // draw fresh masks), counter = (e/4, site, offset).
+// the same with (seed, offset) already in registers: a kernel whose loop holds inline-asm barriers with
+// "memory" clobbers would otherwise reload rng[0], rng[1] (a scalar-load round trip) before every call
+__device__ __forceinline__ void dropout_keep4v(unsigned long long seed, unsigned long long off, int site,
+                                               unsigned long long e, float p, bool keep[4]) {
+  uint32_t r[4];
+  philox((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)(e >> 2), (uint32_t)(e >> 34), (uint32_t)site,
+         (uint32_t)off, r);
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) keep[i] = r[i] >= thr;
+}
 __device__ __forceinline__ void dropout_keep4(const unsigned long long* rng, int site, unsigned long long e,
                                               float p, bool keep[4]) {
   const unsigned long long seed = rng[0], off = rng[1];

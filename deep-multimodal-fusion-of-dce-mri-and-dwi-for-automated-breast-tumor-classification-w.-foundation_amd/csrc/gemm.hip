@@ -165,6 +165,8 @@ __device__ __forceinline__ void gemm_epilogue_act(const GemmArgs& g, const float
   const int z1 = z / g.H, z2 = z - (z / g.H) * g.H;
   OutT* __restrict__ C = (OutT*)g.C + z1 * g.sC1 + z2 * g.sC2;
   const float ks = g.dp > 0.f ? 1.f / (1.f - g.dp) : 1.f;
+  // Philox (seed, offset) read once: the epilogue's stores would otherwise force a reload per mask
+  const unsigned long long rseed = g.dp > 0.f ? g.rng[0] : 0ull, roff = g.dp > 0.f ? g.rng[1] : 0ull;
   const unsigned long long ebase = (unsigned long long)z * g.M * g.N;
   const int chn = tid % CPR, r0 = tid / CPR;
   const int n = n0 + chn * EPC;
@@ -220,7 +222,7 @@ __device__ __forceinline__ void gemm_epilogue_act(const GemmArgs& g, const float
 #pragma unroll
         for (int e = 0; e < EPC; e += 4) {
           bool keep[4];
-          dropout_keep4(g.rng, g.site, ebase + (unsigned long long)m * g.N + n + e, g.dp, keep);
+          dropout_keep4v(rseed, roff, g.site, ebase + (unsigned long long)m * g.N + n + e, g.dp, keep);
 #pragma unroll
           for (int t = 0; t < 4; ++t) w[e + t] = keep[t] ? w[e + t] * ks : 0.f;
         }
@@ -395,6 +397,7 @@ template <typename PT>
 __global__ void __launch_bounds__(256) k_softmax_drop(const float* __restrict__ S, int lds_, long long rows, int L,
                                                       int Lv, float scale, float dp, const unsigned long long* rng,
                                                       int site, PT* __restrict__ Ps, PT* __restrict__ Pd, int ldp) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -433,7 +436,7 @@ __global__ void __launch_bounds__(256) k_softmax_drop(const float* __restrict__ 
     g_store_aux(Ps + row * ldp + c, p);
     if (dp > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)(row * L + c), dp, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)(row * L + c), dp, keep);
 #pragma unroll
       for (int e = 0; e < 4; ++e) p[e] = keep[e] ? p[e] * ks : 0.f;
     }
@@ -448,6 +451,7 @@ __global__ void __launch_bounds__(256) k_softmax_drop_bwd(const PT* __restrict__
                                                           int L, float scale, float dp,
                                                           const unsigned long long* rng, int site,
                                                           PT* __restrict__ dS, int lds_) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -459,7 +463,7 @@ __global__ void __launch_bounds__(256) k_softmax_drop_bwd(const PT* __restrict__
     float gg[4] = {gv.x, gv.y, gv.z, gv.w};
     if (dp > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)(row * L + c), dp, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)(row * L + c), dp, keep);
 #pragma unroll
       for (int e = 0; e < 4; ++e) gg[e] = keep[e] ? gg[e] * ks : 0.f;
     }
@@ -473,7 +477,7 @@ __global__ void __launch_bounds__(256) k_softmax_drop_bwd(const PT* __restrict__
     float gg[4] = {gv.x, gv.y, gv.z, gv.w};
     if (dp > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)(row * L + c), dp, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)(row * L + c), dp, keep);
 #pragma unroll
       for (int e = 0; e < 4; ++e) gg[e] = keep[e] ? gg[e] * ks : 0.f;
     }

@@ -122,6 +122,7 @@ __global__ void k_affine_act(const T* __restrict__ x, int ldx, const float* __re
                              const T* __restrict__ res, int ldr, const float* __restrict__ ssr, int act,
                              float p, const unsigned long long* rng, int site, T* __restrict__ y, int ldy,
                              long long M, int C) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   constexpr int V = 4;
   const int cv = C / V;
   const long long total = M * cv;
@@ -144,7 +145,7 @@ __global__ void k_affine_act(const T* __restrict__ x, int ldx, const float* __re
     }
     if (p > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)(m * C + c0), p, keep);
 #pragma unroll
       for (int k = 0; k < V; ++k) v[k] = keep[k] ? v[k] * sc : 0.f;
     }
@@ -159,6 +160,7 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
                               const T* __restrict__ res, int ldr, const float* __restrict__ ssr, float p,
                               const unsigned long long* rng, int site, T* __restrict__ y, int ldy, long long M,
                               int C) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   // 32-bit index math (the host routes M*C/8 >= 2^31 to k_affine_act)
   const unsigned cv = (unsigned)C >> 3;
   const unsigned total = (unsigned)(M * cv);
@@ -191,10 +193,10 @@ __global__ void k_affine_act8(const T* __restrict__ x, int ldx, const float* __r
     }
     if (p > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * sc : 0.f;
-      dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0 + 4, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * sc : 0.f;
     }
@@ -253,6 +255,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
                                                    const T* __restrict__ res, int ldr, BnApplySrc R, float p,
                                                    const unsigned long long* rng, int site, T* __restrict__ y, int ldy,
                                                    int M, int C, int rows_per_blk) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   __shared__ float sa[2][64], sr[2][64];
   const int tid = threadIdx.x;
   const int cg = blockIdx.x * 64;
@@ -317,10 +320,10 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
     }
     if (p > 0.f) {
       bool keep[4];
-      dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * dsc : 0.f;
-      dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
+      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0 + 4, p, keep);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * dsc : 0.f;
     }
@@ -334,6 +337,7 @@ __global__ void k_act_bwd(const T* __restrict__ dy, int lddy, const T* __restric
                           const float* __restrict__ ssa, const T* __restrict__ res, int ldr,
                           const float* __restrict__ ssr, int act, float p, const unsigned long long* rng, int site,
                           T* __restrict__ dz, int lddz, long long M, int C) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   constexpr int V = 4;
   const int cv = C / V;
   const long long total = M * cv;
@@ -343,7 +347,7 @@ __global__ void k_act_bwd(const T* __restrict__ dy, int lddy, const T* __restric
     const long long m = i / cv;
     const int c0 = (int)(i - m * cv) * V;
     bool keep[4] = {true, true, true, true};
-    if (p > 0.f) dropout_keep4(rng, site, (unsigned long long)(m * C + c0), p, keep);
+    if (p > 0.f) dropout_keep4v(rseed_, roff_, site, (unsigned long long)(m * C + c0), p, keep);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       float g = ld(dy + m * lddy + c0 + k);
@@ -514,6 +518,7 @@ __global__ void __launch_bounds__(256, (F & 5) ? 1 : 4) k_act_bwd_bnred8(const T
                                                         const float* __restrict__ save, T* __restrict__ dz, int lddz,
                                                         long long M, int C, float* __restrict__ part,
                                                         double* __restrict__ acc, int replicas) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   constexpr bool HR = (F & 1) && ACT != DMF_ACT_NONE, HD = F & 2, HP = F & 4;
   __shared__ float red[32][65 * 2];
   __shared__ __attribute__((aligned(16))) float rss[2][64];  // the residual's BN scale / shift (HR): read per row
@@ -573,10 +578,10 @@ __global__ void __launch_bounds__(256, (F & 5) ? 1 : 4) k_act_bwd_bnred8(const T
       unpack8(vx[j], xv);
       if (HP && p > 0.f) {
         bool keep[4];
-        dropout_keep4(rng, site, (unsigned long long)m * C + c0, p, keep);
+        dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] = keep[k] ? g[k] * sc : 0.f;
-        dropout_keep4(rng, site, (unsigned long long)m * C + c0 + 4, p, keep);
+        dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0 + 4, p, keep);
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[4 + k] = keep[k] ? g[4 + k] * sc : 0.f;
       }

@@ -146,6 +146,7 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
                                                     const unsigned long long* rng, int site,
                                                     T* __restrict__ dy, float* __restrict__ slab0,
                                                     float* __restrict__ slab1) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   extern __shared__ float red[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nj = E >> 8;
@@ -168,7 +169,7 @@ __global__ void __launch_bounds__(256) k_lsdrop_bwd(const float* __restrict__ go
         float m[4] = {ks, ks, ks, ks};
         if (p > 0.f) {
           bool keep[4];
-          dropout_keep4(rng, site, (unsigned long long)(r * E + c), p, keep);
+          dropout_keep4v(rseed_, roff_, site, (unsigned long long)(r * E + c), p, keep);
 #pragma unroll
           for (int q = 0; q < 4; ++q) m[q] = keep[q] ? ks : 0.f;
         }
@@ -370,10 +371,11 @@ extern "C" int dmf_cast_f32(const void* x, long long n, float* y, void* stream) 
 // test/inspection helper, n % 4 == 0.
 __global__ void k_dropout_keep_mask(const unsigned long long* rng, int site, long long n, float p,
                                     unsigned char* __restrict__ keep) {
+  const unsigned long long rseed_ = rng ? rng[0] : 0ull, roff_ = rng ? rng[1] : 0ull;  // read once (see dropout_keep4v)
   const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= n) return;
   bool k[4];
-  dropout_keep4(rng, site, (unsigned long long)i, p, k);
+  dropout_keep4v(rseed_, roff_, site, (unsigned long long)i, p, k);
   *(uchar4*)(keep + i) = make_uchar4(k[0], k[1], k[2], k[3]);
 }
 
