@@ -1261,6 +1261,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
       const int epi = (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
                       : a.y == nullptr ? 12
                       : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
+                      : a.dp > 0.f ? 14
                                               : 1 + a.act;
       a.dbg = g_ps_dbg;
 #define DMF_PS(E)                                                                                                \
@@ -1283,6 +1284,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
         case 2: DMF_PS(2); break;
         case 3: DMF_PS(3); break;
         case 5: DMF_PS(5); break;
+        case 14: DMF_PS_AFF(14); break;
         default: DMF_PS(4); break;
       }
 #undef DMF_PS
@@ -1396,6 +1398,9 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
+  DMF_CHECK_ARG(a.dp == 0.f || (!dgrad && plan.ps && a.x2 == nullptr && a.act == DMF_ACT_GELU && a.rng &&
+                                 a.partials == nullptr && a.y != nullptr),
+                "%s: dropout needs the persistent 1x1 form with the GELU epilogue (one source, rng state)", what);
   DMF_CHECK_ARG((a.out_ss == nullptr && !a.aff_acc) || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
                 "%s: the affine epilogue needs the persistent 1x1 form (no bias, one source, a shortcut)", what);
   DMF_CHECK_ARG(a.y != nullptr || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.M % QBM == 0 &&
@@ -1633,6 +1638,31 @@ extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int
   if (rc) return rc;
   a.partials = bn_partials;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd");
+}
+
+static ConvArgs affine_args(int dtype, int N, int H, int W, int Cin, int ldx, int Cout, int stride);
+
+// token linear (1x1 conv over the rows' NHWC view) -> bias -> GELU -> dropout in one launch (forward-only
+// transformer blocks' fc1 under MLP dropout, transformer_model.py:128-134)
+extern "C" int dmf_conv2d_fwd_drop_ok(int dtype, int N, int H, int W, int Cin, int Cout) {
+  if (!is16(dtype)) return 0;
+  ConvArgs a = affine_args(dtype, N, H, W, Cin, Cin, Cout, 1);
+  return conv_plan(dtype, false, a).ps && (size_t)PS_LDS + (size_t)Cout * 4 <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int dmf_conv2d_fwd_drop(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                                   int Cout, const float* bias, void* y, int ldy, int act, float dropout_p,
+                                   const unsigned long long* rng, int site, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, 1, 1, 1, 0, 1, bias, y, H, W, ldy,
+                           act, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_drop");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && act == DMF_ACT_GELU && dropout_p > 0.f && dropout_p < 1.f && rng,
+                "dmf_conv2d_fwd_drop: a 16-bit dtype, GELU, 0 < p < 1 and rng state");
+  a.dp = dropout_p;
+  a.rng = rng;
+  a.site = site;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_drop");
 }
 
 extern "C" int dmf_conv2d_fwd_acc(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,

@@ -58,6 +58,12 @@ struct ConvArgs {
   // replicas, fin) when they stage them, instead of from out_ss (dmf_conv2d_fwd_affine_acc: the
   // finalize launch between the two passes folded in); block 0 also moves the running statistics
   int aff_acc;
+  // dropout after the bias + GELU epilogue of k_conv_fwd_ps (EPI 14, dmf_conv2d_fwd_drop): Philox keep
+  // masks on element m * Nout + n, the token GEMM's index (k_gemm_bf16 epilogue), so a forward-only
+  // token block draws the same masks as the training path
+  float dp;
+  const unsigned long long* rng;
+  int site;
   // grid-barrier BatchNorm apply (dmf_conv2d_fwd_bn_act; k_conv_fwd_pp EPI 13, conv_epilogue of
   // k_conv_fwd_wide): [counter 0, counter 1, generation] of this BatchNorm's launch site, or null
   unsigned* gbar;
@@ -309,6 +315,14 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   // applied by the second, affine pass -- dmf_conv2d_fwd_stats)
   constexpr bool stats = EPI == 0 || EPI == 5 || EPI == 12, fast = EPI == 5 || EPI == 12, nostore = EPI == 12;
   constexpr bool aff = EPI == 8 || EPI == 11, rbn = EPI == 11;
+  // EPI 14: the Philox (seed, offset) once per tile
+  unsigned long long dseed = 0, doff = 0;
+  float dks = 1.f;
+  if constexpr (EPI == 14) {
+    dseed = a.rng[0];
+    doff = a.rng[1];
+    dks = 1.f / (1.f - a.dp);
+  }
   // staged [scale | shift (+ the residual's shift) | residual scale] x Nout (k_conv_fwd_ps)
   float bsv[16], shv[16], rsv[16];
 #pragma unroll
@@ -366,12 +380,24 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
       const float w = ok ? 1.f : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { s[e] += w * v[e]; q[e] += w * v[e] * v[e]; }
-    } else if constexpr (EPI - 1 == DMF_ACT_GELU) {
+    } else if constexpr (EPI - 1 == DMF_ACT_GELU || EPI == 14) {
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
         const dmf_f2 g = gelu_f2(dmf_f2{v[e], v[e + 1]});
         v[e] = g.x;
         v[e + 1] = g.y;
+      }
+      if constexpr (EPI == 14) {
+        // values 8h .. 8h+7 are channels n0 + cl + 32 h .. +7 of row m
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q4 = 0; q4 < 2; ++q4) {
+            bool keep[4];
+            dropout_keep4v(dseed, doff, a.site, (unsigned long long)m * a.Nout + n0 + cl + 32 * h + 4 * q4, a.dp, keep);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[8 * h + 4 * q4 + t] = keep[t] ? v[8 * h + 4 * q4 + t] * dks : 0.f;
+          }
       }
     } else if constexpr (EPI > 1 && EPI < 5) {
 #pragma unroll

@@ -392,6 +392,8 @@ class _BlockFn(torch.autograd.Function):
 # follows the GELU (the conv epilogue has none). Knob "token_fwd_fused" = False keeps the training
 # path's kernels.
 FWD_FUSED = True
+# fc1 under MLP dropout on the conv engine too (dmf_conv2d_fwd_drop; knob "fc1_drop_conv")
+FC1_DROP_CONV = True
 _FA_HEAD_DIM = 128
 
 
@@ -419,6 +421,35 @@ def _linear_conv(x2d, lin, b, n, act="none"):
     finally:
         O.PROBE["conv_fwd"] = saved
     return y.permute(0, 2, 3, 1).reshape(r, nout)
+
+
+def _linear_conv_drop(x2d, lin, b, n, p, rng, site):
+    """dropout(gelu(x W^T + bias)) on the conv engine's persistent 1x1 form in one launch
+    (dmf_conv2d_fwd_drop): the keep masks are the token GEMM's (element row * Nout + col, same site)."""
+    r, k = x2d.shape
+    nout = lin.weight.shape[0]
+    caches = lin.__dict__.get("_dmf_conv_caches")
+    if caches is None:
+        caches = lin.__dict__["_dmf_conv_caches"] = (O.WeightCache(), O.WeightCache())
+    wk = caches[0].get(lin.weight.view(nout, k, 1, 1), x2d.dtype, k, 0)
+    y = torch.empty((r, nout), dtype=x2d.dtype, device=x2d.device)
+    x4 = x2d.view(b, n, 1, k).permute(0, 3, 1, 2)
+    saved = O.PROBE["conv_fwd"]
+    O.PROBE["conv_fwd"] = O.PROBE["tok_gemm"]
+    try:
+        O._conv_launch("dmf_conv2d_fwd_drop",
+                       (O.dt(x2d), x2d.data_ptr(), b, n, 1, k, k, wk.data_ptr(), nout, O._p(lin.bias), y.data_ptr(),
+                        nout, N.ACT_GELU, float(p), O._p(rng), int(site)),
+                       (x2d, wk, y, lin.bias, rng), x4, b, n, 1, k, nout, 1, 1, _G1, n, 1)
+    finally:
+        O.PROBE["conv_fwd"] = saved
+    return y
+
+
+def _linear_conv_drop_ok(x2d, lin, n):
+    r, k = x2d.shape
+    return (_linear_conv_ok(x2d, lin, n) and lin.bias is not None
+            and bool(N.load().dmf_conv2d_fwd_drop_ok(N.BF16, r // n, n, 1, k, lin.weight.shape[0])))
 
 
 def _linear_conv_ok(x2d, lin, n):
@@ -481,6 +512,8 @@ def _block_fwd_nograd(x, blk, rng, cfg, g1, g2):
     hid = ml.fc1.weight.shape[0]
     if p_mlp == 0.0 and _linear_conv_ok(ln2, ml.fc1, n):
         h = _linear_conv(ln2, ml.fc1, b, n, act="gelu")
+    elif p_mlp > 0.0 and rng is not None and FC1_DROP_CONV and _linear_conv_drop_ok(ln2, ml.fc1, n):
+        h = _linear_conv_drop(ln2, ml.fc1, b, n, p_mlp, rng, s_m1)
     else:
         (w1,) = _wcast(cdt, ml.fc1.weight)
         h = gemm(torch.empty((r, hid), **bf), ln2, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=ml.fc1.bias,

@@ -136,6 +136,14 @@ int dmf_conv2d_fwd_acc(int dtype, const void* x, int N, int H, int W, int Cin, i
  * a second K loop. dmf_conv2d_fwd_affine_ok: 1 when a 1x1 conv of this shape runs the persistent
  * 256x256 form both passes need (16-bit dtype, Cout % 256 == 0, N*Ho*Wo % 256 == 0). */
 int dmf_conv2d_fwd_affine_ok(int dtype, int N, int H, int W, int Cin, int Cout, int stride);
+/* a 1x1 conv (a token linear over its rows' NHWC view) -> bias -> GELU -> dropout(p) in one launch on
+ * the persistent 256x256 form (forward-only transformer blocks' fc1 under MLP dropout,
+ * transformer_model.py:128-134); keep masks on element m * Cout + n with (rng, site), the token GEMM's
+ * index, so the masks equal dmf_gemm_bf16's. dmf_conv2d_fwd_drop_ok: 1 when the shape takes that form. */
+int dmf_conv2d_fwd_drop_ok(int dtype, int N, int H, int W, int Cin, int Cout);
+int dmf_conv2d_fwd_drop(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                        const float* bias, void* y, int ldy, int act, float dropout_p, const unsigned long long* rng,
+                        int site, void* stream);
 int dmf_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
                          int stride, int Ho, int Wo, double* bn_acc, int replicas, void* stream);
 int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,

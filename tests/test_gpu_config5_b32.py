@@ -79,14 +79,24 @@ def test_config5_b32_captured_step_production_plan_vs_oracle():
         for k in recs:
             O.PROBE[k] = None
     forms = sorted({r["form"] for r in recs["conv_fwd"]})
-    tok_m = sorted({r["shape"][1] for r in recs["tok_gemm"]})
+    # token rows per record: dmf_gemm_* (batch, M, ...) / conv-engine linears (N, H, W, ...: the rows' NHWC
+    # view) / the fused attention ("flash", b, n, ...)
+    def _rows(r):
+        sh = r["shape"]
+        if r["fn"].startswith("dmf_conv2d"):
+            return sh[0] * sh[1] * sh[2]
+        if r["fn"] == "dmf_flash_attn_fwd":
+            return sh[1] * sh[2]
+        return sh[1]
+    tok_m = sorted({_rows(r) for r in recs["tok_gemm"]})
+    tok_fns = sorted({r["fn"] for r in recs["tok_gemm"]})
     fp8_shapes = sorted({tuple(r["shape"]) for r in recs["fp8_gemm"]})
     for v in recs.values():
         v.clear()
     # the production plan: 256-wide LDS-DMA forward forms and the 7x7 stem kernel on the 48x48 maps,
     # token GEMMs over all 18,432 token rows, the e4m3 patch-embed GEMM at M = 18,432
     assert {"ps", "stem"} <= set(forms) and ({"pp", "wide"} & set(forms)), forms
-    assert TOKENS in tok_m, (TOKENS, tok_m)
+    assert tok_m == [TOKENS] and "dmf_flash_attn_fwd" in tok_fns, (TOKENS, tok_m, tok_fns)
     assert fp8_shapes and all(s[0] == TOKENS for s in fp8_shapes), fp8_shapes
     loss = tr.step(bd).item()  # one replay of the captured step
     assert tr.captures == 1 and tr.eager_steps == 0

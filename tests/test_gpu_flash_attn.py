@@ -111,3 +111,27 @@ def test_forward_only_block_matches_autograd_forward():
         O.PROBE["tok_gemm"] = None
     names = [r["fn"] for r in recs]
     assert "dmf_flash_attn_fwd" in names and any(n.startswith("dmf_conv2d") for n in names), names
+
+
+def test_fc1_dropout_on_conv_engine_matches_token_gemm():
+    """fc1 -> GELU -> dropout of a forward-only block on the conv engine (dmf_conv2d_fwd_drop, persistent
+    1x1 form, packed GELU) against the token GEMM's epilogue (k_gemm_bf16) with the same rng and site:
+    identical keep masks (element row * Nout + col), values within bf16 rounding."""
+    torch.manual_seed(4)
+    b, n, e, hid, p, site = 32, 576, 512, 2048, 0.1, 5  # config 5's B = 32: the persistent plan's tile count
+    lin = torch.nn.Linear(e, hid).to(DEV)
+    x = torch.randn(b * n, e, device=DEV).bfloat16()
+    rng = O.RNG.snapshot(torch.device(DEV))
+    assert D._linear_conv_drop_ok(x, lin, n)
+    with torch.no_grad():
+        yc = D._linear_conv_drop(x, lin, b, n, p, rng, site)
+        (w1,) = D._wcast(torch.bfloat16, lin.weight)
+        yg = D.gemm(torch.empty((b * n, hid), dtype=torch.bfloat16, device=DEV), x, w1, b * n, hid, e, lda=e, ldb=e,
+                    ldc=hid, bias=lin.bias, act="gelu", dropout_p=p, rng=rng, site=site)
+    torch.cuda.synchronize()
+    dropped_c, dropped_g = yc == 0, yg == 0
+    frac = dropped_g.float().mean().item()
+    assert 0.08 < frac < 0.12, frac
+    assert (dropped_c != dropped_g).float().mean().item() < 1e-4  # (a GELU output that is exactly 0 aside)
+    d = (yc.float() - yg.float()).abs().max().item()
+    assert d <= 2e-2 * yg.float().abs().max().item(), d

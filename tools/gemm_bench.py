@@ -82,6 +82,14 @@ def main():
         return run
     cases["qkv  conv-engine"] = conv_case(wq, bq, e, "none")
     cases["fc1  conv-engine gelu"] = conv_case(w1, b1, e, "gelu")
+    lin1 = torch.nn.Linear(e, hid).to(dev)
+    with torch.no_grad():
+        lin1.weight.copy_(w1.float())
+        lin1.bias.copy_(b1)
+    lin1.requires_grad_(False)
+    cases["fc1  gemm gelu + dropout 0.1"] = lambda: D.gemm(out_h, x, w1, r, hid, e, lda=e, ldb=e, ldc=hid, bias=b1,
+                                                           act="gelu", dropout_p=0.1, rng=rng, site=3)
+    cases["fc1  conv-engine gelu + dropout 0.1"] = lambda: D._linear_conv_drop(x, lin1, b, n, 0.1, rng, 3)
     cases["fc2  conv-engine (bf16 out)"] = conv_case(w2, bp, hid, "none")
     cases["proj conv-engine (bf16 out)"] = conv_case(wp, bp, e, "none")
     sm_p = torch.empty((b, h, n, n), **bf)
