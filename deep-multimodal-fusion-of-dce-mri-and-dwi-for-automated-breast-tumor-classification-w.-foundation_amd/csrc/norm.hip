@@ -653,7 +653,7 @@ __global__ void k_bn_bwd_apply8(const T* __restrict__ dz, int lddz, const T* __r
 // column sums accumulated by dmf_act_bwd_bn_reduce_acc into [replicas][C][2]
 // doubles (summed in a fixed order, the arithmetic of k_bn_bwd_finalize_wide);
 // the blockIdx.x == 0 blocks also add dgamma / dbeta. dx = A*dz + Cc*x + B.
-template <typename T>
+template <typename T, int U = 1>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ dz, int lddz, const T* __restrict__ x,
                                                           int ldx, const double* __restrict__ acc, int replicas,
                                                           double count, int training, const float* __restrict__ gamma,
@@ -701,14 +701,36 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
   }
   const int mbeg = blockIdx.y * rows_per_blk;
   const int mend = min(M, mbeg + rows_per_blk);
-  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
-    float g[8], xv[8];
-    ld8(dz + (size_t)m * lddz + c0, g);
-    ld8(x + (size_t)m * ldx + c0, xv);
+  // U rows per thread per round, every load of the round issued before any row is converted
+  for (int m = mbeg + (tid >> 3); m < mend; m += 32 * U) {
+    Vec8<T> vg[U], vx[U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
-    st8(dx + (size_t)m * lddx + c0, g);
+    for (int u = 0; u < U; ++u) {
+      const int mu = m + 32 * u;
+      vg[u] = mu < mend ? ldv8(dz + (size_t)mu * lddz + c0) : zero8<T>();
+      vx[u] = mu < mend ? ldv8(x + (size_t)mu * ldx + c0) : zero8<T>();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int mu = m + 32 * u;
+      if (mu >= mend) break;
+      float g[8], xv[8];
+      unpack8(vg[u], g);
+      unpack8(vx[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = a8[e] * g[e] + c8[e] * xv[e] + b8[e];
+      st8(dx + (size_t)mu * lddx + c0, g);
+    }
   }
+}
+
+// rows of k_bn_bwd_apply_acc's loads in flight per thread (1 default; dmf_bn_bwd_apply_tune)
+static int g_bwd_apply_u = 1;
+extern "C" int dmf_bn_bwd_apply_tune(int rows_in_flight) {
+  DMF_CHECK_ARG(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4, "dmf_bn_bwd_apply_tune: %d",
+                rows_in_flight);
+  g_bwd_apply_u = rows_in_flight;
+  return 0;
 }
 
 // dmf_bn_bwd_finalize for many tiles: 16 channels x 64 tile lanes per block
@@ -1028,9 +1050,15 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
   while (rows > 32 && (long long)cdiv(M, rows) * gy < 1024) rows >>= 1;
   if (cdiv(M, rows) > 65535) rows = (int)(cdiv(cdiv(M, 65535), 32) * 32);  // (gridDim.y <= 65535)
   const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
-  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_bn_bwd_apply_acc<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)dz, lddz,
-                       (const T*)x, ldx, acc, replicas, count, training, gamma, save_mean_invstd, dgamma, dbeta,
-                       (T*)dx, lddx, (int)M, C, rows));
+#define DMF_BBA(U)                                                                                          \
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_bn_bwd_apply_acc<T, U>), g, dim3(256), 0, (hipStream_t)stream, \
+                                                  (const T*)dz, lddz, (const T*)x, ldx, acc, replicas, count,     \
+                                                  training, gamma, save_mean_invstd, dgamma, dbeta, (T*)dx, lddx, \
+                                                  (int)M, C, rows))
+  if (g_bwd_apply_u == 4) DMF_BBA(4);
+  else if (g_bwd_apply_u == 2) DMF_BBA(2);
+  else DMF_BBA(1);
+#undef DMF_BBA
   DMF_LAUNCH_CHECK("dmf_bn_bwd_apply_acc");
   return 0;
 }

@@ -315,6 +315,8 @@ int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* d
 int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int ldx, const double* acc, int replicas,
                          double count, int training, const float* gamma, const float* save_mean_invstd, float* dgamma,
                          float* dbeta, void* dx, int lddx, long long M, int C, void* stream);
+/* rows of dmf_bn_bwd_apply_acc's loads in flight per thread: 1 (default), 2 or 4 (A/B runs) */
+int dmf_bn_bwd_apply_tune(int rows_in_flight);
 int dmf_col_stats_tiles(long long M);
 int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
 
