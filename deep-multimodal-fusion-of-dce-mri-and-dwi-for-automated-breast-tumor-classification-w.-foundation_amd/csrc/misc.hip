@@ -1253,12 +1253,49 @@ __global__ void k_adaptive_avgpool_bwd(const T* __restrict__ dy, int lddy, T* __
     st(dx + p * lddx + c, s);
   }
 }
+// the same on 8-channel (16-B) vectors with 32-bit index math: one thread per (output pixel, 8 channels),
+// the window summed in the same (h, w) order per channel (bit-identical to k_adaptive_avgpool); the
+// scalar form's 64-bit div / mod per element made it ~3x a copy of its bytes
+template <typename T>
+__global__ void __launch_bounds__(256) k_adaptive_avgpool8(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
+                                                           int N, int H, int W, int C, int Ho, int Wo, int total8) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total8) return;
+  const int C8 = C >> 3;
+  const int c = (e % C8) * 8;
+  const int p = e / C8;
+  const int j = p % Wo, q = p / Wo, i = q % Ho, n = q / Ho;
+  const int h0 = ap_lo(i, H, Ho), h1 = ap_hi(i, H, Ho), w0 = ap_lo(j, W, Wo), w1 = ap_hi(j, W, Wo);
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+  for (int h = h0; h < h1; ++h)
+    for (int w = w0; w < w1; ++w) {
+      float v[8];
+      ld8(x + ((size_t)(n * H + h) * W + w) * ldx + c, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+  const float d = (float)((h1 - h0) * (w1 - w0));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = s[k] / d;
+  st8(y + (size_t)p * ldy + c, s);
+}
 }  // namespace dmf
 
 extern "C" int dmf_adaptive_avgpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho,
                                       int Wo, int ldy, void* stream) {
   DMF_CHECK_ARG(x && y && N > 0 && H > 0 && W > 0 && C > 0 && Ho > 0 && Wo > 0, "dmf_adaptive_avgpool2d: bad args");
   const long long total = (long long)N * Ho * Wo * C;
+  if (C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 &&
+      total / 8 < (1LL << 31) && (long long)N * H * W * ldx < (1LL << 31)) {
+    const int total8 = (int)(total / 8);
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_adaptive_avgpool8<T>, dim3((unsigned)cdiv(total8, 256)), dim3(256),
+                                                    0, (hipStream_t)stream, (const T*)x, ldx, (T*)y, ldy, N, H, W, C,
+                                                    Ho, Wo, total8));
+    DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d");
+    return 0;
+  }
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_adaptive_avgpool<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
                        (const T*)x, ldx, (T*)y, ldy, N, H, W, C, Ho, Wo));
   DMF_LAUNCH_CHECK("dmf_adaptive_avgpool2d");

@@ -529,6 +529,17 @@ def test_adaptive_avgpool_any_ratio(hw_out):
     assert torch.allclose(xd.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("c,dtype", [(256, torch.bfloat16), (72, torch.float32), (12, torch.bfloat16)])
+def test_adaptive_avgpool_vector_form(c, dtype):
+    """The 8-channel vector form (C % 8 == 0) and the scalar fallback (C = 12), 48 -> 64 as at S=384."""
+    torch.manual_seed(15)
+    x = torch.randn(3, c, 48, 48).to(dtype).float()
+    ref = F.adaptive_avg_pool2d(x.double(), (64, 64))
+    y = O.adaptive_avgpool(_to_dev(x, dtype), 64, 64)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(y.float().cpu().double(), ref, atol=tol * ref.abs().max().item(), rtol=tol)
+
+
 def test_fused_recon_mixed_map_sizes():
     """config 5: encoder recon maps 8x8 beside a 4x4 fused map (48x48 / 24x24 at
     S=384) -- one launch per size, same value and grads as the oracle's three
