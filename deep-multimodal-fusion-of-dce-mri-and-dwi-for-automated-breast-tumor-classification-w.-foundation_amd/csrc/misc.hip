@@ -839,17 +839,39 @@ __global__ void k_maxpool8(const T* __restrict__ x, int N, int H, int W, int C, 
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
-    for (int r = 0; r < k; ++r) {
-      const int hi = ho * s - p + r;
-      if (hi < 0 || hi >= H) continue;
-      for (int q = 0; q < k; ++q) {
-        const int wi = wo * s - p + q;
-        if (wi < 0 || wi >= W) continue;
+    if (k == 3) {
+      // the stem's 3x3 window: all nine 16-B loads in flight before any compare (the runtime-k loop
+      // below waits out one load latency per tap); out-of-range taps are skipped exactly as there
+      Vec8<T> vv[9];
+      bool ok[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int hi = ho * s - p + t / 3, wi = wo * s - p + t % 3;
+        ok[t] = hi >= 0 && hi < H && wi >= 0 && wi < W;
+        vv[t] = ok[t] ? ldv8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8) : zero8<T>();
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
         float v[8];
-        ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+        unpack8(vv[t], v);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (v[j] > m[j] || isnan(v[j])) m[j] = v[j];
+      }
+    } else {
+      for (int r = 0; r < k; ++r) {
+        const int hi = ho * s - p + r;
+        if (hi < 0 || hi >= H) continue;
+        for (int q = 0; q < k; ++q) {
+          const int wi = wo * s - p + q;
+          if (wi < 0 || wi >= W) continue;
+          float v[8];
+          ld8(x + ((size_t)(n * H + hi) * W + wi) * ldx + cv * 8, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (v[j] > m[j] || isnan(v[j])) m[j] = v[j];
+        }
       }
     }
     st8(y + pix * ldy + cv * 8, m);
