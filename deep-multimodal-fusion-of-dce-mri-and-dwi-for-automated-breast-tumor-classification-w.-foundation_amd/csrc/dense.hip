@@ -1021,6 +1021,68 @@ __global__ void __launch_bounds__(SE1_THREADS) k_se_mlp1(const float* __restrict
   se_layer<DMF_ACT_SIGMOID>(hs, N, mid, w2, b2, C, nullptr, gate, nullptr, red, tid);
 }
 
+// One dense layer of a larger SE as a grid of 16 x 16 output tiles, one workgroup (4 waves) per tile with
+// its K-steps split over the waves (partials summed in LDS in a fixed order), on the fp32 MFMA as
+// se_layer. The fc1 launch (S > 0) squeezes on the fly: X[n][k] = scale * sum_z ws[z][n][k], and the
+// workgroups of the first column tile write `pooled`. Two launches in place of k_sum_planes + two
+// k_dense_rows passes (whose per-column wave sums made them latency chains: ~17 + 14 us at C = 256).
+template <int ACT>
+__global__ void __launch_bounds__(256) k_se_dense(const float* __restrict__ X, int S, float scale, int N, int K,
+                                                  const float* __restrict__ W, const float* __restrict__ b, int J,
+                                                  float* __restrict__ pooled, float* __restrict__ pre,
+                                                  float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float red[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, fr = lane & 15, q = lane >> 4;
+  const int tn = (N + 15) / 16;
+  const int n0 = (blockIdx.x % tn) * 16, j0 = (blockIdx.x / tn) * 16;
+  const int n = n0 + fr, j = j0 + fr;
+  const int St = (K + 15) / 16, s0 = wv * St / 4, s1 = (wv + 1) * St / 4;
+  const bool wpool = pooled && j0 == 0;
+  const long long NK = (long long)N * K;
+  se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = s0; c0 < s1; c0 += SE1_PF) {
+    float4 wb[SE1_PF], xb[SE1_PF];
+#pragma unroll
+    for (int i = 0; i < SE1_PF; ++i) {
+      const int k = (c0 + i) * 16 + 4 * q;  // K % 4 == 0: a float4 is wholly in or out
+      const bool kin = c0 + i < s1 && k < K;
+      wb[i] = (kin && j < J) ? *(const float4*)(W + (size_t)j * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kin && n < N) {
+        if (S > 0) {
+          for (int z = 0; z < S; ++z) {
+            const float4 v = *(const float4*)(X + z * NK + (size_t)n * K + k);
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+          }
+          a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
+          if (wpool) *(float4*)(pooled + (size_t)n * K + k) = a;
+        } else {
+          a = *(const float4*)(X + (size_t)n * K + k);
+        }
+      }
+      xb[i] = a;
+    }
+#pragma unroll
+    for (int i = 0; i < SE1_PF; ++i) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i].x, wb[i].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i].y, wb[i].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i].z, wb[i].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i].w, wb[i].w, acc, 0, 0, 0);
+    }
+  }
+  *(float4*)(&red[wv][lane * 4]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  // D[row 4q + r][col fr]: output row n0 + 4q + r, column j0 + fr
+  const int e = tid, ln = e >> 2, r = e & 3;
+  const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+  const int nr = n0 + 4 * (ln >> 4) + r, jc = j0 + (ln & 15);
+  if (nr < N && jc < J) {
+    const float z = v + (b ? b[jc] : 0.f);
+    if (pre) pre[(size_t)nr * J + jc] = z;
+    out[(size_t)nr * J + jc] = ACT == DMF_ACT_GELU ? gelu_f(z) : sigmoid_f(z);
+  }
+}
+
 // pooled[n][c] = scale * sum_z ws[z][n][c] (the squeeze's stage-1 partial planes)
 __global__ void k_sum_planes(const float* __restrict__ ws, int S, long long NC, float scale, float* __restrict__ out) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < NC; i += (long long)gridDim.x * blockDim.x) {
@@ -1272,10 +1334,13 @@ extern "C" int dmf_gate_bwd(const float* pv_dwi, const float* pv_dce, const floa
   return 0;
 }
 
-// 1 (default): the one-workgroup excitation (k_se_mlp1) where it fits; 0: the three-launch form
+// 1 (default): two launches of fp32-MFMA tiles (k_se_dense); 2: the one-workgroup form (k_se_mlp1) where it
+// fits, else as 1; 0: the three-launch form (k_sum_planes + two k_dense_rows). tools/se_bench.py, N = 32:
+// C = 128: 25.8 (0) / 10.6 (2) us; C = 256: 28.7 (0) / 6.8 (1) us; C = 512: 35.8 (0) / 11.8 (1) us
 static int g_se_one_launch = 1;
-extern "C" int dmf_se_mlp_tune(int one_launch) {
-  g_se_one_launch = one_launch != 0;
+extern "C" int dmf_se_mlp_tune(int mode) {
+  DMF_CHECK_ARG(mode >= 0 && mode <= 2, "dmf_se_mlp_tune: mode %d (0..2)", mode);
+  g_se_one_launch = mode;
   return 0;
 }
 
@@ -1292,12 +1357,22 @@ extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, con
   const size_t lds1 = (size_t)N * (C + mid) * 4 + 16 * 256 * 4;
   // (one CU runs both layers on the fp32 MFMA, 2*N*C*mid FMAs each: it wins up to the C = 128 SEs --
   // 11.8 vs 26.0 us at N = 32, C = 128 -- and ties at C = 256, tools/se_bench.py)
-  if (g_se_one_launch && N <= 64 && C % 4 == 0 && mid % 4 == 0 && lds1 <= 96 * 1024 &&
+  if (g_se_one_launch == 2 && N <= 64 && C % 4 == 0 && mid % 4 == 0 && lds1 <= 96 * 1024 &&
       (long long)N * C * mid <= 32LL * 128 * 64 &&
       (!pooled || pooled != ws || S == 1)) {
     // (pooled == ws with S == 1: the squeeze read and its write touch the same element in one thread)
     hipLaunchKernelGGL(k_se_mlp1, dim3(1), dim3(SE1_THREADS), lds1, st, ws, S, N, C, scale, w1, b1, mid, w2, b2,
                        pooled, hpre, hact, gate);
+    DMF_LAUNCH_CHECK("dmf_se_mlp");
+    return 0;
+  }
+  if (g_se_one_launch && C % 4 == 0 && mid % 4 == 0 && (!pooled || pooled != ws)) {
+    // two launches of MFMA tiles (k_se_dense); fc1 squeezes the partial planes on the fly
+    const int tn = cdiv(N, 16);
+    hipLaunchKernelGGL(k_se_dense<DMF_ACT_GELU>, dim3((unsigned)(tn * cdiv(mid, 16))), dim3(256), 0, st, ws, S, scale,
+                       N, C, w1, b1, mid, pooled, hpre, hact);
+    hipLaunchKernelGGL(k_se_dense<DMF_ACT_SIGMOID>, dim3((unsigned)(tn * cdiv(C, 16))), dim3(256), 0, st,
+                       (const float*)hact, 0, 1.f, N, mid, w2, b2, C, (float*)nullptr, (float*)nullptr, gate);
     DMF_LAUNCH_CHECK("dmf_se_mlp");
     return 0;
   }

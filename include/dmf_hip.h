@@ -419,10 +419,10 @@ int dmf_sig_grad_f32(const float* dg, const float* s, float* dz, long long n, vo
  * 16-B aligned. */
 int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, const float* w1, const float* b1, int mid,
                const float* w2, const float* b2, float* pooled, float* hpre, float* hact, float* gate, void* stream);
-/* 1 (default): dmf_se_mlp runs as ONE workgroup (squeeze sum, both layers on the exact fp32 MFMA, the
- * activations in LDS) where N <= 64, C and mid are multiples of 4 and N*(C+mid) floats fit 96 KiB;
- * 0: always the three-launch form (A/B runs). */
-int dmf_se_mlp_tune(int one_launch);
+/* dmf_se_mlp's form (A/B runs): 1 (default) two launches of 16 x 16 fp32-MFMA output tiles, the squeeze
+ * summed on the fly (C and mid multiples of 4); 2 one workgroup for both layers where N <= 64 and
+ * N*(C+mid) floats fit 96 KiB; 0 the three-launch form. */
+int dmf_se_mlp_tune(int mode);
 int dmf_row_l2norm(const float* x, int R, int C, float eps, float* y, float* norms, void* stream);
 int dmf_row_l2norm_bwd(const float* dy, const float* y, const float* norms, int R, int C, float eps, float* dx,
                        void* stream);

@@ -30,7 +30,7 @@ def main():
         outs = [torch.empty(n, c, device="cuda"), torch.empty(n, mid, device="cuda"),
                 torch.empty(n, mid, device="cuda"), torch.empty(n, c, device="cuda")]
         res = []
-        for one in (1, 0):
+        for one in (1, 2, 0):
             N.call("dmf_se_mlp_tune", one)
 
             def run():
@@ -39,7 +39,8 @@ def main():
                        O._stream())
             res.append(timed(run, a.reps))
         N.call("dmf_se_mlp_tune", 1)
-        print(f"N={n} C={c} mid={mid} S={s}: one launch {res[0]:6.1f} us   three launches {res[1]:6.1f} us", flush=True)
+        print(f"N={n} C={c} mid={mid} S={s}: two MFMA-tile launches {res[0]:6.1f} us   one workgroup {res[1]:6.1f} us"
+              f"   three launches {res[2]:6.1f} us", flush=True)
 
 
 if __name__ == "__main__":
