@@ -116,6 +116,54 @@ __global__ void __launch_bounds__(256) k_sgemm(int tA, int tB, int M, int N, int
     }
 }
 
+// The small fusion GEMMs (M, N <= 512) as a grid of 16 x 16 output tiles on the exact fp32 MFMA
+// (v_mfma_f32_16x16x4f32), one workgroup per tile, its K-steps split over 4 waves and the 4 partial tiles
+// summed in LDS in a fixed order (deterministic, no split-K workspace or reduce launch). Lane group q
+// takes k = 16 s + 4 q + e in MFMA e of step s for both operands (any op(A) / op(B) layout: element loads,
+// up to SG_PF steps in flight). k_sgemm ran 12-16 us on these shapes whatever their size (a per-launch
+// floor of its staged K loop, profiles/r04q_sgemm_shapes.txt).
+constexpr int SG_PF = 4;
+typedef __attribute__((ext_vector_type(4))) float sg_f32x4;
+__global__ void __launch_bounds__(256) k_sgemm_mfma(int tA, int tB, int M, int N, int K, float alpha,
+                                                    const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                    int ldb, float beta, float* __restrict__ C, int ldc,
+                                                    const float* __restrict__ bias, int act) {
+  __shared__ __attribute__((aligned(16))) float red[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, fr = lane & 15, q = lane >> 4;
+  const int tm = (M + 15) / 16;
+  const int m0 = (blockIdx.x % tm) * 16, n0 = (blockIdx.x / tm) * 16;
+  const int m = m0 + fr, n = n0 + fr;
+  const int St = (K + 15) / 16, s0 = wv * St / 4, s1 = (wv + 1) * St / 4;
+  sg_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = s0; c0 < s1; c0 += SG_PF) {
+    float av[SG_PF][4], bv[SG_PF][4];
+#pragma unroll
+    for (int i = 0; i < SG_PF; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = (c0 + i) * 16 + 4 * q + e;
+        const bool kin = c0 + i < s1 && k < K;
+        av[i][e] = (kin && m < M) ? (tA ? A[(size_t)k * lda + m] : A[(size_t)m * lda + k]) : 0.f;
+        bv[i][e] = (kin && n < N) ? (tB ? B[(size_t)n * ldb + k] : B[(size_t)k * ldb + n]) : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < SG_PF; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][e], bv[i][e], acc, 0, 0, 0);
+  }
+  *(float4*)(&red[wv][lane * 4]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  // D[row 4q + r][col fr]: output row m0 + 4q + r, column n0 + fr
+  const int ln = tid >> 2, r = tid & 3;
+  const int mr = m0 + 4 * (ln >> 4) + r, nc = n0 + (ln & 15);
+  if (mr < M && nc < N) {
+    float v = alpha * (((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]);
+    if (beta != 0.f) v += beta * C[(size_t)mr * ldc + nc];
+    if (bias) v += bias[nc];
+    C[(size_t)mr * ldc + nc] = actf(act, v);
+  }
+}
+
 __global__ void k_sgemm_reduce(int S, int M, int N, float alpha, const float* __restrict__ ws, float beta,
                                float* __restrict__ C, int ldc, const float* __restrict__ bias, int act) {
   const long long total = (long long)M * N;
@@ -1109,6 +1157,13 @@ static int sgemm_splits(int M, int N, int K) {
 }
 
 
+// 1 (default): the small GEMMs (M * N <= 512^2, K <= 8192) on k_sgemm_mfma; 0: always k_sgemm
+static int g_sgemm_mfma = 1;
+extern "C" int dmf_sgemm_tune(int mfma) {
+  g_sgemm_mfma = mfma != 0;
+  return 0;
+}
+
 extern "C" int dmf_sgemm_ws_size(int M, int N, int K) {
   const int S = sgemm_splits(M, N, K);
   return S > 1 ? S * M * N : 0;
@@ -1120,6 +1175,12 @@ extern "C" int dmf_sgemm(int transA, int transB, int M, int N, int K, float alph
   DMF_CHECK_ARG(A && B && C && M >= 0 && N >= 0 && K >= 0, "dmf_sgemm: bad args");
   if (M == 0 || N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (g_sgemm_mfma && (long long)M * N <= 512LL * 512 && K <= 8192) {
+    hipLaunchKernelGGL(k_sgemm_mfma, dim3((unsigned)(cdiv(M, 16) * cdiv(N, 16))), dim3(256), 0, st, transA, transB, M,
+                       N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, act);
+    DMF_LAUNCH_CHECK("dmf_sgemm");
+    return 0;
+  }
   // (beta != 0 -- an accumulating weight gradient -- splits too: the ordered reduce adds beta * C)
   int S = workspace ? sgemm_splits(M, N, K) : 1;
   const int kchunk = S > 1 ? cdiv(cdiv(K, S), 16) * 16 : std::max(K, 1);

@@ -406,6 +406,10 @@ int dmf_mix_bwd(int dtype, const void* dz, int lddz, const void* a, int lda, con
 int dmf_sgemm_ws_size(int M, int N, int K);
 int dmf_sgemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
               int ldb, float beta, float* C, int ldc, const float* bias, int act, float* workspace, void* stream);
+/* 1 (default): dmf_sgemm's small GEMMs (M * N <= 512^2, K <= 8192) on 16 x 16 fp32-MFMA output tiles, one
+ * workgroup per tile with the K-steps split over its 4 waves (no split-K workspace); 0: the 64 x 64 VALU
+ * tile with split-K (A/B runs) */
+int dmf_sgemm_tune(int mfma);
 int dmf_colsum_f32(const float* X, int ldx, int M, int N, float* out, int accumulate, void* stream);
 int dmf_act_grad_f32(const float* dy, const float* z, float* dx, long long n, int act, void* stream);
 int dmf_act_f32(const float* x, float* y, long long n, int act, void* stream);
