@@ -1428,10 +1428,23 @@ extern "C" int dmf_se_mlp(const float* ws, int S, int N, int C, float scale, con
     return 0;
   }
   if (g_se_one_launch && C % 4 == 0 && mid % 4 == 0 && (!pooled || pooled != ws)) {
-    // two launches of MFMA tiles (k_se_dense); fc1 squeezes the partial planes on the fly
+    // two launches of MFMA tiles (k_se_dense); fc1 squeezes the partial planes on the fly, up to 2 of them
+    // (every column tile re-reads the planes: beyond that one k_sum_planes pass first is cheaper)
     const int tn = cdiv(N, 16);
-    hipLaunchKernelGGL(k_se_dense<DMF_ACT_GELU>, dim3((unsigned)(tn * cdiv(mid, 16))), dim3(256), 0, st, ws, S, scale,
-                       N, C, w1, b1, mid, pooled, hpre, hact);
+    const float* xs = ws;
+    int S1 = S;
+    float sc1 = scale;
+    float* pool1 = pooled;
+    if (S > 2) {
+      const long long nc = (long long)N * C;
+      hipLaunchKernelGGL(k_sum_planes, dim3(gsz(nc)), dim3(256), 0, st, ws, S, nc, scale, pooled);
+      xs = pooled;
+      S1 = 0;
+      sc1 = 1.f;
+      pool1 = nullptr;
+    }
+    hipLaunchKernelGGL(k_se_dense<DMF_ACT_GELU>, dim3((unsigned)(tn * cdiv(mid, 16))), dim3(256), 0, st, xs, S1, sc1,
+                       N, C, w1, b1, mid, pool1, hpre, hact);
     hipLaunchKernelGGL(k_se_dense<DMF_ACT_SIGMOID>, dim3((unsigned)(tn * cdiv(C, 16))), dim3(256), 0, st,
                        (const float*)hact, 0, 1.f, N, mid, w2, b2, C, (float*)nullptr, (float*)nullptr, gate);
     DMF_LAUNCH_CHECK("dmf_se_mlp");

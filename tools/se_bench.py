@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
-    for n, c, s in ((32, 128, 1), (32, 128, 8), (32, 256, 1), (32, 256, 8), (32, 512, 4)):
+    for n, c, s in ((32, 128, 1), (32, 128, 8), (32, 256, 1), (32, 256, 8), (32, 256, 32), (32, 512, 4)):
         mid = c // 2
         ws = torch.randn(s, n, c, device="cuda")
         w1, b1 = torch.randn(mid, c, device="cuda"), torch.randn(mid, device="cuda")
