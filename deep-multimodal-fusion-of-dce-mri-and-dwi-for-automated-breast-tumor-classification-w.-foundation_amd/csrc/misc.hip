@@ -727,14 +727,14 @@ __global__ void k_input_prep8(const float* __restrict__ x, int N, int C, int H, 
   }
 }
 
-template <typename T>
+template <typename T, typename I = long long>
 __global__ void k_up_nearest8(const T* __restrict__ x, int ldx, T* __restrict__ y, int N, int H, int W, int C, int r) {
   const int CV = C >> 3;
-  const long long total = (long long)N * r * H * r * W * CV;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  const I total = (long long)N * r * H * r * W * CV;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (I)gridDim.x * blockDim.x) {
     const int cv = (int)(i % CV);
-    long long t = i / CV;
+    I t = i / CV;
     const int wo = (int)(t % (r * W)); t /= (r * W);
     const int ho = (int)(t % (r * H));
     const int n = (int)(t / (r * H));
@@ -878,16 +878,16 @@ __global__ void k_maxpool8(const T* __restrict__ x, int N, int H, int W, int C, 
   }
 }
 
-template <typename T>
+template <typename T, typename I = long long>
 __global__ void k_channel_scale8(const T* __restrict__ x, int ldx, const float* __restrict__ gate,
                                  T* __restrict__ y, int ldy, long long N, int HW, int C) {
   const int CV = C >> 3;
-  const long long total = N * HW * CV;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long row = i / CV;
+  const I total = N * HW * CV;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (I)gridDim.x * blockDim.x) {
+    const I row = i / CV;
     const int c = (int)(i - row * CV) * 8;
-    const long long n = row / HW;
+    const I n = row / HW;
     float v[8];
     ld8(x + row * ldx + c, v);
     const float4 g0 = *(const float4*)(gate + n * C + c), g1 = *(const float4*)(gate + n * C + c + 4);
@@ -897,15 +897,15 @@ __global__ void k_channel_scale8(const T* __restrict__ x, int ldx, const float* 
   }
 }
 
-template <typename T>
+template <typename T, typename I = long long>
 __global__ void k_mix8(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb,
                        const float* __restrict__ wlogit, T* __restrict__ z, int ldz, long long M, int C) {
   const float al = 1.f / (1.f + __expf(-wlogit[0]));
   const int CV = C >> 3;
-  const long long total = M * CV;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long m = i / CV;
+  const I total = M * CV;
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (I)gridDim.x * blockDim.x) {
+    const I m = i / CV;
     const int c = (int)(i - m * CV) * 8;
     float va[8], vb[8];
     ld8(a + m * lda + c, va);
@@ -1019,6 +1019,12 @@ extern "C" int dmf_channel_scale(int dtype, const void* x, int ldx, const float*
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, ldy, x, y, gate)) {
+    // 32-bit index math when every offset fits (a 64-bit div per chunk otherwise)
+    if ((long long)N * HW * std::max(ldx, ldy) < (1LL << 30))
+      DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_channel_scale8<T, int>), dim3(gsz(total / 8)), dim3(256), 0,
+                                                      (hipStream_t)stream, (const T*)x, ldx, gate, (T*)y, ldy,
+                                                      (long long)N, HW, C));
+    else
     DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_channel_scale8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
                          (const T*)x, ldx, gate, (T*)y, ldy, (long long)N, HW, C));
     DMF_LAUNCH_CHECK("dmf_channel_scale");
@@ -1035,6 +1041,11 @@ extern "C" int dmf_mix(int dtype, const void* a, int lda, const void* b, int ldb
   DMF_CHECK_ARG(a && b && wlogit && z, "dmf_mix: bad args");
   if (M * C == 0) return 0;
   if (v8ok(C, lda, ldb, a, b) && ldz % 8 == 0 && a16(z)) {
+    if (M * std::max(std::max(lda, ldb), std::max(ldz, C)) < (1LL << 30))
+      DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_mix8<T, int>), dim3(gsz(M * C / 8)), dim3(256), 0,
+                                                      (hipStream_t)stream, (const T*)a, lda, (const T*)b, ldb, wlogit,
+                                                      (T*)z, ldz, M, C));
+    else
     DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_mix8<T>, dim3(gsz(M * C / 8)), dim3(256), 0, (hipStream_t)stream, (const T*)a,
                          lda, (const T*)b, ldb, wlogit, (T*)z, ldz, M, C));
     DMF_LAUNCH_CHECK("dmf_mix");
@@ -1143,6 +1154,10 @@ extern "C" int dmf_upsample_nearest(int dtype, const void* x, int ldx, void* y, 
   const long long total = (long long)N * r * r * H * W * C;
   if (total == 0) return 0;
   if (v8ok(C, ldx, 8, x, y)) {
+    if (total < (1LL << 30) && (long long)N * H * W * ldx < (1LL << 30))
+      DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_up_nearest8<T, int>), dim3(gsz(total / 8)), dim3(256), 0,
+                                                      (hipStream_t)stream, (const T*)x, ldx, (T*)y, N, H, W, C, r));
+    else
     DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_up_nearest8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream,
                          (const T*)x, ldx, (T*)y, N, H, W, C, r));
     DMF_LAUNCH_CHECK("dmf_upsample_nearest");
