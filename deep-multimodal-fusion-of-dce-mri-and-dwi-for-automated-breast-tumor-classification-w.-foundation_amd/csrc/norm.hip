@@ -250,7 +250,7 @@ __device__ __forceinline__ void bn_src_affine(const BnApplySrc& s, int c, int C,
 // channel chunks x 32 rows; the block's 64 (scale, shift) pairs are
 // finalized once into LDS. Dropout elements are indexed m*C + c exactly as
 // k_affine_act8 / k_act_bwd, so backward regenerates the same masks.
-template <typename T, int ACT, int RES>
+template <typename T, int ACT, int RES, int U>
 __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int ldx, BnApplySrc A,
                                                    const T* __restrict__ res, int ldr, BnApplySrc R, float p,
                                                    const unsigned long long* rng, int site, T* __restrict__ y, int ldy,
@@ -293,41 +293,58 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
   const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int mbeg = blockIdx.y * rows_per_blk;
   const int mend = min(M, mbeg + rows_per_blk);
-  for (int m = mbeg + (tid >> 3); m < mend; m += 32) {
-    float v[8];
-    ld8(x + (size_t)m * ldx + c0, v);
+  // U rows per thread in flight: all U (x, res) loads issue before the first conversion
+  for (int mu = mbeg + (tid >> 3); mu < mend; mu += 32 * U) {
+    Vec8<T> xr[U], rr[U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = v[k] * s8[k] + h8[k];
-    if (RES != 0) {
-      float r[8];
-      ld8(res + (size_t)m * ldr + c0, r);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += RES == 2 ? r[k] * rs8[k] + rh8[k] : r[k];
-    }
-    if constexpr (ACT == DMF_ACT_GELU) {
-#pragma unroll
-      for (int k = 0; k < 8; k += 2) {
-        const dmf_f2 g = gelu_f2(dmf_f2{v[k], v[k + 1]});
-        v[k] = g.x;
-        v[k + 1] = g.y;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
-        else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+    for (int u = 0; u < U; ++u) {
+      const int m = mu + 32 * u;
+      xr[u] = zero8<T>();
+      rr[u] = zero8<T>();
+      if (m < mend) {
+        xr[u] = ldv8(x + (size_t)m * ldx + c0);
+        if (RES != 0) rr[u] = ldv8(res + (size_t)m * ldr + c0);
       }
     }
-    if (p > 0.f) {
-      bool keep[4];
-      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0, p, keep);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * dsc : 0.f;
-      dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0 + 4, p, keep);
+    for (int u = 0; u < U; ++u) {
+      const int m = mu + 32 * u;
+      if (m >= mend) break;
+      float v[8];
+      unpack8(xr[u], v);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * dsc : 0.f;
+      for (int k = 0; k < 8; ++k) v[k] = v[k] * s8[k] + h8[k];
+      if (RES != 0) {
+        float r[8];
+        unpack8(rr[u], r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += RES == 2 ? r[k] * rs8[k] + rh8[k] : r[k];
+      }
+      if constexpr (ACT == DMF_ACT_GELU) {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const dmf_f2 g = gelu_f2(dmf_f2{v[k], v[k + 1]});
+          v[k] = g.x;
+          v[k + 1] = g.y;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (ACT == DMF_ACT_RELU) v[k] = fmaxf(v[k], 0.f);
+          else if (ACT == DMF_ACT_SIGMOID) v[k] = sigmoid_f(v[k]);
+        }
+      }
+      if (p > 0.f) {
+        bool keep[4];
+        dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0, p, keep);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = keep[k] ? v[k] * dsc : 0.f;
+        dropout_keep4v(rseed_, roff_, site, (unsigned long long)m * C + c0 + 4, p, keep);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 + k] = keep[k] ? v[4 + k] * dsc : 0.f;
+      }
+      st8(y + (size_t)m * ldy + c0, v);
     }
-    st8(y + (size_t)m * ldy + c0, v);
   }
 }
 
@@ -866,6 +883,15 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
   return 0;
 }
 
+// rows of k_bn_apply's loads in flight per thread (1 default; dmf_bn_apply_tune, tools/apply_bench.py --rows)
+static int g_bn_apply_rows = 1;
+extern "C" int dmf_bn_apply_tune(int rows_in_flight) {
+  DMF_CHECK_ARG(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4, "dmf_bn_apply_tune: %d",
+                rows_in_flight);
+  g_bn_apply_rows = rows_in_flight;
+  return 0;
+}
+
 static BnApplySrc bn_src(const dmf_bn_desc* d, const float* ss) {
   BnApplySrc s{};
   if (d) {
@@ -908,9 +934,15 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
   const dim3 g((unsigned)gy, (unsigned)cdiv(M, rows));  // channel groups fastest: resident blocks cover whole rows
   const int resk = res == nullptr ? 0 : ((res_bn || res_scale_shift) ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-#define DMF_BA(TT, AC, RK)                                                                                     \
-  hipLaunchKernelGGL((k_bn_apply<TT, AC, RK>), g, dim3(256), 0, s, (const TT*)x, ldx, A, (const TT*)res, ldr, R, \
-                     dropout_p, rng, site, (TT*)y, ldy, (int)M, C, rows)
+#define DMF_BA_U(TT, AC, RK, UU)                                                                             \
+  hipLaunchKernelGGL((k_bn_apply<TT, AC, RK, UU>), g, dim3(256), 0, s, (const TT*)x, ldx, A, (const TT*)res, ldr, \
+                     R, dropout_p, rng, site, (TT*)y, ldy, (int)M, C, rows)
+#define DMF_BA(TT, AC, RK)                          \
+  do {                                              \
+    if (g_bn_apply_rows == 4) DMF_BA_U(TT, AC, RK, 4); \
+    else if (g_bn_apply_rows == 2) DMF_BA_U(TT, AC, RK, 2); \
+    else DMF_BA_U(TT, AC, RK, 1);                   \
+  } while (0)
 #define DMF_BA_R(TT, AC)                 \
   do {                                   \
     if (resk == 0) DMF_BA(TT, AC, 0);     \
@@ -930,6 +962,7 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
 #undef DMF_BA_A
 #undef DMF_BA_R
 #undef DMF_BA
+#undef DMF_BA_U
   DMF_LAUNCH_CHECK("dmf_bn_apply");
   return 0;
 }

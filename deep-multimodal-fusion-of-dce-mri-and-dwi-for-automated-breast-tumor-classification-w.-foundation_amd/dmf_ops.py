@@ -2653,6 +2653,7 @@ KNOBS = {
     "two_pass_max_k": ("dmf_ops", "TWO_PASS_MAX_K"),
     "fc1_drop_conv": ("dmf_tokens", "FC1_DROP_CONV"),
     "bwd_apply_rows": ("call", "dmf_bn_bwd_apply_tune"),
+    "fwd_apply_rows": ("call", "dmf_bn_apply_tune"),
     "sgemm_mfma": ("call", "dmf_sgemm_tune"),
     "wgrad_xcd": ("wgrad_tune", 6),
     "conc_min_tiles": ("dmf_ops", "CONC_MIN_TILES"),

@@ -317,6 +317,8 @@ int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int
                          float* dbeta, void* dx, int lddx, long long M, int C, void* stream);
 /* rows of dmf_bn_bwd_apply_acc's loads in flight per thread: 1 (default), 2 or 4 (A/B runs) */
 int dmf_bn_bwd_apply_tune(int rows_in_flight);
+/* rows of dmf_bn_apply's loads in flight per thread: 1 (default), 2 or 4 (A/B runs) */
+int dmf_bn_apply_tune(int rows_in_flight);
 int dmf_col_stats_tiles(long long M);
 int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
 
