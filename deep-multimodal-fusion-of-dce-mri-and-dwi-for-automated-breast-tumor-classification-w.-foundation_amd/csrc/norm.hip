@@ -260,6 +260,26 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
   const int tid = threadIdx.x;
   const int cg = blockIdx.x * 64;
   const bool first = blockIdx.y == 0;
+  const int cl = (tid & 7) * 8, c0 = cg + cl;
+  const int mbeg = blockIdx.y * rows_per_blk;
+  const int mend = min(M, mbeg + rows_per_blk);
+  // U rows per thread in flight: all U (x, res) loads issue before the first conversion; the first
+  // group's loads go out before the finalize prologue, so its arena reads hide under them
+  Vec8<T> xr[U], rr[U];
+  auto load = [&](int mu) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = mu + 32 * u;
+      xr[u] = zero8<T>();
+      rr[u] = zero8<T>();
+      if (m < mend) {
+        xr[u] = ldv8(x + (size_t)m * ldx + c0);
+        if (RES != 0) rr[u] = ldv8(res + (size_t)m * ldr + c0);
+      }
+    }
+  };
+  int mu = mbeg + (tid >> 3);
+  if (c0 < C) load(mu);
   if (tid < 64) {
     const int c = cg + tid;
     float sc = 1.f, sh = 0.f;
@@ -278,7 +298,6 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
     if (RES == 2 && R.acc && R.fin.nbt) *R.fin.nbt += 1;
   }
   __syncthreads();
-  const int cl = (tid & 7) * 8, c0 = cg + cl;
   if (c0 >= C) return;
   float s8[8], h8[8], rs8[8], rh8[8];
 #pragma unroll
@@ -291,21 +310,8 @@ __global__ void __launch_bounds__(256) k_bn_apply(const T* __restrict__ x, int l
     }
   }
   const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int mbeg = blockIdx.y * rows_per_blk;
-  const int mend = min(M, mbeg + rows_per_blk);
-  // U rows per thread in flight: all U (x, res) loads issue before the first conversion
-  for (int mu = mbeg + (tid >> 3); mu < mend; mu += 32 * U) {
-    Vec8<T> xr[U], rr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int m = mu + 32 * u;
-      xr[u] = zero8<T>();
-      rr[u] = zero8<T>();
-      if (m < mend) {
-        xr[u] = ldv8(x + (size_t)m * ldx + c0);
-        if (RES != 0) rr[u] = ldv8(res + (size_t)m * ldr + c0);
-      }
-    }
+  for (; mu < mend; mu += 32 * U) {
+    if (mu != mbeg + (tid >> 3)) load(mu);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int m = mu + 32 * u;
@@ -680,6 +686,22 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
   __shared__ float sco[3][64];
   const int tid = threadIdx.x;
   const int cg = blockIdx.x * 64;
+  const int cl = (tid & 7) * 8, c0 = cg + cl;
+  const int mbeg = blockIdx.y * rows_per_blk;
+  const int mend = min(M, mbeg + rows_per_blk);
+  // U rows per thread per round, every load of the round issued before any row is converted; the
+  // first round's loads go out before the finalize prologue (its arena reads hide under them)
+  Vec8<T> vg[U], vx[U];
+  auto load = [&](int m) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int mu = m + 32 * u;
+      vg[u] = mu < mend ? ldv8(dz + (size_t)mu * lddz + c0) : zero8<T>();
+      vx[u] = mu < mend ? ldv8(x + (size_t)mu * ldx + c0) : zero8<T>();
+    }
+  };
+  int m = mbeg + (tid >> 3);
+  if (c0 < C) load(m);
   if (tid < 64) {
     const int c = cg + tid;
     float A = 0.f, Cc = 0.f, B = 0.f;
@@ -707,7 +729,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
     sco[2][tid] = B;
   }
   __syncthreads();
-  const int cl = (tid & 7) * 8, c0 = cg + cl;
   if (c0 >= C) return;
   float a8[8], c8[8], b8[8];
 #pragma unroll
@@ -716,17 +737,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
     c8[k] = sco[1][cl + k];
     b8[k] = sco[2][cl + k];
   }
-  const int mbeg = blockIdx.y * rows_per_blk;
-  const int mend = min(M, mbeg + rows_per_blk);
-  // U rows per thread per round, every load of the round issued before any row is converted
-  for (int m = mbeg + (tid >> 3); m < mend; m += 32 * U) {
-    Vec8<T> vg[U], vx[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int mu = m + 32 * u;
-      vg[u] = mu < mend ? ldv8(dz + (size_t)mu * lddz + c0) : zero8<T>();
-      vx[u] = mu < mend ? ldv8(x + (size_t)mu * ldx + c0) : zero8<T>();
-    }
+  for (; m < mend; m += 32 * U) {
+    if (m != mbeg + (tid >> 3)) load(m);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int mu = m + 32 * u;

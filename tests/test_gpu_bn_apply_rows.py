@@ -51,3 +51,46 @@ def test_rows_in_flight_bitwise(m, c, rk, act, p):
         z = torch.where(kept, z / (1 - p), torch.zeros_like(z))
         assert abs(kept.float().mean().item() - (1 - p)) < 0.02
     assert torch.allclose(y1.float(), z, rtol=2 ** -7, atol=1e-5)
+
+
+@pytest.mark.parametrize("m,c", [(32768, 256), (1000, 72), (4133, 2048)])
+def test_bwd_apply_rows_in_flight(m, c):
+    """dmf_bn_bwd_apply_acc (training BN backward, finalize from the float64 arena) against the
+    torch statement dx = g*inv*(dz - mean(dz) - xhat*mean(dz*xhat)), and its 2 / 4 rows-in-flight
+    forms bitwise against the one-row form."""
+    torch.manual_seed(2)
+    reps = O.BN_ACC_REPLICAS
+    x = (torch.randn(m, c, device=DEV) * 2 + 0.5).bfloat16()
+    dz = torch.randn(m, c, device=DEV).bfloat16()
+    xf = x.double()
+    mean = xf.mean(0)
+    inv = (xf.var(0, unbiased=False) + 1e-5).rsqrt()
+    xhat = (xf - mean) * inv
+    s, q = dz.double().sum(0), (dz.double() * xhat).sum(0)
+    w = torch.rand(reps, 1, device=DEV, dtype=torch.float64)
+    w = w / w.sum()
+    acc = torch.stack([w * s, w * q], -1).contiguous()  # [reps][C][2], sums to (s, q)
+    save = torch.cat([mean, inv]).float()
+    gamma = torch.rand(c, device=DEV) + 0.5
+
+    def run(u):
+        N.call("dmf_bn_bwd_apply_tune", u)
+        dx = torch.empty_like(x)
+        dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+        N.call("dmf_bn_bwd_apply_acc", N.BF16, dz.data_ptr(), c, x.data_ptr(), c, acc.data_ptr(), reps, float(m), 1,
+               gamma.data_ptr(), save.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), c, m, c,
+               N.stream_ptr())
+        torch.cuda.synchronize()
+        return dx, dg, db
+
+    try:
+        dx1, dg1, db1 = run(1)
+        for u in (2, 4):
+            dxu, dgu, dbu = run(u)
+            assert torch.equal(dx1, dxu) and torch.equal(dg1, dgu) and torch.equal(db1, dbu), u
+    finally:
+        N.call("dmf_bn_bwd_apply_tune", 1)
+    ref = gamma.double() * inv * (dz.double() - s / m - xhat * q / m)
+    assert torch.allclose(dx1.double(), ref, rtol=2 ** -7, atol=2e-3 * ref.abs().max().item())
+    assert torch.allclose(db1.double(), s, rtol=1e-6, atol=1e-3)
+    assert torch.allclose(dg1.double(), q, rtol=1e-6, atol=1e-3)
