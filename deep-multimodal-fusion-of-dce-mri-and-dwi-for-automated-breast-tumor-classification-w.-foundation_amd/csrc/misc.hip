@@ -142,6 +142,70 @@ __global__ void k_gn_apply(const T* __restrict__ z, int ldz, const float* __rest
   }
 }
 
+__device__ __forceinline__ void ldf8(const float* p, float v[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// k_gn_apply on 8-channel 16-B vectors with 32-bit index math (C % 8 == 0, rows * C < 2^31): the
+// same per-element arithmetic, one 16-B load / store per thread instead of eight 2-B ones and two
+// 64-bit divisions per element
+template <typename T>
+__global__ void __launch_bounds__(256) k_gn_apply8(const T* __restrict__ z, int ldz, const float* __restrict__ mean,
+                                                   const float* __restrict__ m2, const float* __restrict__ g,
+                                                   const float* __restrict__ b, float eps, T* __restrict__ y, int ldy,
+                                                   int rows, int HW, int C) {
+  const int cv = C >> 3, total = rows * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int row = i / cv;
+    const int c0 = (i - row * cv) * 8;
+    const int nc = (row / HW) * C + c0;
+    float v[8], mu[8], q[8], gg[8], bb[8];
+    ld8(z + (size_t)row * ldz + c0, v);
+    ldf8(mean + nc, mu);
+    ldf8(m2 + nc, q);
+    ldf8(g + c0, gg);
+    ldf8(b + c0, bb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float var = fmaxf(q[k] - mu[k] * mu[k], 0.f);
+      v[k] = (v[k] - mu[k]) * rsqrtf(var + eps) * gg[k] + bb[k];
+    }
+    st8(y + (size_t)row * ldy + c0, v);
+  }
+}
+
+// k_gn_bwd_apply on 8-channel vectors (same conditions and arithmetic as k_gn_apply8 / k_gn_bwd_apply)
+template <typename T>
+__global__ void __launch_bounds__(256) k_gn_bwd_apply8(const T* __restrict__ dy, int lddy, const T* __restrict__ z,
+                                                       int ldz, const float* __restrict__ mean,
+                                                       const float* __restrict__ m2, const float* __restrict__ s1,
+                                                       const float* __restrict__ s2, const float* __restrict__ g,
+                                                       float eps, T* __restrict__ dz, int lddz, int rows, int HW, int C) {
+  const int cv = C >> 3, total = rows * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int row = i / cv;
+    const int c0 = (i - row * cv) * 8;
+    const int nc = (row / HW) * C + c0;
+    float d[8], zz[8], mu[8], q[8], a1[8], a2[8], gg[8];
+    ld8(dy + (size_t)row * lddy + c0, d);
+    ld8(z + (size_t)row * ldz + c0, zz);
+    ldf8(mean + nc, mu);
+    ldf8(m2 + nc, q);
+    ldf8(s1 + nc, a1);
+    ldf8(s2 + nc, a2);
+    ldf8(g + c0, gg);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float rs = rsqrtf(fmaxf(q[k] - mu[k] * mu[k], 0.f) + eps);
+      const float xh = (zz[k] - mu[k]) * rs;
+      d[k] = gg[k] * rs / (float)HW * ((float)HW * d[k] - a1[k] - xh * a2[k]);
+    }
+    st8(dz + (size_t)row * lddz + c0, d);
+  }
+}
+
 // GroupNorm(C,C) backward given per-(n,c) sums S1 = sum dy, S2 = sum dy*xhat:
 // dz = g*rstd/HW * (HW*dy - S1 - xhat*S2)
 template <typename T>
@@ -1062,6 +1126,15 @@ extern "C" int dmf_gn_apply(int dtype, const void* z, int ldz, const float* mean
   DMF_CHECK_ARG(z && mean && m2 && gamma && beta && y, "dmf_gn_apply: bad args");
   const long long total = (long long)N * HW * C;
   if (total == 0) return 0;
+  const long long rows = (long long)N * HW;
+  if (v8ok(C, ldz, ldy, z, y) && a16(mean) && a16(m2) && a16(gamma) && a16(beta) && rows * C < (1LL << 31) &&
+      rows * ldz < (1LL << 31) && rows * ldy < (1LL << 31)) {
+    DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gn_apply8<T>, dim3(gsz(total / 8)), dim3(256), 0,
+                                                    (hipStream_t)stream, (const T*)z, ldz, mean, m2, gamma, beta, eps,
+                                                    (T*)y, ldy, (int)rows, HW, C));
+    DMF_LAUNCH_CHECK("dmf_gn_apply");
+    return 0;
+  }
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_gn_apply<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)z, ldz,
                        mean, m2, gamma, beta, eps, (T*)y, ldy, (long long)N, HW, C));
   DMF_LAUNCH_CHECK("dmf_gn_apply");
@@ -1074,15 +1147,23 @@ extern "C" int dmf_gn_bwd(int dtype, const void* dy, int lddy, const void* z, in
   DMF_CHECK_ARG(dy && z && mean && m2 && gamma && s1 && s2 && dz, "dmf_gn_bwd: bad args");
   dim3 grid(N, cdiv(C, 64));
   const long long total = (long long)N * HW * C;
+  const long long rows = (long long)N * HW;
+  const bool apply8 = v8ok(C, lddy, ldz, dy, z, dz) && lddz % 8 == 0 && a16(mean) && a16(m2) && a16(s1) &&
+                      a16(s2) && a16(gamma) && rows * C < (1LL << 31) && rows * lddy < (1LL << 31) &&
+                      rows * ldz < (1LL << 31) && rows * lddz < (1LL << 31);
   DMF_DISPATCH_DTYPE(dtype, T, if (v8ok(C, lddy, ldz, dy, z))
       hipLaunchKernelGGL(k_gn_bwd_reduce8<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dy, lddy,
                          (const T*)z, ldz, mean, m2, eps, HW, C, s1, s2);
     else
       hipLaunchKernelGGL(k_gn_bwd_reduce<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)dy, lddy,
                          (const T*)z, ldz, mean, m2, eps, HW, C, s1, s2);
-    hipLaunchKernelGGL(k_gn_bwd_apply<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
-                       lddy, (const T*)z, ldz, mean, m2, s1, s2, gamma, eps, (T*)dz, lddz, (long long)N, HW,
-                       C));
+    if (apply8)
+      hipLaunchKernelGGL(k_gn_bwd_apply8<T>, dim3(gsz(total / 8)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                         lddy, (const T*)z, ldz, mean, m2, s1, s2, gamma, eps, (T*)dz, lddz, (int)rows, HW, C);
+    else
+      hipLaunchKernelGGL(k_gn_bwd_apply<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)dy,
+                         lddy, (const T*)z, ldz, mean, m2, s1, s2, gamma, eps, (T*)dz, lddz, (long long)N, HW,
+                         C));
   DMF_LAUNCH_CHECK("dmf_gn_bwd");
   return 0;
 }
