@@ -339,7 +339,9 @@ def pmc_traffic(family=""):
     *_pmc_traffic_<family>.json for others; written by tools/pmc_traffic.py from
     two rocprofv3 --pmc passes of this bench on an MI355X)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic%s.json" % ("_" + family if family else ""))))
+    # newest by modification time (run tags are not in lexicographic order: r05n predates r05f4)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic%s.json" % ("_" + family if family else ""))),
+                   key=lambda p: (os.path.getmtime(p), p))
     if not files:
         return None
     with open(files[-1]) as f:
