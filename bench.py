@@ -333,21 +333,35 @@ def roofline_probe(trainer, batch, dtype):
     }
 
 
-def pmc_traffic(family=""):
-    """HBM bytes per launch of a kernel family from the newest committed PMC
-    summary (profiles/*_pmc_traffic.json for the conv forward,
-    *_pmc_traffic_<family>.json for others; written by tools/pmc_traffic.py from
-    two rocprofv3 --pmc passes of this bench on an MI355X)."""
-    import glob
-    # newest by modification time (run tags are not in lexicographic order: r05n predates r05f4)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic%s.json" % ("_" + family if family else ""))),
-                   key=lambda p: (os.path.getmtime(p), p))
-    if not files:
+PMC_LATEST = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def pmc_summary(key):
+    """The PMC summary a committed pointer names: profiles/pmc_latest.json maps a
+    key ("traffic" = conv forward HBM bytes, "traffic_wgrad", "mfma", "mfma_wgrad")
+    to the summary file that tools/pmc_traffic.py / tools/pmc_mfma.py wrote for
+    this tree (--latest KEY updates the pointer). The pointer is data in the
+    repo, so a fresh clone reads the same file whatever the checkout's mtimes."""
+    try:
+        with open(PMC_LATEST) as f:
+            rel = json.load(f).get(key)
+    except (OSError, ValueError):
         return None
-    with open(files[-1]) as f:
+    if not rel:
+        return None
+    path = os.path.join(ROOT, rel)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
         d = json.load(f)
-    d["source"] = os.path.relpath(files[-1], ROOT)
+    d["source"] = rel
     return d
+
+
+def pmc_traffic(family=""):
+    """HBM bytes per launch of a kernel family (FETCH_SIZE x2 + WRITE_SIZE from
+    two rocprofv3 --pmc passes of this bench on an MI355X; tools/pmc_traffic.py)."""
+    return pmc_summary("traffic_" + family if family else "traffic")
 
 
 def _cpu_params(PR, args):

@@ -247,6 +247,9 @@ extern "C" int dmf_flash_attn_fwd(const void* qkv, int ldq, int batch, int n, in
   DMF_CHECK_ARG((long long)batch * n * ldq * 2 < (1LL << 31), "dmf_flash_attn_fwd: qkv exceeds 2 GiB");
   DMF_CHECK_ARG(dropout_p <= 0.f || rng, "dmf_flash_attn_fwd: dropout needs rng state");
   DMF_CHECK_ARG(dropout_p < 1.f, "dmf_flash_attn_fwd: p must be < 1");
+  // dropout_keep4v draws one Philox block per 4 consecutive elements of (bh*n + q)*n + key: the
+  // element index must stay 4-aligned for the masks to equal dmf_softmax_dropout's
+  DMF_CHECK_ARG(dropout_p <= 0.f || n % 4 == 0, "dmf_flash_attn_fwd: dropout needs n %% 4 == 0 (n=%d)", n);
   DMF_CHECK_ARG(batch * heads < 65536, "dmf_flash_attn_fwd: batch x heads too large");
   const int nq = g_fa_var == 1 ? 1 : 2;
   const dim3 grid((unsigned)cdiv(n, FA_QT * nq), (unsigned)(batch * heads));

@@ -235,8 +235,12 @@ class FusionTrainer:
         bwd = self.scaler.backward if self.scaler is not None else (lambda t: t.backward())
         import dmf_ops as O
 
-        # both encoders differentiate (mode B): their backwards run on two streams
-        two = all(any(p.requires_grad for p in m.parameters()) for m in (self.lm.dwi_model, self.lm.dce_model))
+        # both encoders differentiate (mode B) AND the forward forked them onto two streams
+        # (train_fusion._encode): only then do their backwards run concurrently and the dgrad
+        # launches take half-chip tiles; a serial forward keeps chip-filling launches
+        two = (self.lm.__dict__.get("_encoders_forked", False)
+               and all(any(p.requires_grad for p in m.parameters())
+                       for m in (self.lm.dwi_model, self.lm.dce_model)))
         if two:
             O.concurrent_tiles(True, bwd=True)
         try:

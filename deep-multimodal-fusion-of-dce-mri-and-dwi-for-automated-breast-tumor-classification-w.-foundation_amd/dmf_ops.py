@@ -2498,9 +2498,13 @@ def branch(owner, name, fn, *inputs):
     side = side_stream(owner, name, dev)
     side.wait_stream(main)
     CONCURRENT[0] += 1  # until the join: no grid-barrier launch on either stream
-    with torch.cuda.stream(side):
-        record_tree(list(inputs), side)
-        out = fn()
+    try:
+        with torch.cuda.stream(side):
+            record_tree(list(inputs), side)
+            out = fn()
+    except BaseException:
+        CONCURRENT[0] -= 1  # no join will follow
+        raise
 
     def join():
         if keep:

@@ -110,6 +110,9 @@ class LightningFusionModel(nn.Module):
         snapshots are taken up front in the sequential order (DWI, DCE), so
         the masks match a sequential run; autograd replays each encoder's
         backward on the stream its forward ran on."""
+        # read by dmf_dp.FusionTrainer: the backward's half-chip dgrad tiles only pay when the
+        # two encoders' backwards really run on two streams, i.e. when this forward forked
+        self.__dict__["_encoders_forked"] = False
         if not (dwi_inputs.is_cuda and O.PARALLEL_BRANCHES):
             return self.dwi_model(dwi_inputs), self.dce_model(dce_inputs)
         main = torch.cuda.current_stream(dwi_inputs.device)
@@ -125,9 +128,11 @@ class LightningFusionModel(nn.Module):
         side.wait_stream(main)
         prev = O.RNG_CURRENT[0]
         O.ORIGIN_STREAM[0] = main
-        O.CONCURRENT[0] += 1  # the two encoders overlap: no grid-barrier launches (dmf_ops.GRID_BARRIER_BN)
-        O.concurrent_tiles(True)
+        entered = False
         try:
+            O.CONCURRENT[0] += 1  # the two encoders overlap: no grid-barrier launches (dmf_ops.GRID_BARRIER_BN)
+            entered = True
+            O.concurrent_tiles(True)
             O.RNG_CURRENT[0] = snap_dwi
             out_dwi = self.dwi_model(dwi_inputs)
             O.RNG_CURRENT[0] = snap_dce
@@ -137,9 +142,11 @@ class LightningFusionModel(nn.Module):
         finally:
             O.RNG_CURRENT[0] = prev
             O.ORIGIN_STREAM[0] = None
-            O.CONCURRENT[0] -= 1
-            O.concurrent_tiles(False)
+            if entered:
+                O.CONCURRENT[0] -= 1
+            O.concurrent_tiles(False)  # idempotent: restores the single-stream tile sizing
         main.wait_stream(side)
+        self.__dict__["_encoders_forked"] = True
         O.record_tree(out_dce, main)
         return out_dwi, out_dce
 

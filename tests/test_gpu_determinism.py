@@ -15,8 +15,11 @@ reduction of the step is a fixed-order one -- the fusion LayerNorm / gating
 column sums by one owner per column, mask-attention, gated-mix, mimic, token
 LayerNorm / LayerScale / bias sums through per-block slab rows summed in row
 order (dmf_colsum_f32), the weight gradient through k_wgrad_reduce's slab
-order -- and the BN statistics' float64 accumulations of fp32 tile partials are
-exact (order-free) sums. The reference's torch CPU LayerNorm / Linear backward
+order. The BN statistics stay float64 atomic sums of fp32 tile partials: those
+are order-free only in practice, not by construction -- a float64 sum of fp32
+values is exact while the partials' magnitudes span fewer than ~29 bits (53 - 24),
+and rounds (so depends on the atomics' order) beyond that. This test is the
+empirical check that the production shapes stay inside that range. The reference's torch CPU LayerNorm / Linear backward
 is deterministic in the same sense (model_module.py:745-780, :799-818)."""
 import copy
 

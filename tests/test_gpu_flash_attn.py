@@ -77,6 +77,21 @@ def test_flash_attention_matches_unfused_with_dropout(p):
         assert (o3.float() - o2.float()).abs().max().item() > 5e-2 * scale
 
 
+def test_flash_attention_refuses_dropout_at_unaligned_n():
+    """the dropout masks are drawn 4 elements per Philox block, so the launcher refuses
+    p > 0 when n % 4 != 0 (a loud error, not correlated masks); p = 0 at the same n still runs."""
+    b, n, heads = 1, 102, 2
+    e = 128 * heads
+    qkv = _qkv(b, n, e, seed=3)
+    rng = torch.tensor([0x1234_5678_9ABC, 77], dtype=torch.int64, device=DEV)
+    with pytest.raises(RuntimeError, match="n % 4"):
+        D.flash_attention(qkv, b, n, n, e, heads, 0.1, rng, 0)
+    o = D.flash_attention(qkv, b, n, n, e, heads, 0.0, None, 0)
+    torch.cuda.synchronize()
+    ref = _ref64(qkv, b, n, n, e, heads)
+    assert (o.double() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
 def test_forward_only_block_matches_autograd_forward():
     """dmf_tokens.transformer_block with no grad (the conv-engine qkv, the fused attention, no backward
     copies) against the same block's autograd forward (train mode: dropout on, same rng snapshot)."""

@@ -498,6 +498,12 @@ def test_hybrid_encoder_under_16_mixed():
     l32, aux32, _ = e32(x)
     assert aux["raw_feats"][2].dtype == torch.float16
     _close(lo, l32, 3e-2, "logits fp16 vs f32")
+    # the token stage itself runs bf16 (8-bit mantissa) where the reference's fp16 autocast
+    # runs fp16 (11-bit); its error against the f32 parity mode is pinned here, as a relative L2 of the
+    # stage output (bf16 rounding of a 2-block, 256-wide stage: a few 2^-9 per op).
+    f16, f32 = aux["raw_feats"][2].float(), aux32["raw_feats"][2].float()
+    rel = ((f16 - f32).norm() / f32.norm()).item()
+    assert rel <= 1.5e-2, f"TransformerStage under 16-mixed (bf16 tokens) vs f32: rel L2 {rel:.3e}"
     (aux["raw_feats"][2].float().square().mean()).backward()
     grads = [p.grad for n, p in enc.named_parameters() if n.startswith("transformer.") and p.grad is not None]
     assert grads and all(torch.isfinite(g_).all() for g_ in grads)

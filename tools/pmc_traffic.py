@@ -7,6 +7,7 @@ of wide streaming reads -> x2. WRITE_SIZE is exact for 16-B/lane stores.
     python tools/pmc_traffic.py gpurun_out/pmc1 [--match REGEX]
 """
 import argparse
+import os
 import csv
 import json
 import re
@@ -25,6 +26,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--match", default=r"k_conv_fwd_ps|k_conv_fwd_pp|k_conv_fwd_sq|k_conv_fwd_wide|k_conv_fwd_buf|k_conv_stem|k_conv_igemm<unsigned short, false")
     ap.add_argument("--json", default="")
+    ap.add_argument("--latest", default="", help="also point profiles/pmc_latest.json's KEY at --json "
+                    "(bench.py reads the pointer: 'traffic' for the conv forward, 'traffic_wgrad', ...)")
     ap.add_argument("--count", default="", help="launches = dispatches matching this regex (default: every "
                     "matched dispatch); e.g. the weight-gradient kernel of a wgrad + split-reduce pair")
     a = ap.parse_args()
@@ -46,6 +49,22 @@ def main():
                        "write_mb_per_launch": round(write / 1e6, 2),
                        "traffic_mb_per_launch": round((fetch + write) / 1e6, 2),
                        "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is"}, f, indent=1)
+        if a.latest:
+            set_latest(a.latest, a.json)
+
+
+def set_latest(key, path):
+    """Point profiles/pmc_latest.json's key at a summary (path relative to the repo root)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ptr = os.path.join(root, "profiles", "pmc_latest.json")
+    try:
+        with open(ptr) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    d[key] = os.path.relpath(os.path.abspath(path), root)
+    with open(ptr, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
