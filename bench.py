@@ -430,6 +430,63 @@ def cpu_baseline(args, P_fn):
                       f"(1 warm-up step)"}
 
 
+def cpu_baseline_mode_b(args, P_fn, batch=4, steps=2):
+    """BASELINE.md's mode-B CPU line: the fp32 oracle's mode-B step (every
+    encoder parameter trainable) on a bounded sample -- `batch` volumes at SxS,
+    1 warm-up then the median of `steps` timed steps (a B=32 mode-B CPU step
+    runs ~20 s; the sample keeps the default bench within minutes)."""
+    import copy
+    a = copy.copy(args)
+    a.mode, a.cpu_batch, a.cpu_steps = "B", batch, steps
+    out = cpu_baseline(a, P_fn)
+    out["sample"] = out["sample"].replace("mode B", "mode B (all trainable)")
+    return out
+
+
+def cpu_baseline_config1(batch=4, size=128, chans=16, steps=2):
+    """BASELINE.md's config-1 CPU line (config 1 IS the reference's CPU case:
+    'CPU PyTorch, train.py one epoch'): the oracle's single-modality DWI CNN
+    training step (use_backbone=False, C=16, S=128, B=4; oracle.losses.
+    single_shared_step = train.py:294-466) + torch AdamW, fp32, 1 warm-up then
+    the median of `steps` timed steps."""
+    import parameters as PR
+    from oracle import losses as OL
+    from oracle import model as OM
+
+    torch.set_num_threads(cpu_threads())
+    P = PR.default_parameters()
+    mp = P["dwi_model_parameters"]
+    mp["use_backbone"] = False
+    mp["input_size"] = size
+    P["dwi_channel_num"] = chans
+    torch.manual_seed(0)
+    ref = OM.ModelMaskHeadBackbone("dwi", P, None)
+    ref.train()
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-4, weight_decay=4e-5)
+    g = torch.Generator().manual_seed(0)
+    x = (0.5 + torch.randn(batch, chans, size, size, generator=g) / 6).clamp(0, 1)
+    masks = (torch.rand(batch, 1, 32, 32, generator=g) > 0.5).float()
+    labels = torch.arange(batch) % 4
+    cw = OL.class_weights_from_labels(torch.arange(1024) % 4)
+
+    def step():
+        opt.zero_grad()
+        OL.single_shared_step(ref, (x, masks, labels), P, cw, "dwi", epoch=0)["total"].backward()
+        opt.step()
+
+    step()
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(batch / med, 3), "unit": "volumes/s", "cores": torch.get_num_threads(),
+            "host_cpu_count": os.cpu_count(), "kind": "port", "step_s": [round(t, 3) for t in times],
+            "sample": f"oracle fp32 CPU, config 1 (DWI CNN, use_backbone=False, C={chans}, S={size}, B={batch}) "
+                      f"training step + AdamW, median of {steps} timed steps (1 warm-up)"}
+
+
 def _graph(fn):
     """Capture fn() (GPU work only, inputs resident) into a hipGraph after
     two eager runs on a side stream (allocator / weight-cache warm-up)."""
@@ -676,6 +733,8 @@ def main():
                                 size=128 if args.size == 256 else args.size)
         out.update({"n_gpus": 1, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                     "data": "synthetic volumes, random-init weights"})
+        if args.config == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_config1(batch=args.batch or 4)
         print(json.dumps(out), flush=True)
         return
 
@@ -791,6 +850,16 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args, lambda: _cpu_params(PR, args))
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
+        if extras:
+            # CPU volumes/s for config 1 (B=4) and config 3 modes A and B
+            for key, fn in (("cpu_baseline_mode_b", lambda: cpu_baseline_mode_b(args, lambda: _cpu_params(PR, args))),
+                            ("cpu_baseline_config1", cpu_baseline_config1)):
+                try:
+                    out[key] = fn()
+                except Exception as e:
+                    out[key] = {"error": repr(e)}
+            if "mode_b" in out and "value" in out.get("cpu_baseline_mode_b", {}):
+                out["mode_b"]["cpu_baseline"] = out["cpu_baseline_mode_b"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -131,7 +131,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         acc[i][j][r] = v;
       }
     }
-    if (!stats) apply_act_col(a.act, acc, j);
+    if (!stats && !a.res_add) apply_act_col(a.act, acc, j);  // (with a residual: after its add, below)
     if (stats) {
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
@@ -226,7 +226,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     const int row = idx / CPR, chn = idx - (idx / CPR) * CPR;
     const int m = m0 + row, n = n0 + chn * EPC;
     if (m < a.M && n < a.Nout) {
-      *(uint4*)(Y + (size_t)m * a.ldy + n) = *(const uint4*)(Cs + row * CST + chn * EPC);
+      uint4 v = *(const uint4*)(Cs + row * CST + chn * EPC);
+      if (a.res_add) {
+        // act(y + residual) on the 16-B chunk (the staged y already holds the folded bias)
+        const uint4 r = *(const uint4*)((const T*)a.res + (size_t)m * a.ldr + n);
+        T yv[EPC], rv[EPC];
+        __builtin_memcpy(yv, &v, 16);
+        __builtin_memcpy(rv, &r, 16);
+        float f[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) f[e] = Cvt<T>::load(yv[e]) + Cvt<T>::load(rv[e]);
+        apply_act_arr(a.act, f);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) yv[e] = Cvt<T>::store(f[e]);
+        __builtin_memcpy(&v, yv, 16);
+      }
+      *(uint4*)(Y + (size_t)m * a.ldy + n) = v;
     }
   }
   if (a.tickets && *(const int*)xtra) {
@@ -1641,6 +1656,41 @@ extern "C" int dmf_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int
 }
 
 static ConvArgs affine_args(int dtype, int N, int H, int W, int Cin, int ldx, int Cout, int stride);
+
+// conv (+ bias) -> + residual -> act on the forms whose epilogue stages the C tile (buf / wide / sq / igemm):
+// an eval-mode Bottleneck conv3 with its BatchNorm folded into w / bias where the persistent affine form
+// (dmf_conv2d_fwd_affine) does not apply. Refuses shapes the planner would give the persistent forms.
+extern "C" int dmf_conv2d_fwd_res(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                                  int Cout, int KH, int KW, int stride, int pad, int dil, const float* bias,
+                                  const void* res, int ldr, int act, void* y, int Ho, int Wo, int ldy, void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                           Ho, Wo, ldy, act, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_res");
+  if (rc) return rc;
+  const int epc = is16(dtype) ? 8 : 4;
+  DMF_CHECK_ARG(res != nullptr && ldr >= Cout && ldr % epc == 0 && ((uintptr_t)res % 16) == 0 && Cout % epc == 0 &&
+                    ldy % epc == 0,
+                "dmf_conv2d_fwd_res: residual / output need 16-B aligned rows and whole 16-B channel chunks");
+  const ConvPlan p = conv_plan(dtype, false, a);
+  DMF_CHECK_ARG(!p.ps && !p.pp && !p.stem,
+                "dmf_conv2d_fwd_res: this shape runs on a persistent form (use dmf_conv2d_fwd_affine)");
+  a.res = res;
+  a.ldr = ldr;
+  a.res_add = 1;
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_res");
+}
+
+extern "C" int dmf_conv2d_fwd_res_ok(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                     int pad, int dil) {
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = Cin; a.ldx = Cin; a.C1 = Cin;
+  a.Nout = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil; a.Ktot = KH * KW * Cin;
+  a.Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  a.Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  a.M = N * a.Ho * a.Wo; a.ldy = Cout;
+  const ConvPlan p = conv_plan(dtype, false, a);
+  return (!p.ps && !p.pp && !p.stem && Cout % (is16(dtype) ? 8 : 4) == 0) ? 1 : 0;
+}
 
 // token linear (1x1 conv over the rows' NHWC view) -> bias -> GELU -> dropout in one launch (forward-only
 // transformer blocks' fc1 under MLP dropout, transformer_model.py:128-134)

@@ -58,6 +58,10 @@ struct ConvArgs {
   // replicas, fin) when they stage them, instead of from out_ss (dmf_conv2d_fwd_affine_acc: the
   // finalize launch between the two passes folded in); block 0 also moves the running statistics
   int aff_acc;
+  // residual epilogue of the conv_epilogue forms (buf / wide / sq / igemm; dmf_conv2d_fwd_res): after the
+  // bias, y = act(y + res[m][n]) with res / ldr above -- an eval-mode Bottleneck conv3 whose BatchNorm is
+  // folded into its weights and bias (dmf_ops._eval_fold)
+  int res_add;
   // dropout after the bias + GELU epilogue of k_conv_fwd_ps (EPI 14, dmf_conv2d_fwd_drop): Philox keep
   // masks on element m * Nout + n, the token GEMM's index (k_gemm_bf16 epilogue), so a forward-only
   // token block draws the same masks as the training path

@@ -23,8 +23,9 @@
 // bank conflicts under gfx950's ds_read_b128 lane grouping (C = 8 is
 // conflict-free as is).
 //
-// Epilogue (per 64-pixel column block): bf16 stores, 4 channels x 8 B per
-// lane; in the training forward the BN batch statistics of the workgroup's
+// Epilogue (per 64-pixel column block): optional bias (+ activation without
+// statistics: eval-mode BatchNorm folded into the weights), bf16 stores, 4
+// channels x 8 B per lane; in the training forward the BN batch statistics of the workgroup's
 // pixels are summed in registers across all its rows and added once at the end
 // (float64 arena replicas, or one slab row per workgroup).
 #include <algorithm>
@@ -92,6 +93,12 @@ __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plan
 
   for (int k = 0; k < 7; ++k) stage_row(2 * ho0 - 3 + k);
   float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  // bias (an eval-mode BatchNorm folded into the weights: dmf_ops._eval_fold) of this lane's 4 channels
+  float bj[4] = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = a.bias[wid * 16 + fg * 4 + j];
+  }
   const int ncb = a.Wo / 64;  // 64-pixel column blocks per output row
   int prev_st = 0;            // stores the previous step issued (younger than the rows this step needs)
   for (int ho = ho0; ho < ho1; ++ho) {
@@ -125,17 +132,21 @@ __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plan
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = (n * a.Ho + ho) * a.Wo + cb * 64 + i * 16 + fr;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[i][j] + bj[j];
+        if (!STATS) apply_act_arr(a.act, v);  // (the statistics path runs act-free: the BN apply follows)
         uint32_t w2[2];
-        w2[0] = B16<T>::pack(acc[i][0], acc[i][1]);
-        w2[1] = B16<T>::pack(acc[i][2], acc[i][3]);
+        w2[0] = B16<T>::pack(v[0], v[1]);
+        w2[1] = B16<T>::pack(v[2], v[3]);
         const unsigned off = (unsigned)(((size_t)m * a.ldy + wid * 16 + fg * 4) * 2);
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, w2), ry, off, 0, 0);
         if (STATS) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            s[j] += acc[i][j];
-            q[j] = __builtin_fmaf(acc[i][j], acc[i][j], q[j]);
+            s[j] += v[j];
+            q[j] = __builtin_fmaf(v[j], v[j], q[j]);
           }
         }
       }
@@ -174,7 +185,8 @@ bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a) {
   if (!is16(dtype) || dgrad || a.KH != 7 || a.KW != 7 || a.stride != 2 || a.pad != 3 || a.dil != 1) return false;
   if ((a.C != 8 && a.C != 16) || a.ldx != a.C || a.x2 != nullptr || a.in_ss != nullptr || a.tickets != nullptr)
     return false;
-  if (a.Nout != 64 || a.bias != nullptr || a.act != DMF_ACT_NONE || a.ldy % 4 != 0) return false;
+  // bias in either mode; an activation only without the statistics epilogue (whose callers pass none)
+  if (a.Nout != 64 || (a.act != DMF_ACT_NONE && a.partials != nullptr) || a.ldy % 4 != 0) return false;
   if (a.Wo % 64 != 0 || a.W != 2 * a.Wo || a.H != 2 * a.Ho) return false;
   const int plane = stem_plane(a.W);
   const long long lds = (long long)STEM_SLOTS * (a.C == 16 ? 2 * plane + 16 : plane);

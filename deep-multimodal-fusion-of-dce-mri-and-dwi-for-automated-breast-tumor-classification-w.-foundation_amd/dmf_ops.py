@@ -502,8 +502,21 @@ class _BwdAcc:
         return buf if ok else None
 
 
+def _train_bn_mark(bn):
+    """A training-mode forward of ``bn`` is being launched: its running statistics change on the device
+    (raw-pointer kernels, no torch version bump). The eval-mode fold cache (_eval_fold) keys on this
+    generation; a launch recorded into a captured graph may re-run at any replay, so such a BatchNorm is
+    never folded again (its eval forwards keep reading the live statistics)."""
+    d = bn.__dict__
+    d["_dmf_sgen"] = d.get("_dmf_sgen", 0) + 1
+    if torch.cuda.is_current_stream_capturing():
+        d["_dmf_svolatile"] = True
+
+
 def _bn_desc(bn, acc, count, unbias_count, ss, save):
     track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        _train_bn_mark(bn)
     d = N.BnDesc()
     d.acc = acc.data_ptr()
     d.gamma = _p(bn.weight)
@@ -598,6 +611,8 @@ def _conv_bn_forward(x, w, b, g, caches, bn, unbias_mult=1, x2=None, in_ss=None,
     tickets = _bn_site(bn, dev)
     partials = torch.empty((mtiles, co, 2), dtype=torch.float32, device=dev)
     track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        _train_bn_mark(bn)
     mom = bn.momentum if bn.momentum is not None else 0.1
     wk = caches[0].get(w, x.dtype, cx + cx2, 0)
     _conv_launch("dmf_conv2d_fwd_bn",
@@ -863,6 +878,8 @@ def _bn_finalize(partials, count, bn, unbias_count=0.0):
     save = torch.empty(2 * c, dtype=torch.float32, device=dev)
     training = bn.training or bn.running_mean is None
     track = bn.training and bn.track_running_stats and bn.running_mean is not None
+    if track:
+        _train_bn_mark(bn)
     mom = bn.momentum if bn.momentum is not None else 0.1
     ntiles = 0 if partials is None else partials.shape[0]
     wsn = N.load().dmf_bn_finalize_ws_size(ntiles, c) if training else 0
@@ -1037,6 +1054,10 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
         raise RuntimeError("dropout requested without an rng snapshot")
     if _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
         return _conv_bn_two_pass(x, conv, caches, bn, res, skip)
+    if _eval_fold_ok(x, conv, bn, act, p, res, skip, in_ss, unbias_mult, x2):
+        return _conv_bn_eval_folded(x, conv, bn, act, x2)
+    if _eval_res_ok(x, conv, bn, act, p, res, skip, in_ss, unbias_mult, x2):
+        return _conv_bn_eval_res(x, conv, bn, act, res, skip)
     if _gbar_ok(x, conv, bn, act, p, res, skip, x2, in_ss):
         return _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult)
     if skip is not None:
@@ -1110,12 +1131,129 @@ TWO_PASS_MAX_K = 256
 TWO_PASS_FOLD = True
 
 
+# Eval-mode BatchNorm folded into the conv (config 2's inference forward, prediction, any frozen eval
+# forward): act(bn(conv(x))) = act(conv_{W*s}(x) + (b - mean)*s + beta), s = gamma / sqrt(var + eps). The
+# folded weight goes through the weight cache like any frozen weight and the shift is the conv's bias, so
+# every conv form runs it with its bias + activation epilogue: no raw output, no apply pass, no finalize
+# launch. Only for frozen parameters and a BatchNorm whose running statistics no training forward moves
+# behind Python's back (_train_bn_mark). Knob "eval_bn_fold".
+EVAL_BN_FOLD = True
+
+
+def _eval_frozen(bn, *ts):
+    """bn in eval mode with running statistics that are safe to cache, and no parameter needing grad."""
+    return (not bn.training and bn.running_mean is not None and bn.running_var is not None
+            and not bn.__dict__.get("_dmf_svolatile", False)
+            and not any(t is not None and t.requires_grad for t in (bn.weight, bn.bias) + ts))
+
+
+def _eval_fold(conv, bn):
+    """(folded fp32 weight, fp32 bias, WeightCache) of conv -> eval bn, cached per parameter version and
+    training-statistics generation."""
+    key = tuple((t.data_ptr(), t._version) if t is not None else None
+                for t in (conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var))
+    key = key + (float(bn.eps), bn.__dict__.get("_dmf_sgen", 0))
+    ent = conv.__dict__.get("_dmf_fold")
+    if ent is not None and ent[0] == key:
+        return ent[1], ent[2], ent[3]
+    with torch.no_grad():
+        rv, rm = bn.running_var.double(), bn.running_mean.double()
+        s = torch.rsqrt(rv + bn.eps)
+        if bn.weight is not None:
+            s = s * bn.weight.double()
+        sh = -rm * s
+        if conv.bias is not None:
+            sh = sh + conv.bias.double() * s
+        if bn.bias is not None:
+            sh = sh + bn.bias.double()
+        wf = (conv.weight.double() * s.view(-1, 1, 1, 1)).to(conv.weight.dtype).contiguous()
+        bf = sh.float().contiguous()
+    conv.__dict__["_dmf_fold"] = (key, wf, bf, WeightCache())
+    return wf, bf, conv.__dict__["_dmf_fold"][3]
+
+
+def _eval_fold_ok(x, conv, bn, act, p, res, skip, in_ss, unbias_mult, x2):
+    return (EVAL_BN_FOLD and p == 0 and res is None and skip is None and in_ss is None and unbias_mult == 1
+            and act in ("relu", "gelu", "none") and conv.groups == 1 and x.is_cuda
+            and _eval_frozen(bn, conv.weight, conv.bias) and not needs_grad(x, x2))
+
+
+def _conv_bn_eval_folded(x, conv, bn, act, x2):
+    wf, bf, cache = _eval_fold(conv, bn)
+    with torch.no_grad():
+        y, _ = _conv_forward_raw(x, wf, bf, ConvGeom(conv), (cache, None), False, act, x2=x2)
+    return y
+
+
+def _eval_res_ok(x, conv, bn, act, p, res, skip, in_ss, unbias_mult, x2):
+    """eval-mode conv -> bn -> + shortcut -> act on dmf_conv2d_fwd_res (the persistent affine form,
+    _two_pass_ok, takes the shapes it covers first)."""
+    if not (EVAL_BN_FOLD and p == 0 and x2 is None and in_ss is None and unbias_mult == 1 and x.is_cuda
+            and (res is None) != (skip is None) and act in ("relu", "gelu", "none") and conv.groups == 1
+            and _eval_frozen(bn, conv.weight, conv.bias) and not needs_grad(x, res)):
+        return False
+    if skip is not None:
+        xr, conv_r, _, bn_r = skip
+        if not _eval_frozen(bn_r, conv_r.weight, conv_r.bias) or needs_grad(xr) or conv_r.groups != 1:
+            return False
+    n, c, h, w, _ = nhwc(x)
+    g = ConvGeom(conv)
+    if c != conv.in_channels and not (c == channel_pad(conv.in_channels, x.dtype)):
+        return False
+    if res is not None:
+        ho, wo = g.out_hw(h, w)
+        _, rc, rh, rw, ldr = nhwc(res)
+        if (rc, rh, rw) != (conv.out_channels, ho, wo) or res.dtype != x.dtype or ldr % 8 or res.data_ptr() % 16:
+            return False
+    return bool(N.load().dmf_conv2d_fwd_res_ok(dt(x), n, h, w, c, conv.out_channels, g.kh, g.kw, g.stride, g.pad,
+                                               g.dil))
+
+
+def _conv_bn_eval_res(x, conv, bn, act, res, skip):
+    g = ConvGeom(conv)
+    with torch.no_grad():
+        if skip is not None:
+            xr, conv_r, _, bn_r = skip
+            wfr, bfr, cache_r = _eval_fold(conv_r, bn_r)
+            res, _ = _conv_forward_raw(xr, wfr, bfr, ConvGeom(conv_r), (cache_r, None), False, "none")
+            if nhwc(res)[4] % 8 or res.data_ptr() % 16:
+                res = as_nhwc(res.contiguous(memory_format=torch.channels_last))
+        wf, bf, cache = _eval_fold(conv, bn)
+        n, cx, h, wd, ldx = nhwc(x)
+        ho, wo = g.out_hw(h, wd)
+        wk = cache.get(wf, x.dtype, cx, 0)
+        y = empty_nhwc(n, conv.out_channels, ho, wo, x.dtype, x.device)
+        _conv_launch("dmf_conv2d_fwd_res",
+                     (dt(x), x.data_ptr(), n, h, wd, cx, ldx, wk.data_ptr(), conv.out_channels, g.kh, g.kw, g.stride,
+                      g.pad, g.dil, bf.data_ptr(), res.data_ptr(), nhwc(res)[4], ACT[act], y.data_ptr(), ho, wo,
+                      nhwc(y)[4]),
+                     (x, wk, bf, res, y), x, n, h, wd, cx, conv.out_channels, g.kh, g.kw, g, ho, wo, y_maps=2)
+    return y
+
+
+def _eval_ss(bn, m):
+    """[scale | shift] of an eval-mode BatchNorm, cached while its statistics and affine are unchanged
+    (the same dmf_bn_finalize launch as the uncached path, run once per version)."""
+    if not EVAL_BN_FOLD or not _eval_frozen(bn):
+        return _bn_finalize(None, m, bn)[0]
+    key = tuple((t.data_ptr(), t._version) if t is not None else None
+                for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
+    key = key + (float(bn.eps), bn.__dict__.get("_dmf_sgen", 0))
+    ent = bn.__dict__.get("_dmf_ss")
+    if ent is None or ent[0] != key:
+        ent = (key, _bn_finalize(None, m, bn)[0])
+        bn.__dict__["_dmf_ss"] = ent
+    return ent[1]
+
+
 def _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
     if not (TWO_PASS_BN and x2 is None and in_ss is None and conv.bias is None and p == 0 and act == "relu"
             and unbias_mult == 1 and (res is None) != (skip is None)):
         return False
+    # eval mode runs the affine pass alone (no statistics pass to pay back): any K
+    kmax = TWO_PASS_MAX_K if (bn.training or bn.running_mean is None) else 1 << 30
     if (x.dtype not in (torch.bfloat16, torch.float16) or conv.groups != 1 or tuple(conv.kernel_size) != (1, 1)
-            or conv.in_channels > TWO_PASS_MAX_K
+            or conv.in_channels > kmax
             or conv.padding[0] != 0 or conv.dilation[0] != 1 or conv.stride[0] != conv.stride[1]):
         return False
     if needs_grad(x, conv.weight, bn.weight, bn.bias, res):
@@ -1215,6 +1353,8 @@ def _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult):
     m = n * ho * wo
     dev = x.device
     track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        _train_bn_mark(bn)
     mom = bn.momentum if bn.momentum is not None else 0.1
     with torch.no_grad():
         wk = caches[0].get(conv.weight, x.dtype, cx + cx2, 0)
@@ -1263,14 +1403,20 @@ def _conv_bn_two_pass(x, conv, caches, bn, res, skip):
                 _finalize_acc(desc, co)
                 desc = None
         else:
-            ss, _ = _bn_finalize(None, m, bn)
+            ss = _eval_ss(bn, m)
         ss_r = None
         if skip is not None:
             xr, conv_r, caches_r, bn_r = skip
-            res, ss_r, _, desc_r = _conv_bn_forward(xr, conv_r.weight, None, ConvGeom(conv_r), caches_r, bn_r,
-                                                    defer=True)
-            if desc_r is not None:
-                _finalize_acc(desc_r, co)
+            if EVAL_BN_FOLD and _eval_frozen(bn_r, conv_r.weight):
+                # eval shortcut: its BatchNorm folded into the projection conv (bias epilogue), so the
+                # second pass adds a plain residual
+                wf, bf, cache = _eval_fold(conv_r, bn_r)
+                res, _ = _conv_forward_raw(xr, wf, bf, ConvGeom(conv_r), (cache, None), False, "none")
+            else:
+                res, ss_r, _, desc_r = _conv_bn_forward(xr, conv_r.weight, None, ConvGeom(conv_r), caches_r, bn_r,
+                                                        defer=True)
+                if desc_r is not None:
+                    _finalize_acc(desc_r, co)
         out = empty_nhwc(n, co, ho, wo, x.dtype, dev)
         if desc is not None:
             _conv_launch("dmf_conv2d_fwd_affine_acc",
@@ -2655,6 +2801,7 @@ KNOBS = {
     "two_pass_bn": ("dmf_ops", "TWO_PASS_BN"),
     "two_pass_fold": ("dmf_ops", "TWO_PASS_FOLD"),
     "two_pass_max_k": ("dmf_ops", "TWO_PASS_MAX_K"),
+    "eval_bn_fold": ("dmf_ops", "EVAL_BN_FOLD"),
     "fc1_drop_conv": ("dmf_tokens", "FC1_DROP_CONV"),
     "bwd_apply_rows": ("call", "dmf_bn_bwd_apply_tune"),
     "fwd_apply_rows": ("call", "dmf_bn_apply_tune"),

@@ -149,6 +149,17 @@ int dmf_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int Cin,
 int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
                           int stride, void* y, int Ho, int Wo, int ldy, const float* scale_shift, const void* res,
                           int ldr, const float* res_scale_shift, void* stream);
+/* conv (+ bias) -> + res -> act in one launch on the forms that stage the C tile through LDS (buffer-
+ * load / 256x128 / 256x256 / general implicit GEMM): an eval-mode Bottleneck conv3 -> bn3 -> + shortcut
+ * -> act3 (foundation_model.py:260-267) with the BatchNorm folded into w and bias by the caller, where
+ * the persistent dmf_conv2d_fwd_affine form does not take the shape. res / y: NHWC rows, 16-B aligned,
+ * whole 16-B channel chunks. dmf_conv2d_fwd_res_ok: 1 when the planner gives this shape such a form
+ * (dmf_conv2d_fwd_res refuses the others). */
+int dmf_conv2d_fwd_res_ok(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                          int dil);
+int dmf_conv2d_fwd_res(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                       int KH, int KW, int stride, int pad, int dil, const float* bias, const void* res, int ldr,
+                       int act, void* y, int Ho, int Wo, int ldy, void* stream);
 /* conv -> BatchNorm2d (batch statistics) -> act in ONE launch, for a forward that is never
  * differentiated (frozen encoders, mode A: timm Bottleneck conv1 / conv2, the necks; the apply
  * passes of foundation_model.py:260-267 and model_module.py:401-476). The epilogue adds the

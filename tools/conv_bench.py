@@ -136,7 +136,11 @@ def main():
                                                 "lists), timed interleaved in this process")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--acc", action="store_true", help="BN statistics into the float64 arena (the training forward's mode)")
+    ap.add_argument("--shapes", default="", help="custom shapes 'N,H,W,Cin,Cout,k,stride,dil;...' (count 1 each) "
+                                                 "instead of the hot-path list")
     a = ap.parse_args()
+    if a.shapes:
+        SHAPES[:] = [(tuple(int(v) for v in s.split(",")), 1) for s in a.shapes.split(";") if s]
     ACC[0] = a.acc
     if a.tunes:
         return ab(a)
