@@ -165,6 +165,15 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
     for (int q = 0; q < 2; ++q) dma16(rw, vb[ch][q], k.koff, dst + q * 8 * 128);
   };
 
+  // timing ablation, diagnostic builds only (-DDMF_PP_ABLATE=<bits>, tools/pp_ablate.sh; results are garbage
+  // when any bit is set): bit 1 skips the steady state's vmcnt waits, bit 2 its LDS-DMA issue, bit 4 its
+  // fragment reads, bit 8 its MFMAs. A compile-time constant (a run-time mask changes the register
+  // allocation and spills); in the product build it is 0.
+#ifdef DMF_PP_ABLATE
+  constexpr int dbg = DMF_PP_ABLATE;  // one diagnostic library per bit set
+#else
+  constexpr int dbg = 0;
+#endif
   f32x4_t acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -208,7 +217,8 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if (p == 0) mma_q(0, cv0, 0);
+    if (dbg & 8) {
+    } else if (p == 0) mma_q(0, cv0, 0);
     else if (p == 1) mma_q(0, cv1, 1);
     else if (p == 2) mma_q(1, cv1, 1);
     else mma_q(1, cv0, 0);
@@ -249,20 +259,20 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   for (; g + 2 < G; ++g) {
     const char* slot = smem + (g & 1) * PP_SLOT;
     const int s1 = (g + 1) & 1, s2 = g & 1;
-    read_p(slot, 0); read_c(slot, 0, cv0);
-    stage_c(k1, s1, 1);
-    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // C1(g) landed
+    if (!(dbg & 4)) { read_p(slot, 0); read_c(slot, 0, cv0); }
+    if (!(dbg & 2)) stage_c(k1, s1, 1);
+    if (!(dbg & 1)) { if (after_epi) vm_wait<24>(); else vm_wait<8>(); }  // C1(g) landed
     mfma_segment(0);
-    read_c(slot, 1, cv1);
-    stage_p(k1, s1, 1);
-    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // P1(g)
+    if (!(dbg & 4)) read_c(slot, 1, cv1);
+    if (!(dbg & 2)) stage_p(k1, s1, 1);
+    if (!(dbg & 1)) { if (after_epi) vm_wait<24>(); else vm_wait<8>(); }  // P1(g)
     mfma_segment(1);
-    read_p(slot, 1);
-    stage_p(k2, s2, 0);
-    if (after_epi) vm_wait<26>(); else vm_wait<10>();
+    if (!(dbg & 4)) read_p(slot, 1);
+    if (!(dbg & 2)) stage_p(k2, s2, 0);
+    if (!(dbg & 1)) { if (after_epi) vm_wait<26>(); else vm_wait<10>(); }
     mfma_segment(2);
-    stage_c(k2, s2, 0);
-    if (after_epi) vm_wait<24>(); else vm_wait<8>();  // P0(g+1), C0(g+1)
+    if (!(dbg & 2)) stage_c(k2, s2, 0);
+    if (!(dbg & 1)) { if (after_epi) vm_wait<24>(); else vm_wait<8>(); }  // P0(g+1), C0(g+1)
     mfma_segment(3);
     after_epi = false;
     k1 = k2;
@@ -310,6 +320,7 @@ int conv_pp_tune(int value) {
   g_pp_persist = value;
   return 0;
 }
+
 
 // dmf_conv_tune key 18: blocks of a persistent launch (k_conv_fwd_ps / k_conv_fwd_pp), 0 = one per CU;
 // a two-stream region may cap it (dmf_ops.CONC_PERSIST) so the other stream keeps CUs
