@@ -166,32 +166,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       }
     }
   }
-  if (a.gbar) {
-    // grid-barrier BatchNorm apply (dmf_conv2d_fwd_bn_act, one resident block per tile): every block's
-    // statistics are in the arena after the barrier; the tile's (scale, shift) pairs replace the consumed
-    // statistics scratch, then BN + activation on the accumulators
-    if (a.dbg & 64) __syncthreads();  // (timing only, dmf_conv_tune key 17)
-    else gbar_sync(a.gbar, tid);
-    if (tid < BN) {
-      const int col = n0 + tid;
-      const float2 v = (a.dbg & 128) ? make_float2(1.f, 0.f)
-                       : col < a.Nout ? gbar_bn_channel(a, col, mt == 0) : make_float2(0.f, 0.f);
-      red[tid] = v.x;
-      red[BN + tid] = v.y;
-    }
-    if (mt == 0 && nt == 0 && tid == 0 && a.fin.nbt) *a.fin.nbt += 1;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int lc = wn * (BN / WNW) + j * 16 + fr;
-      const float sc = red[lc], sh = red[BN + lc];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_fmaf(acc[i][j][r], sc, sh);
-      apply_act_col(a.act, acc, j);
-    }
-  }
   __syncthreads();
   // stage C tile through LDS: [128 rows][128 + pad] of T
   constexpr int CPAD = 16 / sizeof(T);
@@ -610,10 +584,10 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
 // the other stage. Requires Nout % 256 == 0 plus the wide form's conditions.
 
 // VAR bit 0: waves 4-7 at static priority 1; bit 1: s_setprio around each MFMA group.
-// WM_ x WN_ waves: 2 x 4 (8 waves, 128x64 each, two per SIMD) or 2 x 2 (4 waves, ONE per SIMD,
-// 128x128 each: 8x8 fragments = 256 accumulator registers in the AGPR half of the 512-entry file,
-// 2/3 of the LDS fragment reads per MFMA of the 8-wave split, 16 LDS-DMA pieces per wave per K-step;
-// DESIGN.md section 9.1)
+// WM_ x WN_ waves: launched as 2 x 4 (8 waves, 128x64 each, two per SIMD). The 2 x 2 split (4 waves,
+// one per SIMD, 128x128 each, accumulators in the AGPR half of the register file) computes the same bits
+// and was measured slower on every hot shape (round 5, profiles/r05c_sq_4wave_ab.txt); its launch path
+// was removed in round 6.
 template <bool PADCHK, bool DUAL, int VAR, typename T = bf16_t, int WM_ = QWM, int WN_ = QWN>
 __global__ void __launch_bounds__(64 * WM_ * WN_, 1) k_conv_fwd_sq(ConvArgs a) {
   constexpr int ES = 2, EPC = 8, BK = 64;
@@ -816,7 +790,7 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
     // (aff_acc: the BatchNorm finalized here from the float64 arena, dmf_conv2d_fwd_affine_acc; block 0
     // also moves the running statistics)
     for (int i = tid; i < a.Nout; i += NTH) {
-      const float2 ss = a.aff_acc ? gbar_bn_channel(a, i, blockIdx.x == 0) : make_float2(a.out_ss[i], a.out_ss[a.Nout + i]);
+      const float2 ss = a.aff_acc ? arena_bn_channel(a, i, blockIdx.x == 0) : make_float2(a.out_ss[i], a.out_ss[a.Nout + i]);
       sbias[i] = ss.x;
       sbias[a.Nout + i] = ss.y + (EPI == 11 ? a.res_ss[a.Nout + i] : 0.f);
       if (EPI == 11) sbias[2 * a.Nout + i] = a.res_ss[i];
@@ -1127,11 +1101,6 @@ static int g_stem_enable = 1;
 static int g_fast_epi = 1;
 // runtime knobs (dmf_conv_tune): 0 = square tile on/off, 1 = square-tile VAR
 static int g_sq_enable = 1, g_sq_var = 1;
-// 16 = k_conv_fwd_sq with 4 waves of 128x128 (one per SIMD) instead of 8 of 128x64: 0 off (default) / 1 on
-static int g_sq_w4 = 0;
-// 17 = timing bits of the grid-barrier BatchNorm apply (tools/gbar_bench.py only; outputs are wrong with
-// either set): 64 skips the barrier, 128 the arena reads
-static int g_gbar_dbg = 0;
 // 2 = forced forward tile for A/B sweeps: 0 auto, 1 buf 128x128, 2 buf 64x128,
 // 3 buf 128x64, 4 buf 64x64, 5 wide 256x128, 6 square 256x256 (only where legal)
 static int g_force = 0;
@@ -1270,7 +1239,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
   }
   if constexpr (sizeof(T) == 2) {
     if (plan.ps) {
-      const dim3 gp((unsigned)std::min<long long>(nblk, conv_persist_blocks(cu_count()))), bq(QTHREADS);
+      const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
       // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
       // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
       const int epi = (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
@@ -1308,13 +1277,6 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
     }
     if (plan.sq) {
       const dim3 bq(QTHREADS);
-      if (g_sq_w4) {
-        const dim3 b4(256);
-        if (dual) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, 0, T, 2, 2>), g, b4, lds_total, st, a);
-        else if (plain) hipLaunchKernelGGL((k_conv_fwd_sq<false, false, 0, T, 2, 2>), g, b4, lds_total, st, a);
-        else hipLaunchKernelGGL((k_conv_fwd_sq<true, false, 0, T, 2, 2>), g, b4, lds_total, st, a);
-        return;
-      }
 #define DMF_SQ(V)                                                                                         \
   do {                                                                                                    \
     if (dual) hipLaunchKernelGGL((k_conv_fwd_sq<true, true, V, T>), g, bq, lds_total, st, a);             \
@@ -1404,12 +1366,9 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   if (plan.stem) return launch_conv_stem(a, st, dtype);
   if (!dgrad && plan.pp) {
     // statistics without bias over whole tiles: the fast epilogue (EPI 5)
-    // (the grid-barrier BatchNorm apply: EPI 13)
-    const int epi = a.gbar != nullptr ? 13
-                    : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
-                                            : 1 + a.act;
-    DMF_CHECK_ARG(((epi >= 0 && epi <= 5) || epi == 13) && a.act >= 0 && a.act <= 3, "%s: activation %d", what,
-                  a.act);
+    const int epi = a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
+                                          : 1 + a.act;
+    DMF_CHECK_ARG(epi >= 0 && epi <= 5 && a.act >= 0 && a.act <= 3, "%s: activation %d", what, a.act);
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
@@ -1581,9 +1540,6 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 11: g_fast_epi = value != 0; return 0;
     case 14: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: wide min tiles %d", value); g_wide_min_tiles = value; return 0;
     case 15: DMF_CHECK_ARG(value >= 1, "dmf_conv_tune: square min tiles %d", value); g_min_tiles = value; return 0;
-    case 16: g_sq_w4 = value != 0; return 0;
-    case 17: g_gbar_dbg = value & (64 | 128); return 0;
-    case 18: DMF_CHECK_ARG(value >= 0, "dmf_conv_tune: persistent grid cap %d", value); return conv_persist_cap(value);
     default: DMF_CHECK_ARG(false, "dmf_conv_tune: unknown key %d", key);
   }
 }
@@ -1808,10 +1764,10 @@ extern "C" int dmf_conv2d_fwd_affine_acc(int dtype, const void* x, int N, int H,
                            Wo, ldy, DMF_ACT_RELU, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_affine_acc");
   if (rc) return rc;
   DMF_CHECK_ARG(is16(dtype) && bn && bn->acc && ((uintptr_t)bn->acc % 16) == 0 && bn->replicas >= 1 &&
-                    bn->replicas <= GBAR_MAX_REPLICAS && bn->count > 0.0 && res && ldr % 8 == 0 &&
+                    bn->replicas <= ARENA_MAX_REPLICAS && bn->count > 0.0 && res && ldr % 8 == 0 &&
                     ((uintptr_t)res % 16) == 0 && ((long long)a.M * ldr * 2 < (1LL << 31)),
                 "dmf_conv2d_fwd_affine_acc: needs a 16-bit dtype, a float64 arena of <= %d replicas and an aligned "
-                "shortcut", GBAR_MAX_REPLICAS);
+                "shortcut", ARENA_MAX_REPLICAS);
   a.aff_acc = 1;
   a.partials = (float*)const_cast<double*>(bn->acc);
   a.stat_acc = bn->replicas;
@@ -1821,60 +1777,6 @@ extern "C" int dmf_conv2d_fwd_affine_acc(int dtype, const void* x, int N, int H,
   a.ldr = ldr;
   a.res_ss = res_scale_shift;
   return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_affine_acc");
-}
-
-// The grid-barrier BatchNorm apply needs one output tile per block and every block resident: the
-// ping-pong 256x256 form (one 512-thread block per CU, whole tiles, no bias: EPI 13's statistics) or the
-// 256x128 wide form (one 512-thread block per CU; conv_epilogue), at no more tiles than CUs.
-static bool gbar_plan_ok(const ConvPlan& p, const ConvArgs& a) {
-  const long long tiles = (long long)cdiv(a.M, p.bm) * cdiv(a.Nout, p.bn);
-  if (tiles > cu_count()) return false;
-  if (p.pp) return a.bias == nullptr && a.M % QBM == 0;
-  return p.wide && !p.sq && !p.ps && !p.stem;
-}
-
-extern "C" int dmf_conv2d_fwd_bn_act_ok(int dtype, int N, int H, int W, int Cin, int Cin2, int Cout, int KH, int KW,
-                                        int stride, int pad, int dil, int has_bias) {
-  if (!is16(dtype) || stride < 1 || dil < 1 || KH < 1 || KW < 1) return 0;
-  ConvArgs a{};
-  a.N = N; a.H = H; a.W = W; a.C = Cin + Cin2; a.ldx = Cin; a.C1 = Cin; a.ldx2 = Cin2;
-  a.x2 = Cin2 > 0 ? (const void*)&a : nullptr;  // (only its presence matters to the plan)
-  a.bias = has_bias ? (const float*)&a : nullptr;
-  a.Nout = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad; a.dil = dil; a.Ktot = KH * KW * a.C;
-  a.Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
-  a.Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
-  a.M = N * a.Ho * a.Wo; a.ldy = Cout;
-  if (a.M <= 0 || a.C % 8 || Cout % 8) return 0;
-  return gbar_plan_ok(conv_plan(dtype, false, a), a) ? 1 : 0;
-}
-
-extern "C" int dmf_conv2d_fwd_bn_act(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2,
-                                     int Cin2, int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad,
-                                     int dil, const float* bias, void* y, int Ho, int Wo, int ldy, int act,
-                                     double* bn_acc, int replicas, unsigned* gbar, const float* gamma,
-                                     const float* beta, float* running_mean, float* running_var,
-                                     long long* num_batches_tracked, float momentum, float eps, double count,
-                                     double unbias_count, void* stream) {
-  ConvArgs a{};
-  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, x2, Cin2, ldx2, w, Cout, KH, KW, stride, pad, dil, bias, y,
-                           Ho, Wo, ldy, act, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_bn_act");
-  if (rc) return rc;
-  DMF_CHECK_ARG(is16(dtype) && bn_acc && ((uintptr_t)bn_acc % 16) == 0 && replicas >= 1 &&
-                    replicas <= GBAR_MAX_REPLICAS && gbar &&
-                    ((uintptr_t)gbar % 4) == 0 && count > 0 &&
-                    (act == DMF_ACT_NONE || act == DMF_ACT_RELU || act == DMF_ACT_GELU),
-                "dmf_conv2d_fwd_bn_act: needs a 16-bit dtype, a float64 arena slice, the barrier words and "
-                "activation none / relu / gelu");
-  a.partials = (float*)bn_acc;
-  a.stat_acc = replicas;
-  a.gbar = gbar;
-  a.dbg = g_gbar_dbg;
-  a.fin = BnFin{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, count, unbias_count, 1,
-                nullptr, nullptr};
-  DMF_CHECK_ARG(gbar_plan_ok(conv_plan(dtype, false, a), a),
-                "dmf_conv2d_fwd_bn_act: this shape does not run one resident block per output tile "
-                "(dmf_conv2d_fwd_bn_act_ok)");
-  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_bn_act");
 }
 
 extern "C" int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt,

@@ -68,9 +68,6 @@ struct ConvArgs {
   float dp;
   const unsigned long long* rng;
   int site;
-  // grid-barrier BatchNorm apply (dmf_conv2d_fwd_bn_act; k_conv_fwd_pp EPI 13, conv_epilogue of
-  // k_conv_fwd_wide): [counter 0, counter 1, generation] of this BatchNorm's launch site, or null
-  unsigned* gbar;
 };
 
 template <int ACT>
@@ -168,67 +165,23 @@ __device__ __forceinline__ void acc_stats(const ConvArgs& a, int mt, int col, fl
 
 typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
 
-// ------------------------------------------------ grid-barrier BatchNorm apply (forward only)
-// A launch whose blocks are ALL resident (one block per CU, one output tile per block; checked at plan
-// time, dmf_conv2d_fwd_bn_act_ok) finishes its BatchNorm inside the epilogue: statistics into the
-// float64 arena, a grid-wide barrier, then scale / shift from the arena and BN + activation on the
-// accumulators -- the raw conv output is never written and no apply pass runs.
-// gb = [counter 0, counter 1, generation] of the launch site (zero at first use). A launch of
-// generation g arrives on counter g & 1 and waits for it to reach the grid size; its last arriver
-// bumps the generation and zeroes the other counter for the next launch (so no counter is reset while
-// a block of its own launch may still be polling it). The hand-off carries only the statistics, which
-// are agent-scope float64 atomics (performed past the XCD L2s): every wave drains them (vmcnt(0)) before
-// the workgroup barrier, lane 0 arrives with an agent-scope atomic add, the pollers read the counter and
-// afterwards the arena with sc1 loads -- the sc1 form of cdna_hip_programming.md 6 G16 (MI355X_MICROARCH
-// "Valid forms", first row), no release / acquire fence (measured: an agent release writes back the whole
-// XCD L2, whose lines the previous kernels left dirty: +20-60 us per launch). The poll is bounded: a grid
-// that is not fully resident within ~2 s traps (a launch error) instead of hanging.
-constexpr unsigned long long GBAR_TIMEOUT_TICKS = 200000000ull;  // s_memrealtime runs at 100 MHz
-__device__ __forceinline__ void gbar_sync(unsigned* gb, int tid) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics were performed
-  __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
-    // wave 0 (a wave-uniform branch); lane 0 arrives, every lane polls the same word and the loop
-    // condition is read from lane 0, so the spin is a scalar loop
-    const unsigned nblk = gridDim.x;
-    const unsigned gen =
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load(gb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    unsigned* cnt = gb + (gen & 1u);
-    unsigned prev = 0;
-    if (tid == 0) prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_readfirstlane(prev) == nblk - 1) {
-      if (tid == 0) {
-        __hip_atomic_store(gb + ((gen & 1u) ^ 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gb + 2, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      const unsigned long long t0 = wall_clock64();
-      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-             nblk) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > GBAR_TIMEOUT_TICKS) __builtin_trap();
-      }
-    }
-  }
-  __syncthreads();
-}
-
 // (scale, shift) of channel c from the arena's replica sums in a fixed order -- the finalize k_bn_apply
 // folds in (norm.hip bn_src_affine); `update`: this block also moves the running statistics (one block
 // per channel: the tile row mt == 0). The replicas' (sum, sum^2) pairs are read with one 16-B sc1
-// buffer load each (L1-bypassing, see gbar_sync), all eight in flight together.
-constexpr int GBAR_MAX_REPLICAS = 8;
-__device__ __forceinline__ float2 gbar_bn_channel(const ConvArgs& a, int c, bool update) {
+// buffer load each (L1-bypassing), all eight in flight together. Used by the two-pass conv3's second
+// pass (aff_acc: its BatchNorm finalized while it stages scale / shift).
+constexpr int ARENA_MAX_REPLICAS = 8;
+__device__ __forceinline__ float2 arena_bn_channel(const ConvArgs& a, int c, bool update) {
   const __amdgpu_buffer_rsrc_t rp =
       __builtin_amdgcn_make_buffer_rsrc(a.partials, 0, a.stat_acc * a.Nout * 16, BUF_FLAGS_EP);
-  v4u_t pr[GBAR_MAX_REPLICAS];
+  v4u_t pr[ARENA_MAX_REPLICAS];
 #pragma unroll
-  for (int r = 0; r < GBAR_MAX_REPLICAS; ++r)
+  for (int r = 0; r < ARENA_MAX_REPLICAS; ++r)
     pr[r] = __builtin_bit_cast(v4u_t, __builtin_amdgcn_raw_buffer_load_b128(
                                           rp, r < a.stat_acc ? (unsigned)((r * a.Nout + c) * 16) : BUF_OOB, 0, 16));
   double s = 0.0, q = 0.0;
 #pragma unroll
-  for (int r = 0; r < GBAR_MAX_REPLICAS; ++r) {
+  for (int r = 0; r < ARENA_MAX_REPLICAS; ++r) {
     s += __builtin_bit_cast(double, ((unsigned long long)pr[r].y << 32) | pr[r].x);
     q += __builtin_bit_cast(double, ((unsigned long long)pr[r].w << 32) | pr[r].z);
   }
@@ -450,73 +403,6 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
   }
 }
 
-// The register epilogue of the grid-barrier BatchNorm apply (EPI 13, see gbar_sync): the tile's BN
-// statistics (whole tiles, no bias: the EPI 5 sums) into the arena, the grid barrier, the tile's 256
-// (scale, shift) pairs finalized once into LDS, then act(acc * scale + shift) stored as ps_epilogue
-// stores. One tile per block: nothing is in flight behind it.
-template <int TBN = QBN, int FM = 8, int TBM = QBM, typename T = bf16_t>
-__device__ __forceinline__ void ps_epilogue_gbar(const ConvArgs& a, f32x4_t (&acc)[FM][4], int lin,
-                                                 __amdgpu_buffer_rsrc_t ry, float* sred, int tid, int wm, int wn,
-                                                 int fr, int fg) {
-  const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
-  const int m0 = mt * TBM, n0 = nt * TBN;
-  const int cl = wn * 64 + fg * 8;
-  float s[16], q[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) { s[e] = 0.f; q[e] = 0.f; }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = acc[i][j][r];
-        s[j * 4 + r] += v;
-        q[j * 4 + r] = __builtin_fmaf(v, v, q[j * 4 + r]);
-      }
-  const float S = row_reduce_scatter16(s, fr), Q = row_reduce_scatter16(q, fr);
-  const int ch = ps_chan(wn, fg, fr);
-  if (wm == 1) {
-    sred[ch * 2] = S;
-    sred[ch * 2 + 1] = Q;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (wm == 0) acc_stats(a, mt, n0 + ch, make_float2(S + sred[ch * 2], Q + sred[ch * 2 + 1]));
-  if (a.dbg & 64) __syncthreads();  // (timing only, dmf_conv_tune key 17)
-  else gbar_sync(a.gbar, tid);  // (its first barrier also retires every wave's sred reads above)
-  if (tid < TBN) {
-    const float2 v = (a.dbg & 128) ? make_float2(1.f, 0.f) : gbar_bn_channel(a, n0 + tid, mt == 0);
-    sred[tid] = v.x;
-    sred[TBN + tid] = v.y;
-  }
-  if (lin == 0 && tid == 0 && a.fin.nbt) *a.fin.nbt += 1;
-  __syncthreads();
-  float sc[16], sh[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    sc[e] = sred[ps_chan(wn, fg, e)];
-    sh[e] = sred[TBN + ps_chan(wn, fg, e)];
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[j * 4 + r] = __builtin_fmaf(acc[i][j][r], sc[j * 4 + r], sh[j * 4 + r]);
-    apply_act_arr(a.act, v);
-    uint32_t w8[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) w8[e] = B16<T>::pack(v[2 * e], v[2 * e + 1]);
-    const unsigned off = (unsigned)(((size_t)m * a.ldy + n0 + cl) * 2);
-    __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[0], w8[1], w8[2], w8[3]}, ry, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(v4u_t{w8[4], w8[5], w8[6], w8[7]}, ry, off + 64, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (the instruction takes an immediate): one
 // scalar branch per call
 __device__ __forceinline__ void vm_wait_rt(int n) {
@@ -540,12 +426,8 @@ bool conv_stem_ok(int dtype, bool dgrad, const ConvArgs& a);
 int conv_stem_m_tile(const ConvArgs& a);
 int launch_conv_stem(ConvArgs& a, hipStream_t st, int dtype);
 
-// persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 / 5 BN statistics, 1 + act: bias + act,
-// 13 grid-barrier BatchNorm apply)
+// persistent / ping-pong 256x256 launcher of conv_pp.hip (epi: 0 / 5 BN statistics, 1 + act: bias + act)
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype);
-// persistent-grid cap (dmf_conv_tune key 18): set / blocks for a device of ncu CUs
-int conv_persist_cap(int value);
-int conv_persist_blocks(int ncu);
 int conv_pp_tune(int value);  // dmf_conv_tune key 8
 constexpr int PP_THREADS = 512;
 constexpr int PP_HALF = 128 * 128;  // one half-tile: 128 rows x 128 B

@@ -230,8 +230,7 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
   // store / reduce from the accumulators (ps_epilogue zeroes them), re-stagger
   auto epilogue = [&](int j, bool restagger) {
     if (wm == 0) pp_barrier();
-    if constexpr (EPI == 13) ps_epilogue_gbar<QBN, 8, QBM, T>(a, acc, tile_lin(j), ry, sred, tid, wm, wn, fr, fg);
-    else ps_epilogue<EPI, QBN, 8, QBM, T>(a, acc, tile_lin(j), ry, sred, sbias, tid, wm, wn, fr, fg);
+    ps_epilogue<EPI, QBN, 8, QBM, T>(a, acc, tile_lin(j), ry, sred, sbias, tid, wm, wn, fr, fg);
     __builtin_amdgcn_sched_barrier(0);
     if (restagger && wm == 1) pp_barrier();
   };
@@ -277,12 +276,7 @@ __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
     after_epi = false;
     k1 = k2;
     if (g + 3 < G) k2 = next_kp();
-    if constexpr (EPI == 13) {
-      // one tile per block (dmf_conv2d_fwd_bn_act): its epilogue is the drain loop's; keeping this call
-      // site out leaves the steady state's fragments and staging rows dead across the barrier epilogue
-      // (with it, the kernel spilled 664 VGPRs)
-      ++kt;
-    } else if (++kt == nk) {
+    if (++kt == nk) {
       epilogue(j, true);
       kt = 0;
       ++j;
@@ -322,15 +316,6 @@ int conv_pp_tune(int value) {
 }
 
 
-// dmf_conv_tune key 18: blocks of a persistent launch (k_conv_fwd_ps / k_conv_fwd_pp), 0 = one per CU;
-// a two-stream region may cap it (dmf_ops.CONC_PERSIST) so the other stream keeps CUs
-static int g_persist_cap = 0;
-int conv_persist_cap(int value) {
-  g_persist_cap = value;
-  return 0;
-}
-int conv_persist_blocks(int ncu) { return g_persist_cap > 0 && g_persist_cap < ncu ? g_persist_cap : ncu; }
-
 int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_t st, int dtype) {
   static int ncu = 0;
   if (!ncu) {
@@ -340,12 +325,10 @@ int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_
     if (ncu <= 0) ncu = 256;
   }
   const int ntile = a.mtiles * a.ntiles;
-  // (the grid-barrier form needs one tile per block: never capped)
-  const int pcap = a.gbar ? ncu : conv_persist_blocks(ncu);
-  const dim3 g((unsigned)(g_pp_persist ? std::min(ntile, pcap) : ntile)), b(PP_THREADS);
+  const dim3 g((unsigned)(g_pp_persist ? std::min(ntile, ncu) : ntile)), b(PP_THREADS);
   const size_t lds = (size_t)PP_LDS + lds_bias;
   DMF_CHECK_ARG(lds <= 160 * 1024, "conv_pp: %d output channels of bias exceed the LDS staging", a.Nout);
-  if (!a.gbar) a.dbg = 0;  // (dmf_conv2d_fwd_bn_act's timing bits pass through)
+  a.dbg = 0;
 #define DMF_PP(E, TT)                                                                                    \
   do {                                                                                                   \
     if (a.x2 != nullptr) hipLaunchKernelGGL((k_conv_fwd_pp<true, true, E, TT>), g, b, lds, st, a);      \
@@ -360,7 +343,6 @@ int launch_conv_pp(ConvArgs& a, int epi, bool plain, size_t lds_bias, hipStream_
       case 2: DMF_PP(2, TT); break;   \
       case 3: DMF_PP(3, TT); break;   \
       case 5: DMF_PP(5, TT); break;   \
-      case 13: DMF_PP(13, TT); break; \
       default: DMF_PP(4, TT); break;  \
     }                                 \
   } while (0)

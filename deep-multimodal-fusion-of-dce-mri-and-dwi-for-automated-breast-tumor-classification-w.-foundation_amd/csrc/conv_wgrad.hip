@@ -32,19 +32,11 @@ struct WgArgs {
   int KH, KW, stride, pad, dil;
   int Ktot, M;  // Ktot = KH*KW*Cin, M = N*Ho*Wo
   int mtiles, ntiles, splits, pix_per_split;
-  int xcd_split;  // wg_block: split-major block order per XCD (dmf_conv_wgrad_tune key 6)
 };
 
-// (tile, split) of this block. The hardware deals a 2-D grid's blocks to the 8 XCDs round-robin in
-// x-fastest order, so the tiles of one pixel split (which share its dY and X rows) land on every XCD and
-// each XCD's L2 fetches those rows again. xcd_split undoes the deal (xcd_remap over the linear id): each
-// XCD runs a contiguous split-major range, the tiles of a split together in one L2.
-__device__ __forceinline__ int2 wg_block(const WgArgs& a) {
-  if (!a.xcd_split) return make_int2(blockIdx.x, blockIdx.y);
-  const int T = gridDim.x;
-  const int lin = xcd_remap(blockIdx.y * T + blockIdx.x, T * gridDim.y);
-  return make_int2(lin % T, lin / T);
-}
+// (tile, split) of this block. (Ordering the blocks split-major per XCD, so the tiles of one pixel split
+// share one L2, was measured within noise -- profiles/r05n_wgrad_xcd_ab.txt -- and removed in round 6.)
+__device__ __forceinline__ int2 wg_block(const WgArgs&) { return make_int2(blockIdx.x, blockIdx.y); }
 
 template <typename T>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(WgArgs a) {
@@ -990,8 +982,6 @@ static bool wgrad_sq_ok(int dtype, int Cout, long long Ktot) {
 
 // key 4: split-lane reducers for many-split sums (k_wgrad_reduce_sl): 0 off, 1 (default) on
 static int g_reduce_sl = 1;
-// key 6: split-major block order per XCD (wg_block) on (1) / off (0)
-static int g_wgrad_xcd = 0;
 // key 5: the block count the pixel splits aim for, in percent of one chip-filling wave. Default 50:
 // a weight gradient runs beside the other encoder's backward (and its own dX chain), and a launch
 // sized to fill the chip alone holds CUs those need -- mode B, interleaved A/B: 20 % 944, 30 % 992,
@@ -999,9 +989,8 @@ static int g_wgrad_xcd = 0;
 static int g_wgrad_fill = 50;
 
 extern "C" int dmf_conv_wgrad_tune(int key, int value) {
-  DMF_CHECK_ARG(key >= 0 && key <= 6, "dmf_conv_wgrad_tune: unknown key %d", key);
-  if (key == 6) g_wgrad_xcd = value != 0;
-  else if (key == 5) {
+  DMF_CHECK_ARG(key >= 0 && key <= 5, "dmf_conv_wgrad_tune: unknown key %d", key);
+  if (key == 5) {
     DMF_CHECK_ARG(value >= 10 && value <= 400, "dmf_conv_wgrad_tune: fill %d%%", value);
     g_wgrad_fill = value;
   } else if (key == 4) g_reduce_sl = value != 0;
@@ -1068,7 +1057,6 @@ extern "C" int dmf_conv2d_wgrad(int dtype, const void* x, int N, int H, int W, i
   a.splits = splits;
   const int bk = is16(dtype) ? 64 : 8 * epc;
   a.pix_per_split = cdiv(cdiv(a.M, splits), bk) * bk;
-  a.xcd_split = g_wgrad_xcd;
   dim3 grid(a.mtiles * a.ntiles, splits);
   const size_t lds = 2 * 2 * 128 * 128;
   DMF_CHECK_ARG((uintptr_t)x % 16 == 0 && (uintptr_t)dy % 16 == 0 && (!x2 || (uintptr_t)x2 % 16 == 0),

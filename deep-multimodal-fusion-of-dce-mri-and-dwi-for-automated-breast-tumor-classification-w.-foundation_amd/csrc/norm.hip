@@ -753,14 +753,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply_acc(const T* __restrict__ 
   }
 }
 
-// rows of k_bn_bwd_apply_acc's loads in flight per thread (1 default; dmf_bn_bwd_apply_tune)
-static int g_bwd_apply_u = 1;
-extern "C" int dmf_bn_bwd_apply_tune(int rows_in_flight) {
-  DMF_CHECK_ARG(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4, "dmf_bn_bwd_apply_tune: %d",
-                rows_in_flight);
-  g_bwd_apply_u = rows_in_flight;
-  return 0;
-}
 
 // dmf_bn_bwd_finalize for many tiles: 16 channels x 64 tile lanes per block
 __global__ void __launch_bounds__(1024) k_bn_bwd_finalize_wide(const float* __restrict__ part, int T, int C,
@@ -895,14 +887,6 @@ extern "C" int dmf_affine_act(int dtype, const void* x, int ldx, const float* sc
   return 0;
 }
 
-// rows of k_bn_apply's loads in flight per thread (1 default; dmf_bn_apply_tune, tools/apply_bench.py --rows)
-static int g_bn_apply_rows = 1;
-extern "C" int dmf_bn_apply_tune(int rows_in_flight) {
-  DMF_CHECK_ARG(rows_in_flight == 1 || rows_in_flight == 2 || rows_in_flight == 4, "dmf_bn_apply_tune: %d",
-                rows_in_flight);
-  g_bn_apply_rows = rows_in_flight;
-  return 0;
-}
 
 static BnApplySrc bn_src(const dmf_bn_desc* d, const float* ss) {
   BnApplySrc s{};
@@ -949,12 +933,9 @@ extern "C" int dmf_bn_apply(int dtype, const void* x, int ldx, const dmf_bn_desc
 #define DMF_BA_U(TT, AC, RK, UU)                                                                             \
   hipLaunchKernelGGL((k_bn_apply<TT, AC, RK, UU>), g, dim3(256), 0, s, (const TT*)x, ldx, A, (const TT*)res, ldr, \
                      R, dropout_p, rng, site, (TT*)y, ldy, (int)M, C, rows)
-#define DMF_BA(TT, AC, RK)                          \
-  do {                                              \
-    if (g_bn_apply_rows == 4) DMF_BA_U(TT, AC, RK, 4); \
-    else if (g_bn_apply_rows == 2) DMF_BA_U(TT, AC, RK, 2); \
-    else DMF_BA_U(TT, AC, RK, 1);                   \
-  } while (0)
+// (2 or 4 rows of loads in flight per thread computed the same bits and measured within noise or slower,
+// round 5: profiles/r05fb_apply_rows{1,2,4}.txt, r05fb_modeA_apply_rows_ab.txt; the launch path is U = 1)
+#define DMF_BA(TT, AC, RK) DMF_BA_U(TT, AC, RK, 1)
 #define DMF_BA_R(TT, AC)                 \
   do {                                   \
     if (resk == 0) DMF_BA(TT, AC, 0);     \
@@ -1100,9 +1081,7 @@ extern "C" int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const v
                                                   (const T*)dz, lddz, (const T*)x, ldx, acc, replicas, count,     \
                                                   training, gamma, save_mean_invstd, dgamma, dbeta, (T*)dx, lddx, \
                                                   (int)M, C, rows))
-  if (g_bwd_apply_u == 4) DMF_BBA(4);
-  else if (g_bwd_apply_u == 2) DMF_BBA(2);
-  else DMF_BBA(1);
+  DMF_BBA(1);  // (2 / 4 rows in flight: within noise, profiles/r05aa_bwd_apply_rows_modeB_ab.txt)
 #undef DMF_BBA
   DMF_LAUNCH_CHECK("dmf_bn_bwd_apply_acc");
   return 0;

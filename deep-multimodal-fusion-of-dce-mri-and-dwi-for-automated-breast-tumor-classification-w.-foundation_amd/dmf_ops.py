@@ -1058,8 +1058,6 @@ def conv_bn_act(x, conv, caches, bn, act="none", dropout_p=0.0, rng=None, site=0
         return _conv_bn_eval_folded(x, conv, bn, act, x2)
     if _eval_res_ok(x, conv, bn, act, p, res, skip, in_ss, unbias_mult, x2):
         return _conv_bn_eval_res(x, conv, bn, act, res, skip)
-    if _gbar_ok(x, conv, bn, act, p, res, skip, x2, in_ss):
-        return _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult)
     if skip is not None:
         xr, conv_r, caches_r, bn_r = skip
         gr = ConvGeom(conv_r)
@@ -1272,19 +1270,6 @@ def _two_pass_ok(x, conv, bn, act, p, res, skip, x2, in_ss, unbias_mult):
     return bool(N.load().dmf_conv2d_fwd_affine_ok(dt(x), n, h, w, c, conv.out_channels, conv.stride[0]))
 
 
-# Grid-barrier BatchNorm apply of a forward-only conv -> BN (batch statistics) -> act with no shortcut
-# (dmf_conv2d_fwd_bn_act): the conv's epilogue accumulates the statistics, meets the other blocks at a
-# grid-wide barrier and writes act(bn(y)) once -- no raw output, no dmf_bn_apply pass. Every block of the
-# launch is resident (one tile per block, dmf_conv2d_fwd_bn_act_ok) and spins once, so a second such
-# kernel spinning beside it on another stream could hold CUs the first still needs: it runs only outside a
-# concurrent region (CONCURRENT: raised by train_fusion._encode's two-stream fork and by branch()).
-# Measured and left OFF (knob "grid_barrier_bn"; profiles/r05g_grid_barrier_bench.txt, _enc_ab.txt): the
-# barrier itself costs 7-11 us per launch (the guide's barrier-counter row: 7.4), about what the apply pass
-# it removes costs (8-14 us), and the 3x3 ping-pong form spills under the epilogue's registers (512->512
-# dilated: 160 -> 216 us); it also needs the encoders on one stream, and the serial forward is 9.89 ms
-# against 8.47 ms for the two-stream one (10.55 ms serial with the barrier).
-GRID_BARRIER_BN = False
-CONCURRENT = [0]
 # dmf_conv_tune values set through set_knobs (key -> value), so a region can restore what it changes
 TUNE_VALUES = {}
 # CONC_MIN_TILES > 0: inside the two-encoder fork (train_fusion._encode) the 256x256 and 256x128 forward
@@ -1292,9 +1277,6 @@ TUNE_VALUES = {}
 # rest) instead of the chip-filling 256 (dmf_conv_tune keys 14 / 15); single-stream runs keep 256.
 # Knob "conc_min_tiles" (0 = off).
 CONC_MIN_TILES = 128
-# CONC_PERSIST > 0: the persistent 1x1 / ping-pong forms run this many blocks inside the fork instead of
-# one per CU (dmf_conv_tune key 18). Knob "conc_persist" (0 = off).
-CONC_PERSIST = 0
 
 
 # CONC_BWD_MIN_TILES > 0: the same threshold for the dgrad launches (forward tiles) of a training backward
@@ -1304,7 +1286,7 @@ CONC_BWD_MIN_TILES = 128
 
 
 def concurrent_tiles(enter, bwd=False):
-    """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES, CONC_PERSIST;
+    """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES;
     bwd: CONC_BWD_MIN_TILES for a two-encoder backward)."""
     mt = CONC_BWD_MIN_TILES if bwd else CONC_MIN_TILES
     if mt > 0:
@@ -1312,65 +1294,6 @@ def concurrent_tiles(enter, bwd=False):
             N.call("dmf_conv_tune", key, mt if enter else TUNE_VALUES.get(key, 256))
     if bwd:
         return
-    if CONC_PERSIST > 0:
-        N.call("dmf_conv_tune", 18, CONC_PERSIST if enter else TUNE_VALUES.get(18, 0))
-
-
-def _gbar_site(bn, dev):
-    """The barrier words of one BatchNorm2d's launch site (zero at first use, self-resetting; kept out of
-    the state_dict)."""
-    st = bn.__dict__.get("_dmf_gbar")
-    if st is None or st.device != dev:
-        st = torch.zeros(4, dtype=torch.int32, device=dev)
-        bn.__dict__["_dmf_gbar"] = st
-    return st
-
-
-def _gbar_ok(x, conv, bn, act, p, res, skip, x2, in_ss):
-    if not (GRID_BARRIER_BN and CONCURRENT[0] == 0 and res is None and skip is None and in_ss is None and p == 0
-            and act in ("relu", "gelu", "none") and (bn.training or bn.running_mean is None) and x.is_cuda
-            and x.dtype in (torch.bfloat16, torch.float16) and conv.groups == 1
-            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
-            and conv.dilation[0] == conv.dilation[1]):
-        return False
-    if needs_grad(x, x2, conv.weight, conv.bias, bn.weight, bn.bias):
-        return False
-    n, c, h, w, _ = nhwc(x)
-    c2 = nhwc(x2)[1] if x2 is not None else 0
-    if c + c2 != conv.in_channels:
-        return False
-    g = ConvGeom(conv)
-    return bool(N.load().dmf_conv2d_fwd_bn_act_ok(dt(x), n, h, w, c, c2, conv.out_channels, g.kh, g.kw, g.stride,
-                                                  g.pad, g.dil, 0 if conv.bias is None else 1))
-
-
-def _conv_bn_gbar(x, conv, caches, bn, act, x2, unbias_mult):
-    g = ConvGeom(conv)
-    n, cx, h, wd, ldx = nhwc(x)
-    cx2, ldx2 = (nhwc(x2)[1], nhwc(x2)[4]) if x2 is not None else (0, 0)
-    co = conv.out_channels
-    ho, wo = g.out_hw(h, wd)
-    m = n * ho * wo
-    dev = x.device
-    track = bn.track_running_stats and bn.running_mean is not None
-    if track:
-        _train_bn_mark(bn)
-    mom = bn.momentum if bn.momentum is not None else 0.1
-    with torch.no_grad():
-        wk = caches[0].get(conv.weight, x.dtype, cx + cx2, 0)
-        acc = _bn_acc(co, dev)
-        gb = _gbar_site(bn, dev)
-        y = empty_nhwc(n, co, ho, wo, x.dtype, dev)
-        _conv_launch("dmf_conv2d_fwd_bn_act",
-                     (dt(x), x.data_ptr(), n, h, wd, cx, ldx, _p(x2), cx2, ldx2, wk.data_ptr(), co, g.kh, g.kw,
-                      g.stride, g.pad, g.dil, _p(conv.bias), y.data_ptr(), ho, wo, nhwc(y)[4], ACT[act],
-                      acc.data_ptr(), BN_ACC_REPLICAS, gb.data_ptr(), _p(bn.weight), _p(bn.bias),
-                      _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None,
-                      _p(bn.num_batches_tracked) if track else None, float(mom), float(bn.eps), float(m),
-                      float(m * unbias_mult) if unbias_mult != 1 else 0.0),
-                     (x, x2, wk, conv.bias, y, acc, gb, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                      bn.num_batches_tracked), x, n, h, wd, cx + cx2, co, g.kh, g.kw, g, ho, wo)
-    return y
 
 
 def _finalize_acc(d, c):
@@ -2643,18 +2566,11 @@ def branch(owner, name, fn, *inputs):
         return out, (lambda: out)
     side = side_stream(owner, name, dev)
     side.wait_stream(main)
-    CONCURRENT[0] += 1  # until the join: no grid-barrier launch on either stream
-    try:
-        with torch.cuda.stream(side):
-            record_tree(list(inputs), side)
-            out = fn()
-    except BaseException:
-        CONCURRENT[0] -= 1  # no join will follow
-        raise
+    with torch.cuda.stream(side):
+        record_tree(list(inputs), side)
+        out = fn()
 
     def join():
-        if keep:
-            CONCURRENT[0] -= 1
         main.wait_stream(side)
         record_tree(out, main)
         del keep[:]
@@ -2803,16 +2719,11 @@ KNOBS = {
     "two_pass_max_k": ("dmf_ops", "TWO_PASS_MAX_K"),
     "eval_bn_fold": ("dmf_ops", "EVAL_BN_FOLD"),
     "fc1_drop_conv": ("dmf_tokens", "FC1_DROP_CONV"),
-    "bwd_apply_rows": ("call", "dmf_bn_bwd_apply_tune"),
-    "fwd_apply_rows": ("call", "dmf_bn_apply_tune"),
     "sgemm_mfma": ("call", "dmf_sgemm_tune"),
-    "wgrad_xcd": ("wgrad_tune", 6),
     "conc_min_tiles": ("dmf_ops", "CONC_MIN_TILES"),
-    "conc_persist": ("dmf_ops", "CONC_PERSIST"),
     "conc_bwd_min_tiles": ("dmf_ops", "CONC_BWD_MIN_TILES"),
     "se_one_launch": ("call", "dmf_se_mlp_tune"),
     "fp8_gemm_scaled": ("call", "dmf_gemm_fp8_tune"),
-    "grid_barrier_bn": ("dmf_ops", "GRID_BARRIER_BN"),
     "token_fwd_fused": ("dmf_tokens", "FWD_FUSED"),
     "parallel_encoders": ("dmf_ops", "PARALLEL_BRANCHES"),
     "parallel_dead": ("model_module", "PARALLEL_DEAD"),
@@ -2827,7 +2738,6 @@ KNOBS = {
     "conv_fast_epi": ("tune", 11),
     "conv_wide_min_tiles": ("tune", 14),
     "conv_sq_min_tiles": ("tune", 15),
-    "conv_sq_w4": ("tune", 16),
     "wgrad_dma": ("wgrad_tune", 0),
     "wgrad_wide": ("wgrad_tune", 1),
     "wgrad_tr": ("wgrad_tune", 2),

@@ -128,10 +128,7 @@ class LightningFusionModel(nn.Module):
         side.wait_stream(main)
         prev = O.RNG_CURRENT[0]
         O.ORIGIN_STREAM[0] = main
-        entered = False
         try:
-            O.CONCURRENT[0] += 1  # the two encoders overlap: no grid-barrier launches (dmf_ops.GRID_BARRIER_BN)
-            entered = True
             O.concurrent_tiles(True)
             O.RNG_CURRENT[0] = snap_dwi
             out_dwi = self.dwi_model(dwi_inputs)
@@ -142,8 +139,6 @@ class LightningFusionModel(nn.Module):
         finally:
             O.RNG_CURRENT[0] = prev
             O.ORIGIN_STREAM[0] = None
-            if entered:
-                O.CONCURRENT[0] -= 1
             O.concurrent_tiles(False)  # idempotent: restores the single-stream tile sizing
         main.wait_stream(side)
         self.__dict__["_encoders_forked"] = True

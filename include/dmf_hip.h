@@ -67,9 +67,7 @@ int dmf_conv_last_form(void);
  * mode; 4 = persistent 256x256 form on / off; 6 = benchmark-only skip bits of the
  * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
  * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 14 / 15 = tiles a launch
- * needs for the 256x128 / 256x256 forms; 16 = 4-wave square tile; 17 = timing-only
- * bits of dmf_conv2d_fwd_bn_act (64 skip the barrier, 128 the arena reads); 18 = blocks of a persistent
- * launch (0 = one per CU; a two-stream region may cap it).
+ * needs for the 256x128 / 256x256 forms.
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
@@ -79,8 +77,7 @@ int dmf_conv_tune(int key, int value);
  * key 3 = the 256x256 LDS-DMA tile where Cout and KH*KW*Cin are multiples of 256:
  * 0 off / 1 (default) for weights of >= 2^18 entries / 2 wherever legal;
  * key 4 = split-lane reducers of dmf_conv2d_wgrad_reduce at >= 16 splits on (1) / off;
- * key 5 = blocks the pixel splits aim for, percent of one chip-filling wave (10..400, default 50);
- * key 6 = split-major block order per XCD (the tiles of one pixel split share one L2) on (1) / off (0). */
+ * key 5 = blocks the pixel splits aim for, percent of one chip-filling wave (10..400, default 50). */
 int dmf_conv_wgrad_tune(int key, int value);
 /* rows (M tiles) of the bn_partials slab that dmf_conv2d_fwd / _fwd_bn write
  * for this shape (the launcher picks 64- or 128-row tiles per shape) */
@@ -160,26 +157,6 @@ int dmf_conv2d_fwd_res_ok(int dtype, int N, int H, int W, int Cin, int Cout, int
 int dmf_conv2d_fwd_res(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
                        int KH, int KW, int stride, int pad, int dil, const float* bias, const void* res, int ldr,
                        int act, void* y, int Ho, int Wo, int ldy, void* stream);
-/* conv -> BatchNorm2d (batch statistics) -> act in ONE launch, for a forward that is never
- * differentiated (frozen encoders, mode A: timm Bottleneck conv1 / conv2, the necks; the apply
- * passes of foundation_model.py:260-267 and model_module.py:401-476). The epilogue adds the
- * statistics into bn_acc [replicas][Cout][2] (zeroed by the caller), every block meets the others at
- * a grid-wide barrier, then finalizes its tile's channels from bn_acc (the running statistics and
- * num_batches_tracked move once, as dmf_bn_finalize with count / unbias_count) and writes
- * act(conv * scale + shift) -- no raw conv output, no apply pass. Legal only where every block of the
- * launch is resident and owns one output tile: dmf_conv2d_fwd_bn_act_ok (the 256x256 ping-pong form
- * without bias over whole tiles, or the 256x128 wide form, at <= one tile per CU). gbar: three
- * counters of this BatchNorm's launch site, zero on the first call (the launches self-reset them).
- * A grid that is not fully resident within ~2 s traps instead of hanging. act: DMF_ACT_NONE / RELU /
- * GELU. */
-int dmf_conv2d_fwd_bn_act_ok(int dtype, int N, int H, int W, int Cin, int Cin2, int Cout, int KH, int KW, int stride,
-                             int pad, int dil, int has_bias);
-int dmf_conv2d_fwd_bn_act(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* x2, int Cin2,
-                          int ldx2, const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
-                          const float* bias, void* y, int Ho, int Wo, int ldy, int act, double* bn_acc, int replicas,
-                          unsigned* gbar, const float* gamma, const float* beta, float* running_mean,
-                          float* running_var, long long* num_batches_tracked, float momentum, float eps,
-                          double count, double unbias_count, void* stream);
 int dmf_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, int lddy, const void* wt, int Cin,
                      int KH, int KW, int stride, int pad, int dil, void* dx, int H, int W, int lddx, void* stream);
 int dmf_conv_weight_prep(int dtype, const float* w, void* out, int Cout, int Cin, int CinP, int KH, int KW, int mode,
@@ -326,10 +303,6 @@ int dmf_act_bwd_bn_reduce_acc(int dtype, const void* dy, int lddy, const void* d
 int dmf_bn_bwd_apply_acc(int dtype, const void* dz, int lddz, const void* x, int ldx, const double* acc, int replicas,
                          double count, int training, const float* gamma, const float* save_mean_invstd, float* dgamma,
                          float* dbeta, void* dx, int lddx, long long M, int C, void* stream);
-/* rows of dmf_bn_bwd_apply_acc's loads in flight per thread: 1 (default), 2 or 4 (A/B runs) */
-int dmf_bn_bwd_apply_tune(int rows_in_flight);
-/* rows of dmf_bn_apply's loads in flight per thread: 1 (default), 2 or 4 (A/B runs) */
-int dmf_bn_apply_tune(int rows_in_flight);
 int dmf_col_stats_tiles(long long M);
 int dmf_col_stats(int dtype, const void* x, int ldx, long long M, int C, float* partials, void* stream);
 

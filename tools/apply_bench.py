@@ -4,7 +4,7 @@ finalize-folded dmf_bn_apply (statistics from a float64 arena) against a
 plain streaming copy of the same bytes. HIP events around a hipGraph of R
 launches; each launch reads a freshly written arena (as in the forward).
 
-    python tools/apply_bench.py [--reps 20] [--rows 1|2|4]
+    python tools/apply_bench.py [--reps 20]
 """
 import argparse
 import ctypes
@@ -60,9 +60,7 @@ def desc(c, acc, ss, save, m):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--rows", type=int, default=1, help="rows in flight per thread (dmf_bn_apply_tune)")
     a = ap.parse_args()
-    N.call("dmf_bn_apply_tune", a.rows)
     tot_a = tot_c = 0.0
     for (m, c, act, rk), cnt in SHAPES:
         x = torch.randn(m, c, device="cuda").bfloat16()

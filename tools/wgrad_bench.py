@@ -72,8 +72,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--sq", action="store_true", help="A/B the 256x256 form against the default")
-    ap.add_argument("--xcd", action="store_true",
-                    help="A/B the split-major block order per XCD (key 6) on the default forms")
     ap.add_argument("--reduce", action="store_true",
                     help="time dmf_conv2d_wgrad_reduce alone, split-lane reducers off / on (key 4)")
     a = ap.parse_args()
@@ -83,9 +81,8 @@ def main():
     shapes = [s for s in sorted(cnt, key=lambda s: -cnt[s] * s[0] * s[1] * s[2] * s[3] * s[4] * s[5] ** 2 / s[6] ** 2)
               if s[3] >= 8 and s[4] >= 8]
     sel = [int(i) for i in a.only.split(",")] if a.only else range(len(shapes))
-    # (LDS-DMA, 128x256, 256x256[, XCD split-major order])
-    variants = (((1, 1, 1, 0), (1, 1, 1, 1)) if a.xcd else ((1, 1, 0), (1, 1, 1)) if a.sq
-                else ((0, 0, 0), (1, 0, 0), (1, 1, 0)))
+    # (LDS-DMA, 128x256, 256x256)
+    variants = ((1, 1, 0), (1, 1, 1)) if a.sq else ((0, 0, 0), (1, 0, 0), (1, 1, 0))
     tot = [0.0] * len(variants)
     torch.manual_seed(0)
     for i in sel:
@@ -95,7 +92,7 @@ def main():
 
         def tune(v):
             for key, val in enumerate(v):
-                N.call("dmf_conv_wgrad_tune", key if key < 2 else 3 if key == 2 else 6, val)
+                N.call("dmf_conv_wgrad_tune", key if key < 2 else 3, val)
 
         for v in variants:
             tune(v)  # the split count (and so the workspace) depends on the tile form
