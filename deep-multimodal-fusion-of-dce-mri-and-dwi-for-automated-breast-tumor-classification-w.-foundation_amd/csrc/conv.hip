@@ -23,6 +23,7 @@
 // an LDS-staged, 16-B coalesced store with an output channel stride (so
 // producers can write straight into a channel slice of a concat buffer).
 #include <algorithm>
+#include <vector>
 
 #include "conv_core.h"
 
@@ -282,6 +283,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 // activated tensor is never written to HBM.
 template <typename T, bool PADCHK, bool DUAL, int BM, int BN, int INA = -1>
 __global__ void __launch_bounds__(CTHREADS, (BM * BN <= 64 * 64) ? 4 : ((BM * BN <= 64 * 128) ? 3 : 2)) k_conv_fwd_buf(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per K-step
   constexpr int SB = (BM + BN) * 128;        // LDS stage bytes
   constexpr int ES = sizeof(T);
@@ -466,6 +468,7 @@ constexpr int WLDS = WNSTAGE * WSTAGE;  // 147456 B: also holds the C staging ti
 
 template <bool PADCHK, bool DUAL, typename T = bf16_t>
 __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int ES = 2, EPC = 8, BK = 64;
   constexpr int NW = WTHREADS / 64;
   constexpr int NA = WBM / 8 / NW;  // A row-groups (8 rows) per wave: 4
@@ -590,6 +593,7 @@ __global__ void __launch_bounds__(WTHREADS, 1) k_conv_fwd_wide(ConvArgs a) {
 // was removed in round 6.
 template <bool PADCHK, bool DUAL, int VAR, typename T = bf16_t, int WM_ = QWM, int WN_ = QWN>
 __global__ void __launch_bounds__(64 * WM_ * WN_, 1) k_conv_fwd_sq(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int ES = 2, EPC = 8, BK = 64;
   constexpr int NW = WM_ * WN_;
   constexpr int NA = QBM / 8 / NW;  // A row-groups (8 rows) per wave: 4 (8 waves) / 8 (4 waves)
@@ -751,6 +755,7 @@ __global__ void __launch_bounds__(64 * WM_ * WN_, 1) k_conv_fwd_sq(ConvArgs a) {
 // half" or "all 8 after the barrier" measured no better).
 template <bool PADCHK, bool DUAL, int EPI, int TBM = QBM, int TBN = QBN, int TWN = QWN, typename T = bf16_t>
 __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int ES = 2, BK = 64;
   constexpr int TWM = 2;  // two pixel-half waves per 64-channel slab (ps_epilogue)
   constexpr int NTH = 64 * TWM * TWN, NW = TWM * TWN;
@@ -947,6 +952,7 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
 // (scalar) instead of two integer divisions per lane and step.
 template <typename T, bool DGRAD, int INA, bool FASTC>
 __global__ void __launch_bounds__(CTHREADS, 2) k_conv_igemm(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   constexpr int BK = 8 * EPC;          // 8 chunks per LDS row
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1339,6 +1345,30 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
 #undef DMF_CONV_LAUNCH
 }
 
+// In-kernel timing stamps (tools/stream_stamps.py): while armed, every forward-conv launch made from this
+// process takes the next [start, end] pair of the armed device buffer (StampScope in the kernel) and its
+// stream, form and GEMM shape are recorded here -- so the concurrency of a captured two-stream step can be
+// read without a profiler (rocprofv3's kernel trace serialises a graph's branches).
+struct StampRec { void* stream; int form, m, n, k; };
+static unsigned long long* g_stamp_buf = nullptr;
+static int g_stamp_cap = 0;
+static std::vector<StampRec> g_stamp_rec;
+
+extern "C" int dmf_stamp_arm(unsigned long long* buf, int capacity) {
+  DMF_CHECK_ARG(buf == nullptr || (capacity > 0 && ((uintptr_t)buf % 8) == 0), "dmf_stamp_arm: bad buffer");
+  g_stamp_buf = buf;
+  g_stamp_cap = buf ? capacity : 0;
+  g_stamp_rec.clear();
+  return 0;
+}
+extern "C" int dmf_stamp_count(void) { return (int)g_stamp_rec.size(); }
+extern "C" int dmf_stamp_info(int i, void** stream, int* form, int* m, int* n, int* k) {
+  DMF_CHECK_ARG(i >= 0 && i < (int)g_stamp_rec.size() && stream && form && m && n && k, "dmf_stamp_info: %d", i);
+  const StampRec& r = g_stamp_rec[i];
+  *stream = r.stream; *form = r.form; *m = r.m; *n = r.n; *k = r.k;
+  return 0;
+}
+
 static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const char* what) {
   DMF_CHECK_ARG(dtype == DMF_F32 || is16(dtype), "%s: bad dtype %d", what, dtype);
   const int epc = is16(dtype) ? 8 : 4;
@@ -1356,6 +1386,10 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
               : plan.buf ? (a.in_ss != nullptr ? DMF_FORM_BUF_INA : DMF_FORM_BUF) : DMF_FORM_IGEMM;
   a.mtiles = cdiv(a.M, plan.bm);
   a.ntiles = cdiv(a.Nout, plan.bn);
+  if (g_stamp_buf && !dgrad && (int)g_stamp_rec.size() < g_stamp_cap) {
+    a.stamp = g_stamp_buf + g_stamp_rec.size() * (size_t)STAMP_MAX_BLOCKS * 16;
+    g_stamp_rec.push_back(StampRec{(void*)st, g_last_form, a.M, a.Nout, a.Ktot});
+  }
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = is16(dtype) ? 2 : 4;

@@ -68,6 +68,30 @@ struct ConvArgs {
   float dp;
   const unsigned long long* rng;
   int site;
+  // in-kernel timing stamps (dmf_stamp_arm, tools/stream_stamps.py), null in production: this launch's
+  // region of per-wave [start, end] s_memrealtime ticks (100 MHz, one clock for the whole chip)
+  unsigned long long* stamp;
+};
+
+// Timing stamps without contention: lane 0 of every wave writes its own start / end (plain vector stores,
+// no atomics -- one shared atomic per wave measurably stretched every launch) into this launch's region,
+// [STAMP_MAX_BLOCKS blocks][8 waves][start, end]; the reader takes the min / max. One wave-uniform branch on
+// the null pointer in production launches.
+constexpr unsigned STAMP_MAX_BLOCKS = 4096;
+struct StampScope {
+  unsigned long long* q;
+  __device__ __forceinline__ explicit StampScope(unsigned long long* p) : q(nullptr) {
+    if (p) {
+      const unsigned blk = blockIdx.x + blockIdx.y * gridDim.x, w = threadIdx.x >> 6;
+      if (blk < STAMP_MAX_BLOCKS && w < 8 && (threadIdx.x & 63) == 0) {
+        q = p + (blk * 8 + w) * 2;
+        __builtin_nontemporal_store(wall_clock64(), q);
+      }
+    }
+  }
+  __device__ __forceinline__ ~StampScope() {
+    if (q) __builtin_nontemporal_store(wall_clock64(), q + 1);
+  }
 };
 
 template <int ACT>

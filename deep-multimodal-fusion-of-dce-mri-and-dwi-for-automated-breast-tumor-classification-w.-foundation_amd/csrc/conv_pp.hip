@@ -65,6 +65,7 @@ __device__ __forceinline__ void vm_wait() {
 // epilogue waits with 16 more).
 template <bool PADCHK, bool DUAL, int EPI, typename T = bf16_t>
 __global__ void __launch_bounds__(PP_THREADS, 1) k_conv_fwd_pp(ConvArgs a) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   constexpr int ES = 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;

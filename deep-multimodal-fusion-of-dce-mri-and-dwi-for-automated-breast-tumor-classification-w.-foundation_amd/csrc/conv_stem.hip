@@ -40,6 +40,7 @@ constexpr int STEM_SLOTS = 9;  // 7 rows in use + the next step's 2
 // C: padded input channels (8 / 16); STATS: BN statistics epilogue (a.partials)
 template <int C, bool STATS, bool F16 = false>
 __global__ void __launch_bounds__(256) k_conv_stem(ConvArgs a, int rpw, int plane) {
+  const StampScope stamp_scope_(a.stamp);  // (null unless tools/stream_stamps.py armed it)
   typedef typename std::conditional<F16, f16_t, bf16_t>::type T;  // storage type (bf16 / f16)
   constexpr int NPL = C / 8;               // 16-B channel planes per pixel
   constexpr int CP = 32 / C;               // taps per K-chunk

@@ -70,6 +70,15 @@ int dmf_conv_last_form(void);
  * needs for the 256x128 / 256x256 forms.
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
+/* In-kernel timing stamps of the forward-conv launches (tools/stream_stamps.py): dmf_stamp_arm(buf, n)
+ * arms a zeroed device buffer of n launch regions of 4096 blocks x 8 waves x [start, end] u64 (NULL
+ * disarms and clears the record); each following forward-conv launch from this process takes the next
+ * region, into which lane 0 of each wave writes its start and end in s_memrealtime ticks (100 MHz) --
+ * graph captures keep the regions, so one replay fills them. dmf_stamp_info(i, ...): launch i's stream
+ * handle, DMF_FORM_* and GEMM shape (M, N, K). */
+int dmf_stamp_arm(unsigned long long* buf, int capacity);
+int dmf_stamp_count(void);
+int dmf_stamp_info(int i, void** stream, int* form, int* m, int* n, int* k);
 /* Benchmark knobs of the weight-gradient engine: key 0 = LDS-DMA staging of the
  * bf16 transposed-read kernel on (1, default) / off; key 1 = its 128x256 tile
  * (one workgroup per CU) where K >= 256 on (1, default) / off; key 2 = the
