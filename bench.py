@@ -234,7 +234,8 @@ def wgrad_probe(trainer, batch, dtype):
             "avg_reduce_us": round((avg_ms - avg_ms_wg) * 1e3, 2),
             "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
             "algorithmic_mb_per_launch": round(byt / n / 1e6, 2),
-            "per_launch": "one launch = dmf_conv2d_wgrad + its dmf_conv2d_wgrad_reduce"}
+            "per_launch": "one launch = dmf_conv2d_wgrad + its dmf_conv2d_wgrad_reduce",
+            **mfma_busy("mfma_wgrad", "wgrad")}
 
 
 FP8_MFMA_PEAK_TFLOPS = 5000.0  # dense e4m3 (spec, no sparsity)
@@ -250,9 +251,10 @@ def gemm_probes(trainer, batch):
     fam = {"fp8_gemm": ("e4m3 patch-embed GEMM (k_gemm_fp8_dma: 144x256 tiles, v_mfma_scale_f32_16x16x128_f8f6f4 "
                         "with unit scales; k_gemm_fp8 128x128 where those tiles do not fill the chip)",
                         FP8_MFMA_PEAK_TFLOPS),
-           "tok_gemm": ("token GEMMs of the frozen encoders' blocks: qkv on the conv engine's persistent 1x1 form, "
-                        "QK^T + PV inside the fused attention (dmf_flash_attn_fwd), fc1 on k_gemm_bf16 (its dropout); "
-                        "proj / fc2 (f32 residual epilogues) not probed", BF16_MFMA_PEAK_TFLOPS)}
+           "tok_gemm": ("every token GEMM of the frozen encoders' blocks: qkv on the conv engine's persistent 1x1 "
+                        "form, QK^T + PV inside the fused attention (dmf_flash_attn_fwd), fc1 (+ GELU + dropout) on "
+                        "the conv engine, proj / fc2 on k_gemm_bf16 with their LayerScale + dropout + f32 residual "
+                        "epilogues", BF16_MFMA_PEAK_TFLOPS)}
     recs = {k: [] for k in fam}
     for k in fam:
         O.PROBE[k] = recs[k]
@@ -269,14 +271,17 @@ def gemm_probes(trainer, batch):
         if not r:
             continue
         n = len(r)
-        avg_ms, _ = O.probe_replay(r)
+        avg_ms, per = O.probe_replay(r)
         flops = sum(x["flops"] for x in r)
         byt = sum(x["bytes"] for x in r)
         ach = flops / n / (avg_ms * 1e-3) / 1e12
+        fl_of = {x["shape"]: x["flops"] for x in r}
         out[k] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                   "frac": round(ach / peak, 4), "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
                   "algorithmic_gflop_per_launch": round(flops / n / 1e9, 4),
-                  "algorithmic_mb_per_launch": round(byt / n / 1e6, 3)}
+                  "algorithmic_mb_per_launch": round(byt / n / 1e6, 3),
+                  "per_shape": [{"shape": list(map(str, shp)), "launches": c, "us": round(t * 1e3, 2),
+                                 "frac": round(fl_of[shp] / (t * 1e-3) / 1e12 / peak, 4)} for shp, c, t in per]}
         r.clear()
     return out
 
@@ -330,6 +335,7 @@ def roofline_probe(trainer, batch, dtype):
         "algorithmic_gflop_per_launch": round(flops / n / 1e9, 3),
         "algorithmic_mb_per_launch": round(byt / n / 1e6, 2),
         "hbm_gbs_per_launch_avg": round(byt / (ms * 1e-3) / 1e9, 1),
+        **mfma_busy("mfma", "conv_fwd"),
     }
 
 
@@ -356,6 +362,18 @@ def pmc_summary(key):
         d = json.load(f)
     d["source"] = rel
     return d
+
+
+def mfma_busy(key, form):
+    """MFMA utilisation of a kernel family from the committed counter summary (tools/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x CUs x GRBM_GUI_ACTIVE/8), PMC passes serialise dispatches)."""
+    d = pmc_summary(key)
+    row = (d or {}).get("forms", {}).get(form)
+    if not row:
+        return {"mfma_busy": None}
+    return {"mfma_busy": row["mfma_busy_cu"], "mfma_busy_chip": row["mfma_busy_chip"],
+            "mfma_busy_unit": "SQ_VALU_MFMA_BUSY_CYCLES / (4 x occupied CUs x GRBM_GUI_ACTIVE/8) over the family's "
+                              "dispatches (chip: over all 256 CUs), " + d["source"]}
 
 
 def pmc_traffic(family=""):

@@ -766,7 +766,7 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
   static_assert(NA == 4 && NB == 4 && FN == 4, "k_conv_fwd_ps geometry");
   // an epilogue's stores per wave (+2 float64 atomics, pixel-half 0, stat_acc); the statistics-only
   // epilogue (12) stores nothing, so nothing younger than the in-flight DMA may be waited out
-  constexpr int EPI_VM = EPI == 12 ? 0 : 2 * FM;
+  constexpr int EPI_VM = EPI == 12 ? 0 : EPI == 15 ? 4 * FM : 2 * FM;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -801,6 +801,13 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
       if (EPI == 11) sbias[2 * a.Nout + i] = a.res_ss[i];
     }
     if (a.aff_acc && blockIdx.x == 0 && tid == 0 && a.fin.nbt) *a.fin.nbt += 1;
+    __syncthreads();
+  } else if constexpr (EPI == 15) {
+    // the token residual epilogue: [bias | colscale] x Nout
+    for (int i = tid; i < a.Nout; i += NTH) {
+      sbias[i] = a.bias ? a.bias[i] : 0.f;
+      sbias[a.Nout + i] = a.colscale ? a.colscale[i] : 1.f;
+    }
     __syncthreads();
   } else if (a.bias) {
     for (int i = tid; i < a.Nout; i += NTH) sbias[i] = a.bias[i];
@@ -937,7 +944,8 @@ __global__ void __launch_bounds__(64 * 2 * TWN, TWN == 4 ? 1 : 2) k_conv_fwd_ps(
       continue;
     }
     // ---------------- epilogue of tile `lin` (the next tile's step 0 is in flight)
-    if (!(a.dbg & 4)) ps_epilogue<EPI, TBN, FM, TBM, T>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
+    if constexpr (EPI == 15) ps_epilogue_tokres<TBN, FM, TBM>(a, acc, lin, sbias, wm, wn, fr, fg);
+    else if (!(a.dbg & 4)) ps_epilogue<EPI, TBN, FM, TBM, T>(a, acc, lin, ry, sred, sbias, tid, wm, wn, fr, fg);
     epi = !(a.dbg & 4);
     if (!more) break;
     t = tnext;
@@ -1174,7 +1182,9 @@ static ConvPlan conv_plan(int dtype, bool dgrad, const ConvArgs& a) {
   const bool sq_ps_ok = is16(dtype) && a.tickets == nullptr && a.Nout % QBN == 0 &&
                         a.Ktot >= 64 && (long long)cdiv(a.M, QBM) * (a.Nout / QBN) >= g_min_tiles &&
                         (long long)a.M * a.ldy * 2 < (1LL << 31);
-  if (sq_ps_ok && (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 1024 && a.KH * a.KW == 1)))) {
+  // (the token-residual epilogue exists on the persistent 1x1 form only)
+  if (sq_ps_ok && !a.tok_res &&
+      (g_pp_mode >= 2 || (g_pp_mode == 1 && !(g_ps_enable && a.Ktot < 1024 && a.KH * a.KW == 1)))) {
     p.wide = p.sq = p.pp = true;
     p.bm = QBM;
     p.bn = QBN;
@@ -1248,7 +1258,8 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
       const dim3 gp((unsigned)std::min<long long>(nblk, cu_count())), bq(QTHREADS);
       // statistics without bias over whole tiles: the fast epilogue (EPI 5); a known BatchNorm: the
       // affine epilogue (EPI 8, plain shortcut / 11, BN'd shortcut)
-      const int epi = (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
+      const int epi = a.tok_res ? 15
+                      : (a.out_ss != nullptr || a.aff_acc) ? (a.res_ss != nullptr ? 11 : 8)
                       : a.y == nullptr ? 12
                       : a.partials != nullptr ? ((g_fast_epi && a.bias == nullptr && a.M % 256 == 0) ? 5 : 0)
                       : a.dp > 0.f ? 14
@@ -1275,6 +1286,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
         case 3: DMF_PS(3); break;
         case 5: DMF_PS(5); break;
         case 14: DMF_PS_AFF(14); break;
+        case 15: DMF_PS_AFF(15); break;
         default: DMF_PS(4); break;
       }
 #undef DMF_PS
@@ -1393,7 +1405,7 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
   const long long nblk = (long long)a.mtiles * a.ntiles;
   DMF_CHECK_ARG(nblk < (1LL << 31), "%s: grid too large", what);
   const int es = is16(dtype) ? 2 : 4;
-  const size_t lds_total = plan.ps ? (size_t)PS_LDS + ((a.out_ss || a.aff_acc) ? (a.res_ss ? 3 : 2) * (size_t)a.Nout * 4
+  const size_t lds_total = plan.ps ? (size_t)PS_LDS + ((a.out_ss || a.aff_acc || a.tok_res) ? (a.res_ss ? 3 : 2) * (size_t)a.Nout * 4
                                                      : a.bias ? (size_t)a.Nout * 4 : 0)
                           : plan.sq ? (size_t)QLDS
                           : plan.wide ? (size_t)WLDS : conv_lds_main(es, plan.bm, plan.bn) + CONV_LDS_EXTRA;
@@ -1406,8 +1418,8 @@ static int launch_conv(int dtype, bool dgrad, ConvArgs& a, hipStream_t st, const
     const bool plain = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     return launch_conv_pp(a, epi, plain, a.bias ? (size_t)a.Nout * 4 : 0, st, dtype);
   }
-  DMF_CHECK_ARG(a.dp == 0.f || (!dgrad && plan.ps && a.x2 == nullptr && a.act == DMF_ACT_GELU && a.rng &&
-                                 a.partials == nullptr && a.y != nullptr),
+  DMF_CHECK_ARG(a.dp == 0.f || (!dgrad && plan.ps && a.x2 == nullptr && (a.act == DMF_ACT_GELU || a.tok_res) &&
+                                 a.rng && a.partials == nullptr && a.y != nullptr),
                 "%s: dropout needs the persistent 1x1 form with the GELU epilogue (one source, rng state)", what);
   DMF_CHECK_ARG((a.out_ss == nullptr && !a.aff_acc) || (!dgrad && plan.ps && a.bias == nullptr && a.x2 == nullptr && a.res),
                 "%s: the affine epilogue needs the persistent 1x1 form (no bias, one source, a shortcut)", what);
@@ -1748,6 +1760,41 @@ static ConvArgs affine_args(int dtype, int N, int H, int W, int Cin, int ldx, in
   a.Ho = (H - 1) / stride + 1; a.Wo = (W - 1) / stride + 1; a.M = N * a.Ho * a.Wo; a.ldy = Cout;
   (void)dtype;
   return a;
+}
+
+// token linear -> + bias -> dropout -> x colscale -> + f32 residual, f32 out, on the persistent 1x1 form
+// (forward-only transformer blocks' proj / fc2, transformer_model.py:83-134; the k_gemm_bf16 epilogue of
+// those linears with the same Philox masks)
+extern "C" int dmf_conv2d_fwd_tokres_ok(int dtype, int N, int H, int W, int Cin, int Cout) {
+  if (!is16(dtype)) return 0;
+  ConvArgs a = affine_args(dtype, N, H, W, Cin, Cin, Cout, 1);
+  a.tok_res = 1;
+  return conv_plan(dtype, false, a).ps && (size_t)PS_LDS + (size_t)2 * Cout * 4 <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int dmf_conv2d_fwd_tokres(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w,
+                                     int Cout, const float* bias, const float* colscale, const float* res, int ldr,
+                                     float dropout_p, const unsigned long long* rng, int site, float* y, int ldy,
+                                     void* stream) {
+  ConvArgs a{};
+  int rc = conv_fwd_common(a, dtype, x, N, H, W, Cin, ldx, nullptr, 0, 0, w, Cout, 1, 1, 1, 0, 1, bias, y, H, W, ldy,
+                           DMF_ACT_NONE, nullptr, DMF_ACT_NONE, "dmf_conv2d_fwd_tokres");
+  if (rc) return rc;
+  DMF_CHECK_ARG(is16(dtype) && res && ldr >= Cout && ldr % 4 == 0 && ((uintptr_t)res % 16) == 0 &&
+                    ldy % 4 == 0 && (dropout_p <= 0.f || (rng && dropout_p < 1.f)),
+                "dmf_conv2d_fwd_tokres: a 16-bit dtype, a 16-B aligned f32 residual / output and rng for dropout");
+  DMF_CHECK_ARG((long long)a.M * ldr * 4 < (1LL << 31) && (long long)a.M * ldy * 4 < (1LL << 31),
+                "dmf_conv2d_fwd_tokres: residual / output exceed a 32-bit buffer offset");
+  a.tok_res = 1;
+  a.colscale = colscale;
+  a.res = res;
+  a.ldr = ldr;
+  a.dp = dropout_p > 0.f ? dropout_p : 0.f;
+  a.rng = rng;
+  a.site = site;
+  DMF_CHECK_ARG(conv_plan(dtype, false, a).ps, "dmf_conv2d_fwd_tokres: the shape does not take the persistent 1x1 "
+                "form (dmf_conv2d_fwd_tokres_ok)");
+  return launch_conv(dtype, false, a, (hipStream_t)stream, "dmf_conv2d_fwd_tokres");
 }
 
 extern "C" int dmf_conv2d_fwd_affine_ok(int dtype, int N, int H, int W, int Cin, int Cout, int stride) {

@@ -62,6 +62,11 @@ struct ConvArgs {
   // bias, y = act(y + res[m][n]) with res / ldr above -- an eval-mode Bottleneck conv3 whose BatchNorm is
   // folded into its weights and bias (dmf_ops._eval_fold)
   int res_add;
+  // token-residual epilogue of k_conv_fwd_ps (EPI 15, dmf_conv2d_fwd_tokres): a transformer block's proj /
+  // fc2 linear, out_f32 = res_f32 + colscale * dropout(acc + bias), the k_gemm_bf16 epilogue of those
+  // linears (res / ldr: the f32 residual stream; y / ldy: f32 out; dp / rng / site: the dropout)
+  int tok_res;
+  const float* colscale;
   // dropout after the bias + GELU epilogue of k_conv_fwd_ps (EPI 14, dmf_conv2d_fwd_drop): Philox keep
   // masks on element m * Nout + n, the token GEMM's index (k_gemm_bf16 epilogue), so a forward-only
   // token block draws the same masks as the training path
@@ -424,6 +429,77 @@ __device__ __forceinline__ void ps_epilogue(const ConvArgs& a, f32x4_t (&acc)[FM
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+  }
+}
+
+// Register epilogue of EPI 15 (see ConvArgs::tok_res) for the 256x256 persistent form: the lane's 16
+// channels of each pixel row (ps_chan) get + bias, the token GEMM's Philox keep mask on element
+// m * Nout + n (the same masks as k_gemm_bf16's epilogue), x colscale, + the f32 residual, and leave as
+// four 16-B f32 stores. Kept light on registers (it is inlined into the K loop's body): bias / colscale
+// re-read from LDS per fragment row, the residual loaded one fragment row ahead (2 x 4 loads in flight).
+template <int TBN = QBN, int FM = 8, int TBM = QBM>
+__device__ __forceinline__ void ps_epilogue_tokres(const ConvArgs& a, f32x4_t (&acc)[FM][4], int lin,
+                                                   const float* sbias, int wm, int wn, int fr, int fg) {
+  const int mt = lin / a.ntiles, nt = lin - (lin / a.ntiles) * a.ntiles;
+  const int m0 = mt * TBM, n0 = nt * TBN;
+  const int cl = wn * 64 + fg * 8;
+  const bool drop = a.dp > 0.f;
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.res), 0, (int)((long long)a.M * a.ldr * 4), BUF_FLAGS_EP);
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)((long long)a.M * a.ldy * 4), BUF_FLAGS_EP);
+  // chunk q of a row: channels cl + 4 (q & 1) + 32 (q >> 1) .. +3 = values 4q .. 4q+3 (ps_chan)
+  auto load_res = [&](int i, v4u_t (&rv)[4]) {
+    const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
+    const unsigned ro = (unsigned)(((size_t)m * a.ldr + n0 + cl) * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      rv[q] = __builtin_bit_cast(v4u_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rr, m < a.M ? ro + (q & 1) * 16 + (q >> 1) * 128 : BUF_OOB, 0, 0));
+  };
+  v4u_t rcur[4], rnext[4];
+  load_res(0, rcur);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if (i + 1 < FM) load_res(i + 1, rnext);
+    const int m = m0 + wm * (TBM / 2) + i * 16 + fr;
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + cl + (q & 1) * 4 + (q >> 1) * 32;
+      const float4 bq = *(const float4*)(sbias + n);
+      const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[4 * q + t] = acc[i][q][t] + bb[t];
+    }
+    if (drop) {
+      const float dks = 1.f / (1.f - a.dp);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bool keep[4];
+        dropout_keep4v(a.rng[0], a.rng[1], a.site,
+                       (unsigned long long)m * a.Nout + n0 + cl + (q & 1) * 4 + (q >> 1) * 32, a.dp, keep);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[4 * q + t] = keep[t] ? v[4 * q + t] * dks : 0.f;
+      }
+    }
+    const unsigned yo = (unsigned)(((size_t)m * a.ldy + n0 + cl) * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + cl + (q & 1) * 4 + (q >> 1) * 32;
+      const float4 g = *(const float4*)(sbias + a.Nout + n);
+      const v4u_t r = rcur[q];
+      v4u_t o;
+      o.x = __float_as_uint(__builtin_fmaf(v[4 * q], g.x, __uint_as_float(r.x)));
+      o.y = __float_as_uint(__builtin_fmaf(v[4 * q + 1], g.y, __uint_as_float(r.y)));
+      o.z = __float_as_uint(__builtin_fmaf(v[4 * q + 2], g.z, __uint_as_float(r.z)));
+      o.w = __float_as_uint(__builtin_fmaf(v[4 * q + 3], g.w, __uint_as_float(r.w)));
+      __builtin_amdgcn_raw_buffer_store_b128(o, ry, m < a.M ? yo + (q & 1) * 16 + (q >> 1) * 128 : BUF_OOB, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rcur[q] = rnext[q];
   }
 }
 

@@ -2719,6 +2719,7 @@ KNOBS = {
     "two_pass_max_k": ("dmf_ops", "TWO_PASS_MAX_K"),
     "eval_bn_fold": ("dmf_ops", "EVAL_BN_FOLD"),
     "fc1_drop_conv": ("dmf_tokens", "FC1_DROP_CONV"),
+    "tokres_conv": ("dmf_tokens", "TOKRES_CONV"),
     "sgemm_mfma": ("call", "dmf_sgemm_tune"),
     "conc_min_tiles": ("dmf_ops", "CONC_MIN_TILES"),
     "conc_bwd_min_tiles": ("dmf_ops", "CONC_BWD_MIN_TILES"),

@@ -161,6 +161,15 @@ int dmf_conv2d_fwd_affine(int dtype, const void* x, int N, int H, int W, int Cin
  * the persistent dmf_conv2d_fwd_affine form does not take the shape. res / y: NHWC rows, 16-B aligned,
  * whole 16-B channel chunks. dmf_conv2d_fwd_res_ok: 1 when the planner gives this shape such a form
  * (dmf_conv2d_fwd_res refuses the others). */
+/* a token linear (1x1 conv over the rows' NHWC view) -> + bias -> dropout(p) -> x colscale -> + res, f32
+ * out, on the persistent 256x256 form: the proj / fc2 linears of a transformer block that is never
+ * differentiated (transformer_model.py:83-134), with k_gemm_bf16's epilogue and Philox masks (element
+ * m * Cout + n, (rng, site)). res: the f32 residual stream (ldr), y: f32 (ldy), may not alias res.
+ * dmf_conv2d_fwd_tokres_ok: 1 when the shape takes that form. */
+int dmf_conv2d_fwd_tokres_ok(int dtype, int N, int H, int W, int Cin, int Cout);
+int dmf_conv2d_fwd_tokres(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,
+                          const float* bias, const float* colscale, const float* res, int ldr, float dropout_p,
+                          const unsigned long long* rng, int site, float* y, int ldy, void* stream);
 int dmf_conv2d_fwd_res_ok(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                           int dil);
 int dmf_conv2d_fwd_res(int dtype, const void* x, int N, int H, int W, int Cin, int ldx, const void* w, int Cout,

@@ -150,3 +150,40 @@ def test_fc1_dropout_on_conv_engine_matches_token_gemm():
     assert (dropped_c != dropped_g).float().mean().item() < 1e-4  # (a GELU output that is exactly 0 aside)
     d = (yc.float() - yg.float()).abs().max().item()
     assert d <= 2e-2 * yg.float().abs().max().item(), d
+
+
+@pytest.mark.parametrize("hid,p", [(512, 0.0), (512, 0.1), (2048, 0.1)])
+def test_proj_fc2_residual_on_conv_engine_matches_token_gemm(hid, p):
+    """proj (K = E) / fc2 (K = 4E) of a forward-only block on the conv engine (dmf_conv2d_fwd_tokres: + bias,
+    dropout, x LayerScale, + the f32 residual stream, f32 out) against k_gemm_bf16's epilogue with the same rng
+    and site: identical keep masks (a dropped element equals its residual exactly), values within the bf16
+    operands' accumulation-order differences. Config 5's B = 32 inside the two-encoder fork's tile threshold
+    (O.concurrent_tiles), where the production forward takes this form."""
+    torch.manual_seed(6 + hid)
+    b, n, e, site = 32, 576, 512, 9
+    lin = torch.nn.Linear(hid, e).to(DEV)
+    x = torch.randn(b * n, hid, device=DEV).bfloat16()
+    res = torch.randn(b * n, e, device=DEV)
+    gamma = torch.rand(e, device=DEV) + 0.5
+    rng = O.RNG.snapshot(torch.device(DEV))
+    O.concurrent_tiles(True)
+    try:
+        assert D._linear_conv_tokres_ok(x, lin, n, res)
+        with torch.no_grad():
+            yc = D._linear_conv_tokres(x, lin, b, n, gamma, res, p, rng, site)
+    finally:
+        O.concurrent_tiles(False)
+    with torch.no_grad():
+        (w,) = D._wcast(torch.bfloat16, lin.weight)
+        yg = D.gemm(torch.empty((b * n, e), dtype=torch.float32, device=DEV), x, w, b * n, e, hid, lda=hid, ldb=hid,
+                    ldc=e, bias=lin.bias, colscale=gamma, res=res, dropout_p=p, rng=rng, site=site)
+    torch.cuda.synchronize()
+    assert not D._linear_conv_tokres_ok(x, lin, n, res)  # single-stream threshold: the GEMM path
+    if p > 0:
+        dc, dg = yc == res, yg == res
+        frac = dg.float().mean().item()
+        assert 0.08 < frac < 0.12, frac
+        assert torch.equal(dc, dg)
+    scale = (yg - res).abs().max().item()
+    d = (yc - yg).abs().max().item()
+    assert d <= 2e-3 * scale, (d, scale)
