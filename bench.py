@@ -63,9 +63,6 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "fp16", "fp32"], default="bf16",
                     help="compute dtype; fp16 = precision '16-mixed' (fp16 MFMA operands + dynamic loss scale)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="mode A: time the sequential captured step instead of the pipelined steps "
-                         "(step k+1's frozen-encoder forward beside step k's fusion phase)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=32)
@@ -672,12 +669,8 @@ def bench_config1(device, batch, steps, warmup, size=128, chans=16):
                        "size": size, "in_chans": chans, "hipgraph": True}}
 
 
-def bench_fusion(P, device, dtype, mode, batch_size, size, steps, warmup, world, rank, use_graph=True,
-                 pipeline=False):
-    """Config 3/5 fusion training step -> (trainer, batch, seconds for steps, pipelined?).
-    pipeline: run the K steps through FusionTrainer.run_pipelined where it applies (frozen encoders):
-    the same K full steps, each on its own copy of the batch, step k+1's encoder forward overlapping
-    step k's fusion phase (bit-identical to the sequential steps: tests/test_gpu_pipeline.py)."""
+def bench_fusion(P, device, dtype, mode, batch_size, size, steps, warmup, world, rank, use_graph=True):
+    """Config 3/5 fusion training step -> (trainer, batch, seconds for steps)."""
     from dmf_dp import FusionTrainer
 
     lm = build(P, device, dtype, mode, seed=0)
@@ -685,22 +678,15 @@ def bench_fusion(P, device, dtype, mode, batch_size, size, steps, warmup, world,
     batch = synthetic_batch(batch_size, size, device, seed=2 + rank)
     if use_graph:
         trainer.capture(batch)
-    pipelined = pipeline and trainer.pipeline_ok([batch, batch])
-    if pipelined:
-        trainer.run_pipelined([batch] * max(2, warmup))
-    else:
-        for _ in range(warmup):
-            trainer.step(batch)
+    for _ in range(warmup):
+        trainer.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if pipelined:
-        trainer.run_pipelined([batch] * steps)
-    else:
-        for _ in range(steps):
-            trainer.step(batch)
+    for _ in range(steps):
+        trainer.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -710,7 +696,7 @@ def bench_fusion(P, device, dtype, mode, batch_size, size, steps, warmup, world,
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    return trainer, batch, dt, pipelined
+    return trainer, batch, dt
 
 
 # algorithmic work per volume of the fusion step
@@ -782,11 +768,8 @@ def main():
         if args.size == 256:
             args.size = 384
     P["dwi_model_parameters"]["input_size"] = args.size
-    # pipelined steps: one process per GPU at N=1; with N > 1 the fusion phase's overlapped RCCL
-    # exchange would run inside the pipelined graphs -- kept sequential there (not rehearsed on one GPU)
-    trainer, batch, dt, pipelined = bench_fusion(P, device, dtype, args.mode, args.batch, args.size, args.steps,
-                                                 args.warmup, world, rank, use_graph=not args.no_graph,
-                                                 pipeline=not args.no_pipeline and world == 1)
+    trainer, batch, dt = bench_fusion(P, device, dtype, args.mode, args.batch, args.size, args.steps, args.warmup,
+                                      world, rank, use_graph=not args.no_graph)
     loss_val = float(trainer.loss.item()) if trainer.loss is not None else None
     comm_ranks = trainer._rccl.count() if getattr(trainer, "_rccl", None) is not None else None
     if loss_val is not None and loss_val != loss_val:
@@ -809,8 +792,6 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
         "ms_per_step_median": round(med, 3) if med is not None else None,
-        "ms_per_step_median_kind": "sequential captured step (trainer.step), each timed alone",
-        "pipelined": pipelined,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -842,7 +823,7 @@ def main():
         # mode B (all unfrozen) is the DP-scaling headline; measured on every rank (it is a
         # second fusion step, same exchange), reported by rank 0
         torch.cuda.empty_cache()
-        tb, bb_, dtb, _ = bench_fusion(PR.default_parameters(), device, dtype, "B", args.batch, args.size,
+        tb, bb_, dtb = bench_fusion(PR.default_parameters(), device, dtype, "B", args.batch, args.size,
                                     max(10, args.steps // 2), 3, world, rank, use_graph=not args.no_graph)
         nb = max(10, args.steps // 2)
         msb = dtb * 1e3 / nb
@@ -870,11 +851,11 @@ def main():
         P5["dwi_model_parameters"]["patch_embed_fp8"] = True
         P5["dwi_model_parameters"]["input_size"] = 384
         n5 = max(10, args.steps // 2)
-        t5, b5, dt5, pip5 = bench_fusion(P5, device, dtype, "A", args.batch, 384, n5, 3, world, rank,
-                                         use_graph=not args.no_graph, pipeline=not args.no_pipeline and world == 1)
+        t5, b5, dt5 = bench_fusion(P5, device, dtype, "A", args.batch, 384, n5, 3, world, rank,
+                                   use_graph=not args.no_graph)
         roof5 = gemm_probes(t5, b5) if not args.no_roofline else None
         out["config5"] = {"value": round(args.batch * world * n5 / dt5, 2), "unit": "volumes/s",
-                          "ms_per_step": round(dt5 * 1e3 / n5, 3), "steps": n5, "warmup": 3, "pipelined": pip5,
+                          "ms_per_step": round(dt5 * 1e3 / n5, 3), "steps": n5, "warmup": 3,
                           "loss": float(t5.loss.item()) if t5.loss is not None else None,
                           "workload": "fusion training step, config 5 (hybrid TransformerStage encoders, S=384, "
                                       "fp8-e4m3 patch-embed, bf16 elsewhere), mode A",

@@ -465,137 +465,3 @@ class FusionTrainer:
         self.lm.global_step += 1
         self.loss = self._graph_loss  # (an eager ragged step in between rebinds self.loss)
         return self.loss
-
-    # ------------------------------------------------------------ pipelined steps (frozen encoders)
-    def pipeline_ok(self, batches):
-        """Steps can be pipelined when the encoders are frozen (mode A, the reference's state before the
-        unfreeze: selector_helpers.py:541-584): then step k+1's encoder forward depends on nothing step k
-        computes. Also needs captured graphs, one batch shape, and the exchange inside the graph."""
-        lm = self.lm
-        frozen = not any(p.requires_grad for m in (lm.dwi_model, lm.dce_model) for p in m.parameters())
-        return (self.use_graph and frozen and len(batches) > 1 and lm.device.type == "cuda"
-                and (self.world == 1 or self.overlap)
-                and all(tuple(t.shape for t in b) == tuple(t.shape for t in batches[0]) for b in batches))
-
-    def capture_pipelined(self, batch):
-        """Split the step into two captured phases per batch slot j in {0, 1}: E[j] = the frozen
-        encoders' forward of slot j's volumes (its own stream), F[j] = the fusion forward, losses, backward
-        (+ the overlapped exchange) on E[j]'s outputs; the AdamW graph is shared. Dropout offsets are those
-        of the sequential step: E draws its n_e snapshots from its own Philox state and skips the fusion's
-        n_f, F the reverse, so step k's masks equal trainer.step's (run_pipelined keeps the states)."""
-        import dmf_ops as O
-
-        if self.graphs is None or self._graph_sig != self._signature():
-            self.graphs = None
-            self._bucket_ready = False
-            self.capture(batch)
-        lm, dev = self.lm, self.lm.device
-        key = torch.device(dev).index or 0
-        st = O.RNG.state(dev)
-        slots = [self.static_batch, tuple(t.clone() for t in self.static_batch)]
-        self._rng_e = st.clone()
-        self._rng_f = st.clone()
-        self._enc_stream = torch.cuda.Stream(dev)
-        enc_graphs, fus_graphs, enc_outs, losses = [], [], [], []
-        torch.cuda.synchronize()
-        snap = self._snapshot()
-        try:
-            for j in (0, 1):
-                O.RNG.states[key] = self._rng_e
-                t0 = O.RNG.taken
-                g = torch.cuda.CUDAGraph()
-                self._enc_stream.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.graph(g, stream=self._enc_stream), torch.no_grad():
-                    dwi = slots[j][0].to(dev, non_blocking=True)
-                    dce = slots[j][1].to(dev, non_blocking=True)
-                    out = lm._encode(dwi, dce)
-                    n_e = O.RNG.taken - t0
-                    self._n_e = n_e
-                enc_graphs.append(g)
-                enc_outs.append(out)
-                O.RNG.states[key] = self._rng_f
-                t0 = O.RNG.taken
-                lm.__dict__["_injected_enc"] = out
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    losses.append(self._fwd_bwd(slots[j]).detach())
-                    if self.world > 1 and not self.overlap:
-                        self.opt.pack_grads()
-                    self._n_f = O.RNG.taken - t0
-                fus_graphs.append(g)
-                lm.__dict__["_injected_enc"] = None
-            # (run_pipelined advances each phase's state past the other phase's snapshots of the step)
-            n_tot = self._n_e + self._n_f
-        finally:
-            lm.__dict__["_injected_enc"] = None
-            O.RNG.states[key] = st
-            self._restore(snap)
-        self._pipe = {"slots": slots, "enc": enc_graphs, "fus": fus_graphs, "outs": enc_outs, "losses": losses,
-                      "sig": self._signature(), "shape": tuple(t.shape for t in batch), "n_tot": n_tot}
-        torch.cuda.synchronize()
-
-    def run_pipelined(self, batches):
-        """Train on `batches` in order, step k+1's frozen-encoder forward (its own stream) overlapping step
-        k's fusion forward / backward / exchange / AdamW. Every step does all of its work, on its own batch,
-        with the sequential step's dropout masks: parameters, buffers, optimizer state and the Philox
-        state after the run equal those of `for b in batches: trainer.step(b)` (tests/test_gpu_pipeline.py).
-        Falls back to that loop where pipelining does not apply (pipeline_ok)."""
-        import dmf_ops as O
-
-        if not self.pipeline_ok(batches):
-            for b in batches:
-                self.step(b)
-            return self.loss
-        pipe = getattr(self, "_pipe", None)
-        if (pipe is None or pipe["sig"] != self._signature() or self._graph_sig != self._signature()
-                or pipe["shape"] != tuple(t.shape for t in batches[0])):
-            self.capture_pipelined(batches[0])
-            pipe = self._pipe
-        dev = self.lm.device
-        st = O.RNG.state(dev)
-        n_e, n_tot = self._n_e, pipe["n_tot"]
-        main = torch.cuda.current_stream(dev)
-        es = self._enc_stream
-        # E's state at this step's first encoder snapshot, F's at its first fusion snapshot
-        self._rng_e.copy_(st)
-        self._rng_f.copy_(st)
-        N_ = __import__("dmf_native")
-        N_.call("dmf_rng_advance", self._rng_f.data_ptr(), n_e, O._stream())
-        self.opt.sync_hyper()
-        if hasattr(self.lm, "sync_step_scalars"):
-            self.lm.sync_step_scalars()
-        slots, eg, fg = pipe["slots"], pipe["enc"], pipe["fus"]
-        g2 = self.graphs[1]
-        ev_e = [torch.cuda.Event(), torch.cuda.Event()]
-        ev_f = [torch.cuda.Event(), torch.cuda.Event()]
-        es.wait_stream(main)
-
-        def encode(k):
-            j = k % 2
-            with torch.cuda.stream(es):
-                if k >= 2:
-                    es.wait_event(ev_f[j])  # step k-2's fusion phase read slot j and its encoder outputs
-                for dst, src in zip(slots[j], batches[k]):
-                    if dst.data_ptr() != src.data_ptr():
-                        dst.copy_(src, non_blocking=True)
-                eg[j].replay()
-                # (E advanced its own state by n_e; skip the fusion's snapshots of this step)
-                N_.call("dmf_rng_advance", self._rng_e.data_ptr(), n_tot - n_e, es.cuda_stream)
-                ev_e[j].record(es)
-
-        encode(0)
-        for k in range(len(batches)):
-            j = k % 2
-            if k + 1 < len(batches):
-                encode(k + 1)
-            main.wait_event(ev_e[j])
-            fg[j].replay()
-            N_.call("dmf_rng_advance", self._rng_f.data_ptr(), n_tot - self._n_f, main.cuda_stream)
-            g2.replay()
-            ev_f[j].record(main)
-            self.lm.global_step += 1
-            self.loss = pipe["losses"][j]
-        main.wait_stream(es)
-        # the global Philox state as after the same number of sequential steps
-        st.copy_(self._rng_e)
-        return self.loss

@@ -78,7 +78,6 @@ class _Rng:
     def __init__(self):
         self.states = {}
         self.site_ids = itertools.count(1)
-        self.taken = 0  # snapshots taken so far (the pipelined trainer counts them per phase)
 
     def state(self, device):
         key = torch.device(device).index or 0
@@ -95,7 +94,6 @@ class _Rng:
         st = self.state(device)
         snap = st.clone()
         N.call("dmf_rng_advance", st.data_ptr(), 1, _stream())
-        self.taken += 1
         return snap
 
     def manual_seed(self, seed, device):

@@ -110,12 +110,6 @@ class LightningFusionModel(nn.Module):
         snapshots are taken up front in the sequential order (DWI, DCE), so
         the masks match a sequential run; autograd replays each encoder's
         backward on the stream its forward ran on."""
-        # the pipelined trainer (dmf_dp.FusionTrainer.run_pipelined) captures the fusion phase of a step on
-        # encoder outputs it produced beforehand (a frozen-encoder forward of the same batch, captured in
-        # its own graph): hand them over instead of recomputing
-        injected = self.__dict__.get("_injected_enc")
-        if injected is not None:
-            return injected
         # read by dmf_dp.FusionTrainer: the backward's half-chip dgrad tiles only pay when the
         # two encoders' backwards really run on two streams, i.e. when this forward forked
         self.__dict__["_encoders_forked"] = False
