@@ -1125,6 +1125,10 @@ static int g_ps_enable = 1;
 // benchmarking bits of k_conv_fwd_ps (skip DMA / epilogue / stores / statistics): set only through
 // dmf_conv_tune key 6 by the A/B tools (a stray setting would silently corrupt outputs)
 static int g_ps_dbg = 0;
+// 16 = k_conv_fwd_ps output stores nontemporal (streaming) for outputs of at least this many MiB; 0 off.
+// Default 100 (the 512->2048 / S=384 expansions): mode A +0.3 %, config 5 +0.6 %, mode B / config 2
+// +0.2 % (profiles/r06o_nt_store_ab.txt); at 60 (the 64 MiB outputs too) mode A lost 0.3 %
+static int g_ps_nt_mb = 100;
 // 14 / 15 = tiles a launch needs before the wide (256x128) / square (256x256) forms take it: one per
 // CU. At 128 (half a tile per CU, the other encoder stream filling the rest) the two-stream
 // mode-A step measured -1.2 %, but every single-stream launch runs on half the GPU: config 2
@@ -1265,6 +1269,7 @@ static void launch_conv_t(const ConvPlan& plan, bool dgrad, ConvArgs& a, long lo
                       : a.dp > 0.f ? 14
                                               : 1 + a.act;
       a.dbg = g_ps_dbg;
+      if (g_ps_nt_mb > 0 && a.y && (long long)a.M * a.Nout * 2 >= ((long long)g_ps_nt_mb << 20)) a.dbg |= 32;
 #define DMF_PS(E)                                                                                                \
   do {                                                                                                           \
     if (dual) hipLaunchKernelGGL((k_conv_fwd_ps<true, true, E, QBM, QBN, QWN, T>), gp, bq, lds_total, st, a);    \
@@ -1580,6 +1585,7 @@ extern "C" int dmf_conv_tune(int key, int value) {
     case 3: DMF_CHECK_ARG(value >= -2 && value <= 64, "dmf_conv_tune: stat mode %d", value); g_stat_mode = value; return 0;
     case 4: g_ps_enable = value != 0; return 0;
     case 6: g_ps_dbg = value; return 0;
+    case 16: DMF_CHECK_ARG(value >= 0, "dmf_conv_tune: nontemporal threshold %d", value); g_ps_nt_mb = value; return 0;
     case 7: DMF_CHECK_ARG(value >= 0 && value <= 2, "dmf_conv_tune: ping-pong mode %d", value); g_pp_mode = value; return 0;
     case 8: return conv_pp_tune(value != 0);
     case 10: g_stem_enable = value != 0; return 0;

@@ -2739,6 +2739,7 @@ KNOBS = {
     "conv_fast_epi": ("tune", 11),
     "conv_wide_min_tiles": ("tune", 14),
     "conv_sq_min_tiles": ("tune", 15),
+    "conv_nt_store_mb": ("tune", 16),
     "wgrad_dma": ("wgrad_tune", 0),
     "wgrad_wide": ("wgrad_tune", 1),
     "wgrad_tr": ("wgrad_tune", 2),

@@ -67,7 +67,8 @@ int dmf_conv_last_form(void);
  * mode; 4 = persistent 256x256 form on / off; 6 = benchmark-only skip bits of the
  * persistent form; 7 = ping-pong form mode 0..2; 8 = ping-pong persistent grid;
  * 10 = 7x7 stem kernel; 11 = statistics-only epilogue; 14 / 15 = tiles a launch
- * needs for the 256x128 / 256x256 forms.
+ * needs for the 256x128 / 256x256 forms; 16 = persistent-form output stores
+ * nontemporal for outputs of at least this many MiB (0 = off).
  * Documented with their tests in DESIGN.md "Knobs". */
 int dmf_conv_tune(int key, int value);
 /* In-kernel timing stamps of the forward-conv launches (tools/stream_stamps.py): dmf_stamp_arm(buf, n)

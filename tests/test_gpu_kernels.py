@@ -763,6 +763,39 @@ def test_conv_ps_stream_forward(case):
     assert torch.allclose(bd.running_var.cpu(), bn.running_var, rtol=2e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("act", ["relu", "bn"])
+def test_conv_ps_nontemporal_stores_bitwise(act):
+    """knob conv_nt_store_mb (dmf_conv_tune 16): the persistent form's output stores go out nontemporal
+    for outputs of >= that many MiB (default 100: the 512 -> 2048 expansions at B = 32). Threshold 1 here
+    (a 32 MiB output) against 0: the same bits, the same BN statistics."""
+    import dmf_native as N
+
+    torch.manual_seed(10)
+    conv = nn.Conv2d(256, 1024, 1, bias=act == "relu").to(DEV)
+    x = _to_dev(torch.randn(16, 256, 32, 32), torch.bfloat16)  # 256 tiles: the persistent form
+    outs = []
+    for mb in (0, 1):
+        O.set_knobs(conv_nt_store_mb=mb)
+        try:
+            with torch.no_grad():
+                if act == "relu":
+                    y = O.conv2d(x, conv, (O.WeightCache(), O.WeightCache()), act="relu")
+                    rm = None
+                else:
+                    bd = nn.BatchNorm2d(1024).to(DEV)
+                    with O.bn_scope(conv, DEV):
+                        y = O.conv_bn_act(x, conv, (O.WeightCache(), O.WeightCache()), bd, "relu")
+                    rm = bd.running_mean.clone()
+            assert N.FORMS[N.load().dmf_conv_last_form()] == "ps"
+            torch.cuda.synchronize()
+            outs.append((y.clone(), rm))
+        finally:
+            O.set_knobs(conv_nt_store_mb=100)
+    assert torch.equal(outs[0][0], outs[1][0])
+    if act == "bn":
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
 # the 256x256 LDS-DMA weight-gradient tile (dmf_conv_wgrad_tune key 3, knob "wgrad_sq", default 1 = weights
 # of >= 2^18 entries) forced on (2) and off (0), so both forms stay covered: Cout and
 # KH*KW*Cin multiples of 256, its own pixel split count; a dual-source input (the neck's concat)
