@@ -293,7 +293,7 @@ def _conv_launch(fn, args, keep, x, n, h, w, cxt, co, kh, kw, g, ho, wo, y_maps=
         byts = es * (n * h * w * cxt + co * k_tot + y_maps * n * ho * wo * co) if y_maps else 0.0
         probe.append({"fn": fn, "args": args, "keep": keep, "flops": flops, "bytes": byts,
                       "shape": (n, h, w, cxt, co, kh, g.stride, g.dil),
-                      "form": N.FORMS.get(N.load().dmf_conv_last_form(), "?")})
+                      "form": N.FORMS.get(N.load().dmf_conv_last_form(), "?"), "tiles": TILES_NOW[0]})
 
 
 def _is_mfma_conv(weight, g):
@@ -1285,6 +1285,9 @@ CONC_MIN_TILES = 128
 CONC_BWD_MIN_TILES = 128
 
 
+TILES_NOW = [None]  # the forward tiles' launch-size threshold concurrent_tiles set (None: the defaults)
+
+
 def concurrent_tiles(enter, bwd=False):
     """Switch the forward tiles' launch sizing for a two-stream region (CONC_MIN_TILES;
     bwd: CONC_BWD_MIN_TILES for a two-encoder backward)."""
@@ -1292,6 +1295,7 @@ def concurrent_tiles(enter, bwd=False):
     if mt > 0:
         for key in (14, 15):
             N.call("dmf_conv_tune", key, mt if enter else TUNE_VALUES.get(key, 256))
+        TILES_NOW[0] = mt if enter else None
     if bwd:
         return
 
@@ -2664,18 +2668,30 @@ PROBE = {"conv_fwd": None, "conv_wgrad": None, "tok_gemm": None, "fp8_gemm": Non
 # (tok_gemm: dmf_tokens.gemm launches; fp8_gemm: the e4m3 patch-embed GEMM -- config 5's rooflines)
 
 
-def probe_replay(recs, reps=3):
+def probe_replay(recs, reps=3, as_recorded=False):
     """GPU-only average duration (ms) of the recorded conv-forward launches:
     the same C-ABI calls, same buffers, captured into one hipGraph and
     replayed, HIP events around the replay on the capture stream. Returns
     (avg_ms_per_launch, per-shape list of (shape, ms)) -- the per-shape times
-    come from one graph per shape group."""
+    come from one graph per shape group. The launchers pick each call's form
+    again: at the single-stream tile sizing, or (as_recorded) at the sizing the
+    call ran with (a launch recorded inside the two-encoder fork: half-chip
+    tiles; the token family, whose proj / fc2 form exists only there)."""
     def capture(items):
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for r in items:
-                for fn, args in (r["calls"] if "calls" in r else ((r["fn"], r["args"]),)):
-                    N.call(fn, *args, _stream())
+                tiles = r.get("tiles") if as_recorded else None
+                if tiles:
+                    for key in (14, 15):
+                        N.call("dmf_conv_tune", key, tiles)
+                try:
+                    for fn, args in (r["calls"] if "calls" in r else ((r["fn"], r["args"]),)):
+                        N.call(fn, *args, _stream())
+                finally:
+                    if tiles:
+                        for key in (14, 15):
+                            N.call("dmf_conv_tune", key, TUNE_VALUES.get(key, 256))
         return graph
 
     def timed(graph):

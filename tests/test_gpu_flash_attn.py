@@ -187,3 +187,31 @@ def test_proj_fc2_residual_on_conv_engine_matches_token_gemm(hid, p):
     scale = (yg - res).abs().max().item()
     d = (yc - yg).abs().max().item()
     assert d <= 2e-3 * scale, (d, scale)
+
+
+def test_token_probe_replays_the_fork_sizing():
+    """bench.py's token-GEMM probe replays the recorded launches through the C-ABI: a proj / fc2 launch
+    recorded inside the two-encoder fork (half-chip tile sizing, the only sizing at which its persistent
+    form applies at B = 32) must be replayed at that sizing (probe_replay as_recorded) -- replayed at the
+    single-stream sizing the launcher refuses it."""
+    torch.manual_seed(7)
+    b, n, e, hid = 32, 576, 512, 2048
+    lin = torch.nn.Linear(hid, e).to(DEV)
+    x = torch.randn(b * n, hid, device=DEV).bfloat16()
+    res = torch.randn(b * n, e, device=DEV)
+    gamma = torch.rand(e, device=DEV) + 0.5
+    rng = O.RNG.snapshot(torch.device(DEV))
+    recs = []
+    O.PROBE["tok_gemm"] = recs
+    O.concurrent_tiles(True)
+    try:
+        with torch.no_grad():
+            D._linear_conv_tokres(x, lin, b, n, gamma, res, 0.1, rng, 9)
+    finally:
+        O.concurrent_tiles(False)
+        O.PROBE["tok_gemm"] = None
+    assert [r["fn"] for r in recs] == ["dmf_conv2d_fwd_tokres"] and recs[0]["tiles"] == O.CONC_MIN_TILES
+    ms, per = O.probe_replay(recs, as_recorded=True)
+    assert ms > 0 and len(per) == 1
+    with pytest.raises(RuntimeError, match="persistent 1x1"):
+        O.probe_replay(recs)
