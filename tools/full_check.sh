@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-6 checkpoint: the whole GPU suite, then the default bench line.
-# usage: gpurun --timeout 1200 -- bash tools/r06_full.sh TAG
+# Checkpoint of a tree: the whole GPU suite, then the default bench line.
+# usage: gpurun --timeout 1200 -- bash tools/full_check.sh TAG
 set -o pipefail
 TAG=${1:?tag}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
