@@ -332,6 +332,71 @@ __global__ void k_maxpool(const T* __restrict__ x, int N, int H, int W, int C, i
   }
 }
 
+// ------------------------------------------------------ 2x2 average pool (ResNet-D shortcut)
+// timm resnet.py downsample_avg's pool in front of the 1x1 projection: same = 0 is
+// AvgPool2d(2, s, ceil_mode=True, count_include_pad=False) -- windows clipped at the input edge and
+// divided by their in-range count; same = 1 is AvgPool2dSame(2, 1) of a dilated stage -- pad_same adds
+// one zero row / column at the bottom / right, which avg_pool2d then counts (divisor always 4).
+// One thread per output element (NHWC, channel fastest: coalesced); fp32 sums.
+template <typename T>
+__global__ void k_avgpool2(const T* __restrict__ x, int N, int H, int W, int C, int ldx, T* __restrict__ y, int Ho,
+                           int Wo, int ldy, int s, int same) {
+  const long long total = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / ((long long)Ho * Wo));
+    const int rem = (int)(pix - (long long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+    float sum = 0.f;
+    int cnt = 0;
+    for (int r = 0; r < 2; ++r) {
+      const int hi = ho * s + r;
+      if (hi >= H) continue;
+      for (int q = 0; q < 2; ++q) {
+        const int wi = wo * s + q;
+        if (wi >= W) continue;
+        sum += ld(x + ((size_t)(n * H + hi) * W + wi) * ldx + c);
+        ++cnt;
+      }
+    }
+    st(y + pix * ldy + c, sum / (float)(same ? 4 : cnt));
+  }
+}
+
+// backward: each input element sums dy / divisor over the (at most 2x2) windows that contain it
+template <typename T>
+__global__ void k_avgpool2_bwd(const T* __restrict__ dy, int N, int H, int W, int C, int Ho, int Wo, int lddy,
+                               T* __restrict__ dx, int lddx, int s, int same) {
+  const long long total = (long long)N * H * W * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long pix = i / C;
+    const int n = (int)(pix / ((long long)H * W));
+    const int rem = (int)(pix - (long long)n * H * W);
+    const int hi = rem / W, wi = rem - (rem / W) * W;
+    float acc = 0.f;
+    for (int r = 0; r < 2; ++r) {
+      const int th = hi - r;  // window row start ho * s
+      if (th < 0 || th % s) continue;
+      const int ho = th / s;
+      if (ho >= Ho) continue;
+      const int rows = min(th + 2, H) - th;
+      for (int q = 0; q < 2; ++q) {
+        const int tw = wi - q;
+        if (tw < 0 || tw % s) continue;
+        const int wo = tw / s;
+        if (wo >= Wo) continue;
+        const int cols = min(tw + 2, W) - tw;
+        acc += ld(dy + ((size_t)(n * Ho + ho) * Wo + wo) * lddy + c) / (float)(same ? 4 : rows * cols);
+      }
+    }
+    st(dx + pix * lddx + c, acc);
+  }
+}
+
 // backward: each input element receives dy of every window whose (first) argmax it is
 template <typename T>
 __global__ void k_maxpool_bwd(const T* __restrict__ x, int N, int H, int W, int C, int ldx, const T* __restrict__ dy,
@@ -1182,6 +1247,43 @@ extern "C" int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int 
   DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_maxpool<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream, (const T*)x, N, H,
                        W, C, ldx, (T*)y, Ho, Wo, ldy, k, s, p));
   DMF_LAUNCH_CHECK("dmf_maxpool2d");
+  return 0;
+}
+
+// output size of the 2x2 average pool (see k_avgpool2): same -> H; else ceil((H - 2) / s) + 1, the last
+// window dropped when it would start past the input (torch ceil_mode with no padding)
+static inline int avgpool2_out(int H, int s, int same) {
+  if (same) return H;
+  int o = (H - 2 + s - 1) / s + 1;
+  if ((o - 1) * s >= H) --o;
+  return o;
+}
+
+extern "C" int dmf_avgpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo,
+                             int ldy, int s, int same, void* stream) {
+  DMF_CHECK_ARG(x && y && (s == 1 || s == 2) && (same == 0 || (same == 1 && s == 1)) && H >= 2 && W >= 2,
+                "dmf_avgpool2d: bad args (s=%d same=%d H=%d W=%d)", s, same, H, W);
+  DMF_CHECK_ARG(Ho == avgpool2_out(H, s, same) && Wo == avgpool2_out(W, s, same) && ldx >= C && ldy >= C,
+                "dmf_avgpool2d: output %dx%d does not match the pool of %dx%d", Ho, Wo, H, W);
+  const long long total = (long long)N * Ho * Wo * C;
+  if (total == 0) return 0;
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_avgpool2<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)x, N, H, W, C, ldx, (T*)y, Ho, Wo, ldy, s, same));
+  DMF_LAUNCH_CHECK("dmf_avgpool2d");
+  return 0;
+}
+
+extern "C" int dmf_avgpool2d_bwd(int dtype, const void* dy, int N, int H, int W, int C, int Ho, int Wo, int lddy,
+                                 void* dx, int lddx, int s, int same, void* stream) {
+  DMF_CHECK_ARG(dy && dx && (s == 1 || s == 2) && (same == 0 || (same == 1 && s == 1)) && H >= 2 && W >= 2,
+                "dmf_avgpool2d_bwd: bad args");
+  DMF_CHECK_ARG(Ho == avgpool2_out(H, s, same) && Wo == avgpool2_out(W, s, same) && lddy >= C && lddx >= C,
+                "dmf_avgpool2d_bwd: shapes");
+  const long long total = (long long)N * H * W * C;
+  if (total == 0) return 0;
+  DMF_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_avgpool2_bwd<T>, dim3(gsz(total)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dy, N, H, W, C, Ho, Wo, lddy, (T*)dx, lddx, s, same));
+  DMF_LAUNCH_CHECK("dmf_avgpool2d_bwd");
   return 0;
 }
 

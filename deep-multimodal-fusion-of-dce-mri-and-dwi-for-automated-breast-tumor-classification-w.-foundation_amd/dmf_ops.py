@@ -1741,6 +1741,43 @@ def maxpool2d(x, k=3, s=2, p=1):
     return _MaxPoolFn.apply(x, k, s, p)
 
 
+def avgpool2_out(h, s, same):
+    """Output size of dmf_avgpool2d (torch ceil_mode with no padding; 'same' keeps the size)."""
+    if same:
+        return h
+    o = (h - 2 + s - 1) // s + 1
+    return o - 1 if (o - 1) * s >= h else o
+
+
+class _AvgPool2Fn(torch.autograd.Function):
+    """The ResNet-D shortcut's 2x2 average pool (timm resnet.py downsample_avg): dmf_avgpool2d / _bwd."""
+
+    @staticmethod
+    def forward(ctx, x, s, same):
+        n, c, h, w, ld = nhwc(x)
+        ho, wo = avgpool2_out(h, s, same), avgpool2_out(w, s, same)
+        y = empty_nhwc(n, c, ho, wo, x.dtype, x.device)
+        N.call("dmf_avgpool2d", dt(x), x.data_ptr(), n, h, w, c, ld, y.data_ptr(), ho, wo, nhwc(y)[4], s, int(same),
+               _stream())
+        ctx.cfg = (n, c, h, w, ho, wo, s, int(same), x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w, ho, wo, s, same, dtype = ctx.cfg
+        dy = as_nhwc(dy)
+        dx = empty_nhwc(n, c, h, w, dtype, dy.device)
+        N.call("dmf_avgpool2d_bwd", N.dtype_code(dtype), dy.data_ptr(), n, h, w, c, ho, wo, nhwc(dy)[4],
+               dx.data_ptr(), nhwc(dx)[4], s, same, _stream())
+        return dx, None, None
+
+
+def avgpool2(x, s=2, same=False):
+    """2x2 average pool of a NHWC map (AvgPool2d(2, s, ceil_mode=True, count_include_pad=False), or with
+    same=True timm's AvgPool2dSame(2, 1))."""
+    return _AvgPool2Fn.apply(as_nhwc(x), s, bool(same))
+
+
 # -------------------------------------------------- GroupNorm(C,C) of a mix
 class _GNMixFn(torch.autograd.Function):
     """GroupNorm(C,C)(sig(w)*a + (1-sig(w))*b), model_module.py:673-675."""

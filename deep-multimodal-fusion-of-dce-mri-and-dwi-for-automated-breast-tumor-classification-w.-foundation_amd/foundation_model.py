@@ -83,23 +83,57 @@ class Bottleneck(nn.Module):
         else:
             h = O.conv_bn_act(h, self.conv2, _caches(self.conv2), self.bn2, "relu")
         if self.downsample is not None:
-            ds_conv, ds_bn = self.downsample[0], self.downsample[1]
+            if len(self.downsample) == 3:
+                # ResNet-D (avg_down): the pool, then a stride-1 1x1 projection + BN
+                pool, ds_conv, ds_bn = self.downsample
+                xs = pool(x)
+            else:
+                (ds_conv, ds_bn), xs = self.downsample, x
             return O.conv_bn_act(h, self.conv3, _caches(self.conv3), self.bn3, "relu",
-                                 skip=(x, ds_conv, _caches(ds_conv), ds_bn), **kw)
+                                 skip=(xs, ds_conv, _caches(ds_conv), ds_bn), **kw)
         return O.conv_bn_act(h, self.conv3, _caches(self.conv3), self.bn3, "relu", res=x, **kw)
+
+
+class AvgDown(nn.Module):
+    """The pool of timm's ``downsample_avg`` (resnet.py, ResNet-D): AvgPool2d(2, 2, ceil_mode=True,
+    count_include_pad=False) where the stage strides, AvgPool2dSame(2, 1) where output_stride turned the
+    stride into dilation. No parameters (the projection stays ``downsample.1`` / ``downsample.2``)."""
+
+    def __init__(self, stride, same):
+        super().__init__()
+        self.stride, self.same = stride, same
+
+    def forward(self, x):
+        return O.avgpool2(x, self.stride, self.same)
 
 
 class ResNet50OS8(nn.Module):
     """timm ``resnet50`` as built with ``features_only=True, output_stride=8,
     out_indices=(1,2,3,4)``: stem 7x7/2 + maxpool, layer1 (s1), layer2 (s2),
     layer3 (dilation 2), layer4 (dilation 4). forward(x) -> [C2, C3, C4, C5]
-    (NCHW logical / NHWC physical, compute dtype)."""
+    (NCHW logical / NHWC physical, compute dtype).
 
-    def __init__(self, in_chans=3, output_stride=8, layers=(3, 4, 6, 3), compute_dtype=torch.bfloat16):
+    variant "resnet50d" (the reference's other ImageNet option,
+    foundation_model.py:15-68, dispatch :503): timm's ResNet-D -- the deep
+    stem (3x3/2 32 -> 3x3 32 -> 3x3 64, BN + ReLU between, ``conv1.0/1/3/4/6``
+    then ``bn1``) and avg_down shortcuts (``AvgDown`` -> stride-1 1x1 -> BN)."""
+
+    def __init__(self, in_chans=3, output_stride=8, layers=(3, 4, 6, 3), compute_dtype=torch.bfloat16,
+                 variant="resnet50"):
         super().__init__()
+        if variant not in ("resnet50", "resnet50d"):
+            raise ValueError(f"ResNet50OS8: unknown variant {variant!r}")
+        self.variant = variant
+        deep = variant == "resnet50d"
         self.compute_dtype = compute_dtype
         self.in_chans = in_chans
-        self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
+        if deep:
+            self.conv1 = nn.Sequential(
+                nn.Conv2d(in_chans, 32, 3, stride=2, padding=1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+                nn.Conv2d(32, 32, 3, stride=1, padding=1, bias=False), nn.BatchNorm2d(32), nn.ReLU(inplace=True),
+                nn.Conv2d(32, 64, 3, stride=1, padding=1, bias=False))
+        else:
+            self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
         self.act1 = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, 2, 1)
@@ -114,9 +148,16 @@ class ResNet50OS8(nn.Module):
                 net_stride *= stride
             downsample = None
             if stride != 1 or inplanes != planes * Bottleneck.expansion:
-                downsample = nn.Sequential(
-                    nn.Conv2d(inplanes, planes * Bottleneck.expansion, 1, stride=stride, bias=False),
-                    nn.BatchNorm2d(planes * Bottleneck.expansion))
+                if deep:
+                    # timm downsample_avg: no pool at stride 1 / dilation 1; AvgPool2dSame(2, 1) when dilated
+                    pool = nn.Identity() if stride == 1 and dilation == 1 else AvgDown(stride, dilation > 1)
+                    downsample = nn.Sequential(
+                        pool, nn.Conv2d(inplanes, planes * Bottleneck.expansion, 1, stride=1, bias=False),
+                        nn.BatchNorm2d(planes * Bottleneck.expansion))
+                else:
+                    downsample = nn.Sequential(
+                        nn.Conv2d(inplanes, planes * Bottleneck.expansion, 1, stride=stride, bias=False),
+                        nn.BatchNorm2d(planes * Bottleneck.expansion))
             blocks = []
             for b in range(nblocks):
                 blocks.append(Bottleneck(inplanes, planes, stride if b == 0 else 1, downsample if b == 0 else None,
@@ -161,7 +202,13 @@ class ResNet50OS8(nn.Module):
     def _forward(self, x, on_feature):
         if x.shape[1] == self.in_chans or x.dtype != self.compute_dtype:
             x = self.stage_input(x)
-        x = O.conv_bn_act(x, self.conv1, _caches(self.conv1), self.bn1, "relu")
+        if self.variant == "resnet50d":
+            c = self.conv1
+            x = O.conv_bn_act(x, c[0], _caches(c[0]), c[1], "relu")
+            x = O.conv_bn_act(x, c[3], _caches(c[3]), c[4], "relu")
+            x = O.conv_bn_act(x, c[6], _caches(c[6]), self.bn1, "relu")
+        else:
+            x = O.conv_bn_act(x, self.conv1, _caches(self.conv1), self.bn1, "relu")
         x = O.maxpool2d(x, 3, 2, 1)
         feats = []
         for i in range(1, 5):
@@ -429,12 +476,13 @@ def build_radimagenet_backbone(name="resnet50", device="cuda", in_channels=6, ou
 
 def build_imagenet_backbone(name="resnet50d", pretrained=True, device="cuda", in_channels=6, output_stride=8,
                             use_advanced_adapt=False, skip_adapt=True, compute_dtype=torch.bfloat16):
-    """foundation_model.py:15-68. Only the plain resnet50 stem is provided
-    (resnet50d's deep stem is outside the hot-path scope); ImageNet weights
-    are network-only, so the backbone keeps its random init."""
-    if name != "resnet50":
-        raise NotImplementedError(f"backbone {name!r} is not part of the MI355X build (use 'resnet50')")
-    bb = ResNet50OS8(in_chans=in_channels, output_stride=output_stride, compute_dtype=compute_dtype).to(device)
+    """foundation_model.py:15-68: timm ``resnet50`` or ``resnet50d`` (ResNet-D: deep stem, avg_down
+    shortcuts) at output stride 8; ImageNet weights are network-only, so the backbone keeps timm's
+    random init."""
+    if name not in ("resnet50", "resnet50d"):
+        raise NotImplementedError(f"backbone {name!r} is not an ImageNet ResNet of the reference (resnet50 / resnet50d)")
+    bb = ResNet50OS8(in_chans=in_channels, output_stride=output_stride, compute_dtype=compute_dtype,
+                     variant=name).to(device)
     bb.output_dims = bb.feature_info.channels()
     bb.expected_input = "B, C, H, W"
     bb.is_3d = False

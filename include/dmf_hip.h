@@ -354,6 +354,15 @@ int dmf_gn_bwd(int dtype, const void* dy, int lddy, const void* z, int ldz, cons
                void* stream);
 int dmf_maxpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo, int ldy,
                   int k, int s, int p, void* stream);
+/* 2x2 average pool of timm's ResNet-D shortcut (resnet50d, downsample_avg; reference dispatch
+ * foundation_model.py:503 -> timm.create_model("resnet50d", ...) at :29): same = 0 is
+ * AvgPool2d(2, s, ceil_mode=True, count_include_pad=False), same = 1 (s = 1) AvgPool2dSame(2, 1) of a
+ * dilated stage (one zero row / column padded at the end, divisor 4). NHWC; Ho / Wo must be the
+ * pool's output size. The backward scatters dy / divisor to every input of each window. */
+int dmf_avgpool2d(int dtype, const void* x, int N, int H, int W, int C, int ldx, void* y, int Ho, int Wo, int ldy,
+                  int s, int same, void* stream);
+int dmf_avgpool2d_bwd(int dtype, const void* dy, int N, int H, int W, int C, int Ho, int Wo, int lddy, void* dx,
+                      int lddx, int s, int same, void* stream);
 int dmf_maxpool2d_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* dy, int Ho, int Wo,
                       int lddy, void* dx, int lddx, int k, int s, int p, void* stream);
 /* Max pool forward that also records each output element's window position

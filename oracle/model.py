@@ -259,22 +259,54 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        sc = x if self.downsample is None else _bn(_conv(x, self.downsample[0]), self.downsample[1])
+        if self.downsample is None:
+            sc = x
+        elif len(self.downsample) == 3:  # ResNet-D: pool -> 1x1 -> BN
+            sc = _bn(_conv(self.downsample[0](x), self.downsample[1]), self.downsample[2])
+        else:
+            sc = _bn(_conv(x, self.downsample[0]), self.downsample[1])
         h = F.relu(_bn(_conv(x, self.conv1), self.bn1))
         h = F.relu(_bn(_conv(h, self.conv2), self.bn2))
         h = _bn(_conv(h, self.conv3), self.bn3)
         return F.relu(h + sc)
 
 
+class AvgDown(nn.Module):
+    """timm resnet.py downsample_avg's pool (ResNet-D, reference foundation_model.py:15-68 with
+    name='resnet50d'): AvgPool2d(2, stride, ceil_mode=True, count_include_pad=False), or in a
+    dilated stage AvgPool2dSame(2, 1) -- pad_same's zero row / column at the end, then the same
+    avg_pool2d (the padded zeros are input to it, so they count)."""
+
+    def __init__(self, stride, same):
+        super().__init__()
+        self.stride, self.same = stride, same
+
+    def forward(self, x):
+        if self.same:
+            return F.avg_pool2d(F.pad(x, (0, 1, 0, 1)), 2, 1, 0, ceil_mode=True, count_include_pad=False)
+        return F.avg_pool2d(x, 2, self.stride, 0, ceil_mode=True, count_include_pad=False)
+
+
 class ResNet50OS8(nn.Module):
     """timm.create_model('resnet50', features_only=True, output_stride=8,
-    out_indices=(1,2,3,4)) -- returns [layer1, layer2, layer3, layer4]."""
+    out_indices=(1,2,3,4)) -- returns [layer1, layer2, layer3, layer4].
+    variant='resnet50d': timm's ResNet-D (stem_type='deep', stem_width=32,
+    avg_down=True): conv1 = Sequential(3x3/2 -> 32, BN, ReLU, 3x3 -> 32, BN,
+    ReLU, 3x3 -> 64) then bn1; shortcuts AvgDown -> stride-1 1x1 -> BN."""
 
     LAYOUT = ((64, 3), (128, 4), (256, 6), (512, 3))
 
-    def __init__(self, in_chans=3):
+    def __init__(self, in_chans=3, variant="resnet50"):
         super().__init__()
-        self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
+        self.variant = variant
+        deep = variant == "resnet50d"
+        if deep:
+            self.conv1 = nn.Sequential(
+                nn.Conv2d(in_chans, 32, 3, stride=2, padding=1, bias=False), nn.BatchNorm2d(32), nn.ReLU(),
+                nn.Conv2d(32, 32, 3, stride=1, padding=1, bias=False), nn.BatchNorm2d(32), nn.ReLU(),
+                nn.Conv2d(32, 64, 3, stride=1, padding=1, bias=False))
+        else:
+            self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         cin, net_stride, dil, prev_dil = 64, 4, 1, 1
@@ -289,8 +321,13 @@ class ResNet50OS8(nn.Module):
             for bi in range(n):
                 ds = None
                 if bi == 0 and (stride != 1 or cin != planes * 4):
-                    ds = nn.Sequential(nn.Conv2d(cin, planes * 4, 1, stride=stride, bias=False),
-                                       nn.BatchNorm2d(planes * 4))
+                    if deep:
+                        pool = nn.Identity() if stride == 1 and dil == 1 else AvgDown(stride, dil > 1)
+                        ds = nn.Sequential(pool, nn.Conv2d(cin, planes * 4, 1, stride=1, bias=False),
+                                           nn.BatchNorm2d(planes * 4))
+                    else:
+                        ds = nn.Sequential(nn.Conv2d(cin, planes * 4, 1, stride=stride, bias=False),
+                                           nn.BatchNorm2d(planes * 4))
                 blocks.append(Bottleneck(cin, planes, stride if bi == 0 else 1, dil, prev_dil, ds))
                 prev_dil = dil
                 cin = planes * 4
@@ -301,7 +338,13 @@ class ResNet50OS8(nn.Module):
         self.is_3d = False
 
     def forward(self, x):
-        x = F.relu(_bn(_conv(x, self.conv1), self.bn1))
+        if self.variant == "resnet50d":
+            c = self.conv1
+            x = F.relu(_bn(_conv(x, c[0]), c[1]))
+            x = F.relu(_bn(_conv(x, c[3]), c[4]))
+            x = F.relu(_bn(_conv(x, c[6]), self.bn1))
+        else:
+            x = F.relu(_bn(_conv(x, self.conv1), self.bn1))
         x = F.max_pool2d(x, 3, 2, 1)
         feats = []
         for i in range(1, 5):
