@@ -131,3 +131,38 @@ def test_resnet50d_bf16_close():
     errs = [((a.float().cpu() - b).norm() / b.norm().clamp_min(1e-12)).item() for a, b in zip(got, want)]
     print("resnet50d bf16 relative L2 error C2..C5:", [round(e, 5) for e in errs])
     assert max(errs) < 3e-2, errs
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_encoder_with_resnet50d_backbone_matches_oracle(train):
+    """The whole encoder (ModelMaskHeadBackbone: SE gate, BackboneAdapter over C2..C5, ResNetLite blocks,
+    mask head, projectors) with backbone_str 'resnet50d', built through build_medical_backbone, against the
+    oracle's encoder over OM.ResNet50OS8(variant='resnet50d'): logits 1e-3, every map 2e-3 of its max
+    (test_gpu_parity's encoder bar)."""
+    import copy
+
+    import model_module as MM
+    import parameters as PR
+    from test_gpu_parity import batch
+
+    P = copy.deepcopy(PR.small_parameters(dropout=0.0))
+    P["dwi_model_parameters"]["backbone_str"] = "resnet50d"
+    torch.manual_seed(12)
+    bb = FM.build_medical_backbone(P, "cpu", "dwi", 14)
+    assert bb.variant == "resnet50d"
+    enc = MM.initialize_model(MM.ModelMaskHeadBackbone("dwi", P, bb), True)
+    _randomize_bn(enc, 12)
+    ref = OM.ModelMaskHeadBackbone("dwi", P, OM.ResNet50OS8(14, variant="resnet50d"))
+    ref.load_state_dict(enc.state_dict())
+    MM.set_compute_dtype(enc, torch.float32)
+    enc = enc.to(DEV)
+    enc.train(train)
+    ref.train(train)
+    dwi, _, _, _ = batch(2, 64, 6)
+    with torch.no_grad():
+        lo, aux, mp = enc(dwi.to(DEV))
+        lr_, auxr, mpr = ref(dwi)
+    assert (lo.float().cpu() - lr_).abs().max() < 1e-3
+    assert (mp.float().cpu() - mpr).abs().max() < 1e-3
+    for a, b in zip(aux["raw_feats"], auxr["raw_feats"]):
+        assert (a.float().cpu() - b).abs().max() < 2e-3 * max(1.0, b.abs().max().item())
